@@ -1,0 +1,623 @@
+// Scanner layer of the C ABI: the host-side mirror of recordio.NewScanner /
+// NewShardScanner / Scanner (recordio/scannerv2.go:100-425) on top of the GPU
+// batch decoder. Control flow (header, LimitShard, Trailer, Seek, sticky first
+// error) is host logic on a few bytes; every chunk CRC, block parse and
+// untransform runs in the HIP pipeline.
+#include <hip/hip_runtime.h>
+#include <inttypes.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "pipeline.h"
+#include "rio_internal.h"
+
+namespace {
+
+constexpr uint64_t kCk = RIO_CHUNK_SIZE;
+const uint8_t kMagicHeaderBytes[8] = {0xd9, 0xe1, 0xd9, 0x5c, 0xc2, 0x16, 0x04, 0xf7};
+const uint8_t kMagicTrailerBytes[8] = {0xfe, 0xba, 0x1a, 0xd7, 0xcb, 0xdf, 0x75, 0x3a};
+
+struct KV {
+  std::string key;
+  int32_t type = 0;  // 1 bool 2 int 3 uint 4 string
+  int64_t ival = 0;
+  std::string sval;
+};
+
+void fmt_magic_v(const uint8_t *m, char *out) {
+  sprintf(out, "[%u %u %u %u %u %u %u %u]", m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]);
+}
+
+// binary.Uvarint (Go 1.13-1.15)
+uint64_t uvarint(const uint8_t *p, uint64_t n, int64_t *cnt) {
+  uint64_t x = 0;
+  unsigned s = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint8_t b = p[i];
+    if (b < 0x80) {
+      if (i > 9 || (i == 9 && b > 1)) {
+        *cnt = -(int64_t)(i + 1);
+        return 0;
+      }
+      *cnt = (int64_t)i + 1;
+      return x | ((uint64_t)b << s);
+    }
+    if (s < 64) x |= (uint64_t)(b & 0x7f) << s;
+    s += 7;
+  }
+  *cnt = 0;
+  return 0;
+}
+
+// headerDecoder (header.go:140-198)
+struct HeaderDecoder {
+  const uint8_t *p;
+  uint64_t n;
+  std::string err;
+  void set(const char *m) {
+    if (err.empty()) err = m;
+  }
+  int value(KV &v) {
+    if (n == 0) {
+      set("Failed to read byte in header");
+      return 0;
+    }
+    const uint8_t t = *p++;
+    n--;
+    switch (t) {
+    case 1:
+      v.type = 1;
+      if (n == 0) {
+        set("Failed to read byte in header");
+        return 1;
+      }
+      v.ival = *p++ != 0;
+      n--;
+      return 1;
+    case 2:
+    case 3: {
+      int64_t c;
+      uint64_t u = uvarint(p, n, &c);
+      v.type = t;
+      if (c <= 0) {
+        set("Failed to parse uint");
+        return t;
+      }
+      p += c;
+      n -= (uint64_t)c;
+      if (t == 2) {
+        int64_t x = (int64_t)(u >> 1);
+        if (u & 1) x = ~x;
+        v.ival = x;
+      } else {
+        v.ival = (int64_t)u;
+      }
+      return t;
+    }
+    case 4: {
+      KV len;
+      int lt = value(len);
+      v.type = 4;
+      if (!err.empty()) return 4;
+      if (lt != 3) {
+        set("failed to read string key");
+        return 4;
+      }
+      if (n < (uint64_t)len.ival) {
+        char m[96];
+        snprintf(m, sizeof(m), "header invalid string (%" PRIu64 ")", (uint64_t)len.ival);
+        set(m);
+        return 4;
+      }
+      v.sval.assign((const char *)p, (size_t)len.ival);
+      p += len.ival;
+      n -= (uint64_t)len.ival;
+      return 4;
+    }
+    default:
+      set("illegal header type uint8");
+      return 0;
+    }
+  }
+};
+
+}  // namespace
+
+struct rio_scanner {
+  rio_ctx *ctx = nullptr;
+  rio_reader r{};
+  uint64_t file_size = 0;
+  // errors.Once{Ignored: io.EOF}
+  bool err_set = false;
+  rio_error err{};
+  bool pending_set = false;  // error found in a batch, visible once its items are consumed
+  rio_error pending{};
+  bool error_scanner = false;
+  std::vector<KV> header;
+  int32_t codec = RIO_CODEC_NONE;
+  // ChunkScanner position
+  uint64_t off = 0, limit = UINT64_MAX;
+  // current batch
+  uint8_t *span = nullptr;  // pinned host staging
+  uint64_t span_cap = 0;
+  rio_batch batch{};
+  bool have_batch = false;
+  bool done = false;  // no further batches (EOF or error)
+  uint64_t blk = 0, item = 0;  // next item to deliver (global index in batch), its block
+  uint64_t skip = 0;           // items to skip in the first block of the next batch
+  const uint8_t *cur = nullptr;
+  uint64_t cur_len = 0;
+  uint64_t cur_block = 0;
+  int64_t cur_item = 0;
+  std::vector<uint8_t> trailer;
+
+  void set_err(const rio_error &e) {
+    if (!err_set) {
+      err = e;
+      err_set = true;
+    }
+  }
+  void set_errf(int32_t code, uint64_t file_off, const char *fmt, ...) {
+    if (err_set) return;
+    err.code = code;
+    err.file_off = file_off;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(err.msg, sizeof(err.msg), fmt, ap);
+    va_end(ap);
+    err_set = true;
+  }
+  // io.ReadFull at off: returns bytes read; *st 0 ok, 1 EOF, 2 unexpected EOF, 3 io error
+  uint64_t read_full(uint8_t *buf, uint64_t n, uint64_t at, int *st) {
+    uint64_t got = 0;
+    while (got < n) {
+      int64_t k = r.read_at(r.user, buf + got, n - got, at + got);
+      if (k < 0) {
+        *st = 3;
+        return got;
+      }
+      if (k == 0) break;
+      got += (uint64_t)k;
+    }
+    *st = (got == n) ? 0 : (got == 0 ? 1 : 2);
+    return got;
+  }
+  int ensure_span(uint64_t n) {
+    if (span_cap >= n) return 0;
+    if (span) hipHostFree(span);
+    span = nullptr;
+    if (hipHostMalloc((void **)&span, n, hipHostMallocDefault) != hipSuccess) return -1;
+    span_cap = n;
+    return 0;
+  }
+  // read [at, at+n) and decode it on the GPU
+  int decode(uint64_t at, uint64_t n, int32_t cdc, int32_t mode, uint64_t lim, rio_batch *out) {
+    if (ensure_span(n ? n : 1)) {
+      rio_set_error(&out->err, RIO_ERR_HIP, at, "pinned allocation failed");
+      out->stop = RIO_STOP_ERROR;
+      return 0;
+    }
+    int st;
+    uint64_t got = read_full(span, n, at, &st);
+    if (st == 3) {
+      memset(out, 0, sizeof(*out));
+      rio_set_error(&out->err, RIO_ERR_IO, at, "read error at offset %" PRIu64, at + got);
+      out->stop = RIO_STOP_ERROR;
+      return 0;
+    }
+    const int is_end = (at + got >= file_size);
+    return rio_scan_span_mode(ctx, span, got, at, is_end, lim, cdc, mode, out);
+  }
+};
+
+namespace {
+
+bool has_trailer(const rio_scanner *s) {  // header.go:242-254
+  for (const KV &kv : s->header) {
+    if (kv.key != "trailer") continue;
+    return kv.type == 1 && kv.ival;
+  }
+  return false;
+}
+
+void read_header(rio_scanner *s) {
+  // readSpecialBlock(MagicHeader, idTransform) (scannerv2.go:260-306)
+  const uint64_t maxspan = rio_ctx_max_span(s->ctx);
+  uint64_t n = s->file_size < maxspan ? s->file_size : maxspan;
+  rio_batch b;
+  if (s->decode(0, n, RIO_CODEC_NONE, 1, UINT64_MAX, &b) != 0) {
+    s->set_errf(RIO_ERR_HIP, 0, "%s", rio_last_error());
+    return;
+  }
+  char a[64];
+  if (b.stop == RIO_STOP_ERROR) {
+    s->set_err(b.err);
+    return;
+  }
+  if (b.n_blocks == 0) {
+    if (b.stop == RIO_STOP_MORE) {
+      s->set_errf(RIO_ERR_CAPACITY, 0, "header block larger than the GPU span (%" PRIu64 " bytes)", maxspan);
+      return;
+    }
+    fmt_magic_v(kMagicHeaderBytes, a);
+    s->set_errf(RIO_ERR_HEADER, 0, "Failed to read block %s", a);
+    return;
+  }
+  if (b.n_items != 1) {
+    s->set_errf(RIO_ERR_HEADER, 0, "Wrong # of items in header block, %" PRIu64, b.n_items);
+    return;
+  }
+  const uint8_t *item = b.records + b.block_rec_off[0];
+  const uint64_t ilen = b.item_end[0] - b.block_rec_off[0];
+  // ParsedHeader.unmarshal (header.go:211-239)
+  HeaderDecoder d{item, ilen, {}};
+  KV cnt;
+  int t = d.value(cnt);
+  if (d.err.empty() && t != 3) d.set("Failed to read # header entries");
+  if (d.err.empty()) {
+    for (uint64_t i = 0; i < (uint64_t)cnt.ival; i++) {
+      KV key;
+      int kt = d.value(key);
+      if (!d.err.empty()) break;
+      if (kt != 4) {
+        d.set("failed to read string key");
+        break;
+      }
+      KV v;
+      d.value(v);
+      if (!d.err.empty()) break;
+      v.key = key.sval;
+      s->header.push_back(v);
+    }
+  }
+  if (!d.err.empty()) {
+    s->set_errf(RIO_ERR_HEADER, 0, "%s", d.err.c_str());
+    return;
+  }
+  std::vector<const char *> vals;
+  for (const KV &kv : s->header) {
+    if (kv.key != "transformer") continue;
+    if (kv.type != 4) {
+      char v[64];
+      if (kv.type == 1) snprintf(v, sizeof(v), "%s", kv.ival ? "true" : "false");
+      else if (kv.type == 3) snprintf(v, sizeof(v), "%" PRIu64, (uint64_t)kv.ival);
+      else snprintf(v, sizeof(v), "%" PRId64, kv.ival);
+      s->set_errf(RIO_ERR_HEADER, 0, "Expect string value for key %s, but found %s", kv.key.c_str(), v);
+      return;
+    }
+    vals.push_back(kv.sval.c_str());
+  }
+  rio_error e{};
+  if (rio_codec_for_transformers(vals.data(), (int)vals.size(), &s->codec, &e) != 0) {
+    s->set_err(e);
+    return;
+  }
+  s->off = b.consumed;  // end of the header block
+}
+
+// LimitShard (chunk.go:198-236)
+void limit_shard(rio_scanner *s, int start, int limit, int nshard) {
+  const int64_t num_chunks = ((int64_t)s->file_size - (int64_t)s->off) / (int64_t)kCk;
+  const double cps = (double)num_chunks / (double)nshard;
+  const uint64_t start_off = s->off;
+  s->off = start_off + (uint64_t)((int64_t)((double)start * cps) * (int64_t)kCk);
+  s->limit = start_off + (uint64_t)((int64_t)((double)limit * cps) * (int64_t)kCk);
+  if (start == 0) return;
+  uint8_t hdr[RIO_CHUNK_HEADER_SIZE];
+  int st;
+  s->read_full(hdr, sizeof(hdr), s->off, &st);
+  if (st == 1) return;  // io.EOF: ignored
+  if (st == 2) {
+    s->set_errf(RIO_ERR_UNEXPECTED_EOF, s->off, "unexpected EOF");
+    return;
+  }
+  if (st == 3) {
+    s->set_errf(RIO_ERR_IO, s->off, "read error");
+    return;
+  }
+  uint32_t total, index;
+  memcpy(&total, hdr + 20, 4);
+  memcpy(&index, hdr + 24, 4);
+  if (index == 0) return;
+  if (total <= index) {
+    s->set_errf(RIO_ERR_ARG, s->off, "invalid chunk header");
+    return;
+  }
+  s->off += kCk * (uint64_t)(total - index);
+}
+
+// scanNextBatch: decode blocks from s->off until a batch with items or a stop
+bool next_batch(rio_scanner *s) {
+  for (;;) {
+    if (s->err_set || s->done) return false;
+    if (s->off >= s->limit || s->off >= s->file_size) {  // chunk.go:259-262 / EOF
+      s->done = true;
+      return false;
+    }
+    const uint64_t maxspan = rio_ctx_max_span(s->ctx);
+    uint64_t n = s->file_size - s->off;
+    if (n > maxspan) n = maxspan;
+    rio_batch &b = s->batch;
+    if (s->decode(s->off, n, s->codec, 0, s->limit, &b) != 0) {
+      s->set_errf(RIO_ERR_HIP, s->off, "%s", rio_last_error());
+      return false;
+    }
+    s->have_batch = true;
+    s->blk = 0;
+    s->item = 0;
+    if (s->skip && b.n_blocks > 0) {
+      const uint64_t n0 = b.block_first_item[1];
+      s->item = s->skip < n0 ? s->skip : n0;
+    }
+    s->skip = 0;
+    if (b.stop == RIO_STOP_ERROR) {
+      s->pending = b.err;
+      s->pending_set = true;
+      s->done = true;
+    } else if (b.stop == RIO_STOP_EOF) {
+      s->done = true;
+    } else {
+      if (b.consumed == 0) {
+        s->set_errf(RIO_ERR_CAPACITY, s->off, "block at offset %" PRIu64 " larger than the GPU span",
+                    s->off);
+        return false;
+      }
+      s->off += b.consumed;
+    }
+    if (b.n_items > 0) return true;
+    if (s->pending_set) {
+      s->set_err(s->pending);
+      s->pending_set = false;
+      return false;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec, rio_error *err) {
+  // registry.getTransformers (registry.go:51-73): split on the first space
+  int found = 0;
+  int32_t c = RIO_CODEC_NONE;
+  for (int i = 0; i < n; i++) {
+    const char *v = values[i];
+    const char *sp = strchr(v, ' ');
+    size_t len = sp ? (size_t)(sp - v) : strlen(v);
+    if (len == 5 && strncmp(v, "flate", 5) == 0) c = RIO_CODEC_FLATE;
+    else if (len == 4 && strncmp(v, "zstd", 4) == 0) c = RIO_CODEC_ZSTD;
+    else {
+      rio_set_error(err, RIO_ERR_TRANSFORMER, 0, "Transformer %s not found", v);
+      return RIO_ERR_TRANSFORMER;
+    }
+    found++;
+  }
+  if (found > 1) {
+    rio_set_error(err, RIO_ERR_ARG, 0, "transformer chains are not decoded on the GPU");
+    return RIO_ERR_ARG;
+  }
+  *codec = c;
+  return 0;
+}
+
+rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int limit, int nshard) {
+  rio_scanner *s = new rio_scanner();
+  s->ctx = ctx;
+  s->r = *r;
+  s->file_size = r->size < 0 ? 0 : (uint64_t)r->size;
+  // NewShardScanner (scannerv2.go:211-235)
+  uint8_t magic[8];
+  int st;
+  s->read_full(magic, 8, 0, &st);
+  if (st != 0) {
+    s->error_scanner = true;
+    if (st == 2) s->set_errf(RIO_ERR_UNEXPECTED_EOF, 0, "unexpected EOF");
+    if (st == 3) s->set_errf(RIO_ERR_IO, 0, "read error");
+    return s;
+  }
+  if (start >= limit || limit > nshard || start < 0 || nshard <= 0) {
+    s->error_scanner = true;
+    s->set_errf(RIO_ERR_ARG, 0, "invalid sharding [%d,%d) of %d", start, limit, nshard);
+    return s;
+  }
+  if (memcmp(magic, kMagicHeaderBytes, 8) != 0) {
+    s->error_scanner = true;
+    if (start != 0 || limit != 1 || nshard != 1)
+      s->set_errf(RIO_ERR_ARG, 0, "legacy record IOs do not support sharding");
+    else
+      s->set_errf(RIO_ERR_LEGACY, 0, "legacy recordio file: decode with recordio.NewScanner");
+    return s;
+  }
+  if (!ctx) {
+    s->set_errf(RIO_ERR_ARG, 0, "nil rio_ctx");
+    return s;
+  }
+  read_header(s);
+  if (s->err_set) return s;
+  limit_shard(s, start, limit, nshard);
+  return s;
+}
+
+int rio_scanner_scan(rio_scanner *s) {
+  if (!s || s->error_scanner) return 0;
+  for (;;) {
+    if (s->have_batch && s->item < s->batch.n_items) {
+      const rio_batch &b = s->batch;
+      while (s->item >= b.block_first_item[s->blk + 1]) s->blk++;
+      const uint64_t first = b.block_first_item[s->blk];
+      const uint64_t st = (s->item == first) ? b.block_rec_off[s->blk] : b.item_end[s->item - 1];
+      s->cur = b.records + st;
+      s->cur_len = b.item_end[s->item] - st;
+      s->cur_block = b.block_file_off[s->blk];
+      s->cur_item = (int64_t)(s->item - first);
+      s->item++;
+      return 1;
+    }
+    if (s->pending_set) {
+      s->set_err(s->pending);
+      s->pending_set = false;
+    }
+    if (!next_batch(s)) return 0;
+  }
+}
+
+int rio_scanner_get(rio_scanner *s, const uint8_t **data, uint64_t *len) {
+  if (!s || !s->cur) return 0;
+  *data = s->cur;
+  *len = s->cur_len;
+  return 1;
+}
+
+int64_t rio_scanner_next_batch(rio_scanner *s, const uint8_t **data, uint64_t *lens, int64_t max) {
+  int64_t n = 0;
+  while (n < max) {
+    // do not cross into a new GPU batch: views stay valid for the whole call
+    if (n > 0 && !(s->have_batch && s->item < s->batch.n_items)) break;
+    if (!rio_scanner_scan(s)) break;
+    data[n] = s->cur;
+    lens[n] = s->cur_len;
+    n++;
+  }
+  return n;
+}
+
+int rio_scanner_err(rio_scanner *s, rio_error *err) {
+  if (!s || !s->err_set) return 0;
+  if (err) *err = s->err;
+  return s->err.code ? s->err.code : -1;
+}
+
+int rio_scanner_header_len(rio_scanner *s) { return s ? (int)s->header.size() : 0; }
+
+int rio_scanner_header_kv(rio_scanner *s, int i, const char **key, int32_t *type, int64_t *ival,
+                          const uint8_t **sval, uint64_t *slen) {
+  if (!s || i < 0 || i >= (int)s->header.size()) return 0;
+  const KV &kv = s->header[(size_t)i];
+  *key = kv.key.c_str();
+  *type = kv.type;
+  *ival = kv.ival;
+  *sval = (const uint8_t *)kv.sval.data();
+  *slen = kv.sval.size();
+  return 1;
+}
+
+// Trailer (scannerv2.go:316-342) + ReadLastBlock (chunk.go:380-407)
+int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len) {
+  if (!s || s->error_scanner || !has_trailer(s)) return 0;
+  if (s->err_set) return 0;
+  if (s->file_size < kCk) {
+    s->set_errf(RIO_ERR_TRAILER, 0, "bytes.Reader.Seek: negative position");
+    return 0;
+  }
+  const uint64_t last = s->file_size - kCk;
+  rio_batch b;
+  // the last chunk alone: its size/CRC first (readChunk), then its magic
+  if (s->decode(last, kCk, RIO_CODEC_NONE, 3, UINT64_MAX, &b) != 0) {
+    s->set_errf(RIO_ERR_HIP, last, "%s", rio_last_error());
+    return 0;
+  }
+  if (b.stop == RIO_STOP_ERROR) {
+    s->set_err(b.err);
+    return 0;
+  }
+  uint8_t hdr[RIO_CHUNK_HEADER_SIZE];
+  int st;
+  s->read_full(hdr, sizeof(hdr), last, &st);
+  if (memcmp(hdr, kMagicTrailerBytes, 8) != 0) {
+    char a[64];
+    fmt_magic_v(hdr, a);
+    s->set_errf(RIO_ERR_TRAILER, last, "Missing magic trailer; found %s", a);
+    return 0;
+  }
+  uint32_t total, index;
+  memcpy(&total, hdr + 20, 4);
+  memcpy(&index, hdr + 24, 4);
+  uint64_t start = last;
+  if (!(index == 0 && total == 1)) {
+    const uint64_t back = ((uint64_t)index + 1) * kCk;
+    if (back > s->file_size) {
+      s->set_errf(RIO_ERR_TRAILER, 0, "bytes.Reader.Seek: negative position");
+      return 0;
+    }
+    start = s->file_size - back;
+    if (start >= s->limit) {  // ChunkScanner.Scan honours the shard limit
+      s->set_errf(RIO_ERR_TRAILER, start, "Failed to read trailer");
+      return 0;
+    }
+  }
+  if (s->decode(start, s->file_size - start, s->codec, 2, UINT64_MAX, &b) != 0) {
+    s->set_errf(RIO_ERR_HIP, start, "%s", rio_last_error());
+    return 0;
+  }
+  if (b.stop == RIO_STOP_ERROR) {
+    s->set_err(b.err);
+    return 0;
+  }
+  if (b.n_blocks == 0) {
+    s->set_errf(RIO_ERR_TRAILER, start, "Failed to read trailer");
+    return 0;
+  }
+  if (b.n_items != 1) {
+    s->set_errf(RIO_ERR_TRAILER, start, "Expect exactly one trailer item, but found %" PRIu64, b.n_items);
+    return 0;
+  }
+  const uint64_t st0 = b.block_rec_off[0];
+  s->trailer.assign(b.records + st0, b.records + b.item_end[0]);
+  // The ctx buffers are shared with the scan batches: resume the scan at the
+  // block of the next undelivered item (the deferred Seek(curOff) of Trailer).
+  if (s->have_batch && s->item < s->batch.n_items) {
+    uint64_t bk = s->blk;
+    while (s->item >= s->batch.block_first_item[bk + 1]) bk++;
+    s->off = s->batch.block_file_off[bk];
+    s->skip = s->item - s->batch.block_first_item[bk];
+    s->done = false;
+    s->pending_set = false;
+  }
+  s->have_batch = false;
+  *data = s->trailer.data();
+  *len = s->trailer.size();
+  return 1;
+}
+
+void rio_scanner_seek(rio_scanner *s, uint64_t block, int64_t item) {
+  if (!s || s->error_scanner || s->err_set) return;
+  // Seek (scannerv2.go:348-361): restart at the block, skip `item` items
+  s->have_batch = false;
+  s->pending_set = false;
+  s->done = false;
+  s->off = block;
+  s->cur = nullptr;
+  if (!next_batch(s)) return;
+  const uint64_t nfirst = s->batch.block_first_item[1] - s->batch.block_first_item[0];
+  if (item < 0 || (uint64_t)item >= nfirst) {
+    s->set_errf(RIO_ERR_LOCATION, block, "Invalid location {Block:%" PRIu64 " Item:%" PRId64
+                "}, block has only %" PRIu64 " items", block, item, nfirst);
+  }
+  s->item = (uint64_t)(item < 0 ? 0 : item);
+}
+
+void rio_scanner_location(rio_scanner *s, uint64_t *block, int64_t *item) {
+  *block = s ? s->cur_block : 0;
+  *item = s ? s->cur_item : 0;
+}
+
+int rio_scanner_version(rio_scanner *s) {
+  (void)s;
+  return 2;
+}
+
+int rio_scanner_finish(rio_scanner *s, rio_error *err) {
+  if (!s) return 0;
+  int rc = rio_scanner_err(s, err);
+  if (s->span) hipHostFree(s->span);
+  delete s;
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,387 @@
+"""ctypes binding of librio_gpu.so (include/rio_gpu.h) and the Python mirror of
+the reference scanner surface:
+
+    recordio.NewScanner(in, ScannerOpts)          -> NewScanner(src, ScannerOpts)
+    recordio.NewShardScanner(in, opts, s, l, n)   -> NewShardScanner(src, opts, s, l, n)
+    Scanner.{Header,Scan,Get,Err,Seek,Trailer,Version,Finish}
+
+(recordio/scannerv2.go:100-235). Decoding runs in the HIP pipeline; this module
+only moves views. Loading fails loudly when the library is missing — there is
+no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import os
+import threading
+from typing import Callable, List, Optional, Tuple
+
+from .format import Uint
+from .writer import ItemLocation
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_ROOT, "lib", "librio_gpu.so")
+
+RIO_CODEC_NONE, RIO_CODEC_FLATE, RIO_CODEC_ZSTD = 0, 1, 2
+RIO_STOP_MORE, RIO_STOP_EOF, RIO_STOP_ERROR = 0, 1, 2
+U64_MAX = (1 << 64) - 1
+
+
+class RioError(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int32), ("reserved", ctypes.c_int32), ("file_off", ctypes.c_uint64),
+                ("a", ctypes.c_uint64), ("b", ctypes.c_uint64), ("c", ctypes.c_uint64),
+                ("msg", ctypes.c_char * 512)]
+
+
+class RioConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_int32), ("max_span_bytes", ctypes.c_uint64),
+                ("max_out_bytes", ctypes.c_uint64), ("max_items", ctypes.c_uint64)]
+
+
+class RioBatch(ctypes.Structure):
+    _fields_ = [("records", ctypes.c_void_p), ("records_len", ctypes.c_uint64),
+                ("item_end", ctypes.POINTER(ctypes.c_uint64)), ("n_items", ctypes.c_uint64),
+                ("block_first_item", ctypes.POINTER(ctypes.c_uint64)),
+                ("block_rec_off", ctypes.POINTER(ctypes.c_uint64)),
+                ("block_file_off", ctypes.POINTER(ctypes.c_uint64)), ("n_blocks", ctypes.c_uint64),
+                ("consumed", ctypes.c_uint64), ("stop", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("in_bytes", ctypes.c_uint64), ("kernel_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
+                ("err", RioError)]
+
+
+READ_AT = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                           ctypes.c_uint64)
+
+
+class RioReader(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("read_at", READ_AT), ("size", ctypes.c_int64)]
+
+
+# every symbol include/rio_gpu.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "rio_open", "rio_close", "rio_last_error", "rio_abi_version", "rio_stream", "rio_codec_for_transformers",
+    "rio_scan_span", "rio_scan_device", "rio_scan_device_async", "rio_sync", "rio_stage_times", "rio_decode_block",
+    "rio_scanner_new", "rio_scanner_scan", "rio_scanner_get", "rio_scanner_next_batch", "rio_scanner_err",
+    "rio_scanner_header_len", "rio_scanner_header_kv", "rio_scanner_trailer", "rio_scanner_seek",
+    "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish",
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH):
+    """Load librio_gpu.so; raises if it was not built (no fallback)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run __graft_entry__.build() (there is no CPU fallback)")
+        L = ctypes.CDLL(path)
+        P, U64, I64, I32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32
+        L.rio_open.restype = P
+        L.rio_open.argtypes = [ctypes.POINTER(RioConfig)]
+        L.rio_close.argtypes = [P]
+        L.rio_last_error.restype = ctypes.c_char_p
+        L.rio_abi_version.restype = ctypes.c_int
+        L.rio_stream.restype = P
+        L.rio_stream.argtypes = [P]
+        L.rio_codec_for_transformers.restype = ctypes.c_int
+        L.rio_codec_for_transformers.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                                 ctypes.POINTER(I32), ctypes.POINTER(RioError)]
+        L.rio_scan_span.restype = ctypes.c_int
+        L.rio_scan_span.argtypes = [P, P, U64, U64, I32, U64, I32, ctypes.POINTER(RioBatch)]
+        L.rio_scan_device.restype = ctypes.c_int
+        L.rio_scan_device.argtypes = [P, P, U64, U64, I32, U64, I32, ctypes.POINTER(RioBatch)]
+        L.rio_scan_device_async.restype = ctypes.c_int
+        L.rio_scan_device_async.argtypes = [P, P, U64, U64, I32]
+        L.rio_sync.restype = ctypes.c_int
+        L.rio_sync.argtypes = [P, ctypes.POINTER(RioBatch)]
+        L.rio_stage_times.restype = ctypes.c_int
+        L.rio_stage_times.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        L.rio_decode_block.restype = ctypes.c_int
+        L.rio_decode_block.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32),
+                                       ctypes.c_int, I32, P, U64, ctypes.POINTER(U64), ctypes.POINTER(RioError)]
+        L.rio_scanner_new.restype = P
+        L.rio_scanner_new.argtypes = [P, ctypes.POINTER(RioReader), ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.rio_scanner_scan.restype = ctypes.c_int
+        L.rio_scanner_scan.argtypes = [P]
+        L.rio_scanner_get.restype = ctypes.c_int
+        L.rio_scanner_get.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(U64)]
+        L.rio_scanner_next_batch.restype = I64
+        L.rio_scanner_next_batch.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(U64), I64]
+        L.rio_scanner_err.restype = ctypes.c_int
+        L.rio_scanner_err.argtypes = [P, ctypes.POINTER(RioError)]
+        L.rio_scanner_header_len.restype = ctypes.c_int
+        L.rio_scanner_header_len.argtypes = [P]
+        L.rio_scanner_header_kv.restype = ctypes.c_int
+        L.rio_scanner_header_kv.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                            ctypes.POINTER(I32), ctypes.POINTER(I64),
+                                            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(U64)]
+        L.rio_scanner_trailer.restype = ctypes.c_int
+        L.rio_scanner_trailer.argtypes = [P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(U64)]
+        L.rio_scanner_seek.argtypes = [P, U64, I64]
+        L.rio_scanner_location.argtypes = [P, ctypes.POINTER(U64), ctypes.POINTER(I64)]
+        L.rio_scanner_version.restype = ctypes.c_int
+        L.rio_scanner_version.argtypes = [P]
+        L.rio_scanner_finish.restype = ctypes.c_int
+        L.rio_scanner_finish.argtypes = [P, ctypes.POINTER(RioError)]
+        _lib = L
+        return L
+
+
+class RecordioError(Exception):
+    """An error reported by the scanner; str() is the reference's message."""
+
+    def __init__(self, code: int, msg: str, file_off: int = 0):
+        super().__init__(msg)
+        self.code = code
+        self.file_off = file_off
+
+
+def _err(e: RioError) -> RecordioError:
+    return RecordioError(int(e.code), e.msg.decode(errors="replace"), int(e.file_off))
+
+
+class Context:
+    """One rio_ctx: a device, a HIP stream and fixed-capacity buffers."""
+
+    def __init__(self, device: int = 0, max_span_bytes: int = 0, max_out_bytes: int = 0, max_items: int = 0):
+        self.L = load()
+        cfg = RioConfig(device, 0, max_span_bytes, max_out_bytes, max_items)
+        self.h = self.L.rio_open(ctypes.byref(cfg))
+        if not self.h:
+            raise RuntimeError("rio_open failed: " + self.L.rio_last_error().decode())
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self.L.rio_close(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def scan_span(self, span: bytes, file_off: int = 0, is_file_end: bool = True, limit_off: int = U64_MAX,
+                  codec: int = RIO_CODEC_NONE) -> RioBatch:
+        out = RioBatch()
+        buf = (ctypes.c_char * len(span)).from_buffer_copy(span) if not isinstance(span, ctypes.Array) else span
+        rc = self.L.rio_scan_span(self.h, ctypes.addressof(buf), len(span), file_off, int(is_file_end), limit_off,
+                                  codec, ctypes.byref(out))
+        if rc != 0:
+            raise RuntimeError("rio_scan_span: " + self.L.rio_last_error().decode())
+        return out
+
+    def scan_device_async(self, dev_ptr: int, nbytes: int, file_off: int = 0, codec: int = RIO_CODEC_NONE):
+        rc = self.L.rio_scan_device_async(self.h, dev_ptr, nbytes, file_off, codec)
+        if rc != 0:
+            raise RuntimeError("rio_scan_device_async: " + self.L.rio_last_error().decode())
+
+    def sync(self) -> RioBatch:
+        out = RioBatch()
+        if self.L.rio_sync(self.h, ctypes.byref(out)) != 0:
+            raise RuntimeError("rio_sync: " + self.L.rio_last_error().decode())
+        return out
+
+    def stage_times(self):
+        """Device ms of the last run: [parse, codec, crc_copy, resolve]."""
+        ms = (ctypes.c_float * 4)()
+        n = self.L.rio_stage_times(self.h, ms, 4)
+        return [float(ms[i]) for i in range(n)]
+
+    def scan_device(self, dev_ptr: int, nbytes: int, file_off: int = 0, is_file_end: bool = True,
+                    codec: int = RIO_CODEC_NONE) -> RioBatch:
+        out = RioBatch()
+        rc = self.L.rio_scan_device(self.h, dev_ptr, nbytes, file_off, int(is_file_end), U64_MAX, codec,
+                                    ctypes.byref(out))
+        if rc != 0:
+            raise RuntimeError("rio_scan_device: " + self.L.rio_last_error().decode())
+        return out
+
+
+def batch_items(b: RioBatch) -> List[bytes]:
+    """Materialise the items of a host batch (rio_scan_span) as bytes."""
+    items = []
+    if b.n_items == 0:
+        return items
+    data = ctypes.string_at(b.records, b.records_len) if b.records_len else b""
+    ends = b.item_end
+    k = 0
+    for blk in range(b.n_blocks):
+        lo, hi = b.block_first_item[blk], b.block_first_item[blk + 1]
+        st = b.block_rec_off[blk]
+        for i in range(lo, hi):
+            en = ends[i]
+            items.append(data[st:en])
+            st = en
+            k += 1
+    return items
+
+
+@dataclasses.dataclass
+class ScannerOpts:
+    """scannerv2.go:100-111."""
+    LegacyTransform: Optional[Callable] = None
+    Unmarshal: Optional[Callable] = None
+
+
+_default_ctx = {}
+
+
+def default_context(device: int = 0) -> Context:
+    ctx = _default_ctx.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _default_ctx[device] = ctx
+    return ctx
+
+
+class _BytesReader:
+    def __init__(self, data):
+        self.data = memoryview(data).cast("B") if not isinstance(data, bytes) else data
+        self.size = len(data)
+        self._keep = (ctypes.c_char * self.size).from_buffer_copy(bytes(self.data)) if self.size else None
+
+        def read_at(user, buf, n, off):
+            if off >= self.size:
+                return 0
+            k = min(n, self.size - off)
+            ctypes.memmove(buf, ctypes.addressof(self._keep) + off, k)
+            return k
+        self.cb = READ_AT(read_at)
+
+
+class _FileReader:
+    def __init__(self, f):
+        self.f = f
+        f.seek(0, os.SEEK_END)
+        self.size = f.tell()
+
+        def read_at(user, buf, n, off):
+            try:
+                self.f.seek(off)
+                b = self.f.read(n)
+            except Exception:
+                return -1
+            ctypes.memmove(buf, b, len(b))
+            return len(b)
+        self.cb = READ_AT(read_at)
+
+
+class Scanner:
+    """Mirror of the recordio.Scanner interface (scannerv2.go:120-161)."""
+
+    def __init__(self, src, opts: ScannerOpts = None, start: int = 0, limit: int = 1, nshard: int = 1,
+                 ctx: Optional[Context] = None):
+        self.ctx = ctx or default_context()
+        self.L = self.ctx.L
+        self.opts = opts or ScannerOpts()
+        self.unmarshal = self.opts.Unmarshal or (lambda b: b)
+        self._rd = _BytesReader(src) if isinstance(src, (bytes, bytearray, memoryview)) else _FileReader(src)
+        self._rr = RioReader(None, self._rd.cb, self._rd.size)
+        self.h = self.L.rio_scanner_new(self.ctx.h, ctypes.byref(self._rr), start, limit, nshard)
+        self._item = None
+        self._err = None
+
+    def Header(self) -> List[Tuple[str, object]]:
+        out = []
+        for i in range(self.L.rio_scanner_header_len(self.h)):
+            key = ctypes.c_char_p()
+            typ = ctypes.c_int32()
+            ival = ctypes.c_int64()
+            sval = ctypes.c_void_p()
+            slen = ctypes.c_uint64()
+            self.L.rio_scanner_header_kv(self.h, i, ctypes.byref(key), ctypes.byref(typ), ctypes.byref(ival),
+                                         ctypes.byref(sval), ctypes.byref(slen))
+            t = typ.value
+            if t == 1:
+                v = bool(ival.value)
+            elif t == 2:
+                v = int(ival.value)
+            elif t == 3:
+                v = Uint(ival.value & 0xFFFFFFFFFFFFFFFF)
+            else:
+                v = ctypes.string_at(sval.value, slen.value).decode(errors="surrogateescape") if slen.value else ""
+            out.append((key.value.decode(errors="surrogateescape"), v))
+        return out
+
+    def Scan(self) -> bool:
+        if not self.L.rio_scanner_scan(self.h):
+            return False
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        self.L.rio_scanner_get(self.h, ctypes.byref(p), ctypes.byref(n))
+        raw = ctypes.string_at(p.value, n.value) if n.value else b""
+        try:
+            self._item = self.unmarshal(raw)
+        except Exception as e:  # scannerv2.go:396-399
+            self._err = e
+            return False
+        return True
+
+    def ScanBatch(self, max_items: int = 1 << 16) -> List[bytes]:
+        """Batched Scan+Get (rio_scanner_next_batch): raw item bytes."""
+        ptrs = (ctypes.c_void_p * max_items)()
+        lens = (ctypes.c_uint64 * max_items)()
+        n = self.L.rio_scanner_next_batch(self.h, ptrs, lens, max_items)
+        return [ctypes.string_at(ptrs[i], lens[i]) if lens[i] else b"" for i in range(n)]
+
+    def Get(self):
+        return self._item
+
+    def Location(self) -> ItemLocation:
+        b = ctypes.c_uint64()
+        i = ctypes.c_int64()
+        self.L.rio_scanner_location(self.h, ctypes.byref(b), ctypes.byref(i))
+        return ItemLocation(b.value, i.value)
+
+    def Err(self) -> Optional[Exception]:
+        if self._err is not None:
+            return self._err
+        e = RioError()
+        if self.L.rio_scanner_err(self.h, ctypes.byref(e)) != 0:
+            return _err(e)
+        return None
+
+    def Seek(self, loc: ItemLocation):
+        self.L.rio_scanner_seek(self.h, loc.Block, loc.Item)
+
+    def Trailer(self) -> Optional[bytes]:
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        if not self.L.rio_scanner_trailer(self.h, ctypes.byref(p), ctypes.byref(n)):
+            return None
+        return ctypes.string_at(p.value, n.value) if n.value else b""
+
+    def Version(self) -> int:
+        return self.L.rio_scanner_version(self.h)
+
+    def Finish(self) -> Optional[Exception]:
+        err = self.Err()
+        if self.h:
+            self.L.rio_scanner_finish(self.h, None)
+            self.h = None
+        return err
+
+    def __del__(self):  # pragma: no cover
+        try:
+            if self.h:
+                self.L.rio_scanner_finish(self.h, None)
+        except Exception:
+            pass
+
+
+def NewScanner(src, opts: ScannerOpts = None, ctx: Optional[Context] = None) -> Scanner:
+    """recordio.NewScanner (scannerv2.go:200)."""
+    return Scanner(src, opts, 0, 1, 1, ctx)
+
+
+def NewShardScanner(src, opts: ScannerOpts, start: int, limit: int, nshard: int,
+                    ctx: Optional[Context] = None) -> Scanner:
+    """recordio.NewShardScanner (scannerv2.go:211)."""
+    return Scanner(src, opts, start, limit, nshard, ctx)

@@ -1,0 +1,208 @@
+"""Benchmark: recordio scan GiB/s, device-resident, compressed bytes in.
+
+Workload (BASELINE.json configs[1]): uncompressed ('none')
+recordio, 1,000,000 x 256 B records (splitmix64 bytes, seed 0x5EED0001),
+MaxItems=253 -> 3,953 blocks of exactly 2 chunks (64 KiB); the 7,906 body
+chunks are replicated 64x device-resident (~16.1 GiB, 64M records) behind one
+header chunk. One step = one pass of the scan hot path over that whole file:
+chunk CRC32 verify + block structure + varint unpack + record copy into the
+records buffer + item offsets (k_chunk_meta, scans, k_block_parse, k_items,
+k_crc_copy, k_resolve).
+
+N GPUs (torchrun, one process per GPU): every rank scans its own replica set
+(weak scaling, no data-path collective); value = all ranks' input bytes / max
+time over ranks.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_RECORDS = 1_000_000
+RECORD_SIZE = 256
+MAX_ITEMS = 253
+SEED = 0x5EED0001
+REPLICAS = 64
+CHUNK = 32768
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, GB/s (MI355X_MICROARCH.md)
+
+
+def splitmix64(seed: int, n: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def c2_records() -> np.ndarray:
+    """(1e6, 256) uint8 record bytes."""
+    return splitmix64(SEED, N_RECORDS * RECORD_SIZE // 8).view(np.uint8).reshape(N_RECORDS, RECORD_SIZE)
+
+
+def make_c2_file():
+    """C2 file bytes (header chunk + 3,953 two-chunk blocks) and the record count."""
+    from base_amd.recordio import format as F
+    recs = c2_records()
+    out = [F.chunk_block(F.MAGIC_HEADER, F.packed_block_payload([F.marshal_header([])]))]
+    # every block: uvarint(n) + n x uvarint(256) + n x 256 bytes (writerv2.go:388-441)
+    for b0 in range(0, N_RECORDS, MAX_ITEMS):
+        blk = recs[b0:b0 + MAX_ITEMS]
+        hdr = F.put_uvarint(len(blk)) + F.put_uvarint(RECORD_SIZE) * len(blk)
+        out.append(F.chunk_block(F.MAGIC_PACKED, hdr + blk.tobytes()))
+    data = b"".join(out)
+    return data, N_RECORDS
+
+
+def cpu_baseline(data: bytes, budget_s: float = 10.0):
+    """The C oracle (restatement of recordio.NewScanner's loop) on one host core."""
+    from oracle import oracle as O
+    O.build()
+    t0 = time.perf_counter()
+    passes = 0
+    nbytes = 0
+    while True:
+        n, _ = O.scan_count(data)
+        assert n == N_RECORDS
+        passes += 1
+        nbytes += len(data)
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    cpu = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(nbytes / dt / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{passes} x C2 1x file ({len(data)} B, {N_RECORDS} records), C oracle "
+                      f"(oracle/scanner.c) single thread on {cpu}; the Go reference cannot be built here"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--replicas", type=int, default=REPLICAS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from base_amd import build as B
+    if not os.path.exists(B.LIB):
+        B.build()
+    from base_amd.recordio import gpu
+
+    data, nrec = make_c2_file()
+    body = data[CHUNK:]
+    nbody = len(body)
+    total = CHUNK + args.replicas * nbody
+    dev = torch.empty(total, dtype=torch.uint8, device=f"cuda:{local}")
+    host = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    dev[:len(data)].copy_(host)
+    body_dev = dev[CHUNK:CHUNK + nbody]
+    for r in range(1, args.replicas):
+        dev[CHUNK + r * nbody:CHUNK + (r + 1) * nbody].copy_(body_dev)
+    torch.cuda.synchronize()
+    n_items = nrec * args.replicas
+    rec_bytes = args.replicas * ((N_RECORDS // MAX_ITEMS) * MAX_ITEMS * RECORD_SIZE + 64 * 1024)
+    ctx = gpu.Context(local, max_span_bytes=total, max_out_bytes=rec_bytes, max_items=n_items + 1024)
+    span_ptr = dev.data_ptr() + CHUNK
+    span_len = total - CHUNK
+
+    def step():
+        ctx.scan_device_async(span_ptr, span_len, CHUNK, gpu.RIO_CODEC_NONE)
+        return ctx.sync()
+
+    b = step()
+    assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
+    assert b.n_items == n_items, (b.n_items, n_items)
+    for _ in range(args.warmup):
+        step()
+
+    crc_ms, stage_sum = [], np.zeros(4)
+    kern_ms = []
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        bb = step()
+        st = ctx.stage_times()
+        crc_ms.append(st[2])
+        stage_sum += np.array(st)
+        kern_ms.append(bb.kernel_ms)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt / args.steps * 1e3
+    in_bytes = span_len * world
+    value = in_bytes * args.steps / dt / 2 ** 30
+
+    # roofline of the dominant kernel (k_crc_copy): it reads every chunk byte
+    # and writes every record byte (B_in + B_rec per launch)
+    crc_avg = float(np.mean(crc_ms))
+    b_rec = n_items * RECORD_SIZE
+    alg = span_len + b_rec
+    achieved = alg / (crc_avg * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "k_crc_copy", "kernel_ms": round(crc_avg, 3),
+            "alg_bytes_per_launch": alg,
+            "pipeline_alg_GBs": round((span_len + b_rec + 8 * n_items + 8 * b.n_blocks) /
+                                      (np.mean(kern_ms) * 1e-3) / 1e9, 1),
+            "stage_ms": [round(x / args.steps, 3) for x in stage_sum]}
+
+    out = {"metric": "recordio scan GiB/s device-resident (compressed in) at 1/2/4/8 MI355X",
+           "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": "C2: none codec, 1e6 x 256 B records x %d replicas, MaxItems=253 "
+                                  "(64 KiB blocks), chunk CRC32 + packed-unpack" % args.replicas,
+                      "records_per_gpu": int(n_items), "record_bytes": RECORD_SIZE,
+                      "parallelism": f"{world} GPU(s), independent replica sets",
+                      "bytes_in_per_gpu": span_len},
+           "roofline": roof}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(data)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,211 @@
+/*
+ * rio_gpu.h — C ABI of the MI355X recordio block decoder.
+ *
+ * Drop-in boundary for the reference's v2 scan path (grailbio/base recordio):
+ * plain pointers and sizes, no C++ or torch types, no exceptions across the ABI.
+ * A Go cgo shim binds these symbols one-to-one.
+ *
+ * Two layers:
+ *  1. Scanner layer — mirrors recordio.NewScanner / NewShardScanner / Scanner
+ *     (recordio/scannerv2.go:113-235) and ScannerOpts (scannerv2.go:100-111):
+ *     rio_scanner_*.
+ *  2. Batch layer — decode a 32 KiB-aligned span of chunks (host or device
+ *     resident) into records + item offsets in one call: rio_scan_span,
+ *     rio_scan_device. This replaces the per-block loop
+ *     ChunkScanner.Scan -> TransformFunc -> parseChunksToItems
+ *     (recordio/internal/chunk.go:253-345, recordio/scannerv2.go:53-97, 363-388).
+ *  Plus the TransformFunc analogue rio_decode_block (recordio/recordio.go:12)
+ *  and the transformer-registry lookup rio_codec_for_transformers
+ *  (recordio/registry.go:113-148).
+ *
+ * Threading: one rio_ctx per OS thread / goroutine; a ctx (and every scanner
+ * opened on it) is never used concurrently; each ctx owns its HIP stream(s) on
+ * one device. Pointers passed in are not retained past the call (cgo rule).
+ */
+#ifndef RIO_GPU_H
+#define RIO_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RIO_ABI_VERSION 1
+#define RIO_CHUNK_SIZE 32768        /* internal.ChunkSize, chunk.go:25 */
+#define RIO_CHUNK_HEADER_SIZE 28    /* internal.ChunkHeaderSize, chunk.go:22 */
+#define RIO_MAX_CHUNK_PAYLOAD 32740 /* internal.MaxChunkPayloadSize, chunk.go:28 */
+
+/* Block codecs: the untransformer named by the file header (registry.go:113). */
+enum rio_codec {
+    RIO_CODEC_NONE = 0,  /* idTransform, registry.go:31-39 */
+    RIO_CODEC_FLATE = 1, /* recordioflate.FlateUncompress, recordioflate.go:54-65 */
+    RIO_CODEC_ZSTD = 2,  /* recordiozstd.zstdUncompress, recordiozstd.go:67-78 */
+};
+
+/* Error codes carried in rio_error.code (the reference's error conditions). */
+enum rio_err_code {
+    RIO_OK = 0,
+    RIO_ERR_CHUNK_SIZE = 1,     /* "Invalid chunk size %d"                      chunk.go:334 */
+    RIO_ERR_CHUNK_CRC = 2,      /* "Chunk checksum mismatch, expect %d, got %d" chunk.go:341 */
+    RIO_ERR_MAGIC_CHANGED = 3,  /* "Magic number changed in the middle..."      chunk.go:274 */
+    RIO_ERR_CHUNK_INDEX = 4,    /* "Chunk index mismatch, got %v, expect %v..." chunk.go:279 */
+    RIO_ERR_CHUNK_TOTAL = 5,    /* "Chunk nchunk mismatch, got %v, expect %v.." chunk.go:284 */
+    RIO_ERR_UNEXPECTED_EOF = 6, /* "unexpected EOF" (truncated chunk)          chunk.go:318 */
+    RIO_ERR_BAD_MAGIC = 7,      /* "recordio: invalid magic number: %v"        scannerv2.go:386 */
+    RIO_ERR_NITEMS = 8,         /* "...failed to read number of packed items"  scannerv2.go:72 */
+    RIO_ERR_ITEM_SIZE = 9,      /* "...failed to read size of packed item %v"  scannerv2.go:86 */
+    RIO_ERR_BLOCK_SIZE = 10,    /* "...corrupt block header, got block size"   scannerv2.go:94 */
+    RIO_ERR_ITEM_RANGE = 11,    /* wrapped item sizes (the reference panics)   DESIGN.md */
+    RIO_ERR_FLATE_CORRUPT = 12, /* "flate: corrupt input before offset %d"     klauspost flate */
+    RIO_ERR_FLATE_EOF = 13,     /* "unexpected EOF" from the inflater          */
+    RIO_ERR_ZSTD = 14,          /* libzstd error name (DataDog/zstd)           zstd_cgo.go:40 */
+    RIO_ERR_ZSTD_EMPTY = 15,    /* "Bytes slice is empty"                      DataDog ErrEmptySlice */
+    RIO_ERR_HEADER = 16,        /* header block / header KV errors             scannerv2.go:260-306 */
+    RIO_ERR_TRAILER = 17,       /* trailer lookup errors                       scannerv2.go:316-342 */
+    RIO_ERR_TRANSFORMER = 18,   /* "Transformer %s not found"                  registry.go:58 */
+    RIO_ERR_ARG = 19,           /* invalid argument / sharding                 scannerv2.go:226 */
+    RIO_ERR_LEGACY = 20,        /* v1 file: decode with the reference scanner  scannerv2.go:228 */
+    RIO_ERR_IO = 21,            /* reader callback failed                      */
+    RIO_ERR_LOCATION = 22,      /* "Invalid location %+v, block has only %d items" scannerv2.go:358 */
+    RIO_ERR_CAPACITY = 98,      /* span or output exceeds the ctx capacity      */
+    RIO_ERR_HIP = 99,           /* HIP runtime failure                          */
+};
+
+typedef struct rio_error {
+    int32_t code;       /* enum rio_err_code */
+    int32_t reserved;
+    uint64_t file_off;  /* file offset of the failing chunk / block */
+    uint64_t a, b, c;   /* detail values (expected/actual CRC, got/expect index, ...) */
+    char msg[512];      /* the reference's error text, byte for byte where defined */
+} rio_error;
+
+typedef struct rio_config {
+    int32_t device;             /* HIP device ordinal */
+    int32_t flags;              /* reserved, 0 */
+    uint64_t max_span_bytes;    /* largest span per call (multiple of 32768); 0 = 256 MiB */
+    uint64_t max_out_bytes;     /* decoded-bytes capacity per call; 0 = 4 x max_span_bytes */
+    uint64_t max_items;         /* item-offset capacity per call; 0 = max_span_bytes / 16 */
+} rio_config;
+
+typedef struct rio_ctx rio_ctx;
+
+/* Results of one span. Arrays are owned by the ctx and valid until the next call
+ * on it (like "Scan will reuse storage", scannerv2.go:124-126). For
+ * rio_scan_span they are host (pinned) pointers; for rio_scan_device they are
+ * device pointers.
+ * Block b's items are item_end[block_first_item[b] .. block_first_item[b+1])
+ * and its item i spans records[start, item_end[i]) where start is
+ * block_rec_off[b] for the block's first item, else item_end[i-1]. */
+typedef struct rio_batch {
+    const uint8_t *records;
+    uint64_t records_len;
+    const uint64_t *item_end;
+    uint64_t n_items;
+    const uint64_t *block_first_item; /* n_blocks + 1 entries */
+    const uint64_t *block_rec_off;    /* n_blocks entries */
+    const uint64_t *block_file_off;   /* n_blocks entries (ItemLocation.Block) */
+    uint64_t n_blocks;
+    uint64_t consumed;   /* bytes of the span fully decoded (block boundary) */
+    int32_t stop;        /* RIO_STOP_* */
+    int32_t reserved;
+    uint64_t in_bytes;   /* chunk-stream bytes examined */
+    float kernel_ms;     /* device time of the decode pipeline (HIP events) */
+    float total_ms;      /* including H2D / D2H for rio_scan_span */
+    rio_error err;
+} rio_batch;
+
+enum rio_stop {
+    RIO_STOP_MORE = 0,    /* span exhausted at a block boundary; feed the rest */
+    RIO_STOP_EOF = 1,     /* clean end: trailer block, file end or shard limit */
+    RIO_STOP_ERROR = 2,   /* err holds the first error in file order */
+};
+
+/* ---- context ---- */
+rio_ctx *rio_open(const rio_config *cfg);
+void rio_close(rio_ctx *ctx);
+/* thread-local text of the last rio_open / ABI failure */
+const char *rio_last_error(void);
+int rio_abi_version(void);
+/* the HIP stream the ctx launches on (hipStream_t as void*) */
+void *rio_stream(rio_ctx *ctx);
+
+/* Transformer registry lookup (registry.go:113-148 + recordioflate/zstd Init):
+ * resolves the header's "transformer" values to a codec. Returns 0 and sets
+ * *codec, or RIO_ERR_TRANSFORMER ("Transformer %s not found") / RIO_ERR_ARG
+ * (chains of several transformers are not decoded on the GPU). */
+int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec, rio_error *err);
+
+/* ---- batch layer ----
+ * span: bytes at file offset file_off (a block boundary, multiple of 32768).
+ * is_file_end: the span reaches the end of the file (a tail shorter than 32768
+ * bytes then reads as "unexpected EOF"; an unfinished block ends the scan).
+ * limit_off: ChunkScanner.limit (chunk.go:259): blocks starting at or after it
+ * are not scanned; use UINT64_MAX for none.
+ * Returns 0 on success (check out->stop / out->err), <0 on a runtime failure. */
+int rio_scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
+                  int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_batch *out);
+int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, uint64_t file_off,
+                    int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_batch *out);
+
+/* Device-resident benchmark entry: like rio_scan_device but asynchronous on the
+ * ctx stream and with no host copies; call rio_sync to collect the summary. */
+int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, uint64_t file_off,
+                          int32_t codec);
+int rio_sync(rio_ctx *ctx, rio_batch *out);
+
+/* Device time (HIP events on the ctx stream) of the last completed run, per
+ * stage: [0] chunk headers + scans + block parse + items, [1] codec decode
+ * (compressed codecs), [2] k_crc_copy (CRC32 + record copy), [3] resolve.
+ * Returns the number of stages written. */
+int rio_stage_times(rio_ctx *ctx, float *ms, int n);
+
+/* TransformFunc analogue (recordio.go:12): untransform one block given its
+ * chunk payload views; writes into scratch if it fits (returns the length in
+ * *out_len), else returns RIO_ERR_CAPACITY with the needed size in *out_len. */
+int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, const uint32_t *lens, int n,
+                     int32_t codec, uint8_t *scratch, uint64_t cap, uint64_t *out_len,
+                     rio_error *err);
+
+/* ---- scanner layer ---- */
+typedef struct rio_reader {
+    void *user;
+    /* read up to n bytes at offset off into buf; return bytes read (0 at EOF), <0 on error */
+    int64_t (*read_at)(void *user, uint8_t *buf, uint64_t n, uint64_t off);
+    int64_t size; /* file size in bytes */
+} rio_reader;
+
+typedef struct rio_scanner rio_scanner;
+
+/* NewScanner / NewShardScanner (scannerv2.go:200-235). The reader is used
+ * until rio_scanner_finish. Never returns NULL for valid ctx/reader; errors
+ * are reported through rio_scanner_err like errorScanner. */
+rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int limit, int nshard);
+/* Scan (scannerv2.go:390-404): 1 if a new record is available */
+int rio_scanner_scan(rio_scanner *s);
+/* Get: view of the current record, valid until the next scan of a new batch */
+int rio_scanner_get(rio_scanner *s, const uint8_t **data, uint64_t *len);
+/* Batched Scan+Get: up to max records; returns the count (0 at end/error) */
+int64_t rio_scanner_next_batch(rio_scanner *s, const uint8_t **data, uint64_t *lens, int64_t max);
+/* Err (scannerv2.go:406-412): 0 when nil, else fills err */
+int rio_scanner_err(rio_scanner *s, rio_error *err);
+/* Header (scannerv2.go:312): key/value i; type 1 bool, 2 int, 3 uint, 4 string */
+int rio_scanner_header_len(rio_scanner *s);
+int rio_scanner_header_kv(rio_scanner *s, int i, const char **key, int32_t *type, int64_t *ival,
+                          const uint8_t **sval, uint64_t *slen);
+/* Trailer (scannerv2.go:316-342): 1 and a view when present, 0 = nil */
+int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len);
+/* Seek (scannerv2.go:348-361) to ItemLocation{block, item} */
+void rio_scanner_seek(rio_scanner *s, uint64_t block, int64_t item);
+/* ItemLocation of the current record */
+void rio_scanner_location(rio_scanner *s, uint64_t *block, int64_t *item);
+/* Version (scannerv2.go:308): 2 */
+int rio_scanner_version(rio_scanner *s);
+/* Finish (scannerv2.go:414-425): returns Err() code and frees the scanner */
+int rio_scanner_finish(rio_scanner *s, rio_error *err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RIO_GPU_H */

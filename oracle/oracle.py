@@ -1,0 +1,196 @@
+"""ORACLE — test infrastructure only.
+
+ctypes view of oracle/_build/liboracle.so, the C restatement of the reference
+scan path (see oracle/scanner.c for the file:line map). Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+and only as the checker; the product path never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import os
+import subprocess
+from typing import List, Optional, Tuple
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its committed Makefile (gcc)."""
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        build()
+    L = ctypes.CDLL(_LIB_PATH)
+    P, I64, U64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64
+    L.orc_scan.restype = P
+    L.orc_scan.argtypes = [ctypes.c_char_p, I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.orc_seek_get.restype = P
+    L.orc_seek_get.argtypes = [ctypes.c_char_p, I64, U64, I64]
+    L.orc_free.argtypes = [P]
+    L.orc_n_items.restype = I64
+    L.orc_n_items.argtypes = [P]
+    L.orc_items.restype = ctypes.POINTER(ctypes.c_uint8)
+    L.orc_items.argtypes = [P]
+    L.orc_item_ends.restype = ctypes.POINTER(U64)
+    L.orc_item_ends.argtypes = [P]
+    L.orc_item_block.restype = ctypes.POINTER(U64)
+    L.orc_item_block.argtypes = [P]
+    L.orc_item_index.restype = ctypes.POINTER(I64)
+    L.orc_item_index.argtypes = [P]
+    L.orc_err.restype = ctypes.c_char_p
+    L.orc_err.argtypes = [P]
+    L.orc_has_trailer.restype = ctypes.c_int
+    L.orc_has_trailer.argtypes = [P]
+    L.orc_trailer.restype = ctypes.POINTER(ctypes.c_uint8)
+    L.orc_trailer.argtypes = [P, ctypes.POINTER(I64)]
+    L.orc_header_len.restype = ctypes.c_int
+    L.orc_header_len.argtypes = [P]
+    L.orc_header_kv.restype = ctypes.c_int
+    L.orc_header_kv.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                ctypes.POINTER(ctypes.c_int), ctypes.POINTER(I64),
+                                ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(I64)]
+    L.orc_is_legacy.restype = ctypes.c_int
+    L.orc_is_legacy.argtypes = [P]
+    L.orc_crc32.restype = ctypes.c_uint32
+    L.orc_crc32.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+    L.orc_inflate.restype = ctypes.c_int
+    L.orc_inflate.argtypes = [ctypes.c_char_p, I64, ctypes.c_void_p, I64, ctypes.POINTER(I64),
+                              ctypes.POINTER(I64)]
+    L.orc_zstd_decompress.restype = ctypes.c_int
+    L.orc_zstd_decompress.argtypes = [ctypes.c_char_p, I64, ctypes.c_void_p, I64,
+                                      ctypes.POINTER(I64), ctypes.POINTER(ctypes.c_char_p)]
+    L.orc_zstd_content_size.restype = I64
+    L.orc_zstd_content_size.argtypes = [ctypes.c_char_p, I64]
+    L.orc_shard_range.argtypes = [I64, I64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(I64), ctypes.POINTER(I64)]
+    L.orc_scan_count.restype = I64
+    L.orc_scan_count.argtypes = [ctypes.c_char_p, I64, ctypes.POINTER(I64), ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int]
+    _lib = L
+    return L
+
+
+@dataclasses.dataclass
+class ScanResult:
+    header: List[Tuple[str, object]]
+    items: List[bytes]
+    locations: List[Tuple[int, int]]
+    trailer: Optional[bytes]
+    err: str
+    legacy: bool
+
+
+def _header(L, r):
+    from base_amd.recordio.format import Uint
+    out = []
+    for i in range(L.orc_header_len(r)):
+        key = ctypes.c_char_p()
+        typ = ctypes.c_int()
+        ival = ctypes.c_int64()
+        sval = ctypes.POINTER(ctypes.c_uint8)()
+        slen = ctypes.c_int64()
+        L.orc_header_kv(r, i, ctypes.byref(key), ctypes.byref(typ), ctypes.byref(ival),
+                        ctypes.byref(sval), ctypes.byref(slen))
+        k = key.value.decode(errors="surrogateescape")
+        t = typ.value
+        if t == 1:
+            v = bool(ival.value)
+        elif t == 2:
+            v = int(ival.value)
+        elif t == 3:
+            v = Uint(ival.value & 0xFFFFFFFFFFFFFFFF)
+        else:
+            v = ctypes.string_at(sval, slen.value).decode(errors="surrogateescape") if slen.value else ""
+        out.append((k, v))
+    return out
+
+
+def _collect(L, r) -> ScanResult:
+    n = L.orc_n_items(r)
+    items, locs = [], []
+    if n:
+        ends = L.orc_item_ends(r)
+        blocks = L.orc_item_block(r)
+        idx = L.orc_item_index(r)
+        total = ends[n - 1]
+        data = ctypes.string_at(L.orc_items(r), total) if total else b""
+        st = 0
+        for i in range(n):
+            en = ends[i]
+            items.append(data[st:en])
+            locs.append((int(blocks[i]), int(idx[i])))
+            st = en
+    trailer = None
+    if L.orc_has_trailer(r):
+        ln = ctypes.c_int64()
+        p = L.orc_trailer(r, ctypes.byref(ln))
+        trailer = ctypes.string_at(p, ln.value) if ln.value else b""
+    return ScanResult(_header(L, r), items, locs, trailer, L.orc_err(r).decode(),
+                      bool(L.orc_is_legacy(r)))
+
+
+def scan(data: bytes, start: int = 0, limit: int = 1, nshard: int = 1,
+         read_trailer: bool = True) -> ScanResult:
+    L = lib()
+    r = L.orc_scan(data, len(data), start, limit, nshard, 1 if read_trailer else 0)
+    try:
+        return _collect(L, r)
+    finally:
+        L.orc_free(r)
+
+
+def seek_get(data: bytes, block: int, item: int) -> ScanResult:
+    L = lib()
+    r = L.orc_seek_get(data, len(data), block, item)
+    try:
+        return _collect(L, r)
+    finally:
+        L.orc_free(r)
+
+
+def crc32(data: bytes) -> int:
+    return lib().orc_crc32(0, data, len(data))
+
+
+def inflate(data: bytes, cap: int = 1 << 26):
+    """Returns (rc, output, err_off)."""
+    L = lib()
+    buf = ctypes.create_string_buffer(max(cap, 1))
+    olen = ctypes.c_int64()
+    eoff = ctypes.c_int64()
+    rc = L.orc_inflate(data, len(data), buf, cap, ctypes.byref(olen), ctypes.byref(eoff))
+    return rc, buf.raw[:olen.value], eoff.value
+
+
+def zstd_decompress(data: bytes, cap: int = 1 << 26):
+    L = lib()
+    buf = ctypes.create_string_buffer(max(cap, 1))
+    olen = ctypes.c_int64()
+    msg = ctypes.c_char_p()
+    rc = L.orc_zstd_decompress(data, len(data), buf, cap, ctypes.byref(olen), ctypes.byref(msg))
+    return rc, buf.raw[:olen.value], (msg.value or b"").decode()
+
+
+def shard_range(file_size: int, off: int, start: int, limit: int, nshard: int):
+    L = lib()
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    L.orc_shard_range(file_size, off, start, limit, nshard, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def scan_count(data: bytes, start: int = 0, limit: int = 1, nshard: int = 1):
+    """CPU-baseline entry: (items, bytes) or (-1, bytes) on error."""
+    b = ctypes.c_int64()
+    n = lib().orc_scan_count(data, len(data), ctypes.byref(b), start, limit, nshard)
+    return n, b.value

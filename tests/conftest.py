@@ -1,0 +1,62 @@
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the C ABI on the GPU)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    """The CPU restatement (test infrastructure only)."""
+    from oracle import oracle as O
+    O.build()
+    return O
+
+
+@pytest.fixture(scope="session")
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)["cases"]
+
+
+def golden_bytes(case):
+    with open(os.path.join(GOLDEN, case["file"]), "rb") as f:
+        return f.read()
+
+
+@pytest.fixture(scope="session")
+def gpu_lib():
+    """librio_gpu.so, built in-tree; a GPU test fails loudly when it is missing."""
+    from base_amd import build as B
+    if not os.path.exists(B.LIB):
+        B.build()
+    from base_amd.recordio import gpu
+    return gpu.load()
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx(gpu_lib):
+    from base_amd.recordio import gpu
+    ctx = gpu.Context(0, max_span_bytes=64 << 20)
+    yield ctx
+    ctx.close()
+
+
+def oracle_has_zstd(O):
+    from base_amd.recordio.codecs import have_zstd, zstd_compress
+    return have_zstd() and O.zstd_decompress(zstd_compress(b"probe", 1))[0] == 0
+
+
+def run(cmd):
+    return subprocess.run(cmd, capture_output=True, text=True)
