@@ -16,8 +16,8 @@ LIB = os.path.join(OUT_DIR, "librio_gpu.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RIO_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["kernels.hip", "codec.hip", "codec_flate.hip", "codec_zstd.hip", "pipeline.cpp", "scanner.cpp",
-           "crc_tables.cpp"]
+SOURCES = ["kernels.hip", "blocks.hip", "crc.hip", "codec.hip", "codec_flate.hip", "codec_zstd.hip",
+           "pipeline.cpp", "messages.cpp", "scanner.cpp", "crc_tables.cpp"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
          "-I", CSRC, "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result"]
 

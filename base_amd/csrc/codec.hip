@@ -64,15 +64,6 @@ void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned l
   hipLaunchKernelGGL(k_codec_stub, dim3(g ? g : 1), dim3(256), 0, st, d, nblocks_dev);
 }
 
-void launch_codec_gather(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
-                         uint64_t rec_cap, void *stream) {
-  (void)d;
-  (void)nblocks_dev;
-  (void)max_blocks;
-  (void)rec_cap;
-  (void)stream;
-}
-
 void codec_error_text(uint64_t code, uint64_t off, uint64_t file_off, rio_error *e) {
   switch (code) {
   case kCodecCorrupt:

@@ -57,18 +57,24 @@ uint32_t crc32_host(const uint8_t *p, size_t n) {
   return ~c;
 }
 
-void build_crc_tables(uint32_t *fold, uint32_t *tree, uint32_t *fix_a, uint32_t *fix_b) {
-  // fold[j][b] = R(b || 0^(1023-j)): one 16-byte unit per lane per 1 KiB row,
-  // the row gap of 1008 bytes folded into the table (Horner step in one pass).
-  for (int j = 0; j < 16; j++) {
-    uint32_t sh = gf_xpow8(1023 - j);
-    for (int b = 0; b < 256; b++) fold[j * 256 + b] = gf_mul(byte_table((uint32_t)b), sh);
+void build_crc_tables(uint32_t *fold, uint32_t *mul, uint32_t *fix_a, uint32_t *fix_b) {
+  // fold[j][b] = R(b || 0^(1023-j)): a dword stream with one dword per 1 KiB
+  // row, the 1020-byte gap to its next dword folded into the table (one Horner
+  // step per lookup set). Each table is stored x32, entry b of copy k at word
+  // (j*256 + b)*32 + k, so lane l reading copy (l & 31) always hits bank l & 31.
+  for (int j = 0; j < 4; j++) {
+    const uint32_t sh = gf_xpow8(1023 - j);
+    for (int b = 0; b < 256; b++) {
+      const uint32_t v = gf_mul(byte_table((uint32_t)b), sh);
+      for (int k = 0; k < kFoldCopies; k++) fold[(j * 256 + b) * kFoldCopies + k] = v;
+    }
   }
-  // tree[l][k][b] = (b << 8k) * x^(-128 * 2^l): lane-pair combine at level l.
-  for (int l = 0; l < 6; l++) {
-    uint32_t c = gf_xpow8(-(int64_t)16 << l);
+  // mul[m][k][b] = (b << 8k) * c_m: multiply by c_0 = x^-32 (combine the 4
+  // dword streams of a lane) and c_{l+1} = x^-(128*2^l) (lane tree, level l).
+  for (int m = 0; m < kMulTables; m++) {
+    const uint32_t c = (m == 0) ? gf_xpow8(-4) : gf_xpow8(-((int64_t)16 << (m - 1)));
     for (int k = 0; k < 4; k++)
-      for (int b = 0; b < 256; b++) tree[(l * 4 + k) * 256 + b] = gf_mul((uint32_t)b << (8 * k), c);
+      for (int b = 0; b < 256; b++) mul[(m * 4 + k) * 256 + b] = gf_mul((uint32_t)b << (8 * k), c);
   }
   // per payload size: crc = ~(fix_a[size] ^ V * fix_b[size]) where V is the
   // raw CRC of the whole 32 KiB chunk with bytes outside [12, 28+size) zeroed.

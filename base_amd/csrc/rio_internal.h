@@ -8,9 +8,10 @@
 
 namespace rio {
 
-constexpr int kChunk = RIO_CHUNK_SIZE;        // chunk.go:25
-constexpr int kChunkHdr = RIO_CHUNK_HEADER_SIZE;  // chunk.go:22
+constexpr int kChunk = RIO_CHUNK_SIZE;              // chunk.go:25
+constexpr int kChunkHdr = RIO_CHUNK_HEADER_SIZE;    // chunk.go:22
 constexpr int kMaxPayload = RIO_MAX_CHUNK_PAYLOAD;  // chunk.go:28
+constexpr unsigned long long kItemInRecords = RIO_ITEM_IN_RECORDS;
 
 // Magic classes (magic.go:15-36).
 enum MagicClass : uint32_t { kMagicHeader = 0, kMagicPacked = 1, kMagicTrailer = 2, kMagicOther = 3 };
@@ -19,45 +20,45 @@ enum MagicClass : uint32_t { kMagicHeader = 0, kMagicPacked = 1, kMagicTrailer =
 // checks (chunk.go:273-287, 333-336).
 enum ChunkErr : uint32_t {
   kCkOk = 0,
-  kCkSize = 1,           // size > 32740
-  kCkMagicChanged = 2,   // magic differs from the block's first chunk
-  kCkIndex = 3,          // index != expected
-  kCkTotal = 4,          // total != block's total
+  kCkSize = 1,          // size > 32740
+  kCkMagicChanged = 2,  // magic differs from the block's first chunk
+  kCkIndex = 3,         // index != expected
+  kCkTotal = 4,         // total != block's total
 };
 
 // Block status codes (k_block_parse).
 enum BlockStatus : uint32_t {
   kBlkOk = 0,
-  kBlkIncomplete = 1,   // extends past the span (or total == 0)
-  kBlkBadMagic = 2,     // neither packed nor (mode-appropriate) header/trailer
-  kBlkNItems = 3,       // uvarint item count failed: a = n
-  kBlkItemSize = 4,     // uvarint size failed: a = item index, b = n
-  kBlkBlockSize = 5,    // total + pos != len: a = len, b = total + pos
-  kBlkItemRange = 6,    // wrapped sizes (reference panics)
-  kBlkTrailer = 7,      // trailer block in body mode: clean end of scan
-  kBlkLimit = 8,        // starts at/after the shard limit
-  kBlkCodec = 9,        // decompression failed: a = codec error code, b = offset
+  kBlkIncomplete = 1,  // extends past the span (or total == 0)
+  kBlkBadMagic = 2,    // neither packed nor (mode-appropriate) header/trailer
+  kBlkNItems = 3,      // uvarint item count failed: a = n
+  kBlkItemSize = 4,    // uvarint size failed: a = item index, b = n
+  kBlkBlockSize = 5,   // total + pos != len: a = len, b = total + pos
+  kBlkItemRange = 6,   // wrapped sizes (reference panics)
+  kBlkTrailer = 7,     // trailer block in body mode: clean end of scan
+  kBlkLimit = 8,       // starts at/after the shard limit
+  kBlkCodec = 9,       // decompression failed: a = codec error code, b = offset
 };
 
 enum Mode : int32_t { kModeBody = 0, kModeHeader = 1, kModeTrailer = 2, kModeLastChunk = 3 };
 
 // Control block written by the kernels, read back by the host (one copy).
 struct Ctl {
-  unsigned long long first_chunk_err;   // min chunk with size/structural error
-  unsigned long long first_crc_err;     // min chunk with CRC mismatch
-  unsigned long long first_block_event; // min over block event keys (2*chunk + 1 / 2*c0)
-  unsigned long long first_incomplete;  // min c0 of a block extending past the span
-  unsigned long long out_overflow;      // nonzero if records/items exceeded capacity
+  unsigned long long first_chunk_err;    // min chunk with size/structural error
+  unsigned long long first_crc_err;      // min chunk with CRC mismatch
+  unsigned long long first_block_event;  // min over block event keys (2*chunk + 1 / 2*c0)
+  unsigned long long first_incomplete;   // min c0 of a block extending past the span
+  unsigned long long out_overflow;       // nonzero if side/items exceeded capacity
   unsigned long long pad[3];
   // filled by k_resolve
   unsigned long long stop_key;
   unsigned long long n_valid_blocks;
   unsigned long long n_items;
-  unsigned long long rec_bytes;
-  unsigned long long stop_block;        // block index at the stop (or ~0)
-  unsigned long long stop_kind;         // 0 more, 1 eof, 2 error
-  unsigned long long err_chunk;         // chunk of a chunk-level error (or ~0)
-  unsigned long long err_code;          // ChunkErr / CRC(100) / unexpected EOF(101)
+  unsigned long long rec_bytes;   // side-buffer / decoded bytes used by the valid blocks
+  unsigned long long stop_block;  // block index at the stop (or ~0)
+  unsigned long long stop_kind;   // 0 more, 1 eof, 2 error
+  unsigned long long err_chunk;   // chunk of a chunk-level error (or ~0)
+  unsigned long long err_code;    // ChunkErr / CRC(100) / unexpected EOF(101)
   // details of the stop (filled by k_resolve)
   unsigned long long ck_size, ck_total, ck_index, ck_info;
   unsigned long long ck_crc_stored, ck_crc_actual;
@@ -69,40 +70,49 @@ struct Ctl {
 
 constexpr unsigned long long kNone = ~0ull;
 
-// Device arrays of one context (capacities fixed at rio_open).
+// An item that crosses a chunk payload boundary (the 28-byte chunk header sits
+// inside it): copied from logical payload bytes [src, src+len) of the block
+// starting at chunk c0 to side[dst].
+struct StradDesc {
+  unsigned long long c0, src, len, dst;
+};
+
+// Device arrays of one context (capacities fixed at rio_open, grown on demand).
 struct DevBufs {
   // per chunk
   uint32_t *ck_size, *ck_total, *ck_index, *ck_info;  // info: magic class | err << 8
-  uint32_t *ck_crc;        // computed CRC32 per chunk
-  uint32_t *ck_block;      // block index of the chunk (valid in the consistent prefix)
-  unsigned long long *ck_pay;  // exclusive prefix of payload sizes (nchunks + 1)
+  uint32_t *ck_crc;                                   // computed CRC32 per chunk
+  uint32_t *ck_block;            // block index of the chunk (valid in the consistent prefix)
+  unsigned long long *ck_pay;    // exclusive prefix of payload sizes (nchunks + 1)
   // per block
-  unsigned long long *blk_c0;        // first chunk
-  unsigned long long *blk_nitems;    // item count (0 unless ok)
-  unsigned long long *blk_hdr;       // varint header length
-  unsigned long long *blk_recb;      // record bytes (padded to 16 for the base scan)
-  unsigned long long *blk_item_base; // exclusive scan of nitems (n + 1)
-  unsigned long long *blk_rec_base;  // exclusive scan of recb (n + 1)
-  unsigned long long *blk_status;    // BlockStatus | a << 8 ... (see kernels)
+  unsigned long long *blk_c0;         // first chunk
+  unsigned long long *blk_nitems;     // item count (0 unless ok)
+  unsigned long long *blk_hdr;        // varint header length
+  unsigned long long *blk_item_base;  // exclusive scan of nitems (n + 1)
+  unsigned long long *blk_sb;         // straddler side bytes (padded to 16)
+  unsigned long long *blk_sn;         // straddler count
+  unsigned long long *blk_sb_base;    // exclusive scan of blk_sb (n + 1)
+  unsigned long long *blk_sn_base;    // exclusive scan of blk_sn (n + 1)
+  unsigned long long *blk_status;     // BlockStatus
   unsigned long long *blk_a, *blk_b;
-  unsigned long long *blk_out_len;   // decompressed length (compressed codecs)
-  unsigned long long *blk_dec_off;   // offset of the block's decompressed bytes in dec
-  // outputs
-  uint8_t *records;
-  unsigned long long *item_end;
+  unsigned long long *blk_out_len;    // decoded length (compressed codecs)
+  unsigned long long *blk_dec_off;    // offset of the block's decoded bytes in dec (n + 1)
+  // outputs: item views into the span or the records buffer (side / dec)
+  unsigned long long *item_off, *item_len;
+  uint8_t *side;        // straddling items (none codec)
+  StradDesc *strad;     // straddler copy list
   // scratch
-  unsigned long long *scan_tmp;      // tile partials
-  uint8_t *dec;                      // decompressed blocks (compressed codecs)
+  unsigned long long *scan_tmp;  // tile partials
+  uint8_t *dec;                  // decoded blocks (compressed codecs)
   Ctl *ctl;
   // CRC tables (constant)
-  uint32_t *crc_fold;   // 16 x 256 folded slice tables
-  uint32_t *crc_tree;   // 6 x 4 x 256 multiply-by-constant tables
-  uint32_t *crc_fix_a;  // per payload size: R(~0) shifted over 16+size bytes
+  uint32_t *crc_fold;   // 4 x 256 fold tables, each replicated x32 (bank-private copies)
+  uint32_t *crc_mul;    // 7 x 4 x 256 multiply-by-constant tables
+  uint32_t *crc_fix_a;  // per payload size: ~0 shifted over 16+size bytes
   uint32_t *crc_fix_b;  // per payload size: x^(-8*pad)
 };
 
-
-// Kernel argument blocks (kernels.hip, codec_*.hip; filled by pipeline.cpp).
+// Kernel argument blocks (kernels.hip, codec.hip; filled by pipeline.cpp).
 struct ParseArgs {
   const uint8_t *span;
   uint64_t nchunks;
@@ -110,13 +120,11 @@ struct ParseArgs {
   int32_t mode;
   int32_t codec;
   const unsigned long long *nblocks;  // device count
-  uint64_t item_cap, rec_cap;
+  uint64_t item_cap, side_cap;
 };
-struct CopyArgs {
-  uint8_t *out;  // records
-  uint64_t rec_cap;
-  int32_t mode;
-  int32_t copy;  // codec == none
+struct CrcArgs {
+  int32_t flags;  // measurement-only ablations (RIO_KERNEL_FLAGS): 1 no CRC fold
+  int32_t pad;
 };
 struct ResolveArgs {
   const uint8_t *span;
@@ -124,16 +132,19 @@ struct ResolveArgs {
   int32_t is_file_end;
   int32_t tail_partial;  // bytes after the last whole chunk at file end
   int32_t mode;
-  int32_t pad;
+  int32_t codec;
   const unsigned long long *nblocks;
   uint64_t limit_chunk;  // ChunkScanner.limit in chunks (a partial tail chunk at/after it is never read)
 };
 
 // ---- host helpers: GF(2) arithmetic of the reflected CRC-32 polynomial ----
 constexpr uint32_t kPoly = 0xEDB88320u;
-uint32_t gf_mul(uint32_t a, uint32_t b);          // a*b mod P (reflected; 1 = 0x80000000)
-uint32_t gf_xpow8(int64_t nbytes);                // x^(8*nbytes) mod P, nbytes may be negative
-void build_crc_tables(uint32_t *fold, uint32_t *tree, uint32_t *fix_a, uint32_t *fix_b);
+constexpr int kFoldCopies = 32;                  // bank-private replicas of each fold table
+constexpr int kFoldWords = 4 * 256 * kFoldCopies;  // 128 KiB
+constexpr int kMulTables = 7;                    // x^-32, then x^-(128*2^l), l = 0..5
+uint32_t gf_mul(uint32_t a, uint32_t b);         // a*b mod P (reflected; 1 = 0x80000000)
+uint32_t gf_xpow8(int64_t nbytes);               // x^(8*nbytes) mod P, nbytes may be negative
+void build_crc_tables(uint32_t *fold, uint32_t *mul, uint32_t *fix_a, uint32_t *fix_b);
 uint32_t crc32_host(const uint8_t *p, size_t n);  // plain IEEE CRC (for self-checks)
 
 }  // namespace rio

@@ -22,6 +22,13 @@ constexpr uint64_t kCk = RIO_CHUNK_SIZE;
 const uint8_t kMagicHeaderBytes[8] = {0xd9, 0xe1, 0xd9, 0x5c, 0xc2, 0x16, 0x04, 0xf7};
 const uint8_t kMagicTrailerBytes[8] = {0xfe, 0xba, 0x1a, 0xd7, 0xcb, 0xdf, 0x75, 0x3a};
 
+// host view of item i of a collected batch (rio_gpu.h: span view or records)
+inline const uint8_t *batch_item(const rio_batch &b, uint64_t i, uint64_t *len) {
+  const uint64_t o = b.item_off[i];
+  *len = b.item_len[i];
+  return (o & RIO_ITEM_IN_RECORDS) ? b.records + (o & ~RIO_ITEM_IN_RECORDS) : b.span + o;
+}
+
 struct KV {
   std::string key;
   int32_t type = 0;  // 1 bool 2 int 3 uint 4 string
@@ -252,8 +259,8 @@ void read_header(rio_scanner *s) {
     s->set_errf(RIO_ERR_HEADER, 0, "Wrong # of items in header block, %" PRIu64, b.n_items);
     return;
   }
-  const uint8_t *item = b.records + b.block_rec_off[0];
-  const uint64_t ilen = b.item_end[0] - b.block_rec_off[0];
+  uint64_t ilen = 0;
+  const uint8_t *item = batch_item(b, 0, &ilen);
   // ParsedHeader.unmarshal (header.go:211-239)
   HeaderDecoder d{item, ilen, {}};
   KV cnt;
@@ -451,9 +458,7 @@ int rio_scanner_scan(rio_scanner *s) {
       const rio_batch &b = s->batch;
       while (s->item >= b.block_first_item[s->blk + 1]) s->blk++;
       const uint64_t first = b.block_first_item[s->blk];
-      const uint64_t st = (s->item == first) ? b.block_rec_off[s->blk] : b.item_end[s->item - 1];
-      s->cur = b.records + st;
-      s->cur_len = b.item_end[s->item] - st;
+      s->cur = batch_item(b, s->item, &s->cur_len);
       s->cur_block = b.block_file_off[s->blk];
       s->cur_item = (int64_t)(s->item - first);
       s->item++;
@@ -567,8 +572,9 @@ int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len) {
     s->set_errf(RIO_ERR_TRAILER, start, "Expect exactly one trailer item, but found %" PRIu64, b.n_items);
     return 0;
   }
-  const uint64_t st0 = b.block_rec_off[0];
-  s->trailer.assign(b.records + st0, b.records + b.item_end[0]);
+  uint64_t tlen = 0;
+  const uint8_t *t0 = batch_item(b, 0, &tlen);
+  s->trailer.assign(t0, t0 + tlen);
   // The ctx buffers are shared with the scan batches: resume the scan at the
   // block of the next undelivered item (the deferred Seek(curOff) of Trailer).
   if (s->have_batch && s->item < s->batch.n_items) {

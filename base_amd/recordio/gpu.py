@@ -26,6 +26,7 @@ LIB_PATH = os.path.join(_ROOT, "lib", "librio_gpu.so")
 RIO_CODEC_NONE, RIO_CODEC_FLATE, RIO_CODEC_ZSTD = 0, 1, 2
 RIO_STOP_MORE, RIO_STOP_EOF, RIO_STOP_ERROR = 0, 1, 2
 U64_MAX = (1 << 64) - 1
+ITEM_IN_RECORDS = 1 << 63  # RIO_ITEM_IN_RECORDS
 
 
 class RioError(ctypes.Structure):
@@ -40,10 +41,10 @@ class RioConfig(ctypes.Structure):
 
 
 class RioBatch(ctypes.Structure):
-    _fields_ = [("records", ctypes.c_void_p), ("records_len", ctypes.c_uint64),
-                ("item_end", ctypes.POINTER(ctypes.c_uint64)), ("n_items", ctypes.c_uint64),
+    _fields_ = [("span", ctypes.c_void_p), ("records", ctypes.c_void_p), ("records_len", ctypes.c_uint64),
+                ("item_off", ctypes.POINTER(ctypes.c_uint64)), ("item_len", ctypes.POINTER(ctypes.c_uint64)),
+                ("n_items", ctypes.c_uint64),
                 ("block_first_item", ctypes.POINTER(ctypes.c_uint64)),
-                ("block_rec_off", ctypes.POINTER(ctypes.c_uint64)),
                 ("block_file_off", ctypes.POINTER(ctypes.c_uint64)), ("n_blocks", ctypes.c_uint64),
                 ("consumed", ctypes.c_uint64), ("stop", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("in_bytes", ctypes.c_uint64), ("kernel_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
@@ -175,6 +176,7 @@ class Context:
                                   codec, ctypes.byref(out))
         if rc != 0:
             raise RuntimeError("rio_scan_span: " + self.L.rio_last_error().decode())
+        out._span_buf = buf  # item views point into it
         return out
 
     def scan_device_async(self, dev_ptr: int, nbytes: int, file_off: int = 0, codec: int = RIO_CODEC_NONE):
@@ -189,9 +191,9 @@ class Context:
         return out
 
     def stage_times(self):
-        """Device ms of the last run: [parse, codec, crc_copy, resolve]."""
-        ms = (ctypes.c_float * 4)()
-        n = self.L.rio_stage_times(self.h, ms, 4)
+        """Device ms of the last run: [parse path, codec, k_crc, chunk meta+scans, total]."""
+        ms = (ctypes.c_float * 5)()
+        n = self.L.rio_stage_times(self.h, ms, 5)
         return [float(ms[i]) for i in range(n)]
 
     def scan_device(self, dev_ptr: int, nbytes: int, file_off: int = 0, is_file_end: bool = True,
@@ -209,17 +211,12 @@ def batch_items(b: RioBatch) -> List[bytes]:
     items = []
     if b.n_items == 0:
         return items
-    data = ctypes.string_at(b.records, b.records_len) if b.records_len else b""
-    ends = b.item_end
-    k = 0
-    for blk in range(b.n_blocks):
-        lo, hi = b.block_first_item[blk], b.block_first_item[blk + 1]
-        st = b.block_rec_off[blk]
-        for i in range(lo, hi):
-            en = ends[i]
-            items.append(data[st:en])
-            st = en
-            k += 1
+    for i in range(b.n_items):
+        o, n = b.item_off[i], b.item_len[i]
+        if o & ITEM_IN_RECORDS:
+            items.append(ctypes.string_at(b.records + (o & ~ITEM_IN_RECORDS), n) if n else b"")
+        else:
+            items.append(ctypes.string_at(b.span + o, n) if n else b"")
     return items
 
 

@@ -91,20 +91,29 @@ typedef struct rio_config {
 
 typedef struct rio_ctx rio_ctx;
 
-/* Results of one span. Arrays are owned by the ctx and valid until the next call
- * on it (like "Scan will reuse storage", scannerv2.go:124-126). For
- * rio_scan_span they are host (pinned) pointers; for rio_scan_device they are
- * device pointers.
- * Block b's items are item_end[block_first_item[b] .. block_first_item[b+1])
- * and its item i spans records[start, item_end[i]) where start is
- * block_rec_off[b] for the block's first item, else item_end[i-1]. */
+/* item_off[i] with this bit set is an offset into rio_batch.records; otherwise
+ * it is an offset into rio_batch.span (the caller's chunk bytes). */
+#define RIO_ITEM_IN_RECORDS (1ull << 63)
+
+/* Results of one span: views, not copies. Arrays are owned by the ctx and valid
+ * until the next call on it (like "Scan will reuse storage",
+ * scannerv2.go:124-126). For rio_scan_span they are host (pinned) pointers; for
+ * rio_scan_device they are device pointers (block_file_off is then NULL).
+ * Item i is the bytes [o, o + item_len[i]) of
+ *   records  when item_off[i] & RIO_ITEM_IN_RECORDS (o = item_off[i] without the bit),
+ *   span     otherwise (o = item_off[i]).
+ * Uncompressed items that sit inside one chunk payload are views into the span;
+ * items that straddle a chunk boundary are gathered into records. For flate /
+ * zstd every item is a view into the decoded blocks held in records.
+ * Block b's items are [block_first_item[b], block_first_item[b+1]). */
 typedef struct rio_batch {
-    const uint8_t *records;
+    const uint8_t *span;              /* base of span-relative item offsets */
+    const uint8_t *records;           /* straddling items / decoded blocks */
     uint64_t records_len;
-    const uint64_t *item_end;
+    const uint64_t *item_off;         /* n_items entries */
+    const uint64_t *item_len;         /* n_items entries */
     uint64_t n_items;
     const uint64_t *block_first_item; /* n_blocks + 1 entries */
-    const uint64_t *block_rec_off;    /* n_blocks entries */
     const uint64_t *block_file_off;   /* n_blocks entries (ItemLocation.Block) */
     uint64_t n_blocks;
     uint64_t consumed;   /* bytes of the span fully decoded (block boundary) */
@@ -155,9 +164,10 @@ int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, u
                           int32_t codec);
 int rio_sync(rio_ctx *ctx, rio_batch *out);
 
-/* Device time (HIP events on the ctx stream) of the last completed run, per
- * stage: [0] chunk headers + scans + block parse + items, [1] codec decode
- * (compressed codecs), [2] k_crc_copy (CRC32 + record copy), [3] resolve.
+/* Device time (HIP events) of the last completed run, per stage:
+ * [0] block parse + item views + straddler gather (second stream, overlaps [2]),
+ * [1] codec decode (compressed codecs), [2] k_crc (chunk CRC32 verify),
+ * [3] chunk headers + chunk scans, [4] the whole pipeline.
  * Returns the number of stages written. */
 int rio_stage_times(rio_ctx *ctx, float *ms, int n);
 

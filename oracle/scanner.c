@@ -637,7 +637,7 @@ static int parse_chunks(sc_t *s, cs_t *c, const int *tr, int ntr, vec_t *bytes, 
     for (int64_t i = 0; i < *ncum; i++) {
         int64_t st = i ? (*cum)[i - 1] : 0;
         if ((*cum)[i] < st || pos + (*cum)[i] > blen) {
-            once_set(err, "recordio: corrupt block header, item %" PRId64 " out of range", i);
+            once_set(err, "recordio: corrupt block header, item sizes out of range");
             return 0;
         }
     }
