@@ -71,17 +71,23 @@ __global__ void __launch_bounds__(256) k_block_parse(DevBufs d, ParseArgs a) {
         const Payload pl = block_payload(d, a, b, c0, total);
         const HdrResult none{};
         const ParseOut po{};
-        const HdrResult r = parse_header<kParseCount>(pl, none, po);
+        HdrResult r{};
+        if (fast_header<kParseCount>(pl, r, po)) {
+          sb = r.strad_bytes;
+          sn = r.strad_count;
+        } else {
+          r = parse_header<kParseCount>(pl, none, po);
+          if (r.status == kBlkOk && a.codec == RIO_CODEC_NONE && total > 1 && r.nitems > 0) {
+            const HdrResult s = parse_header<kParseStrad>(pl, r, po);
+            sb = s.strad_bytes;
+            sn = s.strad_count;
+          }
+        }
         status = r.status;
         ea = r.a;
         eb = r.b;
         nitems = r.nitems;
         hdr = r.hdr_len;
-        if (status == kBlkOk && a.codec == RIO_CODEC_NONE && total > 1 && nitems > 0) {
-          const HdrResult s = parse_header<kParseStrad>(pl, r, po);
-          sb = s.strad_bytes;
-          sn = s.strad_count;
-        }
       }
       if (status != kBlkOk && a.mode == kModeBody) event = 2 * end + 1;
     }
@@ -126,7 +132,8 @@ __global__ void __launch_bounds__(256) k_items(DevBufs d, ParseArgs a) {
       if (lane_id() == 0) atomicOr(&d.ctl->out_overflow, 4ull);
       continue;
     }
-    parse_header<kParseWrite>(pl, known, po);
+    HdrResult r{};
+    if (!fast_header<kParseWrite>(pl, r, po)) parse_header<kParseWrite>(pl, known, po);
   }
 }
 

@@ -1,7 +1,7 @@
 // Chunk CRC32-IEEE verify (readChunk, recordio/internal/chunk.go:338-343) at
 // HBM read speed, no carry-less multiply.
 //
-// One wave per 32 KiB chunk, 16 waves per workgroup, one workgroup per CU.
+// One wave per 32 KiB chunk, kCrcWaves waves per workgroup, one workgroup per CU.
 // Lane t loads the 16-byte units at chunk offsets 1024*i + 16*t (i = 0..31): every
 // load instruction is 1 KiB contiguous. Each of the lane's 4 dwords (k = 0..3)
 // is its own CRC stream with one dword per 1 KiB row; the 1020-byte gap to the
@@ -9,12 +9,17 @@
 //   S_k <- fold0[b0] ^ fold1[b1] ^ fold2[b2] ^ fold3[b3],  b = bytes of (u_k ^ S_k),
 //   fold_j[b] = R(b || 0^(1023-j))     (R = raw CRC: zero init, no final xor).
 // Only 4 fold tables exist, so each is replicated 32x in LDS (128 KiB): lane l
-// reads copy l & 31 and every ds_read_b32 is bank-conflict free.
+// reads copy l & 31 and every ds_read_b32 is bank-conflict free. A row's 16
+// lookups are independent and issue back to back; only the row-to-row chain
+// per stream is serial.
 // After row 31, stream (t, k) holds R(message) * x^(8(16t + 4k)); the lane
 // combines its streams with x^-32 (Horner), a 6-level shuffle tree with
 // x^-(128*2^l) combines the lanes (multiply-by-constant = 4 byte lookups).
 // Bytes outside [12, 28+size) are zeroed, so V = R(0^12 || covered || 0^pad) and
 // crc = ~(~0 * x^(8(16+size)) ^ V * x^(-8 pad)).
+// Loads are software-pipelined in 4 KiB stages through 4 register buffers:
+// while one stage is folded the next three are in flight (16 waves per CU keep
+// 192 KiB outstanding).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,29 +40,88 @@ __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
   return p;
 }
 
+// keep the bytes of dword v (at chunk offset off) that lie below chunk offset hi
 __device__ __forceinline__ uint32_t mask_dword(uint32_t v, int off, int hi) {
-  // keep bytes with chunk offset < hi
-  if (off + 4 <= hi) return v;
-  if (off >= hi) return 0u;
-  return v & (0xffffffffu >> (8 * (off + 4 - hi)));
+  int keep = hi - off;
+  keep = keep < 0 ? 0 : (keep > 4 ? 4 : keep);
+  const uint32_t m = keep >= 4 ? 0xffffffffu : ((1u << (8 * keep)) - 1u);
+  return v & m;
 }
 
-// one Horner step of a dword stream: lookups in the lane's private table copies
-__device__ __forceinline__ uint32_t fold_step(const char *__restrict__ tab, uint32_t lb, uint32_t d) {
-  const uint32_t a0 = ((d & 0xffu) << 7) | lb;
-  const uint32_t a1 = (((d >> 8) & 0xffu) << 7) | lb;
-  const uint32_t a2 = (((d >> 16) & 0xffu) << 7) | lb;
-  const uint32_t a3 = ((d >> 24) << 7) | lb;
-  return *reinterpret_cast<const uint32_t *>(tab + a0) ^ *reinterpret_cast<const uint32_t *>(tab + 32768 + a1) ^
-         *reinterpret_cast<const uint32_t *>(tab + 65536 + a2) ^ *reinterpret_cast<const uint32_t *>(tab + 98304 + a3);
+// one Horner step of the lane's 4 dword streams: 16 independent lookups in the
+// lane's private table copies
+__device__ __forceinline__ void fold_row(const char *__restrict__ tab, uint32_t lb, uint4 v, uint32_t (&s)[4]) {
+  const uint32_t d[4] = {v.x ^ s[0], v.y ^ s[1], v.z ^ s[2], v.w ^ s[3]};
+  uint32_t t[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t a = (((d[k] >> (8 * j)) & 0xffu) << 7) | lb;
+      t[k][j] = *reinterpret_cast<const uint32_t *>(tab + j * 32768 + a);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) s[k] = t[k][0] ^ t[k][1] ^ t[k][2] ^ t[k][3];
 }
 
 __device__ __forceinline__ uint32_t mul_const(const uint32_t *__restrict__ T, uint32_t v) {
   return T[v & 0xff] ^ T[256 + ((v >> 8) & 0xff)] ^ T[512 + ((v >> 16) & 0xff)] ^ T[768 + (v >> 24)];
 }
 
+constexpr int kRows = 4;   // rows per pipeline stage (4 KiB per wave)
+constexpr int kBufs = 4;   // register buffers: kBufs - 1 stages in flight during a fold
+constexpr int kStages = 32 / kRows;
+
+// fold stage q (rows kRows*q ..) of a chunk whose covered bytes end at `end`
+__device__ __forceinline__ void fold_stage(const uint4 (&u)[kRows], uint32_t (&s)[4], const char *__restrict__ tab,
+                                           uint32_t lb, int l, int q, int end, bool fold, uint32_t &stored) {
+#pragma unroll
+  for (int r = 0; r < kRows; r++) {
+    uint4 v = u[r];
+    const int row = kRows * q + r;
+    if (row == 0) {  // magic[0:8] and crc[8:12] are not covered
+      stored = v.z;  // lane 0: the chunk's stored checksum
+      const uint32_t keep = (l == 0) ? 0u : 0xffffffffu;
+      v.x &= keep;
+      v.y &= keep;
+      v.z &= keep;
+    }
+    if (1024 * (row + 1) > end) {  // wave-uniform: only rows reaching the payload end
+      const int o = 1024 * row + 16 * l;
+      v.x = mask_dword(v.x, o, end);
+      v.y = mask_dword(v.y, o + 4, end);
+      v.z = mask_dword(v.z, o + 8, end);
+      v.w = mask_dword(v.w, o + 12, end);
+    }
+    if (fold) {
+      fold_row(tab, lb, v, s);
+    } else {  // ablation: keep the loads live
+      s[0] ^= v.x;
+      s[1] ^= v.y;
+      s[2] ^= v.z;
+      s[3] ^= v.w;
+    }
+  }
+}
+
+__device__ __forceinline__ void load_stage(uint4 (&u)[kRows], const uint8_t *ck, int q, int l) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 *row = reinterpret_cast<const u32x4 *>(ck) + 64 * kRows * q + l;
+#pragma unroll
+  for (int r = 0; r < kRows; r++) {
+    const u32x4 x = __builtin_nontemporal_load(row + 64 * r);
+    u[r] = make_uint4(x.x, x.y, x.z, x.w);
+  }
+}
+
+// sizes / fix tables are separate restrict-const arguments so that their
+// wave-uniform reads compile to scalar loads (a vector load of the next
+// chunk's size would make the wave drain its prefetched rows)
 __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restrict__ span, uint64_t nchunks,
-                                                       DevBufs d, CrcArgs ca) {
+                                                       const uint32_t *__restrict__ ck_size,
+                                                       const uint32_t *__restrict__ fix_a,
+                                                       const uint32_t *__restrict__ fix_b, DevBufs d, CrcArgs ca) {
   __shared__ __attribute__((aligned(16))) uint32_t s_fold[kFoldWords];
   __shared__ __attribute__((aligned(16))) uint32_t s_mul[kMulTables * 1024];
   {
@@ -71,47 +135,36 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
   const uint32_t lb = (uint32_t)(l & 31) << 2;
   const char *tab = reinterpret_cast<const char *>(s_fold);
   const bool fold = !(ca.flags & 1);
-  const uint64_t wave = (uint64_t)blockIdx.x * kCrcWaves + (threadIdx.x >> 6);
   const uint64_t nwaves = (uint64_t)gridDim.x * kCrcWaves;
-  for (uint64_t c = wave; c < nchunks; c += nwaves) {
+  // wave-uniform chunk index: sizes are scalar loads and the FULL test a scalar branch
+  uint64_t c = (uint64_t)blockIdx.x * kCrcWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (c >= nchunks) return;
+  uint4 buf[kBufs][kRows];
+  uint32_t size = ck_size[c];
+#pragma unroll
+  for (int q = 0; q < kBufs - 1; q++) load_stage(buf[q], span + c * kChunk, q, l);
+  for (;;) {
     const uint8_t *ck = span + c * kChunk;
-    const uint32_t size = d.ck_size[c];
-    if (size > (uint32_t)kMaxPayload) continue;  // "Invalid chunk size": no CRC
-    const int end = kChunkHdr + (int)size;
-    const bool full = (size == (uint32_t)kMaxPayload);
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    const uint4 *row = reinterpret_cast<const uint4 *>(ck) + l;
-#pragma unroll 8
-    for (int i = 0; i < 32; i++) {
-      uint4 u = row[64 * i];
-      if (i == 0 && l == 0) {  // magic[0:8] and crc[8:12] are not covered
-        u.x = 0;
-        u.y = 0;
-        u.z = 0;
-      }
-      if (!full) {
-        const int o = 1024 * i + 16 * l;
-        u.x = mask_dword(u.x, o, end);
-        u.y = mask_dword(u.y, o + 4, end);
-        u.z = mask_dword(u.z, o + 8, end);
-        u.w = mask_dword(u.w, o + 12, end);
-      }
-      if (fold) {
-        s0 = fold_step(tab, lb, u.x ^ s0);
-        s1 = fold_step(tab, lb, u.y ^ s1);
-        s2 = fold_step(tab, lb, u.z ^ s2);
-        s3 = fold_step(tab, lb, u.w ^ s3);
-      } else {  // ablation: keep the loads live
-        s0 ^= u.x;
-        s1 ^= u.y;
-        s2 ^= u.z;
-        s3 ^= u.w;
-      }
+    const uint64_t cn = c + nwaves;
+    const bool more = cn < nchunks;
+    const uint32_t size_n = ck_size[more ? cn : c];
+    const uint32_t sz = size > (uint32_t)kMaxPayload ? (uint32_t)kMaxPayload : size;
+    const int end = kChunkHdr + (int)sz;
+    const bool full = (sz == (uint32_t)kMaxPayload);
+    uint32_t s[4] = {0, 0, 0, 0};
+    uint32_t stored = 0;
+    const uint32_t fa = fix_a[sz], fb = fix_b[sz];
+#pragma unroll
+    for (int q = 0; q < kStages; q++) {
+      const int nq = q + kBufs - 1;  // stage to prefetch (this chunk or the next)
+      if (nq < kStages) load_stage(buf[nq % kBufs], ck, nq, l);
+      else if (more) load_stage(buf[nq % kBufs], span + cn * kChunk, nq - kStages, l);
+      fold_stage(buf[q % kBufs], s, tab, lb, l, q, end, fold, stored);
     }
     // lane: V_t = s0 + s1 x^-32 + s2 x^-64 + s3 x^-96
-    uint32_t v = mul_const(s_mul, s3) ^ s2;
-    v = mul_const(s_mul, v) ^ s1;
-    v = mul_const(s_mul, v) ^ s0;
+    uint32_t v = mul_const(s_mul, s[3]) ^ s[2];
+    v = mul_const(s_mul, v) ^ s[1];
+    v = mul_const(s_mul, v) ^ s[0];
     // lanes: V = sum_t V_t x^-128t
 #pragma unroll
     for (int lv = 0; lv < 6; lv++) {
@@ -120,13 +173,15 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
       const uint32_t o = __shfl(m, (l + step) & 63, 64);
       v ^= (l + step < 64) ? o : 0u;
     }
-    if (l == 0) {
-      const uint32_t t = full ? v : gf_mul_dev(v, d.crc_fix_b[size]);
-      const uint32_t crc = ~(d.crc_fix_a[size] ^ t);
+    if (l == 0 && size <= (uint32_t)kMaxPayload) {  // "Invalid chunk size": no CRC
+      const uint32_t t = full ? v : gf_mul_dev(v, fb);
+      const uint32_t crc = ~(fa ^ t);
       d.ck_crc[c] = crc;
-      const uint32_t stored = *reinterpret_cast<const uint32_t *>(ck + 8);
-      if (crc != stored) atomicMin(&d.ctl->first_crc_err, (unsigned long long)c);
+      if (crc != stored && fold) atomicMin(&d.ctl->first_crc_err, (unsigned long long)c);
     }
+    if (!more) break;
+    c = cn;
+    size = size_n;
   }
 }
 
@@ -136,7 +191,8 @@ void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const C
   const uint64_t cap = (uint64_t)(ncu > 0 ? ncu : 256);
   if (g > cap) g = cap;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(k_crc, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d, ca);
+  hipLaunchKernelGGL(k_crc, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size, d.crc_fix_a,
+                     d.crc_fix_b, d, ca);
 }
 
 }  // namespace rio

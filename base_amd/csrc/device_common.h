@@ -398,4 +398,177 @@ __device__ HdrResult parse_header(const Payload &pl, const HdrResult &known, con
   return r;
 }
 
+// ---------------------------------------------------------------- fast path
+// The common block shape -- the whole header inside the first 1 KiB of the
+// payload, every varint shorter than 11 bytes, sizes consistent with the block
+// -- parsed from one 16 B/lane window with fully unrolled byte loops (no
+// dynamic register indexing). Anything else returns false and the block goes
+// through parse_header, which also produces the reference's error values.
+
+// lane's terminators in byte order: f(k, i, value, varint_len, last_byte);
+// the lane's first varint continues the previous lane's trailing bytes
+template <class F>
+__device__ __forceinline__ void walk_lane(const uint32_t w[4], uint32_t tmask, unsigned long long c_acc, int c_len,
+                                          F &&f) {
+  unsigned long long acc = 0;
+  int len = 0, k = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xffu;
+    const int sh = 7 * len;
+    if (sh < 64) acc |= (unsigned long long)(b & 0x7fu) << sh;
+    len++;
+    if ((tmask >> i) & 1u) {
+      unsigned long long v = acc;
+      int vl = len;
+      if (k == 0) {
+        const int csh = 7 * c_len;
+        v = c_acc | (csh < 64 ? (acc << csh) : 0ull);
+        vl = c_len + len;
+      }
+      f(k, v, vl, b);
+      acc = 0;
+      len = 0;
+      k++;
+    }
+  }
+}
+
+__device__ __forceinline__ bool uvarint_ok(int vl, uint32_t last) { return vl < 10 || (vl == 10 && last <= 1); }
+
+// MODE kParseCount: r gets nitems, hdr_len, straddler bytes/count.
+// MODE kParseWrite: item views and straddler descriptors as parse_header.
+template <int MODE>
+__device__ bool fast_header(const Payload &pl, HdrResult &r, const ParseOut &po) {
+  const int l = lane_id();
+  const uint64_t plen = pl.len;
+  if (plen >= (1ull << 32)) return false;
+  if (!pl.contig && !pl.regular) return false;
+  const uint32_t pos = 16u * (uint32_t)l;
+  uint32_t w[4];
+  pl.fetch16(pos, w);
+  const uint32_t tmask = term4(w[0]) | (term4(w[1]) << 4) | (term4(w[2]) << 8) | (term4(w[3]) << 12);
+  // the item count: lane 0's first varint
+  unsigned long long n0 = 0;
+  bool n0_ok = false;
+  if (l == 0 && tmask) {
+    walk_lane(w, tmask & (0u - tmask), 0ull, 0, [&](int, unsigned long long v, int vl, uint32_t b) {
+      n0 = v;
+      n0_ok = uvarint_ok(vl, b);
+    });
+  }
+  const unsigned long long nitems = __shfl(n0, 0, 64);
+  if (!__shfl((int)n0_ok, 0, 64)) return false;
+  const uint32_t cnt = __popc(tmask);
+  const uint32_t incl = wave_incl_sum<uint32_t>(cnt);
+  const uint32_t ex = incl - cnt;
+  const uint32_t total = __shfl(incl, 63, 64);
+  if (nitems >= total) return false;  // header not inside the window
+  // header end: the terminator with ordinal nitems
+  const bool mine = nitems >= ex && nitems < incl;
+  int endbit = -1;
+  if (mine) {
+    uint32_t mm = tmask;
+    for (uint32_t k = ex; k < (uint32_t)nitems; k++) mm &= mm - 1;
+    endbit = __ffs(mm) - 1;
+  }
+  const unsigned long long eb = __ballot(mine);
+  const uint32_t hdr = (uint32_t)__shfl((int)pos + endbit, __ffsll((long long)eb) - 1, 64) + 1;
+  // carry-in: the previous lane's bytes after its last terminator
+  const int t_last = tmask ? 31 - __clz(tmask) : -1;
+  unsigned long long tacc = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xffu;
+    const int sh = 7 * (i - t_last - 1);
+    if (i > t_last && sh < 64) tacc |= (unsigned long long)(b & 0x7fu) << sh;
+  }
+  int c_len = __shfl_up(15 - t_last, 1, 64);
+  unsigned long long c_acc = __shfl_up(tacc, 1, 64);
+  if (l == 0) {
+    c_len = 0;
+    c_acc = 0;
+  }
+  // sizes: validity, range, lane sums
+  bool bad = false;
+  unsigned long long lsum = 0;
+  walk_lane(w, tmask, c_acc, c_len, [&](int k, unsigned long long v, int vl, uint32_t b) {
+    const uint32_t o = ex + (uint32_t)k;
+    if (o >= 1 && o <= nitems) {
+      if (!uvarint_ok(vl, b) || v > plen) bad = true;
+      lsum += v;
+    }
+  });
+  if (__ballot(bad)) return false;
+  if (wave_sum<unsigned long long>(lsum) + hdr != plen) return false;
+  const unsigned long long run0 = hdr + wave_incl_sum<unsigned long long>(lsum) - lsum;
+  const bool chunks = !pl.contig && pl.total > 1;
+  // straddlers (items crossing a chunk payload boundary)
+  unsigned long long sb = 0, sn = 0;
+  if (chunks) {
+    unsigned long long run = run0;
+    walk_lane(w, tmask, c_acc, c_len, [&](int k, unsigned long long v, int, uint32_t) {
+      const uint32_t o = ex + (uint32_t)k;
+      if (o >= 1 && o <= nitems) {
+        const uint32_t st = (uint32_t)run;
+        if (v > 0 && st / (uint32_t)kMaxPayload != (st + (uint32_t)v - 1) / (uint32_t)kMaxPayload) {
+          sb += pad16(v);
+          sn += 1;
+        }
+        run += v;
+      }
+    });
+  }
+  if (MODE == kParseCount) {
+    r.status = kBlkOk;
+    r.nitems = nitems;
+    r.hdr_len = hdr;
+    r.strad_bytes = chunks ? wave_sum<unsigned long long>(sb) : 0;
+    r.strad_count = chunks ? wave_sum<unsigned long long>(sn) : 0;
+    return true;
+  }
+  unsigned long long sbx = 0, snx = 0;
+  if (chunks) {
+    sbx = wave_incl_sum<unsigned long long>(sb) - sb;
+    snx = wave_incl_sum<unsigned long long>(sn) - sn;
+  }
+  unsigned long long run = run0;
+  walk_lane(w, tmask, c_acc, c_len, [&](int k, unsigned long long v, int, uint32_t) {
+    const uint32_t o = ex + (uint32_t)k;
+    if (o >= 1 && o <= nitems) {
+      const uint32_t st = (uint32_t)run;
+      const uint64_t slot = po.item_base + (o - 1);
+      unsigned long long off;
+      bool sd = false;
+      if (pl.contig) {
+        off = po.view_base + st;
+      } else {
+        const uint32_t j = st / (uint32_t)kMaxPayload;
+        sd = chunks && v > 0 && j != (st + (uint32_t)v - 1) / (uint32_t)kMaxPayload;
+        if (sd) off = kItemInRecords | (po.side_base + sbx);
+        else if (v == 0 && st >= plen) off = 0;
+        else off = (pl.c0 + j) * (unsigned long long)kChunk + kChunkHdr + (st - j * (uint32_t)kMaxPayload);
+      }
+      if (slot < po.item_cap) {
+        po.item_off[slot] = off;
+        po.item_len[slot] = v;
+      } else {
+        atomicOr(po.overflow, 1ull);
+      }
+      if (sd) {
+        StradDesc dsc;
+        dsc.c0 = po.c0;
+        dsc.src = st;
+        dsc.len = v;
+        dsc.dst = po.side_base + sbx;
+        po.strad[po.strad_idx + snx] = dsc;
+        sbx += pad16(v);
+        snx += 1;
+      }
+      run += v;
+    }
+  });
+  return true;
+}
+
 }  // namespace rio

@@ -2,11 +2,11 @@
 // (include/rio_gpu.h). One rio_ctx = one device, two HIP streams, buffers sized
 // at rio_open and grown only when a span needs more.
 //
-// Stream plan per span:
-//   st : memsets, k_chunk_meta, chunk scans, [codec decode], -> evA, k_crc, wait evB, k_resolve
-//   st2:                                      wait evA, k_block_parse, block scans, k_items, k_strad -> evB
-// k_crc streams the whole span from HBM; the parse path reads ~1% of it and is
-// latency bound, so it runs beside k_crc.
+// Launch order per span (one stream; RIO_TWO_STREAMS=1 puts the parse path on
+// a second stream beside k_crc, which only pays when k_crc leaves CU room):
+//   memsets, k_chunk_meta, chunk scans, [codec decode],
+//   k_block_parse, block scans, k_items, k_strad,   (parse path, ~1% of the bytes)
+//   k_crc (streams every chunk byte), k_resolve
 #include <hip/hip_runtime.h>
 #include <inttypes.h>
 #include <stdarg.h>
@@ -70,7 +70,7 @@ enum { kEvStart, kEvScans, kEvDec, kEvCrc0, kEvCrc1, kEvParse0, kEvParse1, kEvEn
 struct rio_ctx {
   int device = 0;
   int ncu = 256;
-  int kernel_flags = 0;  // RIO_KERNEL_FLAGS: measurement-only ablations
+  int kernel_flags = 0;  // RIO_KERNEL_FLAGS (measurement only): 1 no CRC fold, 2 no parse path, 4 no CRC
   hipStream_t st = nullptr, st2 = nullptr;
   hipEvent_t ev[kNumEv] = {};
   hipEvent_t evA = nullptr, evB = nullptr;  // stream hand-offs (no timing)
@@ -144,7 +144,7 @@ static void free_all(rio_ctx *c) {
   if (c->evA) hipEventDestroy(c->evA);
   if (c->evB) hipEventDestroy(c->evB);
   if (c->st) hipStreamDestroy(c->st);
-  if (c->st2) hipStreamDestroy(c->st2);
+  if (c->st2 && c->st2 != c->st) hipStreamDestroy(c->st2);
 }
 
 static int ctx_init(rio_ctx *c, const rio_config *cfg) {
@@ -163,7 +163,9 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   c->item_cap = (cfg && cfg->max_items) ? cfg->max_items : span / 64 + 1024;
   c->dec_cap = 0;
   HIP_OK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-  HIP_OK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+  const char *two = getenv("RIO_TWO_STREAMS");
+  if (two && atoi(two)) HIP_OK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+  else c->st2 = c->st;
   for (hipEvent_t &e : c->ev) HIP_OK(hipEventCreate(&e));
   HIP_OK(hipEventCreateWithFlags(&c->evA, hipEventDisableTiming));
   HIP_OK(hipEventCreateWithFlags(&c->evB, hipEventDisableTiming));
@@ -198,7 +200,7 @@ void rio_close(rio_ctx *ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->st);
-  hipStreamSynchronize(ctx->st2);
+  if (ctx->st2 != ctx->st) hipStreamSynchronize(ctx->st2);
   free_all(ctx);
   delete ctx;
 }
@@ -240,7 +242,8 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   // parse path on st2, beside the CRC stream on st
   HIP_OK(hipStreamWaitEvent(st2, c->evA, 0));
   HIP_OK(hipEventRecord(c->ev[kEvParse0], st2));
-  if (nchunks > 0) {
+  const bool run_parse = !(c->kernel_flags & 2), run_crc = !(c->kernel_flags & 4);
+  if (nchunks > 0 && run_parse) {
     ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap};
     launch_block_parse(d, pa, max_blocks, st2);
     launch_block_scan(d.blk_nitems, d.blk_item_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
@@ -250,14 +253,14 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     }
     launch_items(d, pa, max_blocks, st2);
     if (codec == RIO_CODEC_NONE) launch_strad(span, d, c->nblocks_dev, nchunks, c->side_cap, st2);
-  } else {
+  } else if (nchunks == 0) {
     HIP_OK(hipMemsetAsync(d.blk_item_base, 0, 8, st2));
     HIP_OK(hipMemsetAsync(d.blk_sb_base, 0, 8, st2));
   }
   HIP_OK(hipEventRecord(c->ev[kEvParse1], st2));
   HIP_OK(hipEventRecord(c->evB, st2));
   HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
-  if (nchunks > 0) {
+  if (nchunks > 0 && run_crc) {
     CrcArgs ca{c->kernel_flags, 0};
     launch_crc(span, nchunks, d, ca, c->ncu, st);
   }

@@ -1,7 +1,7 @@
 """Measurement-only ablations of the none-codec pipeline on the C2 workload.
 
-Runs the scan with RIO_KERNEL_FLAGS = 0 (full), 1 (no CRC fold), 2 (no copy),
-3 (loads only) and times a plain device-to-device copy of the same bytes (the
+Runs the scan with RIO_KERNEL_FLAGS = 0 (full), 2 (CRC alone), 3 (CRC loads
+only, no fold), 4 (parse path alone) and times a plain device-to-device copy of the same bytes (the
 copy ceiling quoted in DESIGN.md). One JSON line per variant.
 """
 import json
@@ -29,9 +29,9 @@ def main():
         dev[bench.CHUNK + r * len(body):bench.CHUNK + (r + 1) * len(body)].copy_(dev[bench.CHUNK:len(data)])
     torch.cuda.synchronize()
     span_len = total - bench.CHUNK
-    for flags in [0, 1, 2, 3]:
+    for flags in [int(x) for x in os.environ.get("FLAGS", "0,2,3,4").split(",")]:
         os.environ["RIO_KERNEL_FLAGS"] = str(flags)
-        ctx = gpu.Context(0, max_span_bytes=total, max_out_bytes=total, max_items=nrec * reps + 1024)
+        ctx = gpu.Context(0, max_span_bytes=total, max_items=nrec * reps + 1024)
         times = []
         for i in range(6):
             ctx.scan_device_async(dev.data_ptr() + bench.CHUNK, span_len, bench.CHUNK, gpu.RIO_CODEC_NONE)
@@ -39,9 +39,8 @@ def main():
             if i:
                 times.append(ctx.stage_times())
         t = np.mean(np.array(times), axis=0)
-        moved = span_len + (0 if flags & 2 else int(b.records_len))
         print(json.dumps({"flags": flags, "stage_ms": [round(x, 3) for x in t],
-                          "crc_copy_GBs": round(moved / (t[2] * 1e-3) / 1e9, 1),
+                          "crc_GBs": round(span_len / (t[2] * 1e-3) / 1e9, 1) if t[2] > 0 else None,
                           "stop": b.stop, "n_items": b.n_items}), flush=True)
         ctx.close()
     # device-to-device copy ceiling on the same byte count

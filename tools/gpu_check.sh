@@ -21,13 +21,16 @@ step() {  # step <name> <timeout> <cmd...>
   return 0
 }
 
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -m pytest tests -x -q -m gpu ${PYTEST_ARGS}
+step smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
+step pytest_gpu 480 python -m pytest tests -x -q -m gpu ${PYTEST_ARGS}
+if [ -n "$ABLATE" ]; then
+  step ablate 300 python tools/ablate.py
+fi
 if [ -n "$BENCH" ]; then
-  step bench 600 python bench.py --steps 5 --warmup 2
+  step bench 300 python bench.py --steps 5 --warmup 2
 fi
 if [ -n "$PROFILE" ]; then
   cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+  step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline
 fi
