@@ -16,143 +16,258 @@
 namespace rio {
 
 constexpr uint32_t kNoBlockId = 0xffffffffu;
+constexpr int kBatch = 4;  // blocks per wave iteration: their loads are issued together
 
-__device__ __forceinline__ bool block_complete(const DevBufs &d, uint64_t c0, uint64_t nchunks, uint64_t &total) {
-  total = d.ck_total[c0];
-  return total != 0 && c0 + total <= nchunks;
+__device__ __forceinline__ Payload desc_payload(const uint8_t *span, const DevBufs &d, uint64_t c0,
+                                                unsigned long long meta, unsigned long long len) {
+  Payload pl;
+  pl.span = span;
+  pl.ck_size = d.ck_size;
+  pl.ck_pay = d.ck_pay;
+  pl.c0 = c0;
+  pl.total = meta & kMetaTotalMask;
+  pl.pay0 = d.ck_pay[c0];
+  pl.len = len;
+  pl.regular = (meta & kMetaRegular) != 0;
+  pl.contig = nullptr;
+  return pl;
 }
 
-__device__ __forceinline__ Payload block_payload(const DevBufs &d, const ParseArgs &a, uint64_t b, uint64_t c0,
-                                                 uint64_t total) {
-  if (a.codec != RIO_CODEC_NONE) return make_contig_payload(d.dec + d.blk_dec_off[b], d.blk_out_len[b]);
-  return make_chunk_payload(a.span, d, c0, total);
-}
-
-// wave per block: block magic handling (scannerv2.go:374-387) + header counts
-__global__ void __launch_bounds__(256) k_block_parse(DevBufs d, ParseArgs a) {
+// Wave per block, kBatch blocks per iteration: block magic handling
+// (scanNextBlock, scannerv2.go:374-387), the header of parseChunksToItems
+// (scannerv2.go:53-97) and one view per item (cumSize, scannerv2.go:83-91)
+// into the item slots reserved by the block scan.
+__global__ void __launch_bounds__(256) k_parse(DevBufs d, ParseArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[4][1024];
+  __shared__ uint16_t s_tpos[4][1024];
+  uint8_t *lwin = s_win[threadIdx.x >> 6];
+  uint16_t *ltpos = s_tpos[threadIdx.x >> 6];
   const uint64_t nb = *a.nblocks;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const int l = lane_id();
-  for (uint64_t b = wave; b < nb; b += nwaves) {
-    const uint64_t c0 = d.blk_c0[b];
-    uint64_t total;
-    unsigned long long status = kBlkOk, ea = 0, eb = 0, nitems = 0, hdr = 0, sb = 0, sn = 0;
-    const uint32_t cls = d.ck_info[c0] & 0xff;
-    const bool complete = block_complete(d, c0, a.nchunks, total);
-    unsigned long long event = kNone;
-    if (c0 >= a.limit_chunk && a.mode == kModeBody) {
-      status = kBlkLimit;
-      event = 2 * c0;
-    } else if (!complete) {
-      status = kBlkIncomplete;
-      if (l == 0) atomicMin(&d.ctl->first_incomplete, (unsigned long long)c0);
-    } else {
-      const uint64_t end = c0 + total - 1;
-      bool parse = false;
-      if (a.mode == kModeBody) {
-        if (cls == kMagicPacked) parse = true;
-        else if (cls == kMagicTrailer) status = kBlkTrailer;
-        else status = kBlkBadMagic;
-      } else if (a.mode == kModeHeader) {
-        parse = (cls == kMagicHeader);
-        if (!parse) status = kBlkBadMagic;
+  for (uint64_t b0 = wave * kBatch; b0 < nb; b0 += nwaves * kBatch) {
+    // round 1: descriptors of the batch (lane j: block b0 + j)
+    unsigned long long m_c0 = 0, m_meta = 0, m_len = 0, m_base = 0;
+    if (l < kBatch && b0 + l < nb) {
+      const uint64_t b = b0 + l;
+      m_c0 = d.blk_c0[b];
+      m_meta = d.blk_meta[b];
+      m_len = (a.codec == RIO_CODEC_NONE) ? d.blk_len[b] : d.blk_out_len[b];
+      m_base = d.blk_item_base[b];
+    }
+    unsigned long long c0s[kBatch], metas[kBatch], lens[kBatch], bases[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; j++) {  // wave-uniform: scalar registers
+      c0s[j] = readlane_u64(m_c0, j);
+      metas[j] = readlane_u64(m_meta, j);
+      lens[j] = readlane_u64(m_len, j);
+      bases[j] = readlane_u64(m_base, j);
+    }
+    // round 2: the first 1 KiB of every block payload (16 B per lane)
+    uint32_t win[kBatch][4];
+#pragma unroll
+    for (int j = 0; j < kBatch; j++) {
+      win[j][0] = win[j][1] = win[j][2] = win[j][3] = 0x80808080u;
+      if (b0 + j >= nb || !(metas[j] & kMetaComplete)) continue;
+      const uint64_t p = 16ull * l;
+      if (a.codec != RIO_CODEC_NONE) {
+        const uint64_t b = b0 + j;
+        if (p + 16 <= lens[j]) {
+          const uint4 v = *reinterpret_cast<const uint4 *>(d.dec + d.blk_dec_off[b] + p);
+          win[j][0] = v.x;
+          win[j][1] = v.y;
+          win[j][2] = v.z;
+          win[j][3] = v.w;
+        }
       } else {
-        parse = (cls == kMagicTrailer);
-        if (!parse) status = kBlkBadMagic;
+        const uint64_t size0 = lens[j] < (uint64_t)kMaxPayload ? lens[j] : (uint64_t)kMaxPayload;
+        if (p + 16 <= size0) {  // 4-byte aligned: 28 + 16 l
+          const uint32_t *q = reinterpret_cast<const uint32_t *>(a.span + c0s[j] * kChunk + kChunkHdr + p);
+          win[j][0] = q[0];
+          win[j][1] = q[1];
+          win[j][2] = q[2];
+          win[j][3] = q[3];
+        }
       }
-      if (parse && a.codec != RIO_CODEC_NONE && d.blk_status[b] == kBlkCodec) {
-        parse = false;
-        status = kBlkCodec;
-        ea = d.blk_a[b];
-        eb = d.blk_b[b];
-      }
-      if (parse) {
-        const Payload pl = block_payload(d, a, b, c0, total);
-        const HdrResult none{};
-        const ParseOut po{};
-        HdrResult r{};
-        if (fast_header<kParseCount>(pl, r, po)) {
-          sb = r.strad_bytes;
-          sn = r.strad_count;
+    }
+#pragma unroll
+    for (int j = 0; j < kBatch; j++) {
+      const uint64_t b = b0 + j;
+      if (b >= nb) break;
+      const uint64_t c0 = c0s[j];
+      const unsigned long long meta = metas[j];
+      const uint64_t total = meta & kMetaTotalMask;
+      const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
+      unsigned long long status = kBlkOk, ea = 0, eb = 0, hdr = 0;
+      unsigned long long event = kNone;
+      if (c0 >= a.limit_chunk && a.mode == kModeBody) {
+        status = kBlkLimit;
+        event = 2 * c0;
+      } else if (!(meta & kMetaComplete)) {
+        status = kBlkIncomplete;
+        if (l == 0) atomicMin(&d.ctl->first_incomplete, (unsigned long long)c0);
+      } else {
+        const uint64_t end = c0 + total - 1;
+        bool parse = false;
+        if (a.mode == kModeBody) {
+          if (cls == kMagicPacked) parse = true;
+          else if (cls == kMagicTrailer) status = kBlkTrailer;
+          else status = kBlkBadMagic;
+        } else if (a.mode == kModeHeader) {
+          parse = (cls == kMagicHeader);
+          if (!parse) status = kBlkBadMagic;
         } else {
-          r = parse_header<kParseCount>(pl, none, po);
-          if (r.status == kBlkOk && a.codec == RIO_CODEC_NONE && total > 1 && r.nitems > 0) {
-            const HdrResult s = parse_header<kParseStrad>(pl, r, po);
-            sb = s.strad_bytes;
-            sn = s.strad_count;
+          parse = (cls == kMagicTrailer);
+          if (!parse) status = kBlkBadMagic;
+        }
+        if (parse && a.codec != RIO_CODEC_NONE && d.blk_status[b] == kBlkCodec) {
+          parse = false;
+          status = kBlkCodec;
+          ea = d.blk_a[b];
+          eb = d.blk_b[b];
+        }
+        if (parse) {
+          Payload pl = (a.codec != RIO_CODEC_NONE) ? make_contig_payload(d.dec + d.blk_dec_off[b], lens[j])
+                                                   : desc_payload(a.span, d, c0, meta, lens[j]);
+          ParseOut po;
+          po.item_off = d.item_off;
+          po.item_len = d.item_len;
+          po.item_base = bases[j];
+          po.item_cap = a.item_cap;
+          po.view_base = (a.codec != RIO_CODEC_NONE) ? (kItemInRecords | d.blk_dec_off[b]) : 0;
+          po.strad = d.strad;
+          po.ssz = d.ck_ssz;
+          po.c0 = c0;
+          po.overflow = &d.ctl->out_overflow;
+          HdrResult r{};
+          if (fast_header(pl, win[j], r, po, lwin, ltpos, a.sparse ? d.side : nullptr)) {
+            status = r.status;
+            hdr = r.hdr_len;
+          } else {
+            status = kBlkSlow;  // k_parse_slow finishes the block (and its event)
           }
         }
-        status = r.status;
-        ea = r.a;
-        eb = r.b;
-        nitems = r.nitems;
-        hdr = r.hdr_len;
+        if (status != kBlkOk && status != kBlkSlow && a.mode == kModeBody) event = 2 * end + 1;
       }
-      if (status != kBlkOk && a.mode == kModeBody) event = 2 * end + 1;
-    }
-    if (l == 0) {
-      d.blk_status[b] = status;
-      d.blk_a[b] = ea;
-      d.blk_b[b] = eb;
-      d.blk_nitems[b] = (status == kBlkOk) ? nitems : 0;
-      d.blk_hdr[b] = hdr;
-      d.blk_sb[b] = (status == kBlkOk) ? sb : 0;
-      d.blk_sn[b] = (status == kBlkOk) ? sn : 0;
-      if (event != kNone) atomicMin(&d.ctl->first_block_event, event);
+      if (l == 0) {
+        d.blk_status[b] = status;
+        d.blk_a[b] = ea;
+        d.blk_b[b] = eb;
+        d.blk_hdr[b] = hdr;
+        if (event != kNone) atomicMin(&d.ctl->first_block_event, event);
+      }
     }
   }
 }
 
-// wave per block: item views + straddler descriptors (cumSize, scannerv2.go:83-91)
-__global__ void __launch_bounds__(256) k_items(DevBufs d, ParseArgs a) {
+// The blocks k_parse left to the general parser (headers past the first 1 KiB,
+// irregular chunk layouts, and every malformed header: parse_header computes
+// the reference's error values).
+__global__ void __launch_bounds__(256) k_parse_slow(DevBufs d, ParseArgs a) {
   const uint64_t nb = *a.nblocks;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  for (uint64_t b = wave; b < nb; b += nwaves) {
-    if (d.blk_status[b] != kBlkOk || d.blk_nitems[b] == 0) continue;
-    const uint64_t c0 = d.blk_c0[b];
-    const uint64_t total = d.ck_total[c0];
-    const Payload pl = block_payload(d, a, b, c0, total);
-    HdrResult known{};
-    known.nitems = d.blk_nitems[b];
-    known.hdr_len = d.blk_hdr[b];
-    ParseOut po;
-    po.item_off = d.item_off;
-    po.item_len = d.item_len;
-    po.item_base = d.blk_item_base[b];
-    po.item_cap = a.item_cap;
-    po.view_base = (a.codec != RIO_CODEC_NONE) ? (kItemInRecords | d.blk_dec_off[b]) : 0;
-    po.strad = d.strad;
-    po.strad_idx = d.blk_sn_base[b];
-    po.side_base = d.blk_sb_base[b];
-    po.c0 = c0;
-    po.overflow = &d.ctl->out_overflow;
-    if (a.codec == RIO_CODEC_NONE && po.side_base + d.blk_sb[b] > a.side_cap) {
-      if (lane_id() == 0) atomicOr(&d.ctl->out_overflow, 4ull);
-      continue;
+  const int l = lane_id();
+  for (uint64_t g = wave * 64; g < nb; g += nwaves * 64) {
+    const bool slow = (g + l < nb) && d.blk_status[g + l] == kBlkSlow;
+    unsigned long long sm = __ballot(slow);
+    while (sm) {
+      const uint64_t b = g + __ffsll((long long)sm) - 1;
+      sm &= sm - 1;
+      const uint64_t c0 = d.blk_c0[b];
+      const unsigned long long meta = d.blk_meta[b];
+      const uint64_t total = meta & kMetaTotalMask;
+      const unsigned long long len = (a.codec == RIO_CODEC_NONE) ? d.blk_len[b] : d.blk_out_len[b];
+      const Payload pl = (a.codec != RIO_CODEC_NONE) ? make_contig_payload(d.dec + d.blk_dec_off[b], len)
+                                                     : desc_payload(a.span, d, c0, meta, len);
+      ParseOut po;
+      po.item_off = d.item_off;
+      po.item_len = d.item_len;
+      po.item_base = d.blk_item_base[b];
+      po.item_cap = a.item_cap;
+      po.view_base = (a.codec != RIO_CODEC_NONE) ? (kItemInRecords | d.blk_dec_off[b]) : 0;
+      po.strad = d.strad;
+      po.ssz = d.ck_ssz;
+      po.c0 = c0;
+      po.overflow = &d.ctl->out_overflow;
+      const HdrResult none{};
+      const HdrResult r = parse_header<kParseCount>(pl, none, po);
+      if (r.status == kBlkOk) {
+        if (r.nitems != d.blk_nitems[b]) {  // the reservation reads the same varint: internal error
+          if (l == 0) atomicOr(&d.ctl->out_overflow, 16ull);
+        } else {
+          parse_header<kParseWrite>(pl, r, po);
+        }
+      }
+      if (l == 0) {
+        d.blk_status[b] = r.status;
+        d.blk_a[b] = r.a;
+        d.blk_b[b] = r.b;
+        d.blk_hdr[b] = r.hdr_len;
+        if (r.status != kBlkOk && a.mode == kModeBody) atomicMin(&d.ctl->first_block_event, 2 * (c0 + total - 1) + 1);
+      }
     }
-    HdrResult r{};
-    if (!fast_header<kParseWrite>(pl, r, po)) parse_header<kParseWrite>(pl, known, po);
   }
 }
 
-// wave per straddling item: gather its bytes across the chunk header into side
-__global__ void __launch_bounds__(256) k_strad(const uint8_t *__restrict__ span, DevBufs d,
-                                               const unsigned long long *nblocks_dev, uint64_t side_cap) {
-  const uint64_t n = d.blk_sn_base[*nblocks_dev];  // straddlers of all blocks
+// compressed codecs: item slots from the decoded blocks' first varint
+__global__ void __launch_bounds__(256) k_dec_nitems(DevBufs d, const unsigned long long *nblocks) {
+  const uint64_t nb = *nblocks;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
+    unsigned long long v = 0, res = 0;
+    const unsigned long long len = d.blk_out_len[b];
+    if (d.blk_status[b] != kBlkCodec) {
+      const uint8_t *p = d.dec + d.blk_dec_off[b];
+      for (int k = 0; k < 10 && (unsigned long long)k < len; k++) {
+        const uint32_t c = p[k];
+        v |= (unsigned long long)(c & 0x7f) << (7 * k);
+        if (c < 0x80) {
+          if (!(k == 9 && c > 1) && v <= len) res = v;
+          break;
+        }
+      }
+    }
+    d.blk_nitems[b] = res;
+  }
+}
+
+// Straddlers recorded by the general parser (and, in compact mode, by the
+// fast path): 64 chunk slots per wave, one straddler at a time gathered by the
+// whole wave across the chunk header(s) into the side buffer -- at its own span
+// offset (sparse) or at ck_sbase[slot] (compact) -- and the item's view set.
+__global__ void __launch_bounds__(256) k_strad(const uint8_t *__restrict__ span, DevBufs d, uint64_t nslots,
+                                               uint64_t side_cap, int32_t sparse) {
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const int l = lane_id();
-  for (uint64_t i = wave; i < n; i += nwaves) {
-    const StradDesc s = d.strad[i];
-    if (s.dst + pad16(s.len) > side_cap) continue;
-    const Payload pl = make_chunk_payload(span, d, s.c0, d.ck_total[s.c0]);
-    for (uint64_t x = 16ull * l; x < s.len; x += 1024) {
-      uint32_t w[4] = {0, 0, 0, 0};
-      const uint64_t m = (s.len - x) < 16 ? (s.len - x) : 16;
-      for (uint64_t k = 0; k < m; k++) w[k >> 2] |= pl.byte_at(s.src + x + k) << (8 * (k & 3));
-      *reinterpret_cast<uint4 *>(d.side + s.dst + x) = make_uint4(w[0], w[1], w[2], w[3]);
+  for (uint64_t c0 = wave * 64; c0 < nslots; c0 += nwaves * 64) {
+    const bool has = (c0 + l < nslots) && d.ck_ssz[c0 + l] != 0;
+    unsigned long long sm = __ballot(has);
+    while (sm) {
+      const uint64_t c = c0 + __ffsll((long long)sm) - 1;
+      sm &= sm - 1;
+      const StradDesc s = d.strad[c];
+      const Payload pl = make_chunk_payload(span, d, s.c0, d.ck_total[s.c0]);
+      uint64_t ch, lo;
+      pl.chunk_of(s.src, ch, lo);
+      const unsigned long long dst = sparse ? ch * kChunk + kChunkHdr + (s.src - lo) : d.ck_sbase[c];
+      if (dst + pad16(s.len) > side_cap) {
+        if (l == 0) atomicOr(&d.ctl->out_overflow, 4ull);
+        continue;
+      }
+      if (l == 0) d.item_off[s.item] = kItemInRecords | dst;
+      // piecewise: each piece is contiguous in one chunk payload
+      unsigned long long p = s.src, o = 0;
+      while (o < s.len) {
+        pl.chunk_of(p, ch, lo);
+        const unsigned long long avail = d.ck_size[ch] - (p - lo);
+        const unsigned long long n = (s.len - o) < avail ? (s.len - o) : avail;
+        const uint8_t *src = span + ch * kChunk + kChunkHdr + (p - lo);
+        for (unsigned long long k = l; k < n; k += 64) d.side[dst + o + k] = src[k];
+        p += n;
+        o += n;
+      }
     }
   }
 }
@@ -163,11 +278,13 @@ __device__ __forceinline__ void load_magic(const uint8_t *span, uint64_t ch, uns
   m = (unsigned long long)h[0] | ((unsigned long long)h[1] << 32);
 }
 
-// records-buffer bytes used by the first n blocks
-__device__ __forceinline__ unsigned long long rec_end(const DevBufs &d, uint64_t n, int codec) {
+// records-buffer bytes used by the first n of nb blocks
+__device__ __forceinline__ unsigned long long rec_end(const DevBufs &d, uint64_t n, uint64_t nb, uint64_t nchunks,
+                                                      int codec, int sparse) {
   if (n == 0) return 0;
   if (codec != RIO_CODEC_NONE) return d.blk_dec_off[n - 1] + d.blk_out_len[n - 1];
-  return d.blk_sb_base[n];
+  const uint64_t c = n < nb ? d.blk_c0[n] : nchunks;  // straddlers of the first n blocks lie before c
+  return sparse ? c * kChunk : d.ck_sbase[c];
 }
 
 __global__ void k_resolve(DevBufs d, ResolveArgs a) {
@@ -257,7 +374,7 @@ __global__ void k_resolve(DevBufs d, ResolveArgs a) {
   c->stop_key = key;
   c->n_valid_blocks = nvalid;
   c->n_items = d.blk_item_base[nvalid];
-  c->rec_bytes = rec_end(d, nvalid, a.codec);
+  c->rec_bytes = rec_end(d, nvalid, nb, a.nchunks, a.codec, a.sparse);
   if (kind == 2) {
     // chunk-level error; within one chunk: size > crc > structural (chunk.go:333-343)
     const uint64_t ch = ce;
@@ -322,17 +439,21 @@ static inline unsigned grid_of(uint64_t n, unsigned per, unsigned cap) {
   return (unsigned)(g > cap ? cap : g);
 }
 
-void launch_block_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_block_parse, dim3(grid_of(max_blocks, 4, 4096)), dim3(256), 0, st, d, a);
+void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_parse, dim3(grid_of(max_blocks, 4 * kBatch, 2048)), dim3(256), 0, st, d, a);
 }
 
-void launch_items(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_items, dim3(grid_of(max_blocks, 4, 4096)), dim3(256), 0, st, d, a);
+void launch_parse_slow(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_parse_slow, dim3(grid_of(max_blocks, 256, 1024)), dim3(256), 0, st, d, a);
 }
 
-void launch_strad(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_strad,
-                  uint64_t side_cap, hipStream_t st) {
-  hipLaunchKernelGGL(k_strad, dim3(grid_of(max_strad, 4, 2048)), dim3(256), 0, st, span, d, nblocks_dev, side_cap);
+void launch_dec_nitems(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_dec_nitems, dim3(grid_of(max_blocks, 256, 1024)), dim3(256), 0, st, d, nblocks);
+}
+
+void launch_strad(const uint8_t *span, const DevBufs &d, uint64_t nslots, uint64_t side_cap, int32_t sparse,
+                  hipStream_t st) {
+  hipLaunchKernelGGL(k_strad, dim3(grid_of(nslots, 256, 1024)), dim3(256), 0, st, span, d, nslots, side_cap, sparse);
 }
 
 void launch_resolve(const DevBufs &d, const ResolveArgs &a, hipStream_t st) {

@@ -11,6 +11,13 @@ namespace rio {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// lane j's value, as a wave-uniform (scalar) value
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int j) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, j);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), j);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 // ---------------------------------------------------------------- wave scans
 template <class T>
 __device__ __forceinline__ T wave_incl_sum(T v) {
@@ -167,13 +174,12 @@ __device__ __forceinline__ Payload make_contig_payload(const uint8_t *p, uint64_
 }
 
 // ---------------------------------------------------------------- header parse
-enum ParseMode : int { kParseCount = 0, kParseStrad = 1, kParseWrite = 2 };
+enum ParseMode : int { kParseCount = 0, kParseWrite = 2 };
 
 struct HdrResult {
   uint32_t status;  // BlockStatus
   unsigned long long a, b;
   unsigned long long nitems, hdr_len;
-  unsigned long long strad_bytes, strad_count;  // kParseStrad
 };
 
 // where kParseWrite puts item views and straddler descriptors
@@ -181,9 +187,8 @@ struct ParseOut {
   unsigned long long *item_off, *item_len;
   uint64_t item_base, item_cap;
   unsigned long long view_base;  // compressed: kItemInRecords | offset of the decoded block
-  StradDesc *strad;
-  uint64_t strad_idx;            // first descriptor slot of the block
-  unsigned long long side_base;  // first side-buffer byte of the block
+  StradDesc *strad;              // per chunk slot
+  unsigned long long *ssz;       // per chunk slot: padded straddler size
   uint64_t c0;
   unsigned long long *overflow;
 };
@@ -200,18 +205,50 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t w[4], int i) {
 
 __device__ __forceinline__ unsigned long long pad16(unsigned long long n) { return (n + 15) & ~15ull; }
 
+// one item view (kParseWrite): a view into the span / decoded block, or, for an
+// item crossing a chunk payload boundary, a straddler descriptor in the slot of
+// the chunk it starts in (k_strad fills item_off)
+__device__ __forceinline__ void emit_item(const Payload &pl, const ParseOut &po, uint64_t o, unsigned long long st,
+                                          unsigned long long v) {
+  const uint64_t slot = po.item_base + (o - 1);
+  if (slot >= po.item_cap) {
+    atomicOr(po.overflow, 1ull);
+    return;
+  }
+  po.item_len[slot] = v;
+  if (pl.contig) {
+    po.item_off[slot] = po.view_base + st;
+    return;
+  }
+  if (v == 0 && st >= pl.len) {
+    po.item_off[slot] = 0;
+    return;
+  }
+  uint64_t c, lo;
+  pl.chunk_of(st, c, lo);
+  if (v > 0 && pl.straddles(st, v)) {
+    StradDesc dsc;
+    dsc.c0 = pl.c0;
+    dsc.src = st;
+    dsc.len = v;
+    dsc.item = slot;
+    po.strad[c] = dsc;
+    po.ssz[c] = pad16(v);
+    return;
+  }
+  po.item_off[slot] = c * kChunk + kChunkHdr + (st - lo);
+}
+
 // parseChunksToItems' header loop with Go 1.13 binary.Uvarint semantics: varint
 // 0 is the item count, varints 1..n are item sizes. One wave; each lane owns
 // 16 consecutive payload bytes of a 1 KiB window; terminator ordinals come from
 // a wave prefix sum, varints crossing lanes read their earlier bytes back.
 //  kParseCount: item count, header length and the reference's error checks.
-//  kParseStrad: (header known valid) bytes/count of items crossing a chunk
-//               payload boundary -- those are copied to the side buffer.
-//  kParseWrite: item views (offset, length) and straddler descriptors.
+//  kParseWrite: (header known valid) item views and straddler descriptors.
 template <int MODE>
 __device__ HdrResult parse_header(const Payload &pl, const HdrResult &known, const ParseOut &po) {
   const int l = lane_id();
-  HdrResult r{kBlkOk, 0, 0, 0, 0, 0, 0};
+  HdrResult r{kBlkOk, 0, 0, 0, 0};
   const uint64_t plen = pl.len;
   uint64_t ord_base = 0;       // terminators before this window
   long long prev_term = -1;    // position of the last terminator before this window
@@ -219,7 +256,6 @@ __device__ HdrResult parse_header(const Payload &pl, const HdrResult &known, con
   unsigned long long nitems = known.nitems;
   const unsigned long long hdr = known.hdr_len;
   unsigned long long sum = 0;  // Go int arithmetic: wraps
-  unsigned long long strad_b = 0, strad_n = 0;
   bool range = false;
   for (uint64_t base = 0; base < plen; base += 1024) {
     const uint64_t pos = base + 16ull * l;
@@ -256,19 +292,15 @@ __device__ HdrResult parse_header(const Payload &pl, const HdrResult &known, con
     }
     if (have_n) {
       // Walk this lane's terminators with ordinals 1..nitems. pass 0: value
-      // sums (+ Go 1.13 overflow checks); pass 1: straddler bytes/count at the
-      // item positions; pass 2: item views and straddler descriptors.
+      // sums (+ Go 1.13 overflow checks); pass 1: item views.
       unsigned long long first_bad = ~0ull;
       long long bad_len = 0;
       bool lrange = false;
-      auto walk = [&](int pass, unsigned long long run, unsigned long long sb, unsigned long long sn,
-                      unsigned long long &o_sb, unsigned long long &o_sn) -> unsigned long long {
+      auto walk = [&](int pass, unsigned long long run) -> unsigned long long {
         unsigned long long lsum = 0;
         uint32_t m = tmask;
         long long prev = before;
         uint64_t ord = ord0;
-        o_sb = 0;
-        o_sn = 0;
         while (m) {
           const int i = __ffs(m) - 1;
           m &= m - 1;
@@ -295,40 +327,13 @@ __device__ HdrResult parse_header(const Payload &pl, const HdrResult &known, con
           if (pass == 0) {
             if (v > plen) lrange = true;
           } else {
-            const unsigned long long st = hdr + run + lsum;  // logical start of item o
-            const bool sd = pl.straddles(st, v);
-            if (pass == 2) {
-              const uint64_t slot = po.item_base + (o - 1);
-              if (slot < po.item_cap) {
-                unsigned long long off;
-                if (pl.contig) off = po.view_base + st;
-                else if (sd) off = kItemInRecords | (po.side_base + sb + o_sb);
-                else off = (v == 0 && st >= plen) ? 0 : pl.phys(st);
-                po.item_off[slot] = off;
-                po.item_len[slot] = v;
-              } else {
-                atomicOr(po.overflow, 1ull);
-              }
-              if (sd) {
-                StradDesc dsc;
-                dsc.c0 = po.c0;
-                dsc.src = st;
-                dsc.len = v;
-                dsc.dst = po.side_base + sb + o_sb;
-                po.strad[po.strad_idx + sn + o_sn] = dsc;
-              }
-            }
-            if (sd) {
-              o_sb += pad16(v);
-              o_sn += 1;
-            }
+            emit_item(pl, po, o, hdr + run + lsum, v);
           }
           lsum += v;
         }
         return lsum;
       };
-      unsigned long long t0, t1;
-      const unsigned long long lsum = walk(0, 0, 0, 0, t0, t1);
+      const unsigned long long lsum = walk(0, 0);
       if (MODE == kParseCount) {
         // the first overflow in the wave (and in file order) stops the header
         const unsigned long long wbad = wave_min_u64(first_bad);
@@ -343,16 +348,7 @@ __device__ HdrResult parse_header(const Payload &pl, const HdrResult &known, con
         if (__ballot(lrange)) range = true;
       } else {
         const unsigned long long incl = wave_incl_sum<unsigned long long>(lsum);
-        const unsigned long long run = sum + incl - lsum;
-        unsigned long long lsb, lsn;
-        walk(1, run, 0, 0, lsb, lsn);
-        if (MODE == kParseWrite) {
-          const unsigned long long ib = wave_incl_sum<unsigned long long>(lsb);
-          const unsigned long long in = wave_incl_sum<unsigned long long>(lsn);
-          walk(2, run, strad_b + ib - lsb, strad_n + in - lsn, t0, t1);
-        }
-        strad_b += wave_sum<unsigned long long>(lsb);
-        strad_n += wave_sum<unsigned long long>(lsn);
+        walk(1, sum + incl - lsum);
       }
       sum += wave_sum<unsigned long long>(lsum);
       // the header ends at the terminator with ordinal nitems
@@ -368,8 +364,6 @@ __device__ HdrResult parse_header(const Payload &pl, const HdrResult &known, con
         const long long hend = __shfl(endp, __ffsll((long long)eb) - 1, 64) + 1;
         r.nitems = nitems;
         r.hdr_len = (unsigned long long)hend;
-        r.strad_bytes = strad_b;
-        r.strad_count = strad_n;
         if (MODE == kParseCount) {
           if (sum + r.hdr_len != plen) {
             r.status = kBlkBlockSize;
@@ -400,174 +394,159 @@ __device__ HdrResult parse_header(const Payload &pl, const HdrResult &known, con
 
 // ---------------------------------------------------------------- fast path
 // The common block shape -- the whole header inside the first 1 KiB of the
-// payload, every varint shorter than 11 bytes, sizes consistent with the block
-// -- parsed from one 16 B/lane window with fully unrolled byte loops (no
-// dynamic register indexing). Anything else returns false and the block goes
-// through parse_header, which also produces the reference's error values.
+// payload, every varint shorter than 11 bytes, sizes consistent with the block,
+// a regular chunk layout -- parsed item-parallel from one prefetched window:
+// the window and the terminator positions go to the wave's LDS, then lane t
+// decodes items t, t+64, ... and writes their views coalesced. Anything else
+// returns false before writing and the block goes through parse_header, which
+// also produces the reference's error values.
 
-// lane's terminators in byte order: f(k, i, value, varint_len, last_byte);
-// the lane's first varint continues the previous lane's trailing bytes
-template <class F>
-__device__ __forceinline__ void walk_lane(const uint32_t w[4], uint32_t tmask, unsigned long long c_acc, int c_len,
-                                          F &&f) {
-  unsigned long long acc = 0;
-  int len = 0, k = 0;
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xffu;
-    const int sh = 7 * len;
-    if (sh < 64) acc |= (unsigned long long)(b & 0x7fu) << sh;
-    len++;
-    if ((tmask >> i) & 1u) {
-      unsigned long long v = acc;
-      int vl = len;
-      if (k == 0) {
-        const int csh = 7 * c_len;
-        v = c_acc | (csh < 64 ? (acc << csh) : 0ull);
-        vl = c_len + len;
-      }
-      f(k, v, vl, b);
-      acc = 0;
-      len = 0;
-      k++;
-    }
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// bytes [s, e] of the LDS window as a uvarint (e - s < 10)
+__device__ __forceinline__ unsigned long long lds_uvarint(const uint8_t *lwin, uint32_t s, uint32_t e) {
+  unsigned long long v = 0;
+  for (uint32_t q = s; q <= e; q++) v |= (unsigned long long)(lwin[q] & 0x7fu) << (7 * (q - s));
+  return v;
+}
+
+// Wave-cooperative copy of n bytes, src and dst congruent mod 4.
+__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, uint64_t n) {
+  const int l = lane_id();
+  const uint64_t head = (4 - ((uintptr_t)src & 3)) & 3;
+  const uint64_t h = head < n ? head : n;
+  if ((uint64_t)l < h) dst[l] = src[l];
+  const uint64_t nw = (n - h) >> 2;
+  const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src + h);
+  uint32_t *d4 = reinterpret_cast<uint32_t *>(dst + h);
+  for (uint64_t k = l; k < nw; k += 64) d4[k] = s4[k];
+  const uint64_t t0 = h + (nw << 2);
+  if (t0 + l < n) dst[t0 + l] = src[t0 + l];
+}
+
+// Straddler of a regular block into the span-shaped side buffer: it starts at
+// its own span offset there and runs contiguously (the chunk headers it crosses
+// are squeezed out), so straddlers never overlap and src == dst (mod 4).
+__device__ __forceinline__ void copy_straddler(const Payload &pl, uint8_t *side, uint64_t st, uint64_t v,
+                                               uint64_t dst0) {
+  uint64_t p = st, done = 0;
+  while (done < v) {
+    const uint64_t j = p / kMaxPayload, in = p - j * kMaxPayload;
+    const uint64_t room = kMaxPayload - in;
+    const uint64_t n = (v - done) < room ? (v - done) : room;
+    wave_copy(side + dst0 + done, pl.span + (pl.c0 + j) * kChunk + kChunkHdr + in, n);
+    p += n;
+    done += n;
   }
 }
 
-__device__ __forceinline__ bool uvarint_ok(int vl, uint32_t last) { return vl < 10 || (vl == 10 && last <= 1); }
-
-// MODE kParseCount: r gets nitems, hdr_len, straddler bytes/count.
-// MODE kParseWrite: item views and straddler descriptors as parse_header.
-template <int MODE>
-__device__ bool fast_header(const Payload &pl, HdrResult &r, const ParseOut &po) {
+// window w = payload bytes [16*lane, 16*lane + 16) (0x80 past the payload);
+// writes the block's item views like parse_header<kParseWrite> and returns
+// nitems / hdr_len in r, or returns false (nothing written).
+// sparse_side != null: straddlers are copied here (span-shaped side buffer);
+// else they get descriptors for k_strad.
+__device__ bool fast_header(const Payload &pl, const uint32_t (&w)[4], HdrResult &r, const ParseOut &po,
+                            uint8_t *lwin, uint16_t *ltpos, uint8_t *sparse_side) {
   const int l = lane_id();
   const uint64_t plen = pl.len;
   if (plen >= (1ull << 32)) return false;
   if (!pl.contig && !pl.regular) return false;
-  const uint32_t pos = 16u * (uint32_t)l;
-  uint32_t w[4];
-  pl.fetch16(pos, w);
   const uint32_t tmask = term4(w[0]) | (term4(w[1]) << 4) | (term4(w[2]) << 8) | (term4(w[3]) << 12);
-  // the item count: lane 0's first varint
-  unsigned long long n0 = 0;
-  bool n0_ok = false;
-  if (l == 0 && tmask) {
-    walk_lane(w, tmask & (0u - tmask), 0ull, 0, [&](int, unsigned long long v, int vl, uint32_t b) {
-      n0 = v;
-      n0_ok = uvarint_ok(vl, b);
-    });
-  }
-  const unsigned long long nitems = __shfl(n0, 0, 64);
-  if (!__shfl((int)n0_ok, 0, 64)) return false;
   const uint32_t cnt = __popc(tmask);
   const uint32_t incl = wave_incl_sum<uint32_t>(cnt);
-  const uint32_t ex = incl - cnt;
   const uint32_t total = __shfl(incl, 63, 64);
-  if (nitems >= total) return false;  // header not inside the window
-  // header end: the terminator with ordinal nitems
-  const bool mine = nitems >= ex && nitems < incl;
-  int endbit = -1;
-  if (mine) {
-    uint32_t mm = tmask;
-    for (uint32_t k = ex; k < (uint32_t)nitems; k++) mm &= mm - 1;
-    endbit = __ffs(mm) - 1;
-  }
-  const unsigned long long eb = __ballot(mine);
-  const uint32_t hdr = (uint32_t)__shfl((int)pos + endbit, __ffsll((long long)eb) - 1, 64) + 1;
-  // carry-in: the previous lane's bytes after its last terminator
-  const int t_last = tmask ? 31 - __clz(tmask) : -1;
-  unsigned long long tacc = 0;
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xffu;
-    const int sh = 7 * (i - t_last - 1);
-    if (i > t_last && sh < 64) tacc |= (unsigned long long)(b & 0x7fu) << sh;
-  }
-  int c_len = __shfl_up(15 - t_last, 1, 64);
-  unsigned long long c_acc = __shfl_up(tacc, 1, 64);
-  if (l == 0) {
-    c_len = 0;
-    c_acc = 0;
-  }
-  // sizes: validity, range, lane sums
-  bool bad = false;
-  unsigned long long lsum = 0;
-  walk_lane(w, tmask, c_acc, c_len, [&](int k, unsigned long long v, int vl, uint32_t b) {
-    const uint32_t o = ex + (uint32_t)k;
-    if (o >= 1 && o <= nitems) {
-      if (!uvarint_ok(vl, b) || v > plen) bad = true;
-      lsum += v;
+  if (total == 0) return false;
+  *reinterpret_cast<uint4 *>(lwin + 16 * l) = make_uint4(w[0], w[1], w[2], w[3]);
+  {
+    uint32_t m = tmask, o = incl - cnt;
+    while (m) {
+      const uint32_t i = __ffs(m) - 1;
+      m &= m - 1;
+      ltpos[o++] = (uint16_t)(16 * l + i);
     }
-  });
+  }
+  wave_lds_sync();
+  // item count: the first varint
+  const uint32_t p0 = ltpos[0];
+  if (p0 > 9 || (p0 == 9 && lwin[9] > 1)) return false;
+  const unsigned long long nitems = lds_uvarint(lwin, 0, p0);
+  if (nitems >= total) return false;  // header not inside the window
+  const uint32_t hdr = (uint32_t)ltpos[nitems] + 1;
+  // pass A: validity, range, sum
+  int bad = 0;
+  unsigned long long lsum = 0;
+  for (unsigned long long g = 0; g < nitems; g += 64) {
+    const unsigned long long o = g + l + 1;
+    if (o <= nitems) {
+      const uint32_t s = (uint32_t)ltpos[o - 1] + 1, e = ltpos[o];
+      if (e - s > 9 || (e - s == 9 && lwin[e] > 1)) {
+        bad = 1;
+      } else {
+        const unsigned long long v = lds_uvarint(lwin, s, e);
+        if (v > plen) bad = 1;
+        lsum += v;
+      }
+    }
+  }
   if (__ballot(bad)) return false;
   if (wave_sum<unsigned long long>(lsum) + hdr != plen) return false;
-  const unsigned long long run0 = hdr + wave_incl_sum<unsigned long long>(lsum) - lsum;
+  // pass B: views, coalesced (lane t: slot base + g + t)
   const bool chunks = !pl.contig && pl.total > 1;
-  // straddlers (items crossing a chunk payload boundary)
-  unsigned long long sb = 0, sn = 0;
-  if (chunks) {
-    unsigned long long run = run0;
-    walk_lane(w, tmask, c_acc, c_len, [&](int k, unsigned long long v, int, uint32_t) {
-      const uint32_t o = ex + (uint32_t)k;
-      if (o >= 1 && o <= nitems) {
-        const uint32_t st = (uint32_t)run;
-        if (v > 0 && st / (uint32_t)kMaxPayload != (st + (uint32_t)v - 1) / (uint32_t)kMaxPayload) {
-          sb += pad16(v);
-          sn += 1;
-        }
-        run += v;
-      }
-    });
-  }
-  if (MODE == kParseCount) {
-    r.status = kBlkOk;
-    r.nitems = nitems;
-    r.hdr_len = hdr;
-    r.strad_bytes = chunks ? wave_sum<unsigned long long>(sb) : 0;
-    r.strad_count = chunks ? wave_sum<unsigned long long>(sn) : 0;
-    return true;
-  }
-  unsigned long long sbx = 0, snx = 0;
-  if (chunks) {
-    sbx = wave_incl_sum<unsigned long long>(sb) - sb;
-    snx = wave_incl_sum<unsigned long long>(sn) - sn;
-  }
-  unsigned long long run = run0;
-  walk_lane(w, tmask, c_acc, c_len, [&](int k, unsigned long long v, int, uint32_t) {
-    const uint32_t o = ex + (uint32_t)k;
-    if (o >= 1 && o <= nitems) {
-      const uint32_t st = (uint32_t)run;
+  unsigned long long carry = hdr;
+  for (unsigned long long g = 0; g < nitems; g += 64) {
+    const unsigned long long o = g + l + 1;
+    const bool have = o <= nitems;
+    unsigned long long v = 0;
+    if (have) v = lds_uvarint(lwin, (uint32_t)ltpos[o - 1] + 1, ltpos[o]);
+    const unsigned long long vi = wave_incl_sum<unsigned long long>(v);
+    const uint32_t st = (uint32_t)(carry + vi - v);
+    carry += __shfl(vi, 63, 64);
+    bool sd = false;
+    unsigned long long phys = 0;
+    if (have) {
       const uint64_t slot = po.item_base + (o - 1);
-      unsigned long long off;
-      bool sd = false;
-      if (pl.contig) {
-        off = po.view_base + st;
-      } else {
-        const uint32_t j = st / (uint32_t)kMaxPayload;
-        sd = chunks && v > 0 && j != (st + (uint32_t)v - 1) / (uint32_t)kMaxPayload;
-        if (sd) off = kItemInRecords | (po.side_base + sbx);
-        else if (v == 0 && st >= plen) off = 0;
-        else off = (pl.c0 + j) * (unsigned long long)kChunk + kChunkHdr + (st - j * (uint32_t)kMaxPayload);
-      }
       if (slot < po.item_cap) {
-        po.item_off[slot] = off;
         po.item_len[slot] = v;
+        if (pl.contig) {
+          po.item_off[slot] = po.view_base + st;
+        } else {
+          const uint32_t j = st / (uint32_t)kMaxPayload;
+          phys = (pl.c0 + j) * (unsigned long long)kChunk + kChunkHdr + (st - j * (uint32_t)kMaxPayload);
+          sd = chunks && v > 0 && j != (st + (uint32_t)v - 1) / (uint32_t)kMaxPayload;
+          if (sd && sparse_side) {
+            po.item_off[slot] = kItemInRecords | phys;
+          } else if (sd) {
+            StradDesc dsc;
+            dsc.c0 = pl.c0;
+            dsc.src = st;
+            dsc.len = v;
+            dsc.item = slot;
+            po.strad[pl.c0 + j] = dsc;
+            po.ssz[pl.c0 + j] = pad16(v);
+          } else {
+            po.item_off[slot] = (v == 0 && st >= plen) ? 0ull : phys;
+          }
+        }
       } else {
         atomicOr(po.overflow, 1ull);
       }
-      if (sd) {
-        StradDesc dsc;
-        dsc.c0 = po.c0;
-        dsc.src = st;
-        dsc.len = v;
-        dsc.dst = po.side_base + sbx;
-        po.strad[po.strad_idx + snx] = dsc;
-        sbx += pad16(v);
-        snx += 1;
-      }
-      run += v;
     }
-  });
+    if (sparse_side) {
+      unsigned long long sm = __ballot(sd);
+      while (sm) {
+        const int L = __ffsll((long long)sm) - 1;
+        sm &= sm - 1;
+        copy_straddler(pl, sparse_side, (uint64_t)__shfl(st, L, 64), __shfl(v, L, 64), __shfl(phys, L, 64));
+      }
+    }
+  }
+  r.status = kBlkOk;
+  r.nitems = nitems;
+  r.hdr_len = hdr;
   return true;
 }
 

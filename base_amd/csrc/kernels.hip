@@ -1,21 +1,18 @@
-// CDNA4 (gfx950) kernels of the recordio scan path: chunk layer, block
-// enumeration, header parse, fused CRC32 + record copy, and the first-error
-// resolve. Host orchestration in pipeline.cpp.
+// CDNA4 (gfx950) kernels of the recordio chunk layer: per-chunk header checks
+// and the scans that enumerate blocks. Host orchestration in pipeline.cpp.
 //
-// Pipeline for one span of whole chunks:
+// Pipeline for one span of whole chunks (none codec):
 //   k_chunk_meta   per chunk: header fields, size check, the structural checks of
 //                  ChunkScanner.Scan against the previous chunk (chunk.go:253-294,
-//                  333-336), block-start flags.
-//   scans          block enumeration (index == 0) and the payload prefix ck_pay.
-//   k_crc_copy     wave per chunk: CRC32-IEEE over [12, 28+size) (chunk.go:338-343)
-//                  fused with idTransform (registry.go:31-39): chunk c's payload
-//                  lands at records + ck_pay[c], so a block's bytes are contiguous
-//                  (the reference's rawItems.bytes) and no copy waits on parsing.
-//   k_block_parse  wave per block: block magic handling (scannerv2.go:374-387) and
-//                  the varint header of parseChunksToItems (scannerv2.go:53-97).
-//   scan           item bases per block.
-//   k_items        wave per block: cumSize -> item_end (scannerv2.go:83-91).
-//   k_resolve      the first event in file order (errors.Once) -> summary.
+//                  333-336).
+//   scans          payload prefix ck_pay; block enumeration (index == 0) with a
+//                  descriptor per block and its item count (first header varint).
+//   block scan     item slots per block.
+//   k_parse        (blocks.hip) wave per block: magic handling, header parse,
+//                  item views (parseChunksToItems, scannerv2.go:53-97, 363-388).
+//   k_strad        (blocks.hip) gather of items that cross a chunk boundary.
+//   k_crc          (crc.hip) CRC32 of every chunk (chunk.go:338-343).
+//   k_resolve      (blocks.hip) the first event in file order (errors.Once).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -78,6 +75,7 @@ __global__ void __launch_bounds__(256) k_chunk_meta(const uint8_t *__restrict__ 
     d.ck_total[c] = total;
     d.ck_index[c] = index;
     d.ck_info[c] = cls | (err << 8);
+    d.ck_ssz[c] = 0;  // straddler slots, filled by k_parse
     if (err != kCkOk) atomicMin(&d.ctl->first_chunk_err, (unsigned long long)c);
   }
 }
@@ -177,12 +175,55 @@ struct FlagLoad {  // block starts: index == 0
   const uint32_t *ck_index;
   __device__ unsigned long long operator()(uint64_t i) const { return ck_index[i] == 0 ? 1ull : 0ull; }
 };
-struct FlagOut {
-  unsigned long long *blk_c0;
-  uint32_t *ck_block;
+// Go 1.13 binary.Uvarint of the block's first payload bytes: the item count
+// (parseChunksToItems, scannerv2.go:65), used to reserve item slots before the
+// headers are parsed. 0 when it does not decode or cannot fit the block.
+__device__ unsigned long long first_uvarint(const uint8_t *span, const DevBufs &d, uint64_t c0, uint32_t total,
+                                            unsigned long long len) {
+  uint64_t c = c0;
+  uint32_t off = 0, csz = d.ck_size[c0];
+  unsigned long long v = 0;
+  for (int k = 0; k < 10 && (unsigned long long)k < len; k++) {
+    while (off >= csz && c + 1 < c0 + total) {
+      c++;
+      off = 0;
+      csz = d.ck_size[c];
+    }
+    if (off >= csz) return 0;
+    const uint32_t b = span[c * kChunk + kChunkHdr + off];
+    off++;
+    v |= (unsigned long long)(b & 0x7f) << (7 * k);
+    if (b < 0x80) {
+      if (k == 9 && b > 1) return 0;
+      return v <= len ? v : 0;
+    }
+  }
+  return 0;
+}
+
+struct FlagOut {  // block starts -> block list + per-block descriptors
+  DevBufs d;
+  const uint8_t *span;
+  uint64_t nchunks;
+  int32_t codec;
   __device__ void operator()(uint64_t i, unsigned long long ex, unsigned long long v) const {
-    if (v) blk_c0[ex] = i;
-    ck_block[i] = (ex + v == 0) ? kNoBlock : (uint32_t)(ex + v - 1);  // chunks before any start: none
+    d.ck_block[i] = (ex + v == 0) ? kNoBlock : (uint32_t)(ex + v - 1);  // chunks before any start: none
+    if (!v) return;
+    d.blk_c0[ex] = i;
+    const uint32_t total = d.ck_total[i];
+    const uint32_t cls = d.ck_info[i] & 0xffu;
+    unsigned long long meta = (unsigned long long)total | ((unsigned long long)cls << kMetaClsShift);
+    unsigned long long len = 0, nres = 0;
+    if (total != 0 && i + total <= nchunks) {
+      meta |= kMetaComplete;
+      const unsigned long long pay0 = d.ck_pay[i];
+      len = d.ck_pay[i + total] - pay0;
+      if (d.ck_pay[i + total - 1] - pay0 == (unsigned long long)(total - 1) * kMaxPayload) meta |= kMetaRegular;
+      if (codec == RIO_CODEC_NONE) nres = first_uvarint(span, d, i, total, len);
+    }
+    d.blk_meta[ex] = meta;
+    d.blk_len[ex] = len;
+    d.blk_nitems[ex] = nres;
   }
 };
 struct SizeLoad {
@@ -223,10 +264,18 @@ static void scan(F f, O o, const unsigned long long *n_dev, uint64_t n_host, uin
   hipLaunchKernelGGL((k_scan_apply<F, O>), dim3(g), dim3(kScanThreads), 0, st, f, o, n_dev, n_host, partial);
 }
 
-void launch_chunk_scans(uint64_t nchunks, const DevBufs &d, unsigned long long *nblocks_dev, hipStream_t st) {
-  scan(FlagLoad{d.ck_index}, FlagOut{d.blk_c0, d.ck_block}, nullptr, nchunks, nchunks, d.scan_tmp, nblocks_dev,
-       nullptr, st);
+void launch_chunk_scans(const uint8_t *span, uint64_t nchunks, const DevBufs &d, unsigned long long *nblocks_dev,
+                        int32_t codec, hipStream_t st) {
+  // payload prefix first: the block descriptors read it
   scan(SizeLoad{d.ck_size}, U64Out{d.ck_pay}, nullptr, nchunks, nchunks, d.scan_tmp, nullptr, d.ck_pay, st);
+  scan(FlagLoad{d.ck_index}, FlagOut{d, span, nchunks, codec}, nullptr, nchunks, nchunks, d.scan_tmp, nblocks_dev,
+       nullptr, st);
+}
+
+// exclusive scan of a per-chunk u64 array into out (n + 1 entries)
+void launch_chunk_scan(const unsigned long long *in, unsigned long long *out, unsigned long long *tmp, uint64_t n,
+                       hipStream_t st) {
+  scan(U64Load{in}, U64Out{out}, nullptr, n, n, tmp, nullptr, out, st);
 }
 
 // exclusive scan of a per-block u64 array into out (n + 1 entries), n on device

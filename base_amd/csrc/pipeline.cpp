@@ -5,7 +5,7 @@
 // Launch order per span (one stream; RIO_TWO_STREAMS=1 puts the parse path on
 // a second stream beside k_crc, which only pays when k_crc leaves CU room):
 //   memsets, k_chunk_meta, chunk scans, [codec decode],
-//   k_block_parse, block scans, k_items, k_strad,   (parse path, ~1% of the bytes)
+//   block scan (item slots), k_parse, straddler scan, k_strad   (parse path)
 //   k_crc (streams every chunk byte), k_resolve
 #include <hip/hip_runtime.h>
 #include <inttypes.h>
@@ -23,14 +23,18 @@
 namespace rio {
 // kernels.hip
 void launch_chunk_meta(const uint8_t *span, uint64_t nchunks, const DevBufs &d, hipStream_t st);
-void launch_chunk_scans(uint64_t nchunks, const DevBufs &d, unsigned long long *nblocks_dev, hipStream_t st);
+void launch_chunk_scans(const uint8_t *span, uint64_t nchunks, const DevBufs &d, unsigned long long *nblocks_dev,
+                        int32_t codec, hipStream_t st);
+void launch_chunk_scan(const unsigned long long *in, unsigned long long *out, unsigned long long *tmp, uint64_t n,
+                       hipStream_t st);
 void launch_block_scan(const unsigned long long *in, unsigned long long *out, unsigned long long *tmp,
                        const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 // blocks.hip
-void launch_block_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
-void launch_items(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
-void launch_strad(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_strad,
-                  uint64_t side_cap, hipStream_t st);
+void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
+void launch_parse_slow(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
+void launch_dec_nitems(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st);
+void launch_strad(const uint8_t *span, const DevBufs &d, uint64_t nslots, uint64_t side_cap, int32_t sparse,
+                  hipStream_t st);
 void launch_resolve(const DevBufs &d, const ResolveArgs &a, hipStream_t st);
 // crc.hip
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
@@ -112,12 +116,12 @@ static int alloc_bufs(rio_ctx *c) {
   DevBufs &d = c->d;
   const uint64_t n = c->max_chunks + 1;
   if (dalloc(&d.ck_size, n) || dalloc(&d.ck_total, n) || dalloc(&d.ck_index, n) || dalloc(&d.ck_info, n) ||
-      dalloc(&d.ck_crc, n) || dalloc(&d.ck_block, n) || dalloc(&d.ck_pay, n + 1))
+      dalloc(&d.ck_crc, n) || dalloc(&d.ck_block, n) || dalloc(&d.ck_pay, n + 1) || dalloc(&d.ck_ssz, n) ||
+      dalloc(&d.ck_sbase, n + 1))
     return -1;
   const uint64_t nb = c->max_blocks + 1;
-  if (dalloc(&d.blk_c0, nb) || dalloc(&d.blk_nitems, nb) || dalloc(&d.blk_hdr, nb) ||
-      dalloc(&d.blk_item_base, nb + 1) || dalloc(&d.blk_sb, nb) || dalloc(&d.blk_sn, nb) ||
-      dalloc(&d.blk_sb_base, nb + 1) || dalloc(&d.blk_sn_base, nb + 1) || dalloc(&d.blk_status, nb) ||
+  if (dalloc(&d.blk_c0, nb) || dalloc(&d.blk_meta, nb) || dalloc(&d.blk_len, nb) || dalloc(&d.blk_nitems, nb) ||
+      dalloc(&d.blk_hdr, nb) || dalloc(&d.blk_item_base, nb + 1) || dalloc(&d.blk_status, nb) ||
       dalloc(&d.blk_a, nb) || dalloc(&d.blk_b, nb) || dalloc(&d.blk_out_len, nb) || dalloc(&d.blk_dec_off, nb + 1))
     return -1;
   if (dalloc(&d.scan_tmp, (n + 2047) / 2048 + 16) || dalloc(&d.strad, n)) return -1;
@@ -128,9 +132,8 @@ static int alloc_bufs(rio_ctx *c) {
 
 static void free_all(rio_ctx *c) {
   DevBufs &d = c->d;
-  void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.blk_c0,
-                d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_sb, d.blk_sn, d.blk_sb_base, d.blk_sn_base,
-                d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.item_off, d.item_len, d.side,
+  void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
+                d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span};
   for (void *p : ps)
@@ -215,10 +218,21 @@ static int ensure_dec(rio_ctx *c, uint64_t need) {
 }
 
 // Enqueue the full pipeline for `nchunks` whole chunks at device span `span`.
+static int ensure_side(rio_ctx *c, uint64_t need) {
+  if (c->side_cap >= need) return 0;
+  if (dalloc(&c->d.side, need)) return -1;
+  c->side_cap = need;
+  return 0;
+}
+
+// sparse: straddlers land at their own span offset in a span-sized side buffer
+// (device-resident results, no straddler scan); else compacted (host results).
 static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t limit_chunk, int is_file_end,
-                   int tail_partial, int32_t codec, int32_t mode) {
+                   int tail_partial, int32_t codec, int32_t mode, bool sparse) {
+  if (sparse && codec == RIO_CODEC_NONE && ensure_side(c, nchunks * (uint64_t)kChunk)) return -1;
   DevBufs &d = c->d;
   hipStream_t st = c->st, st2 = c->st2;
+  c->last_nchunks = nchunks;
   HIP_OK(hipEventRecord(c->ev[kEvStart], st));
   // control words are min-reduced: reset to ~0 (out_overflow to 0)
   HIP_OK(hipMemsetAsync(d.ctl, 0xff, 4 * sizeof(unsigned long long), st));
@@ -227,7 +241,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   const uint64_t max_blocks = nchunks ? nchunks : 1;
   if (nchunks > 0) {
     launch_chunk_meta(span, nchunks, d, st);
-    launch_chunk_scans(nchunks, d, c->nblocks_dev, st);
+    launch_chunk_scans(span, nchunks, d, c->nblocks_dev, codec, st);
   }
   HIP_OK(hipEventRecord(c->ev[kEvScans], st));
   c->last_had_dec = false;
@@ -244,18 +258,18 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   HIP_OK(hipEventRecord(c->ev[kEvParse0], st2));
   const bool run_parse = !(c->kernel_flags & 2), run_crc = !(c->kernel_flags & 4);
   if (nchunks > 0 && run_parse) {
-    ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap};
-    launch_block_parse(d, pa, max_blocks, st2);
+    ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap, sparse, 0};
+    if (codec != RIO_CODEC_NONE) launch_dec_nitems(d, c->nblocks_dev, max_blocks, st2);
     launch_block_scan(d.blk_nitems, d.blk_item_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
+    launch_parse(d, pa, max_blocks, st2);
+    launch_parse_slow(d, pa, max_blocks, st2);
     if (codec == RIO_CODEC_NONE) {
-      launch_block_scan(d.blk_sb, d.blk_sb_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
-      launch_block_scan(d.blk_sn, d.blk_sn_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
+      if (!sparse) launch_chunk_scan(d.ck_ssz, d.ck_sbase, d.scan_tmp, nchunks, st2);
+      launch_strad(span, d, nchunks, c->side_cap, sparse, st2);
     }
-    launch_items(d, pa, max_blocks, st2);
-    if (codec == RIO_CODEC_NONE) launch_strad(span, d, c->nblocks_dev, nchunks, c->side_cap, st2);
   } else if (nchunks == 0) {
     HIP_OK(hipMemsetAsync(d.blk_item_base, 0, 8, st2));
-    HIP_OK(hipMemsetAsync(d.blk_sb_base, 0, 8, st2));
+    HIP_OK(hipMemsetAsync(d.ck_sbase, 0, 8, st2));
   }
   HIP_OK(hipEventRecord(c->ev[kEvParse1], st2));
   HIP_OK(hipEventRecord(c->evB, st2));
@@ -266,7 +280,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   }
   HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
   HIP_OK(hipStreamWaitEvent(st, c->evB, 0));
-  ResolveArgs ra{span, nchunks, is_file_end, tail_partial, mode, codec, c->nblocks_dev, limit_chunk};
+  ResolveArgs ra{span, nchunks, is_file_end, tail_partial, mode, codec, c->nblocks_dev, limit_chunk, sparse, 0};
   launch_resolve(d, ra, st);
   HIP_OK(hipEventRecord(c->ev[kEvEnd], st));
   return 0;
@@ -336,7 +350,7 @@ static int grow_for_overflow(rio_ctx *c, int32_t codec) {
   unsigned long long nb = 0, items = 0, side = 0;
   HIP_OK(hipMemcpy(&nb, c->nblocks_dev, 8, hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(&items, c->d.blk_item_base + nb, 8, hipMemcpyDeviceToHost));
-  if (codec == RIO_CODEC_NONE) HIP_OK(hipMemcpy(&side, c->d.blk_sb_base + nb, 8, hipMemcpyDeviceToHost));
+  if (codec == RIO_CODEC_NONE) HIP_OK(hipMemcpy(&side, c->d.ck_sbase + c->last_nchunks, 8, hipMemcpyDeviceToHost));
   if (items > c->item_cap) {
     c->item_cap = items + items / 8 + 1024;
     if (dalloc(&c->d.item_off, c->item_cap) || dalloc(&c->d.item_len, c->item_cap)) return -1;
@@ -363,7 +377,7 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
   uint64_t limit_chunk = UINT64_MAX;
   if (limit_off != UINT64_MAX) limit_chunk = limit_off <= file_off ? 0 : (limit_off - file_off + kChunk - 1) / kChunk;
   for (int attempt = 0; attempt < 4; attempt++) {
-    if (enqueue(c, dspan, nchunks, limit_chunk, is_file_end, tail_partial, codec, mode)) return -1;
+    if (enqueue(c, dspan, nchunks, limit_chunk, is_file_end, tail_partial, codec, mode, !to_host)) return -1;
     HIP_OK(hipMemcpyAsync(c->h_ctl, c->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipStreamSynchronize(c->st));
     if (c->h_ctl->out_overflow == 0) break;
@@ -441,7 +455,8 @@ extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_
   ctx->last_codec = codec;
   ctx->last_mode = kModeBody;
   ctx->last_span = (const uint8_t *)dev_span;
-  return enqueue(ctx, (const uint8_t *)dev_span, nchunks, UINT64_MAX, 1, (nbytes % kChunk) != 0, codec, kModeBody);
+  return enqueue(ctx, (const uint8_t *)dev_span, nchunks, UINT64_MAX, 1, (nbytes % kChunk) != 0, codec, kModeBody,
+                 true);
 }
 
 extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {

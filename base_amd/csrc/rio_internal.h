@@ -38,6 +38,7 @@ enum BlockStatus : uint32_t {
   kBlkTrailer = 7,     // trailer block in body mode: clean end of scan
   kBlkLimit = 8,       // starts at/after the shard limit
   kBlkCodec = 9,       // decompression failed: a = codec error code, b = offset
+  kBlkSlow = 10,       // (internal) header left to the general parser, k_parse_slow
 };
 
 enum Mode : int32_t { kModeBody = 0, kModeHeader = 1, kModeTrailer = 2, kModeLastChunk = 3 };
@@ -71,11 +72,19 @@ struct Ctl {
 constexpr unsigned long long kNone = ~0ull;
 
 // An item that crosses a chunk payload boundary (the 28-byte chunk header sits
-// inside it): copied from logical payload bytes [src, src+len) of the block
-// starting at chunk c0 to side[dst].
+// inside it). Slot = the chunk where the item starts (at most one straddler
+// starts in a chunk and crosses its end): logical payload bytes [src, src+len)
+// of the block starting at chunk c0, item index `item`. k_strad gathers it into
+// side[ck_sbase[slot]] and points item_off[item] there.
 struct StradDesc {
-  unsigned long long c0, src, len, dst;
+  unsigned long long c0, src, len, item;
 };
+
+// blk_meta bit fields
+constexpr unsigned long long kMetaTotalMask = 0xffffffffull;  // chunks of the block (ck_total)
+constexpr int kMetaClsShift = 32;                             // MagicClass (8 bits)
+constexpr unsigned long long kMetaRegular = 1ull << 40;       // every chunk but the last is full
+constexpr unsigned long long kMetaComplete = 1ull << 41;      // all chunks inside the span
 
 // Device arrays of one context (capacities fixed at rio_open, grown on demand).
 struct DevBufs {
@@ -84,15 +93,15 @@ struct DevBufs {
   uint32_t *ck_crc;                                   // computed CRC32 per chunk
   uint32_t *ck_block;            // block index of the chunk (valid in the consistent prefix)
   unsigned long long *ck_pay;    // exclusive prefix of payload sizes (nchunks + 1)
+  unsigned long long *ck_ssz;    // padded size of the straddler starting in the chunk (0: none)
+  unsigned long long *ck_sbase;  // exclusive scan of ck_ssz (nchunks + 1): side offsets
   // per block
   unsigned long long *blk_c0;         // first chunk
-  unsigned long long *blk_nitems;     // item count (0 unless ok)
+  unsigned long long *blk_meta;       // total | class | regular | complete (kMeta*)
+  unsigned long long *blk_len;        // untransformed payload bytes (none codec)
+  unsigned long long *blk_nitems;     // item slots reserved (the header's item count)
   unsigned long long *blk_hdr;        // varint header length
   unsigned long long *blk_item_base;  // exclusive scan of nitems (n + 1)
-  unsigned long long *blk_sb;         // straddler side bytes (padded to 16)
-  unsigned long long *blk_sn;         // straddler count
-  unsigned long long *blk_sb_base;    // exclusive scan of blk_sb (n + 1)
-  unsigned long long *blk_sn_base;    // exclusive scan of blk_sn (n + 1)
   unsigned long long *blk_status;     // BlockStatus
   unsigned long long *blk_a, *blk_b;
   unsigned long long *blk_out_len;    // decoded length (compressed codecs)
@@ -100,7 +109,7 @@ struct DevBufs {
   // outputs: item views into the span or the records buffer (side / dec)
   unsigned long long *item_off, *item_len;
   uint8_t *side;        // straddling items (none codec)
-  StradDesc *strad;     // straddler copy list
+  StradDesc *strad;     // straddler per chunk slot
   // scratch
   unsigned long long *scan_tmp;  // tile partials
   uint8_t *dec;                  // decoded blocks (compressed codecs)
@@ -121,6 +130,8 @@ struct ParseArgs {
   int32_t codec;
   const unsigned long long *nblocks;  // device count
   uint64_t item_cap, side_cap;
+  int32_t sparse;  // straddlers go to a span-shaped side buffer at their own span offset
+  int32_t pad;
 };
 struct CrcArgs {
   int32_t flags;  // measurement-only ablations (RIO_KERNEL_FLAGS): 1 no CRC fold
@@ -135,6 +146,8 @@ struct ResolveArgs {
   int32_t codec;
   const unsigned long long *nblocks;
   uint64_t limit_chunk;  // ChunkScanner.limit in chunks (a partial tail chunk at/after it is never read)
+  int32_t sparse;        // side buffer layout (ParseArgs::sparse)
+  int32_t pad;
 };
 
 // ---- host helpers: GF(2) arithmetic of the reflected CRC-32 polynomial ----

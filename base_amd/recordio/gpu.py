@@ -220,6 +220,43 @@ def batch_items(b: RioBatch) -> List[bytes]:
     return items
 
 
+def _hip():
+    """The process's HIP runtime (the one librio_gpu.so bound: torch's, when imported first)."""
+    return ctypes.CDLL("libamdhip64.so.7")
+
+
+def dev_to_host(ptr: int, nbytes: int) -> bytes:
+    """Copy nbytes of device memory to host (test / tooling helper)."""
+    if nbytes == 0:
+        return b""
+    buf = ctypes.create_string_buffer(nbytes)
+    H = _hip()
+    H.hipDeviceSynchronize()
+    rc = H.hipMemcpy(buf, ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes), 2)  # hipMemcpyDeviceToHost
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy failed: {rc}")
+    return buf.raw
+
+
+def device_batch_items(b: RioBatch, span_host: bytes) -> List[bytes]:
+    """Items of a device batch (rio_scan_device) as bytes; span_host is the span's host copy."""
+    import numpy as np
+    n = int(b.n_items)
+    if n == 0:
+        return []
+    off = np.frombuffer(dev_to_host(ctypes.cast(b.item_off, ctypes.c_void_p).value, 8 * n), dtype=np.uint64)
+    ln = np.frombuffer(dev_to_host(ctypes.cast(b.item_len, ctypes.c_void_p).value, 8 * n), dtype=np.uint64)
+    rec = dev_to_host(b.records, int(b.records_len)) if b.records_len else b""
+    out = []
+    for o, k in zip(off.tolist(), ln.tolist()):
+        if o & ITEM_IN_RECORDS:
+            o &= ~ITEM_IN_RECORDS
+            out.append(rec[o:o + k])
+        else:
+            out.append(span_host[o:o + k])
+    return out
+
+
 @dataclasses.dataclass
 class ScannerOpts:
     """scannerv2.go:100-111."""

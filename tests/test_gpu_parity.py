@@ -239,3 +239,21 @@ def test_full_size_c2_property(oracle):
     assert first[0] == 0 and first[-1] == nrec
     assert np.all(np.diff(first.astype(np.int64))[:-1] == 253)
     ctx.close()
+
+
+def test_device_path_views(oracle):
+    """rio_scan_device (device-resident span): item views into the span plus
+    straddlers at their own span offset in the records buffer."""
+    import torch
+    from base_amd.recordio import gpu
+    ctx = gpu.Context(0, max_span_bytes=64 << 20)
+    rng = random.Random(11)
+    for trial in range(10):
+        data, recs = _random_file(rng, "", rng.randrange(1, 2500), rng.choice([10, 300, 5000, 70000]))
+        hdr_chunks = struct.unpack_from("<I", data, 20)[0]
+        body = data[hdr_chunks * 32768:]
+        dev = torch.frombuffer(bytearray(body), dtype=torch.uint8).to("cuda:0")
+        b = ctx.scan_device(dev.data_ptr(), len(body), file_off=hdr_chunks * 32768, is_file_end=True)
+        assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, (trial, b.err.msg)
+        assert gpu.device_batch_items(b, body) == recs, trial
+    ctx.close()
