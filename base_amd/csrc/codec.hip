@@ -1,6 +1,6 @@
 // Compressed-codec stages (flate / zstd) of the span pipeline: sizing of the
-// per-block decompression regions, the decoders, and the gather of decoded
-// records. Decoders live in codec_flate.hip / codec_zstd.hip.
+// per-block decode regions and decoder dispatch (codec_flate.hip). Decoded
+// blocks stay where they were decoded; items are views into them.
 #include <hip/hip_runtime.h>
 #include <inttypes.h>
 #include <stdio.h>
@@ -10,31 +10,20 @@
 
 namespace rio {
 
-enum CodecErr : uint32_t {
-  kCodecCorrupt = 1,      // flate: CorruptInputError(offset)
-  kCodecEof = 2,          // flate: io.ErrUnexpectedEOF
-  kCodecFull = 3,         // region too small (internal: retried with a larger bound)
-  kCodecZstd = 4,         // zstd: error, b = ZSTD error enum
-  kCodecZstdEmpty = 5,    // zstd: empty source
-  kCodecUnsupported = 6,
-};
-
-// per block: decompressed-capacity bound (flate: comp * factor; zstd: frame size)
-__global__ void k_codec_prepare(DevBufs d, const unsigned long long *nblocks_dev, uint64_t nchunks, int codec) {
+// per block: the decode region's size bound (flate: compressed bytes x factor;
+// the exact size is known only after decoding); resets the codec status
+__global__ void k_codec_prepare(DevBufs d, const unsigned long long *nblocks_dev, uint32_t factor) {
   const uint64_t nb = *nblocks_dev;
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t c0 = d.blk_c0[b];
-    const uint64_t total = d.ck_total[c0];
-    uint64_t comp = 0;
-    if (total != 0 && c0 + total <= nchunks) comp = d.ck_pay[c0 + total] - d.ck_pay[c0];
-    d.blk_out_len[b] = (comp * 8 + 4096 + 255) & ~255ull;  // bound, refined by the decoder
+    const unsigned long long comp = (d.blk_meta[b] & kMetaComplete) ? d.blk_len[b] : 0;
+    d.blk_out_len[b] = (comp * factor + 4096 + 255) & ~255ull;
     d.blk_status[b] = kBlkOk;
     d.blk_a[b] = 0;
     d.blk_b[b] = 0;
   }
 }
 
-__global__ void k_codec_stub(DevBufs d, const unsigned long long *nblocks_dev) {
+__global__ void k_codec_unsupported(DevBufs d, const unsigned long long *nblocks_dev) {
   const uint64_t nb = *nblocks_dev;
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
     d.blk_status[b] = kBlkCodec;
@@ -43,25 +32,31 @@ __global__ void k_codec_stub(DevBufs d, const unsigned long long *nblocks_dev) {
   }
 }
 
-void launch_codec_prepare(const uint8_t *span, uint64_t nchunks, const DevBufs &d,
-                          const unsigned long long *nblocks_dev, uint64_t max_blocks, int codec, uint64_t dec_cap,
-                          hipStream_t st) {
-  (void)span;
-  (void)dec_cap;
-  unsigned g = (unsigned)((max_blocks + 255) / 256);
+void launch_block_scan(const unsigned long long *in, unsigned long long *out, unsigned long long *tmp,
+                       const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
+void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
+                    uint64_t nchunks, uint64_t dec_cap, hipStream_t st);
+
+static unsigned grid_blocks(uint64_t n) {
+  uint64_t g = (n + 255) / 256;
   if (g > 1024) g = 1024;
-  hipLaunchKernelGGL(k_codec_prepare, dim3(g ? g : 1), dim3(256), 0, st, d, nblocks_dev, nchunks, codec);
+  return (unsigned)(g ? g : 1);
+}
+
+// decode-region bounds and their offsets (exclusive scan into blk_dec_off)
+void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
+                          uint32_t factor, hipStream_t st) {
+  hipLaunchKernelGGL(k_codec_prepare, dim3(grid_blocks(max_blocks)), dim3(256), 0, st, d, nblocks_dev, factor);
+  launch_block_scan(d.blk_out_len, d.blk_dec_off, d.scan_tmp, nblocks_dev, max_blocks, st);
 }
 
 void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks_dev,
-                         uint64_t max_blocks, int codec, uint64_t dec_cap, int ncu, hipStream_t st) {
-  (void)span;
-  (void)codec;
-  (void)dec_cap;
-  (void)ncu;
-  unsigned g = (unsigned)((max_blocks + 255) / 256);
-  if (g > 1024) g = 1024;
-  hipLaunchKernelGGL(k_codec_stub, dim3(g ? g : 1), dim3(256), 0, st, d, nblocks_dev);
+                         uint64_t max_blocks, uint64_t nchunks, int codec, uint64_t dec_cap, hipStream_t st) {
+  if (codec == RIO_CODEC_FLATE) {
+    launch_inflate(span, d, nblocks_dev, max_blocks, nchunks, dec_cap, st);
+    return;
+  }
+  hipLaunchKernelGGL(k_codec_unsupported, dim3(grid_blocks(max_blocks)), dim3(256), 0, st, d, nblocks_dev);
 }
 
 void codec_error_text(uint64_t code, uint64_t off, uint64_t file_off, rio_error *e) {

@@ -40,11 +40,10 @@ void launch_resolve(const DevBufs &d, const ResolveArgs &a, hipStream_t st);
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
                 hipStream_t st);
 // codec.hip
-void launch_codec_prepare(const uint8_t *span, uint64_t nchunks, const DevBufs &d,
-                          const unsigned long long *nblocks_dev, uint64_t max_blocks, int codec, uint64_t dec_cap,
-                          hipStream_t st);
+void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
+                          uint32_t factor, hipStream_t st);
 void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks_dev,
-                         uint64_t max_blocks, int codec, uint64_t dec_cap, int ncu, hipStream_t st);
+                         uint64_t max_blocks, uint64_t nchunks, int codec, uint64_t dec_cap, hipStream_t st);
 }  // namespace rio
 
 using namespace rio;
@@ -81,6 +80,7 @@ struct rio_ctx {
   bool last_had_dec = false;
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
   uint64_t side_cap = 0, item_cap = 0, dec_cap = 0;
+  uint32_t dec_factor = 8;  // decode-region bound: compressed bytes x this (grown on overflow)
   DevBufs d{};
   unsigned long long *nblocks_dev = nullptr;
   uint8_t *d_span = nullptr;  // staging for host spans (lazy)
@@ -246,9 +246,10 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   HIP_OK(hipEventRecord(c->ev[kEvScans], st));
   c->last_had_dec = false;
   if (codec != RIO_CODEC_NONE && nchunks > 0) {
-    if (ensure_dec(c, c->dec_cap ? c->dec_cap : 4 * (nchunks * (uint64_t)kChunk) + (1 << 20))) return -1;
-    launch_codec_prepare(span, nchunks, d, c->nblocks_dev, max_blocks, codec, c->dec_cap, st);
-    launch_codec_decode(span, d, c->nblocks_dev, max_blocks, codec, c->dec_cap, c->ncu, st);
+    // decode regions: factor x the compressed bytes per block (+4 KiB each)
+    if (ensure_dec(c, (uint64_t)c->dec_factor * nchunks * kChunk + nchunks * 4352ull)) return -1;
+    launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
+    launch_codec_decode(span, d, c->nblocks_dev, max_blocks, nchunks, codec, c->dec_cap, st);
     c->last_had_dec = true;
   }
   HIP_OK(hipEventRecord(c->ev[kEvDec], st));
@@ -382,7 +383,7 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
     HIP_OK(hipStreamSynchronize(c->st));
     if (c->h_ctl->out_overflow == 0) break;
     if (grow_for_overflow(c, codec)) return -1;
-    if (codec != RIO_CODEC_NONE && (c->h_ctl->out_overflow & 8) && ensure_dec(c, c->dec_cap * 2)) return -1;
+    if (codec != RIO_CODEC_NONE && (c->h_ctl->out_overflow & 8)) c->dec_factor *= 4;
   }
   float ms = 0;
   hipEventElapsedTime(&ms, c->ev[kEvStart], c->ev[kEvEnd]);

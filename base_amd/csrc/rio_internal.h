@@ -41,6 +41,17 @@ enum BlockStatus : uint32_t {
   kBlkSlow = 10,       // (internal) header left to the general parser, k_parse_slow
 };
 
+// blk_a of a kBlkCodec block (codec.hip: codec_error_text)
+enum CodecErr : uint32_t {
+  kCodecCorrupt = 1,      // flate: CorruptInputError(offset = blk_b)
+  kCodecEof = 2,          // flate: io.ErrUnexpectedEOF
+  kCodecFull = 3,         // output region too small (internal: retried with a larger bound)
+  kCodecZstd = 4,         // zstd: error, blk_b = ZSTD error enum
+  kCodecZstdEmpty = 5,    // zstd: empty source
+  kCodecUnsupported = 6,
+  kCodecPending = 255,    // (internal) left to k_inflate_exact
+};
+
 enum Mode : int32_t { kModeBody = 0, kModeHeader = 1, kModeTrailer = 2, kModeLastChunk = 3 };
 
 // Control block written by the kernels, read back by the host (one copy).

@@ -1,0 +1,81 @@
+"""Multi-GPU scan: one process per GPU, independent shards.
+
+Recordio blocks are independent (per-chunk CRC, no cross-block state), so a file
+is split with the reference's own shard math -- NewShardScanner(start, limit,
+nshard) -> ChunkScanner.LimitShard (recordio/scannerv2.go:211-235,
+recordio/internal/chunk.go:198-236) -- with nshard = world * k and rank r taking
+shards [r*k, (r+1)*k). Every rank decodes its shard on its own GPU; no record
+bytes move between GPUs. The one exchange step is the ordered-output prefix: an
+all_gather of (n_items, n_bytes) per rank, so each rank knows where its records
+land in the file-order result. Many files (config C5) are assigned to ranks by
+size-balanced greedy assignment instead.
+"""
+from __future__ import annotations
+
+import heapq
+from typing import Callable, List, Sequence, Tuple
+
+
+def rank_shard(rank: int, world: int, k: int = 1) -> Tuple[int, int, int]:
+    """(start, limit, nshard) of rank `rank` for NewShardScanner."""
+    if not 0 <= rank < world or k < 1:
+        raise ValueError(f"invalid rank {rank} of {world} (k={k})")
+    return rank * k, (rank + 1) * k, world * k
+
+
+def assign_files(sizes: Sequence[int], world: int) -> List[List[int]]:
+    """Greedy size-balanced assignment of files to ranks (largest first)."""
+    heap = [(0, r) for r in range(world)]
+    out: List[List[int]] = [[] for _ in range(world)]
+    for i in sorted(range(len(sizes)), key=lambda i: (-sizes[i], i)):
+        load, r = heapq.heappop(heap)
+        out[r].append(i)
+        heapq.heappush(heap, (load + sizes[i], r))
+    for files in out:
+        files.sort()
+    return out
+
+
+def ordered_prefix(n_items: int, n_bytes: int, group=None):
+    """All-gather (n_items, n_bytes) of every rank; returns this rank's exclusive
+    (item_offset, byte_offset) and the totals. The backend's collective (RCCL over
+    xGMI for "nccl", gloo on CPU) moves 16 B per rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = "cpu"
+    if dist.get_backend(group) == "nccl":
+        dev = f"cuda:{torch.cuda.current_device()}"
+    mine = torch.tensor([n_items, n_bytes], dtype=torch.int64, device=dev)
+    allv = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(allv, mine, group=group)
+    vals = [tuple(int(x) for x in t.cpu().tolist()) for t in allv]
+    item_off = sum(v[0] for v in vals[:rank])
+    byte_off = sum(v[1] for v in vals[:rank])
+    return item_off, byte_off, sum(v[0] for v in vals), sum(v[1] for v in vals)
+
+
+def scan_rank(data, rank: int, world: int, k: int = 1,
+              scan: Callable = None, group=None):
+    """Decode this rank's shard of one file and place it in file order.
+
+    scan(data, start, limit, nshard) -> list of record bytes; by default the GPU
+    scanner (gpu.NewShardScanner on this rank's device). Returns (records,
+    item_offset, total_items)."""
+    start, limit, nshard = rank_shard(rank, world, k)
+    if scan is None:
+        from base_amd.recordio import gpu
+
+        def scan(d, s, l, n):
+            sc = gpu.NewShardScanner(d, gpu.ScannerOpts(), s, l, n)
+            out = []
+            while sc.Scan():
+                out.append(sc.Get())
+            err = sc.Finish()
+            if err is not None:
+                raise err
+            return out
+    recs = scan(data, start, limit, nshard)
+    off, _, total, _ = ordered_prefix(len(recs), sum(len(r) for r in recs), group)
+    return recs, off, total

@@ -1,0 +1,103 @@
+"""Flate workload (BASELINE.json configs[2]) on one MI355X.
+
+A FASTQ-like flate recordio file (tools/c3_data.py; 1024 records per block) is
+built on the host, copied to HBM and its body replicated to ~10 GiB of records;
+one step = the scan pipeline over the whole device-resident span (chunk CRC +
+DEFLATE decode + packed unpack). Parity: the base file's items (device path)
+against the generator's records. Prints one JSON line.
+
+  python tools/bench_flate.py [--base-mib 128] [--replicas 80] [--steps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--base-mib", type=int, default=128)
+    ap.add_argument("--replicas", type=int, default=80)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--per-block", type=int, default=1024)
+    args = ap.parse_args()
+
+    import torch
+    import c3_data
+    from base_amd.recordio import gpu
+
+    t0 = time.perf_counter()
+    data, nrec, rec_bytes = c3_data.make_file(args.base_mib << 20, args.per_block, workers=16)
+    gen_s = time.perf_counter() - t0
+    CH = 32768
+    body = data[CH:]
+    total = CH + args.replicas * len(body)
+    dev = torch.empty(total, dtype=torch.uint8, device="cuda:0")
+    dev[:len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    for r in range(1, args.replicas):
+        dev[CH + r * len(body):CH + (r + 1) * len(body)].copy_(dev[CH:len(data)])
+    torch.cuda.synchronize()
+
+    # parity on the base file (device path, views into the decoded blocks)
+    ctx1 = gpu.Context(0, max_span_bytes=len(body) + CH)
+    b = ctx1.scan_device(dev.data_ptr() + CH, len(body), file_off=CH, is_file_end=True, codec=gpu.RIO_CODEC_FLATE)
+    assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
+    items = gpu.device_batch_items(b, body)
+    h_got = hashlib.sha256(b"".join(items)).hexdigest()
+    want = []
+    for first in range(0, nrec, args.per_block):
+        want.extend(c3_data.records(first, min(args.per_block, nrec - first)))
+    h_want = hashlib.sha256(b"".join(want)).hexdigest()
+    parity = (len(items) == nrec and h_got == h_want and [len(x) for x in items] == [len(x) for x in want])
+    ctx1.close()
+
+    span_len = total - CH
+    ctx = gpu.Context(0, max_span_bytes=total, max_items=nrec * args.replicas + 1024)
+    ptr = dev.data_ptr() + CH
+
+    def step():
+        ctx.scan_device_async(ptr, span_len, CH, gpu.RIO_CODEC_FLATE)
+        return ctx.sync()
+
+    bb = step()
+    assert bb.stop == gpu.RIO_STOP_EOF and bb.err.code == 0, bb.err.msg
+    assert bb.n_items == nrec * args.replicas
+    for _ in range(args.warmup):
+        step()
+    stages = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        stages.append(ctx.stage_times())
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    import numpy as np
+    st = np.mean(np.array(stages), axis=0)
+    out_bytes = rec_bytes * args.replicas
+    print(json.dumps({
+        "metric": "recordio scan GiB/s device-resident (compressed in), flate",
+        "value": round(span_len / dt / 2 ** 30, 2), "unit": "GiB/s",
+        "out_GiBs": round(out_bytes / dt / 2 ** 30, 2),
+        "ms_per_step": round(dt * 1e3, 3),
+        "stage_ms": {"parse": round(st[0], 3), "decode": round(st[1], 3), "crc": round(st[2], 3),
+                     "meta": round(st[3], 3), "total": round(st[4], 3)},
+        "decode_in_GiBs": round(span_len / (st[1] * 1e-3) / 2 ** 30, 2) if st[1] > 0 else None,
+        "config": {"workload": "C3-like flate FASTQ, %d records/block" % args.per_block,
+                   "base_file_bytes": len(data), "base_records": nrec, "base_record_bytes": rec_bytes,
+                   "replicas": args.replicas, "span_bytes": span_len, "gen_s": round(gen_s, 1)},
+        "parity": parity}), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
