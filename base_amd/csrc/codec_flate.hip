@@ -224,8 +224,8 @@ __device__ void fixed_lens(uint8_t *l) {
 __device__ const uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // lane 0 only; tables in lds (clobbered)
-__device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32_t &err,
-                                                        uint64_t &err_off) {
+__device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32_t &err, uint64_t &err_off,
+                              uint64_t &olen) {
   Exact s{&in, 0, 0, 0, 0, cap, 0, 0};
   bool fixed_built = false;
   for (;;) {
@@ -429,6 +429,7 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
   }
   err = s.err;
   err_off = s.err_off;
+  olen = s.olen;
 }
 
 // ---------------------------------------------------------------- fast mode
@@ -760,9 +761,7 @@ __global__ void __launch_bounds__(64 * kInflWaves) k_inflate(const uint8_t *__re
     f.stage(0);
     const int err = inflate_fast(f);
     if (l == 0) {
-      if (err == kCodecFull) {
-        atomicOr(&d.ctl->out_overflow, 8ull);
-      } else if (err) {  // k_inflate_exact classifies it with Go's lazy byte pulls
+      if (err) {  // k_inflate_exact classifies it (Go's lazy byte pulls) or sizes it
         d.blk_status[b] = kBlkCodec;
         d.blk_a[b] = kCodecPending;
         d.blk_b[b] = (unsigned long long)err;
@@ -797,9 +796,17 @@ __global__ void __launch_bounds__(64) k_inflate_exact(const uint8_t *__restrict_
         in.pay0 = d.ck_pay[in.c0];
         in.regular = (meta & kMetaRegular) != 0;
         uint32_t e = 0;
-        uint64_t eo = 0;
-        inflate_exact(in, L, ~0ull >> 1, e, eo);
-        if (e == 0 || e == kCodecFull) e = kCodecCorrupt;  // fast and exact disagree: never pass silently
+        uint64_t eo = 0, olen = 0;
+        inflate_exact(in, L, ~0ull >> 1, e, eo, olen);
+        if (e == 0 && d.blk_b[b] == kCodecFull) {
+          // a valid stream larger than its decode region: ask for a larger factor
+          const unsigned long long comp = in.n ? in.n : 1;
+          atomicMax(&d.ctl->dec_factor_need, olen / comp + 2);
+          atomicOr(&d.ctl->out_overflow, 8ull);
+          e = kCodecFull;
+        } else if (e == 0 || e == kCodecFull) {
+          e = kCodecCorrupt;  // fast and exact disagree: never pass silently
+        }
         d.blk_a[b] = e;
         d.blk_b[b] = eo;
       }

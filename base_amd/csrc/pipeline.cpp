@@ -236,7 +236,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   HIP_OK(hipEventRecord(c->ev[kEvStart], st));
   // control words are min-reduced: reset to ~0 (out_overflow to 0)
   HIP_OK(hipMemsetAsync(d.ctl, 0xff, 4 * sizeof(unsigned long long), st));
-  HIP_OK(hipMemsetAsync(&d.ctl->out_overflow, 0, sizeof(unsigned long long), st));
+  HIP_OK(hipMemsetAsync(&d.ctl->out_overflow, 0, 2 * sizeof(unsigned long long), st));  // + dec_factor_need
   HIP_OK(hipMemsetAsync(c->nblocks_dev, 0, 2 * sizeof(unsigned long long), st));
   const uint64_t max_blocks = nchunks ? nchunks : 1;
   if (nchunks > 0) {
@@ -363,6 +363,28 @@ static int grow_for_overflow(rio_ctx *c, int32_t codec) {
   return 0;
 }
 
+// RIO_DEBUG=1: per-block state of the last run on stderr (development aid)
+static void debug_dump(rio_ctx *c) {
+  unsigned long long nb = 0;
+  hipMemcpy(&nb, c->nblocks_dev, 8, hipMemcpyDeviceToHost);
+  const uint64_t k = nb < 16 ? nb : 16;
+  std::vector<unsigned long long> a(k), st(k), ol(k), bl(k), me(k), doff(k), ni(k), ib(k);
+  if (k) {
+    hipMemcpy(a.data(), c->d.blk_c0, 8 * k, hipMemcpyDeviceToHost);
+    hipMemcpy(st.data(), c->d.blk_status, 8 * k, hipMemcpyDeviceToHost);
+    hipMemcpy(ol.data(), c->d.blk_out_len, 8 * k, hipMemcpyDeviceToHost);
+    hipMemcpy(bl.data(), c->d.blk_len, 8 * k, hipMemcpyDeviceToHost);
+    hipMemcpy(me.data(), c->d.blk_meta, 8 * k, hipMemcpyDeviceToHost);
+    hipMemcpy(doff.data(), c->d.blk_dec_off, 8 * k, hipMemcpyDeviceToHost);
+    hipMemcpy(ni.data(), c->d.blk_nitems, 8 * k, hipMemcpyDeviceToHost);
+    hipMemcpy(ib.data(), c->d.blk_item_base, 8 * k, hipMemcpyDeviceToHost);
+  }
+  fprintf(stderr, "rio debug: nblocks=%llu overflow=%llu\n", nb, (unsigned long long)c->h_ctl->out_overflow);
+  for (uint64_t b = 0; b < k; b++)
+    fprintf(stderr, "  blk %llu c0=%llu status=%llu meta=%llx len=%llu out_len=%llu dec_off=%llu nitems=%llu base=%llu\n",
+            (unsigned long long)b, a[b], st[b], me[b], bl[b], ol[b], doff[b], ni[b], ib[b]);
+}
+
 static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span, uint64_t nbytes,
                     uint64_t file_off, int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode,
                     bool to_host, rio_batch *out) {
@@ -383,8 +405,12 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
     HIP_OK(hipStreamSynchronize(c->st));
     if (c->h_ctl->out_overflow == 0) break;
     if (grow_for_overflow(c, codec)) return -1;
-    if (codec != RIO_CODEC_NONE && (c->h_ctl->out_overflow & 8)) c->dec_factor *= 4;
+    if (codec != RIO_CODEC_NONE && (c->h_ctl->out_overflow & 8)) {
+      const unsigned long long need = c->h_ctl->dec_factor_need;
+      c->dec_factor = (uint32_t)(need > 4ull * c->dec_factor ? need : 4ull * c->dec_factor);
+    }
   }
+  if (getenv("RIO_DEBUG")) debug_dump(c);
   float ms = 0;
   hipEventElapsedTime(&ms, c->ev[kEvStart], c->ev[kEvEnd]);
   if (collect(c, report_span, file_off, codec, mode, nbytes, out, to_host)) return -1;

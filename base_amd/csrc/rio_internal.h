@@ -61,7 +61,8 @@ struct Ctl {
   unsigned long long first_block_event;  // min over block event keys (2*chunk + 1 / 2*c0)
   unsigned long long first_incomplete;   // min c0 of a block extending past the span
   unsigned long long out_overflow;       // nonzero if side/items exceeded capacity
-  unsigned long long pad[3];
+  unsigned long long dec_factor_need;    // max over blocks of decoded/compressed + 1 (decode overflow)
+  unsigned long long pad[2];
   // filled by k_resolve
   unsigned long long stop_key;
   unsigned long long n_valid_blocks;

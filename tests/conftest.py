@@ -14,6 +14,11 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the C ABI on the GPU)")
     config.addinivalue_line("markers", "slow: long-running")
+    # torch ships its own libamdhip64.so.7: load it before librio_gpu.so so that
+    # one HIP runtime serves both (tests that hand torch device buffers to the ABI)
+    markexpr = getattr(config.option, "markexpr", "") or ""
+    if "gpu" in markexpr and "not gpu" not in markexpr:
+        import torch  # noqa: F401
 
 
 @pytest.fixture(scope="session")
