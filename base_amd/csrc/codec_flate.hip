@@ -543,7 +543,7 @@ struct Fast {
     const int l = lane_id();
     uint32_t done = 0;
     while (done < len) {
-      if (pos + 64 > base + kInBuf) stage(pos);
+      if (pos < base || pos + 64 > base + kInBuf) stage(pos);
       const uint32_t n = (len - done) < 64u ? (len - done) : 64u;
       const uint32_t room = (uint32_t)(kUnit - (olen & (kUnit - 1)));
       const uint32_t m = n < room ? n : room;
@@ -574,7 +574,8 @@ __device__ int inflate_fast(Fast &f) {
       f.nb = 0;
       f.bitbuf = 0;
       if (f.pos + 4 > f.in->n) return kCodecEof;
-      if (f.pos + 4 > f.base + kInBuf) f.stage(f.pos);
+      // the bytes given back may precede the staged window
+      if (f.pos < f.base || f.pos + 4 > f.base + kInBuf) f.stage(f.pos);
       const uint32_t o = (uint32_t)(f.pos - f.base);
       const uint32_t len = L.in[o] | ((uint32_t)L.in[o + 1] << 8);
       const uint32_t nlen = L.in[o + 2] | ((uint32_t)L.in[o + 3] << 8);
@@ -765,6 +766,7 @@ __global__ void __launch_bounds__(64 * kInflWaves) k_inflate(const uint8_t *__re
         d.blk_status[b] = kBlkCodec;
         d.blk_a[b] = kCodecPending;
         d.blk_b[b] = (unsigned long long)err;
+        d.blk_hdr[b] = f.olen | ((unsigned long long)f.pos << 32);  // where the fast pass stopped (debug)
       }
       d.blk_out_len[b] = err ? 0 : f.olen;
     }

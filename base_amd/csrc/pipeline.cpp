@@ -367,22 +367,31 @@ static int grow_for_overflow(rio_ctx *c, int32_t codec) {
 static void debug_dump(rio_ctx *c) {
   unsigned long long nb = 0;
   hipMemcpy(&nb, c->nblocks_dev, 8, hipMemcpyDeviceToHost);
-  const uint64_t k = nb < 16 ? nb : 16;
-  std::vector<unsigned long long> a(k), st(k), ol(k), bl(k), me(k), doff(k), ni(k), ib(k);
-  if (k) {
-    hipMemcpy(a.data(), c->d.blk_c0, 8 * k, hipMemcpyDeviceToHost);
-    hipMemcpy(st.data(), c->d.blk_status, 8 * k, hipMemcpyDeviceToHost);
-    hipMemcpy(ol.data(), c->d.blk_out_len, 8 * k, hipMemcpyDeviceToHost);
-    hipMemcpy(bl.data(), c->d.blk_len, 8 * k, hipMemcpyDeviceToHost);
-    hipMemcpy(me.data(), c->d.blk_meta, 8 * k, hipMemcpyDeviceToHost);
-    hipMemcpy(doff.data(), c->d.blk_dec_off, 8 * k, hipMemcpyDeviceToHost);
-    hipMemcpy(ni.data(), c->d.blk_nitems, 8 * k, hipMemcpyDeviceToHost);
-    hipMemcpy(ib.data(), c->d.blk_item_base, 8 * k, hipMemcpyDeviceToHost);
+  std::vector<unsigned long long> a(nb), st(nb), ol(nb), bl(nb), me(nb), doff(nb), ni(nb), ib(nb), ea(nb), eb(nb),
+      hd(nb);
+  if (nb) {
+    hipMemcpy(a.data(), c->d.blk_c0, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(st.data(), c->d.blk_status, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(ol.data(), c->d.blk_out_len, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(bl.data(), c->d.blk_len, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(me.data(), c->d.blk_meta, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(doff.data(), c->d.blk_dec_off, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(ni.data(), c->d.blk_nitems, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(ib.data(), c->d.blk_item_base, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(ea.data(), c->d.blk_a, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(eb.data(), c->d.blk_b, 8 * nb, hipMemcpyDeviceToHost);
+    hipMemcpy(hd.data(), c->d.blk_hdr, 8 * nb, hipMemcpyDeviceToHost);
   }
   fprintf(stderr, "rio debug: nblocks=%llu overflow=%llu\n", nb, (unsigned long long)c->h_ctl->out_overflow);
-  for (uint64_t b = 0; b < k; b++)
-    fprintf(stderr, "  blk %llu c0=%llu status=%llu meta=%llx len=%llu out_len=%llu dec_off=%llu nitems=%llu base=%llu\n",
-            (unsigned long long)b, a[b], st[b], me[b], bl[b], ol[b], doff[b], ni[b], ib[b]);
+  int shown = 0;
+  for (uint64_t b = 0; b < nb && shown < 24; b++) {
+    if (b >= 4 && st[b] == 0) continue;
+    shown++;
+    fprintf(stderr,
+            "  blk %llu c0=%llu status=%llu meta=%llx len=%llu out_len=%llu dec_off=%llu nitems=%llu base=%llu "
+            "a=%llu b=%llu hdr=%llx\n",
+            (unsigned long long)b, a[b], st[b], me[b], bl[b], ol[b], doff[b], ni[b], ib[b], ea[b], eb[b], hd[b]);
+  }
 }
 
 static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span, uint64_t nbytes,
