@@ -18,7 +18,7 @@ ARCH = os.environ.get("RIO_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["kernels.hip", "blocks.hip", "crc.hip", "codec.hip", "codec_flate.hip", "codec_zstd.hip",
            "pipeline.cpp", "messages.cpp", "scanner.cpp", "crc_tables.cpp"]
-FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
+FLAGS = (["-DRIO_CHECKED"] if os.environ.get("RIO_CHECKED") else []) + ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
          "-I", CSRC, "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result"]
 
 
@@ -38,6 +38,15 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     headers.append(os.path.join(ROOT, "include", "rio_gpu.h"))
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    # a change of compile flags (RIO_CHECKED, arch) rebuilds every object
+    stamp = os.path.join(OUT_DIR, "obj", ".flags")
+    flags_now = " ".join(FLAGS)
+    if not os.path.exists(stamp) or open(stamp).read() != flags_now:
+        for s in srcs:
+            if os.path.exists(_obj(s)):
+                os.remove(_obj(s))
+        with open(stamp, "w") as f:
+            f.write(flags_now)
 
     def compile_one(src):
         path = os.path.join(CSRC, src)

@@ -74,6 +74,12 @@ __global__ void __launch_bounds__(256) k_parse(DevBufs d, ParseArgs a) {
       if (a.codec != RIO_CODEC_NONE) {
         const uint64_t b = b0 + j;
         if (p + 16 <= lens[j]) {
+#ifdef RIO_CHECKED
+          if (d.blk_dec_off[b] + p + 16 > d.dec_cap) {
+            atomicOr(&d.ctl->out_overflow, 0x1000ull);
+            continue;
+          }
+#endif
           const uint4 v = *reinterpret_cast<const uint4 *>(d.dec + d.blk_dec_off[b] + p);
           win[j][0] = v.x;
           win[j][1] = v.y;
@@ -218,6 +224,13 @@ __global__ void __launch_bounds__(256) k_dec_nitems(DevBufs d, const unsigned lo
     unsigned long long v = 0, res = 0;
     const unsigned long long len = d.blk_out_len[b];
     if (d.blk_status[b] != kBlkCodec) {
+#ifdef RIO_CHECKED
+      if (d.blk_dec_off[b] + (len < 10 ? len : 10) > d.dec_cap) {
+        atomicOr(&d.ctl->out_overflow, 0x2000ull);
+        d.blk_nitems[b] = 0;
+        continue;
+      }
+#endif
       const uint8_t *p = d.dec + d.blk_dec_off[b];
       for (int k = 0; k < 10 && (unsigned long long)k < len; k++) {
         const uint32_t c = p[k];

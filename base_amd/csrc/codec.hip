@@ -16,7 +16,9 @@ __global__ void k_codec_prepare(DevBufs d, const unsigned long long *nblocks_dev
   const uint64_t nb = *nblocks_dev;
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
     const unsigned long long comp = (d.blk_meta[b] & kMetaComplete) ? d.blk_len[b] : 0;
-    d.blk_out_len[b] = (comp * factor + 4096 + 255) & ~255ull;
+    unsigned long long bound = comp * factor + 4096;
+    if (d.blk_need[b] > bound) bound = d.blk_need[b];  // exact size from a previous attempt
+    d.blk_out_len[b] = (bound + 255) & ~255ull;
     d.blk_status[b] = kBlkOk;
     d.blk_a[b] = 0;
     d.blk_b[b] = 0;

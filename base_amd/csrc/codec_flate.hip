@@ -28,28 +28,42 @@
 
 namespace rio {
 
-constexpr int kInflWaves = 2;    // waves per workgroup
-constexpr int kInBuf = 2048;     // input staging bytes
-constexpr int kWin = 8192;       // output window ring
+constexpr int kInflWaves = 1;    // waves per workgroup (LDS-bound residency: one wave per workgroup)
+constexpr int kInBuf = 1024;     // input staging bytes
+#ifndef RIO_INFL_WIN
+#define RIO_INFL_WIN 8192
+#endif
+constexpr int kWin = RIO_INFL_WIN;  // output window ring
 constexpr int kUnit = 1024;      // flush granule
-constexpr int kFastBits = 10;
+constexpr int kLitBits = 10;     // root table bits: literal/length
+constexpr int kDistBits = 8;     // root table bits: distance (and code-length codes)
 constexpr int kMaxBits = 15;
 
 struct HuffT {
   uint16_t count[kMaxBits + 1];
-  uint16_t sym[320];
-  uint16_t fast[1 << kFastBits];  // (len << 9) | sym for codes <= kFastBits, 0: longer code
+  uint16_t sym[288];
   int32_t min, max, empty, ok;
 };
 
 struct InflLds {
   uint8_t win[kWin];
-  uint8_t in[kInBuf + 8];
-  HuffT lit, dist, clen;
+  uint32_t in32[kInBuf / 4 + 4];  // staged compressed bytes
+  uint16_t lfast[1 << kLitBits];  // (len << 9) | sym for codes <= kLitBits, 0: longer code
+  uint16_t dfast[1 << kDistBits];
+  HuffT lit, dist;                // code-length codes are decoded through `dist` / dfast
   uint8_t lens[320];
   uint8_t cl[20];
   uint16_t offs[kMaxBits + 2];
 };
+
+// wave-uniform value (LDS loads are per lane; this makes them scalar)
+// (the builtin returns int: widen through uint32_t, never sign-extend)
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+  return ((uint64_t)hi << 32) | lo;
+}
 
 // ---------------------------------------------------------------- tables
 __device__ __forceinline__ uint32_t rev_bits(uint32_t code, int len) { return __brev(code) >> (32 - len); }
@@ -57,7 +71,8 @@ __device__ __forceinline__ uint32_t rev_bits(uint32_t code, int len) { return __
 // huffmanDecoder.init semantics (Go inflate.go): a code set must be complete,
 // except the degenerate single code of length 1; all-zero lengths = empty tree.
 // Built by lane 0 (a few thousand cycles per DEFLATE block).
-__device__ __attribute__((noinline)) void huff_build(HuffT &h, const uint8_t *lens, int n, uint16_t *offs) {
+__device__ __attribute__((noinline)) void huff_build(HuffT &h, const uint8_t *lens, int n, uint16_t *offs,
+                                                     uint16_t *fast, int fbits) {
   for (int i = 0; i <= kMaxBits; i++) h.count[i] = 0;
   int mn = 0, mx = 0;
   for (int i = 0; i < n; i++) {
@@ -82,13 +97,13 @@ __device__ __attribute__((noinline)) void huff_build(HuffT &h, const uint8_t *le
   for (int l = 1; l <= kMaxBits; l++) offs[l + 1] = offs[l] + h.count[l];
   for (int i = 0; i < n; i++)
     if (lens[i]) h.sym[offs[lens[i]]++] = (uint16_t)i;
-  for (int i = 0; i < (1 << kFastBits); i++) h.fast[i] = 0;
+  for (int i = 0; i < (1 << fbits); i++) fast[i] = 0;
   int next = 0, k = 0;
   for (int l = 1; l <= kMaxBits; l++) {
     for (int j = 0; j < h.count[l]; j++, k++) {
-      if (l <= kFastBits) {
+      if (l <= fbits) {
         const uint32_t r = rev_bits((uint32_t)(next + j), l);
-        for (uint32_t f = r; f < (1u << kFastBits); f += (1u << l)) h.fast[f] = (uint16_t)((l << 9) | h.sym[k]);
+        for (uint32_t f = r; f < (1u << fbits); f += (1u << l)) fast[f] = (uint16_t)((l << 9) | h.sym[k]);
       }
     }
     next = (next + h.count[l]) << 1;
@@ -118,6 +133,8 @@ __device__ __forceinline__ int huff_slow(const HuffT &h, uint32_t bits, int &len
 // Logical compressed bytes [0, n): the block's chunk payloads back to back.
 struct CompIn {
   const uint8_t *span;
+  uint64_t span_bytes;            // RIO_CHECKED bounds
+  unsigned long long *flag;       // RIO_CHECKED violation flags (ctl->out_overflow)
   const uint32_t *ck_size;
   const unsigned long long *ck_pay;
   uint64_t c0, total, n, pay0;
@@ -141,7 +158,17 @@ struct CompIn {
     }
     return c * kChunk + kChunkHdr + (p - lo);
   }
-  __device__ __forceinline__ uint32_t byte(uint64_t p) const { return p < n ? span[phys(p)] : 0u; }
+  __device__ __forceinline__ uint32_t byte(uint64_t p) const {
+    if (p >= n) return 0u;
+    const uint64_t q = phys(p);
+#ifdef RIO_CHECKED
+    if (q >= span_bytes) {
+      atomicOr(flag, 0x100ull);
+      return 0u;
+    }
+#endif
+    return span[q];
+  }
 };
 
 // ---------------------------------------------------------------- exact mode
@@ -182,7 +209,7 @@ struct Exact {
       err_off = pos;
     }
   }
-  __device__ int sym(const HuffT &h) {
+  __device__ int sym(const HuffT &h, const uint16_t *fast, int fbits) {
     if (h.empty) {
       if (!need(h.min)) return -1;
       corrupt();
@@ -194,7 +221,7 @@ struct Exact {
       const int avail = nb < kMaxBits ? nb : kMaxBits;
       const uint32_t bits = (uint32_t)(bitbuf & ((1u << avail) - 1));
       int len = 0, s = -1;
-      const uint16_t e = h.fast[bits & ((1u << kFastBits) - 1)];
+      const uint16_t e = fast[bits & ((1u << fbits) - 1)];
       if (e && (e >> 9) <= avail) {
         len = e >> 9;
         s = e & 511;
@@ -263,7 +290,7 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
       if (type == 1) {
         if (!fixed_built) {
           fixed_lens(L.lens);
-          huff_build(L.lit, L.lens, 288, L.offs);
+          huff_build(L.lit, L.lens, 288, L.offs, L.lfast, kLitBits);
         }
         fixed_built = true;
       } else {
@@ -290,15 +317,15 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
           L.cl[kClenOrder[i]] = (uint8_t)s.take(3);
         }
         if (!okc) break;
-        huff_build(L.clen, L.cl, 19, L.offs);
-        if (!L.clen.ok) {
+        huff_build(L.dist, L.cl, 19, L.offs, L.dfast, kDistBits);  // code-length code
+        if (!L.dist.ok) {
           s.corrupt();
           break;
         }
         const int n = nlit + ndist;
         int i = 0;
         while (i < n) {
-          const int x = s.sym(L.clen);
+          const int x = s.sym(L.dist, L.dfast, kDistBits);
           if (x < 0) break;
           if (x < 16) {
             L.lens[i++] = (uint8_t)x;
@@ -331,8 +358,8 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
           for (int j = 0; j < rep; j++) L.lens[i++] = (uint8_t)b;
         }
         if (s.err || i < n) break;
-        huff_build(L.lit, L.lens, nlit, L.offs);
-        huff_build(L.dist, L.lens + nlit, ndist, L.offs);
+        huff_build(L.lit, L.lens, nlit, L.offs, L.lfast, kLitBits);
+        huff_build(L.dist, L.lens + nlit, ndist, L.offs, L.dfast, kDistBits);
         if (!L.lit.ok || !L.dist.ok) {
           s.corrupt();
           break;
@@ -342,7 +369,7 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
       }
       // huffmanBlock
       for (;;) {
-        const int v = s.sym(*hl);
+        const int v = s.sym(*hl, L.lfast, kLitBits);
         if (v < 0) {
           ok = false;
           break;
@@ -385,7 +412,7 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
           }
           dist = (int)rev_bits(s.take(5), 5);
         } else {
-          dist = s.sym(*hd);
+          dist = s.sym(*hd, L.dfast, kDistBits);
           if (dist < 0) {
             ok = false;
             break;
@@ -433,33 +460,41 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
 }
 
 // ---------------------------------------------------------------- fast mode
+// Decoder state is wave-uniform: every value read from LDS goes through uni()
+// (v_readfirstlane), so the bit reader and the Huffman walk run on the scalar
+// unit; the vector lanes do the wave-parallel parts (staging, LZ77 copies,
+// flushes).
 struct Fast {
   const CompIn *in;
   InflLds *L;
   uint8_t *out;      // the block's decode region in HBM
   uint64_t cap;
-  uint64_t base;     // logical offset of L->in[0]
+  uint64_t out_room; // RIO_CHECKED: bytes addressable from out
+  uint64_t base;     // logical offset of the staged bytes (multiple of 4)
   uint64_t pos;      // next logical byte for the bit buffer
   uint64_t bitbuf;
   int nb;
   uint64_t olen, flushed;
-  int err;
 
-  // stage logical bytes [b, b + kInBuf) into LDS, all lanes
+  // stage logical bytes [b & ~3, + kInBuf + 16) into LDS, all lanes
   __device__ void stage(uint64_t b) {
     const int l = lane_id();
+    base = b & ~3ull;
     wave_lds_sync();
-#pragma unroll 4
-    for (int k = l; k < kInBuf + 8; k += 64) L->in[k] = (uint8_t)in->byte(b + k);
-    base = b;
+    uint8_t *dst = reinterpret_cast<uint8_t *>(L->in32);
+    for (int k = l; k < kInBuf + 16; k += 64) dst[k] = (uint8_t)in->byte(base + k);
     wave_lds_sync();
+  }
+  __device__ __forceinline__ uint32_t in_byte(uint64_t p) {
+    const uint32_t o = (uint32_t)(p - base);
+    return (uni(L->in32[o >> 2]) >> (8 * (o & 3))) & 0xffu;
   }
   __device__ __forceinline__ void refill() {
     if (nb > 32) return;
-    if (pos + 4 > base + kInBuf) stage(pos);
+    if (pos < base || pos + 8 > base + kInBuf) stage(pos);
     const uint32_t o = (uint32_t)(pos - base);
-    const uint32_t w = (uint32_t)L->in[o] | ((uint32_t)L->in[o + 1] << 8) | ((uint32_t)L->in[o + 2] << 16) |
-                       ((uint32_t)L->in[o + 3] << 24);
+    const uint32_t d0 = uni(L->in32[o >> 2]), d1 = uni(L->in32[(o >> 2) + 1]);
+    const uint32_t w = (uint32_t)((((uint64_t)d1 << 32) | d0) >> (8 * (o & 3)));
     bitbuf |= (uint64_t)w << nb;
     nb += 32;
     pos += 4;
@@ -472,15 +507,30 @@ struct Fast {
   }
   // bits consumed past the end of the input: the stream is truncated
   __device__ __forceinline__ bool overrun() const { return 8 * pos - (uint64_t)nb > 8 * in->n; }
-  __device__ __forceinline__ int sym(const HuffT &h) {
+  __device__ __forceinline__ int sym(const HuffT &h, const uint16_t *fast, int fbits) {
     const uint32_t bits = (uint32_t)bitbuf;
-    const uint16_t e = h.fast[bits & ((1u << kFastBits) - 1)];
+    const uint32_t e = uni(fast[bits & ((1u << fbits) - 1)]);
     int len, s;
     if (e) {
-      len = e >> 9;
-      s = e & 511;
-    } else {
-      s = huff_slow(h, bits, len);
+      len = (int)(e >> 9);
+      s = (int)(e & 511);
+    } else {  // canonical walk for codes longer than the root table
+      int code = 0, first = 0, index = 0;
+      s = -1;
+      len = 0;
+      for (int l = 1; l <= kMaxBits; l++) {
+        code |= (int)((bits >> (l - 1)) & 1u);
+        const int cnt = (int)uni(h.count[l]);
+        if (code - cnt < first) {
+          len = l;
+          s = (int)uni(h.sym[index + (code - first)]);
+          break;
+        }
+        index += cnt;
+        first += cnt;
+        first <<= 1;
+        code <<= 1;
+      }
       if (s < 0) return -1;
     }
     take(len);
@@ -489,21 +539,33 @@ struct Fast {
   // write completed flush units [flushed, olen rounded down) to HBM
   __device__ void flush_units() {
     const int l = lane_id();
+    if (olen - flushed < (uint64_t)kUnit) return;
+    wave_lds_sync();
     while (olen - flushed >= (uint64_t)kUnit) {
-      wave_lds_sync();
       const uint32_t r = (uint32_t)(flushed & (kWin - 1));
       const uint4 v = *reinterpret_cast<const uint4 *>(L->win + r + 16 * l);
+#ifdef RIO_CHECKED
+      if (flushed + 16 * l + 16 > out_room) {
+        atomicOr(in->flag, 0x200ull);
+      } else
+#endif
       *reinterpret_cast<uint4 *>(out + flushed + 16 * l) = v;
       flushed += kUnit;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   __device__ void flush_tail() {
     flush_units();
     wave_lds_sync();
     const int l = lane_id();
-    for (uint64_t k = flushed + l; k < olen; k += 64) out[k] = L->win[k & (kWin - 1)];
+    for (uint64_t k = flushed + l; k < olen; k += 64) {
+#ifdef RIO_CHECKED
+      if (k >= out_room) {
+        atomicOr(in->flag, 0x400ull);
+        continue;
+      }
+#endif
+      out[k] = L->win[k & (kWin - 1)];
+    }
     flushed = olen;
   }
   __device__ __forceinline__ void literal(uint32_t v) {
@@ -527,10 +589,18 @@ struct Fast {
         if (k < length) L->win[(olen + k) & (kWin - 1)] = v;
       }
     } else {  // older than the ring: the flushed bytes in HBM
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       for (uint32_t k0 = 0; k0 < length; k0 += 64) {
         const uint32_t k = k0 + l;
         if (k < length) {
           const uint32_t kk = (k < dist) ? k : (k % dist);
+#ifdef RIO_CHECKED
+          if (olen - dist + kk >= out_room) {
+            atomicOr(in->flag, 0x800ull);
+            continue;
+          }
+#endif
           L->win[(olen + k) & (kWin - 1)] = out[olen - dist + kk];
         }
       }
@@ -547,7 +617,8 @@ struct Fast {
       const uint32_t n = (len - done) < 64u ? (len - done) : 64u;
       const uint32_t room = (uint32_t)(kUnit - (olen & (kUnit - 1)));
       const uint32_t m = n < room ? n : room;
-      if ((uint32_t)l < m) L->win[(olen + l) & (kWin - 1)] = L->in[pos - base + l];
+      const uint8_t *src = reinterpret_cast<const uint8_t *>(L->in32) + (pos - base);
+      if ((uint32_t)l < m) L->win[(olen + l) & (kWin - 1)] = src[l];
       wave_lds_sync();
       pos += m;
       olen += m;
@@ -575,10 +646,9 @@ __device__ int inflate_fast(Fast &f) {
       f.bitbuf = 0;
       if (f.pos + 4 > f.in->n) return kCodecEof;
       // the bytes given back may precede the staged window
-      if (f.pos < f.base || f.pos + 4 > f.base + kInBuf) f.stage(f.pos);
-      const uint32_t o = (uint32_t)(f.pos - f.base);
-      const uint32_t len = L.in[o] | ((uint32_t)L.in[o + 1] << 8);
-      const uint32_t nlen = L.in[o + 2] | ((uint32_t)L.in[o + 3] << 8);
+      if (f.pos < f.base || f.pos + 8 > f.base + kInBuf) f.stage(f.pos);
+      const uint32_t len = f.in_byte(f.pos) | (f.in_byte(f.pos + 1) << 8);
+      const uint32_t nlen = f.in_byte(f.pos + 2) | (f.in_byte(f.pos + 3) << 8);
       f.pos += 4;
       if ((uint16_t)nlen != (uint16_t)~len) return kCodecCorrupt;
       if (f.olen + len > f.cap) return kCodecFull;
@@ -591,7 +661,7 @@ __device__ int inflate_fast(Fast &f) {
           wave_lds_sync();
           if (l == 0) {
             fixed_lens(L.lens);
-            huff_build(L.lit, L.lens, 288, L.offs);
+            huff_build(L.lit, L.lens, 288, L.offs, L.lfast, kLitBits);
           }
           wave_lds_sync();
         }
@@ -613,25 +683,25 @@ __device__ int inflate_fast(Fast &f) {
           if (l == 0) L.cl[kClenOrder[i]] = (uint8_t)v;
         }
         wave_lds_sync();
-        if (l == 0) huff_build(L.clen, L.cl, 19, L.offs);
+        if (l == 0) huff_build(L.dist, L.cl, 19, L.offs, L.dfast, kDistBits);
         wave_lds_sync();
-        if (!L.clen.ok || L.clen.empty) return kCodecCorrupt;
+        if (!uni(L.dist.ok) || uni(L.dist.empty)) return kCodecCorrupt;
         const int n = nlit + ndist;
-        int i = 0;
+        int i = 0, prev = 0;
         while (i < n) {
           f.refill();
-          const int x = f.sym(L.clen);
+          const int x = f.sym(L.dist, L.dfast, kDistBits);
           if (x < 0) return kCodecCorrupt;
           if (x < 16) {
             if (l == 0) L.lens[i] = (uint8_t)x;
+            prev = x;
             i++;
             continue;
           }
           int rep, b;
           if (x == 16) {
             if (i == 0) return kCodecCorrupt;
-            wave_lds_sync();
-            b = L.lens[i - 1];
+            b = prev;
             rep = 3 + (int)f.take(2);
           } else if (x == 17) {
             b = 0;
@@ -641,23 +711,24 @@ __device__ int inflate_fast(Fast &f) {
             rep = 11 + (int)f.take(7);
           }
           if (i + rep > n) return kCodecCorrupt;
-          if (l == 0)
-            for (int j = 0; j < rep; j++) L.lens[i + j] = (uint8_t)b;
+          for (int j = l; j < rep; j += 64) L.lens[i + j] = (uint8_t)b;
+          prev = b;
           i += rep;
         }
         if (f.overrun()) return kCodecEof;
         wave_lds_sync();
         if (l == 0) {
-          huff_build(L.lit, L.lens, nlit, L.offs);
-          huff_build(L.dist, L.lens + nlit, ndist, L.offs);
+          huff_build(L.lit, L.lens, nlit, L.offs, L.lfast, kLitBits);
+          huff_build(L.dist, L.lens + nlit, ndist, L.offs, L.dfast, kDistBits);
         }
         wave_lds_sync();
-        if (!L.lit.ok || !L.dist.ok || L.lit.empty) return kCodecCorrupt;
+        if (!uni(L.lit.ok) || !uni(L.dist.ok) || uni(L.lit.empty)) return kCodecCorrupt;
       }
+      const bool dist_empty = has_dist && uni(L.dist.empty);
       // huffmanBlock
       for (;;) {
         f.refill();
-        const int v = f.sym(L.lit);
+        const int v = f.sym(L.lit, L.lfast, kLitBits);
         if (v < 0) return kCodecCorrupt;
         if (v < 256) {
           if (f.olen >= f.cap) return kCodecFull;
@@ -681,8 +752,8 @@ __device__ int inflate_fast(Fast &f) {
         if (!has_dist) {
           dist = (int)rev_bits(f.take(5), 5);
         } else {
-          if (L.dist.empty) return kCodecCorrupt;
-          dist = f.sym(L.dist);
+          if (dist_empty) return kCodecCorrupt;
+          dist = f.sym(L.dist, L.dfast, kDistBits);
           if (dist < 0) return kCodecCorrupt;
         }
         if (dist < 4) {
@@ -717,11 +788,12 @@ __global__ void __launch_bounds__(64 * kInflWaves) k_inflate(const uint8_t *__re
   InflLds &L = s_lds[threadIdx.x >> 6];
   const int l = lane_id();
   const uint64_t nb = *nblocks;
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  for (uint64_t b = wave; b < nb; b += nwaves) {
-    const uint64_t c0 = d.blk_c0[b];
-    const unsigned long long meta = d.blk_meta[b];
+  // one wave per workgroup: the block index is wave-uniform, so the decoder
+  // state derived from it lives in scalar registers (no exec-mask branches)
+  static_assert(kInflWaves == 1, "k_inflate assumes one wave per workgroup");
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint64_t c0 = uni64(d.blk_c0[b]);
+    const unsigned long long meta = uni64(d.blk_meta[b]);
     const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
     // incomplete blocks, and magics that are never untransformed (the header
     // block is idTransform, registry.go:31; others are errors): nothing decoded
@@ -731,18 +803,21 @@ __global__ void __launch_bounds__(64 * kInflWaves) k_inflate(const uint8_t *__re
     }
     CompIn in;
     in.span = span;
+    in.span_bytes = nchunks * (uint64_t)kChunk;
+    in.flag = &d.ctl->out_overflow;
     in.ck_size = d.ck_size;
     in.ck_pay = d.ck_pay;
     in.c0 = c0;
     in.total = meta & kMetaTotalMask;
-    in.n = d.blk_len[b];
-    in.pay0 = d.ck_pay[c0];
+    in.n = uni64(d.blk_len[b]);
+    in.pay0 = uni64(d.ck_pay[c0]);
     in.regular = (meta & kMetaRegular) != 0;
-    const uint64_t off = d.blk_dec_off[b];
-    const uint64_t cap = d.blk_out_len[b];  // the bound from k_codec_prepare
-    if (off + cap > dec_cap) {
+    const uint64_t off = uni64(d.blk_dec_off[b]);
+    const uint64_t cap = uni64(d.blk_out_len[b]);  // the bound from k_codec_prepare
+    if (off + cap > dec_cap) {  // the regions need a larger buffer (host retries)
       if (l == 0) {
-        atomicOr(&d.ctl->out_overflow, 8ull);
+        atomicOr(&d.ctl->out_overflow, 0x40ull);
+        atomicMax(&d.ctl->dec_need, (unsigned long long)(off + cap));
         d.blk_out_len[b] = 0;
       }
       continue;
@@ -751,6 +826,7 @@ __global__ void __launch_bounds__(64 * kInflWaves) k_inflate(const uint8_t *__re
     f.in = &in;
     f.L = &L;
     f.out = d.dec + off;
+    f.out_room = dec_cap - off;
     f.cap = cap;
     f.base = 0;
     f.pos = 0;
@@ -758,7 +834,6 @@ __global__ void __launch_bounds__(64 * kInflWaves) k_inflate(const uint8_t *__re
     f.nb = 0;
     f.olen = 0;
     f.flushed = 0;
-    f.err = 0;
     f.stage(0);
     const int err = inflate_fast(f);
     if (l == 0) {
@@ -790,6 +865,8 @@ __global__ void __launch_bounds__(64) k_inflate_exact(const uint8_t *__restrict_
         const unsigned long long meta = d.blk_meta[b];
         CompIn in;
         in.span = span;
+        in.span_bytes = ~0ull;
+        in.flag = &d.ctl->out_overflow;
         in.ck_size = d.ck_size;
         in.ck_pay = d.ck_pay;
         in.c0 = d.blk_c0[b];
@@ -801,9 +878,8 @@ __global__ void __launch_bounds__(64) k_inflate_exact(const uint8_t *__restrict_
         uint64_t eo = 0, olen = 0;
         inflate_exact(in, L, ~0ull >> 1, e, eo, olen);
         if (e == 0 && d.blk_b[b] == kCodecFull) {
-          // a valid stream larger than its decode region: ask for a larger factor
-          const unsigned long long comp = in.n ? in.n : 1;
-          atomicMax(&d.ctl->dec_factor_need, olen / comp + 2);
+          // a valid stream larger than its decode region: the retry sizes it exactly
+          d.blk_need[b] = olen;
           atomicOr(&d.ctl->out_overflow, 8ull);
           e = kCodecFull;
         } else if (e == 0 || e == kCodecFull) {

@@ -80,7 +80,7 @@ struct rio_ctx {
   bool last_had_dec = false;
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
   uint64_t side_cap = 0, item_cap = 0, dec_cap = 0;
-  uint32_t dec_factor = 8;  // decode-region bound: compressed bytes x this (grown on overflow)
+  uint32_t dec_factor = 8;  // first-attempt decode-region bound: compressed bytes x this
   DevBufs d{};
   unsigned long long *nblocks_dev = nullptr;
   uint8_t *d_span = nullptr;  // staging for host spans (lazy)
@@ -122,7 +122,8 @@ static int alloc_bufs(rio_ctx *c) {
   const uint64_t nb = c->max_blocks + 1;
   if (dalloc(&d.blk_c0, nb) || dalloc(&d.blk_meta, nb) || dalloc(&d.blk_len, nb) || dalloc(&d.blk_nitems, nb) ||
       dalloc(&d.blk_hdr, nb) || dalloc(&d.blk_item_base, nb + 1) || dalloc(&d.blk_status, nb) ||
-      dalloc(&d.blk_a, nb) || dalloc(&d.blk_b, nb) || dalloc(&d.blk_out_len, nb) || dalloc(&d.blk_dec_off, nb + 1))
+      dalloc(&d.blk_a, nb) || dalloc(&d.blk_b, nb) || dalloc(&d.blk_out_len, nb) || dalloc(&d.blk_dec_off, nb + 1) ||
+      dalloc(&d.blk_need, nb))
     return -1;
   if (dalloc(&d.scan_tmp, (n + 2047) / 2048 + 16) || dalloc(&d.strad, n)) return -1;
   if (dalloc(&d.item_off, c->item_cap) || dalloc(&d.item_len, c->item_cap) || dalloc(&d.side, c->side_cap))
@@ -133,7 +134,7 @@ static int alloc_bufs(rio_ctx *c) {
 static void free_all(rio_ctx *c) {
   DevBufs &d = c->d;
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
-                d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.item_off, d.item_len, d.side,
+                d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span};
   for (void *p : ps)
@@ -214,6 +215,7 @@ static int ensure_dec(rio_ctx *c, uint64_t need) {
   const uint64_t cap = need + need / 4;
   if (dalloc(&c->d.dec, cap)) return -1;
   c->dec_cap = cap;
+  c->d.dec_cap = cap;
   return 0;
 }
 
@@ -228,7 +230,7 @@ static int ensure_side(rio_ctx *c, uint64_t need) {
 // sparse: straddlers land at their own span offset in a span-sized side buffer
 // (device-resident results, no straddler scan); else compacted (host results).
 static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t limit_chunk, int is_file_end,
-                   int tail_partial, int32_t codec, int32_t mode, bool sparse) {
+                   int tail_partial, int32_t codec, int32_t mode, bool sparse, int attempt) {
   if (sparse && codec == RIO_CODEC_NONE && ensure_side(c, nchunks * (uint64_t)kChunk)) return -1;
   DevBufs &d = c->d;
   hipStream_t st = c->st, st2 = c->st2;
@@ -236,7 +238,9 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   HIP_OK(hipEventRecord(c->ev[kEvStart], st));
   // control words are min-reduced: reset to ~0 (out_overflow to 0)
   HIP_OK(hipMemsetAsync(d.ctl, 0xff, 4 * sizeof(unsigned long long), st));
-  HIP_OK(hipMemsetAsync(&d.ctl->out_overflow, 0, 2 * sizeof(unsigned long long), st));  // + dec_factor_need
+  HIP_OK(hipMemsetAsync(&d.ctl->out_overflow, 0, 2 * sizeof(unsigned long long), st));  // + dec_need
+  if (attempt == 0 && codec != RIO_CODEC_NONE && nchunks > 0)
+    HIP_OK(hipMemsetAsync(d.blk_need, 0, nchunks * sizeof(unsigned long long), st));
   HIP_OK(hipMemsetAsync(c->nblocks_dev, 0, 2 * sizeof(unsigned long long), st));
   const uint64_t max_blocks = nchunks ? nchunks : 1;
   if (nchunks > 0) {
@@ -409,15 +413,14 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
   uint64_t limit_chunk = UINT64_MAX;
   if (limit_off != UINT64_MAX) limit_chunk = limit_off <= file_off ? 0 : (limit_off - file_off + kChunk - 1) / kChunk;
   for (int attempt = 0; attempt < 4; attempt++) {
-    if (enqueue(c, dspan, nchunks, limit_chunk, is_file_end, tail_partial, codec, mode, !to_host)) return -1;
+    if (enqueue(c, dspan, nchunks, limit_chunk, is_file_end, tail_partial, codec, mode, !to_host, attempt)) return -1;
     HIP_OK(hipMemcpyAsync(c->h_ctl, c->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipStreamSynchronize(c->st));
     if (c->h_ctl->out_overflow == 0) break;
     if (grow_for_overflow(c, codec)) return -1;
-    if (codec != RIO_CODEC_NONE && (c->h_ctl->out_overflow & 8)) {
-      const unsigned long long need = c->h_ctl->dec_factor_need;
-      c->dec_factor = (uint32_t)(need > 4ull * c->dec_factor ? need : 4ull * c->dec_factor);
-    }
+    // decode regions: blocks that overflowed theirs carry their exact size (blk_need)
+    // into the next attempt; a buffer too small for all regions grows to fit
+    if (codec != RIO_CODEC_NONE && (c->h_ctl->out_overflow & 0x40) && ensure_dec(c, c->h_ctl->dec_need)) return -1;
   }
   if (getenv("RIO_DEBUG")) debug_dump(c);
   float ms = 0;
@@ -492,7 +495,7 @@ extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_
   ctx->last_mode = kModeBody;
   ctx->last_span = (const uint8_t *)dev_span;
   return enqueue(ctx, (const uint8_t *)dev_span, nchunks, UINT64_MAX, 1, (nbytes % kChunk) != 0, codec, kModeBody,
-                 true);
+                 true, 0);
 }
 
 extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {

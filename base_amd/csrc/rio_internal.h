@@ -61,7 +61,7 @@ struct Ctl {
   unsigned long long first_block_event;  // min over block event keys (2*chunk + 1 / 2*c0)
   unsigned long long first_incomplete;   // min c0 of a block extending past the span
   unsigned long long out_overflow;       // nonzero if side/items exceeded capacity
-  unsigned long long dec_factor_need;    // max over blocks of decoded/compressed + 1 (decode overflow)
+  unsigned long long dec_need;           // decode regions' total size (when it exceeds dec_cap)
   unsigned long long pad[2];
   // filled by k_resolve
   unsigned long long stop_key;
@@ -118,6 +118,7 @@ struct DevBufs {
   unsigned long long *blk_a, *blk_b;
   unsigned long long *blk_out_len;    // decoded length (compressed codecs)
   unsigned long long *blk_dec_off;    // offset of the block's decoded bytes in dec (n + 1)
+  unsigned long long *blk_need;       // decoded size found by the exact pass after a region overflow
   // outputs: item views into the span or the records buffer (side / dec)
   unsigned long long *item_off, *item_len;
   uint8_t *side;        // straddling items (none codec)
@@ -125,6 +126,7 @@ struct DevBufs {
   // scratch
   unsigned long long *scan_tmp;  // tile partials
   uint8_t *dec;                  // decoded blocks (compressed codecs)
+  uint64_t dec_cap;              // bytes at dec
   Ctl *ctl;
   // CRC tables (constant)
   uint32_t *crc_fold;   // 4 x 256 fold tables, each replicated x32 (bank-private copies)
