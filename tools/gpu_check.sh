@@ -34,3 +34,6 @@ if [ -n "$PROFILE" ]; then
   step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline
 fi
+if [ -n "$FLATE" ]; then
+  step bench_flate 400 python tools/bench_flate.py ${FLATE_ARGS}
+fi
