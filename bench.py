@@ -65,6 +65,22 @@ def make_c2_file():
     return data, N_RECORDS
 
 
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_c2_pmc.json")
+
+
+def pmc_traffic(kernel: str, replicas: int):
+    """HBM bytes per launch of `kernel` from the committed PMC pass (tools/pmc.sh:
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over this same bench command, FETCH_SIZE
+    doubled per MI355X_MICROARCH.md). Only valid for the default replica count."""
+    if replicas != REPLICAS or not os.path.exists(PMC_FILE):
+        return None
+    with open(PMC_FILE) as f:
+        e = json.load(f).get("rio::" + kernel)
+    if not e:
+        return None
+    return int(e.get("fetch_bytes", 0) + e.get("write_bytes", 0))
+
+
 def cpu_baseline(data: bytes, budget_s: float = 10.0):
     """The C oracle (restatement of recordio.NewScanner's loop) on one host core."""
     from oracle import oracle as O
@@ -180,7 +196,7 @@ def main():
     # ~1 per block here, are ~0.4 % of the bytes and not counted)
     pipe_alg = span_len + 16 * n_items + 8 * int(b.n_blocks)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_crc", args.replicas),
             "kernel": "k_crc", "kernel_ms": round(crc_avg, 3),
             "alg_bytes_per_launch": alg,
             "pipeline_ms": round(float(np.mean(kern_ms)), 3),
