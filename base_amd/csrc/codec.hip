@@ -37,7 +37,7 @@ __global__ void k_codec_unsupported(DevBufs d, const unsigned long long *nblocks
 void launch_block_scan(const unsigned long long *in, unsigned long long *out, unsigned long long *tmp,
                        const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
-                    uint64_t nchunks, uint64_t dec_cap, hipStream_t st);
+                    uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st);
 
 static unsigned grid_blocks(uint64_t n) {
   uint64_t g = (n + 255) / 256;
@@ -53,9 +53,10 @@ void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_de
 }
 
 void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks_dev,
-                         uint64_t max_blocks, uint64_t nchunks, int codec, uint64_t dec_cap, hipStream_t st) {
+                         uint64_t max_blocks, uint64_t nchunks, int codec, uint64_t dec_cap, int rounds, int ncu,
+                         hipStream_t st) {
   if (codec == RIO_CODEC_FLATE) {
-    launch_inflate(span, d, nblocks_dev, max_blocks, nchunks, dec_cap, st);
+    launch_inflate(span, d, nblocks_dev, max_blocks, nchunks, dec_cap, rounds, ncu, st);
     return;
   }
   hipLaunchKernelGGL(k_codec_unsupported, dim3(grid_blocks(max_blocks)), dim3(256), 0, st, d, nblocks_dev);

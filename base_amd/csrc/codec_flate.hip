@@ -1,25 +1,19 @@
 // Raw DEFLATE (RFC 1951) block decode: the "flate" untransformer
 // (recordioflate.FlateUncompress, recordio/recordioflate/recordioflate.go:54-65,
 // through github.com/klauspost/compress v1.8.6 flate -- Go's compress/flate
-// inflater: go.mod:24). One wave per recordio block.
+// inflater: go.mod:24).
 //
 // The compressed block is the concatenation of its chunk payloads (the
-// IOVecReader view, recordioiov.go:14-58). The wave stages 2 KiB of it at a time
-// into LDS (64 lanes, one coalesced pass), every lane runs the same bit-reader
-// and Huffman decode (uniform state: no divergence, LDS reads broadcast), and
-// output goes through an 8 KiB LDS window ring: literals and near matches are
-// LDS copies (lane-parallel for matches), each completed 1 KiB is flushed to the
-// block's decode region in HBM with one 16 B/lane store, and matches further
-// back than the ring read the flushed bytes from HBM.
+// IOVecReader view, recordioiov.go:14-58); decoding stops at the end of the
+// BFINAL block and trailing bytes are ignored, as in Go.
 //
-// The fast decoder refills the bit buffer greedily. Go's inflater pulls bytes
-// lazily (moreBits), which only matters for *where* an error is reported
-// (CorruptInputError's offset is its roffset) and for rejecting a truncated
-// stream; so on any error the block is re-decoded by inflate_exact, a
-// single-lane restatement with Go's lazy byte pulls that produces the
-// reference's error and offset (it writes nothing: an erroring block yields no
-// records). Decoding stops at the end of the BFINAL block; trailing bytes are
-// ignored, as in Go.
+// The fast path (k_flate_tok + k_flate_lz, below) decodes valid streams. Go's
+// inflater pulls bytes lazily (moreBits), which only matters for *where* an
+// error is reported (CorruptInputError's offset is its roffset) and for
+// rejecting a truncated stream; so on any error the block is re-decoded by
+// inflate_exact, a single-lane restatement with Go's lazy byte pulls that
+// produces the reference's error and offset (it writes nothing: an erroring
+// block yields no records).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,13 +22,6 @@
 
 namespace rio {
 
-constexpr int kInflWaves = 1;    // waves per workgroup (LDS-bound residency: one wave per workgroup)
-constexpr int kInBuf = 1024;     // input staging bytes
-#ifndef RIO_INFL_WIN
-#define RIO_INFL_WIN 8192
-#endif
-constexpr int kWin = RIO_INFL_WIN;  // output window ring
-constexpr int kUnit = 1024;      // flush granule
 constexpr int kLitBits = 10;     // root table bits: literal/length
 constexpr int kDistBits = 8;     // root table bits: distance (and code-length codes)
 constexpr int kMaxBits = 15;
@@ -45,9 +32,8 @@ struct HuffT {
   int32_t min, max, empty, ok;
 };
 
+// LDS of the exact (error-classifying) pass
 struct InflLds {
-  uint8_t win[kWin];
-  uint32_t in32[kInBuf / 4 + 4];  // staged compressed bytes
   uint16_t lfast[1 << kLitBits];  // (len << 9) | sym for codes <= kLitBits, 0: longer code
   uint16_t dfast[1 << kDistBits];
   HuffT lit, dist;                // code-length codes are decoded through `dist` / dfast
@@ -459,397 +445,880 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
   olen = s.olen;
 }
 
-// ---------------------------------------------------------------- fast mode
-// Decoder state is wave-uniform: every value read from LDS goes through uni()
-// (v_readfirstlane), so the bit reader and the Huffman walk run on the scalar
-// unit; the vector lanes do the wave-parallel parts (staging, LZ77 copies,
-// flushes).
-struct Fast {
-  const CompIn *in;
-  InflLds *L;
-  uint8_t *out;      // the block's decode region in HBM
-  uint64_t cap;
-  uint64_t out_room; // RIO_CHECKED: bytes addressable from out
-  uint64_t base;     // logical offset of the staged bytes (multiple of 4)
-  uint64_t pos;      // next logical byte for the bit buffer
-  uint64_t bitbuf;
-  int nb;
-  uint64_t olen, flushed;
 
-  // stage logical bytes [b & ~3, + kInBuf + 16) into LDS, all lanes
-  __device__ void stage(uint64_t b) {
-    const int l = lane_id();
-    base = b & ~3ull;
-    wave_lds_sync();
-    uint8_t *dst = reinterpret_cast<uint8_t *>(L->in32);
-    for (int k = l; k < kInBuf + 16; k += 64) dst[k] = (uint8_t)in->byte(base + k);
-    wave_lds_sync();
+// ================================================================ fast path
+// Two passes per round (SURVEY.md §7 "DEFLATE kernel"):
+//
+// k_flate_tok -- Huffman pass, on the vector ALU: a wave decodes 8 recordio
+//   blocks at once, 8 lanes per block (a "stream"; its state is the same in
+//   all 8 lanes), so every VALU instruction advances 8 streams. Per stream,
+//   ~4.7 KiB of LDS: the two Huffman tables (literal/length 10-bit root of
+//   u16 entries, distance 8-bit root of u32 entries with base and extra bits
+//   precomputed), canonical data for longer codes, a 512 B input ring
+//   refilled every 8 steps from a 16 B/lane prefetch issued 8 steps earlier,
+//   and a 16-token buffer stored to HBM at the same point. Rare events -- a
+//   DEFLATE block header, the table build for a dynamic block, picking up the
+//   next recordio block, writing a block's result -- "escape" to wave-uniform
+//   scalar code for that one stream (readlane in, cndmask back).
+// k_flate_lz -- copy pass: one wave per block with a 64 KiB LDS window (the
+//   DEFLATE history plus the largest token batch, so no match ever reads HBM
+//   and no write of a batch clobbers a source of the same batch): 64 tokens
+//   per step, output positions from a wave prefix sum, literals written in
+//   parallel, each match copied by its own lane once its source bytes are
+//   final, every completed 1 KiB flushed to the block's decode region with
+//   16 B/lane stores.
+//
+// A block whose token region fills yields (FlState) and resumes in the next
+// round: the Huffman pass re-reads the current block header to rebuild its
+// tables, the copy pass reloads the last 32 KiB it wrote.
+//
+// Token (u32):
+//   bit 31 = 0: 1-3 literals, count in bits 25:24, bytes in 7:0, 15:8, 23:16
+//   bit 31 = 1: match, length-3 in bits 23:16, distance-1 in bits 14:0
+
+// Table entries. Literal/length (u16): code length (3:0; 0 = not decodable
+// from the root), bit 4 set for a length or end-of-block, length extra bits
+// (7:5; 7 = end-of-block), literal byte or length base - 3 (15:8).
+// Distance (u32): code length (3:0), extra bits (11:8), base (31:16).
+// Code-length alphabet (u32): code length (3:0), symbol (31:16).
+// Code length 0 with bit 4 set (kLongMark) marks a code longer than the root
+// (canonical walk); an all-zero entry is a bit pattern no code has or a
+// symbol DEFLATE never assigns (literal/length 286-287, distance 30-31):
+// decoding it is a corrupt stream (Go: CorruptInputError).
+constexpr uint32_t kEnLenBit = 0x10;
+constexpr uint32_t kLongMark = kEnLenBit;
+constexpr uint32_t kEobExtra = 7;
+enum : int { kTabLit = 0, kTabDist = 1, kTabClen = 2 };
+enum : int { kTokDone = 0, kTokYield = -1 };
+constexpr int kTokLitRoot = 10;
+constexpr int kTokDistRoot = 8;
+
+// RFC 1951 §3.2.5 length / distance bases and extra bits
+__constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t kDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,    65,    97,    129,
+                                       193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+
+__device__ __forceinline__ uint32_t tab_entry(int kind, uint32_t s, uint32_t len) {
+  if (kind == kTabLit) {
+    if (s < 256) return len | (s << 8);
+    if (s == 256) return len | kEnLenBit | (kEobExtra << 5);
+    if (s < 286)
+      return len | kEnLenBit | ((uint32_t)kLenExtra[s - 257] << 5) | ((uint32_t)(kLenBase[s - 257] - 3) << 8);
+    return 0;
   }
-  __device__ __forceinline__ uint32_t in_byte(uint64_t p) {
-    const uint32_t o = (uint32_t)(p - base);
-    return (uni(L->in32[o >> 2]) >> (8 * (o & 3))) & 0xffu;
+  if (kind == kTabDist) {
+    if (s < 30) return len | ((uint32_t)kDistExtra[s] << 8) | ((uint32_t)kDistBase[s] << 16);
+    return 0;
   }
-  __device__ __forceinline__ void refill() {
-    if (nb > 32) return;
-    if (pos < base || pos + 8 > base + kInBuf) stage(pos);
-    const uint32_t o = (uint32_t)(pos - base);
-    const uint32_t d0 = uni(L->in32[o >> 2]), d1 = uni(L->in32[(o >> 2) + 1]);
-    const uint32_t w = (uint32_t)((((uint64_t)d1 << 32) | d0) >> (8 * (o & 3)));
-    bitbuf |= (uint64_t)w << nb;
-    nb += 32;
-    pos += 4;
-  }
-  __device__ __forceinline__ uint32_t take(int n) {
-    const uint32_t v = (uint32_t)(bitbuf & ((1ull << n) - 1));
-    bitbuf >>= n;
-    nb -= n;
-    return v;
-  }
-  // bits consumed past the end of the input: the stream is truncated
-  __device__ __forceinline__ bool overrun() const { return 8 * pos - (uint64_t)nb > 8 * in->n; }
-  __device__ __forceinline__ int sym(const HuffT &h, const uint16_t *fast, int fbits) {
-    const uint32_t bits = (uint32_t)bitbuf;
-    const uint32_t e = uni(fast[bits & ((1u << fbits) - 1)]);
-    int len, s;
-    if (e) {
-      len = (int)(e >> 9);
-      s = (int)(e & 511);
-    } else {  // canonical walk for codes longer than the root table
-      int code = 0, first = 0, index = 0;
-      s = -1;
-      len = 0;
-      for (int l = 1; l <= kMaxBits; l++) {
-        code |= (int)((bits >> (l - 1)) & 1u);
-        const int cnt = (int)uni(h.count[l]);
-        if (code - cnt < first) {
-          len = l;
-          s = (int)uni(h.sym[index + (code - first)]);
-          break;
-        }
-        index += cnt;
-        first += cnt;
-        first <<= 1;
-        code <<= 1;
-      }
-      if (s < 0) return -1;
-    }
-    take(len);
-    return s;
-  }
-  // write completed flush units [flushed, olen rounded down) to HBM
-  __device__ void flush_units() {
-    const int l = lane_id();
-    if (olen - flushed < (uint64_t)kUnit) return;
-    wave_lds_sync();
-    while (olen - flushed >= (uint64_t)kUnit) {
-      const uint32_t r = (uint32_t)(flushed & (kWin - 1));
-      const uint4 v = *reinterpret_cast<const uint4 *>(L->win + r + 16 * l);
-#ifdef RIO_CHECKED
-      if (flushed + 16 * l + 16 > out_room) {
-        atomicOr(in->flag, 0x200ull);
-      } else
-#endif
-      *reinterpret_cast<uint4 *>(out + flushed + 16 * l) = v;
-      flushed += kUnit;
-    }
-  }
-  __device__ void flush_tail() {
-    flush_units();
-    wave_lds_sync();
-    const int l = lane_id();
-    for (uint64_t k = flushed + l; k < olen; k += 64) {
-#ifdef RIO_CHECKED
-      if (k >= out_room) {
-        atomicOr(in->flag, 0x400ull);
-        continue;
-      }
-#endif
-      out[k] = L->win[k & (kWin - 1)];
-    }
-    flushed = olen;
-  }
-  __device__ __forceinline__ void literal(uint32_t v) {
-    if (lane_id() == 0) L->win[olen & (kWin - 1)] = (uint8_t)v;
-    olen++;
-    if ((olen & (kUnit - 1)) == 0) flush_units();
-  }
-  // LZ77 copy: every source byte precedes olen, so all lanes copy at once
-  __device__ void copy(uint32_t dist, uint32_t length) {
-    const int l = lane_id();
-    wave_lds_sync();
-    if (dist <= (uint32_t)(kWin - kUnit - 258)) {
-      for (uint32_t k0 = 0; k0 < length; k0 += 64) {
-        const uint32_t k = k0 + l;
-        uint8_t v = 0;
-        if (k < length) {
-          const uint32_t kk = (k < dist) ? k : (k % dist);
-          v = L->win[(olen - dist + kk) & (kWin - 1)];
-        }
-        wave_lds_sync();
-        if (k < length) L->win[(olen + k) & (kWin - 1)] = v;
-      }
-    } else {  // older than the ring: the flushed bytes in HBM
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      for (uint32_t k0 = 0; k0 < length; k0 += 64) {
-        const uint32_t k = k0 + l;
-        if (k < length) {
-          const uint32_t kk = (k < dist) ? k : (k % dist);
-#ifdef RIO_CHECKED
-          if (olen - dist + kk >= out_room) {
-            atomicOr(in->flag, 0x800ull);
-            continue;
-          }
-#endif
-          L->win[(olen + k) & (kWin - 1)] = out[olen - dist + kk];
-        }
-      }
-    }
-    wave_lds_sync();
-    olen += length;
-    flush_units();
-  }
-  __device__ void stored(uint32_t len) {
-    const int l = lane_id();
-    uint32_t done = 0;
-    while (done < len) {
-      if (pos < base || pos + 64 > base + kInBuf) stage(pos);
-      const uint32_t n = (len - done) < 64u ? (len - done) : 64u;
-      const uint32_t room = (uint32_t)(kUnit - (olen & (kUnit - 1)));
-      const uint32_t m = n < room ? n : room;
-      const uint8_t *src = reinterpret_cast<const uint8_t *>(L->in32) + (pos - base);
-      if ((uint32_t)l < m) L->win[(olen + l) & (kWin - 1)] = src[l];
-      wave_lds_sync();
-      pos += m;
-      olen += m;
-      done += m;
-      if ((olen & (kUnit - 1)) == 0) flush_units();
-    }
-  }
+  return len | (s << 16);
+}
+
+// canonical code data for codes longer than the root table
+struct TabSlow {
+  uint16_t count[16], first[16], offs[16];
 };
 
-// Returns 0 (ok; olen set) or a CodecErr for the exact pass to classify.
-__device__ int inflate_fast(Fast &f) {
-  InflLds &L = *f.L;
+constexpr int kVS = 8;         // streams per wave
+constexpr int kRingDw = 128;   // input ring per stream (dwords)
+constexpr int kTbuf = 16;      // tokens buffered per stream between input passes
+constexpr int kPass = 8;       // decode steps between input passes
+
+struct __attribute__((aligned(16))) StreamLds {
+  uint32_t ring[kRingDw];
+  uint32_t tbuf[kTbuf];
+  uint32_t dst[1 << kTokDistRoot];  // also the code-length table while a header is read
+  uint16_t lit[1 << kTokLitRoot];
+  uint16_t lsym[288], dsym[32];     // symbols in canonical order
+  TabSlow ls, ds;
+  uint8_t lens[320];
+  uint8_t cl[24];
+};
+
+// Wave-cooperative table build with huffmanDecoder.init's rules (Go
+// compress/flate inflate.go): returns 0 ok, 1 empty (no codes: decoding with
+// it fails), 2 incomplete or oversubscribed (corrupt), except that a single
+// code of length 1 is accepted (its other half decodes as a zero entry).
+// Ranks within a length come from ballots, so every lane places its own
+// symbol; entries of codes up to `root` bits are replicated by their lanes.
+template <class TT>
+__device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, int root, TabSlow &sl,
+                                           uint16_t *sorted, int kind) {
   const int l = lane_id();
-  bool fixed_built = false;
-  for (;;) {
-    f.refill();
-    const int final = (int)f.take(1);
-    const int type = (int)f.take(2);
-    if (f.overrun()) return kCodecEof;
-    if (type == 0) {
-      // discard the rest of the current byte; whole bytes read ahead go back
-      f.take(f.nb & 7);
-      f.pos -= (uint64_t)(f.nb >> 3);
-      f.nb = 0;
-      f.bitbuf = 0;
-      if (f.pos + 4 > f.in->n) return kCodecEof;
-      // the bytes given back may precede the staged window
-      if (f.pos < f.base || f.pos + 8 > f.base + kInBuf) f.stage(f.pos);
-      const uint32_t len = f.in_byte(f.pos) | (f.in_byte(f.pos + 1) << 8);
-      const uint32_t nlen = f.in_byte(f.pos + 2) | (f.in_byte(f.pos + 3) << 8);
-      f.pos += 4;
-      if ((uint16_t)nlen != (uint16_t)~len) return kCodecCorrupt;
-      if (f.olen + len > f.cap) return kCodecFull;
-      if (f.pos + len > f.in->n) return kCodecEof;
-      f.stored(len);
-    } else if (type == 1 || type == 2) {
-      bool has_dist = true;
-      if (type == 1) {
-        if (!fixed_built) {
-          wave_lds_sync();
-          if (l == 0) {
-            fixed_lens(L.lens);
-            huff_build(L.lit, L.lens, 288, L.offs, L.lfast, kLitBits);
-          }
-          wave_lds_sync();
-        }
-        fixed_built = true;
-        has_dist = false;
-      } else {
-        fixed_built = false;
-        f.refill();
-        const int nlit = (int)f.take(5) + 257;
-        const int ndist = (int)f.take(5) + 1;
-        const int nclen = (int)f.take(4) + 4;
-        if (nlit > 286 || ndist > 30) return kCodecCorrupt;
-        wave_lds_sync();
-        if (l == 0)
-          for (int i = 0; i < 19; i++) L.cl[i] = 0;
-        for (int i = 0; i < nclen; i++) {
-          f.refill();
-          const uint32_t v = f.take(3);
-          if (l == 0) L.cl[kClenOrder[i]] = (uint8_t)v;
-        }
-        wave_lds_sync();
-        if (l == 0) huff_build(L.dist, L.cl, 19, L.offs, L.dfast, kDistBits);
-        wave_lds_sync();
-        if (!uni(L.dist.ok) || uni(L.dist.empty)) return kCodecCorrupt;
-        const int n = nlit + ndist;
-        int i = 0, prev = 0;
-        while (i < n) {
-          f.refill();
-          const int x = f.sym(L.dist, L.dfast, kDistBits);
-          if (x < 0) return kCodecCorrupt;
-          if (x < 16) {
-            if (l == 0) L.lens[i] = (uint8_t)x;
-            prev = x;
-            i++;
-            continue;
-          }
-          int rep, b;
-          if (x == 16) {
-            if (i == 0) return kCodecCorrupt;
-            b = prev;
-            rep = 3 + (int)f.take(2);
-          } else if (x == 17) {
-            b = 0;
-            rep = 3 + (int)f.take(3);
-          } else {
-            b = 0;
-            rep = 11 + (int)f.take(7);
-          }
-          if (i + rep > n) return kCodecCorrupt;
-          for (int j = l; j < rep; j += 64) L.lens[i + j] = (uint8_t)b;
-          prev = b;
-          i += rep;
-        }
-        if (f.overrun()) return kCodecEof;
-        wave_lds_sync();
-        if (l == 0) {
-          huff_build(L.lit, L.lens, nlit, L.offs, L.lfast, kLitBits);
-          huff_build(L.dist, L.lens + nlit, ndist, L.offs, L.dfast, kDistBits);
-        }
-        wave_lds_sync();
-        if (!uni(L.lit.ok) || !uni(L.dist.ok) || uni(L.lit.empty)) return kCodecCorrupt;
+  uint32_t cnt[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) cnt[i] = 0;
+  uint32_t myl[5], rank[5];
+#pragma unroll
+  for (int c = 0; c < 5; c++) {
+    myl[c] = 0;
+    rank[c] = 0;
+    if (c * 64 < n) {
+      const int s = c * 64 + l;
+      myl[c] = s < n ? lens[s] : 0u;
+#pragma unroll
+      for (int L = 1; L <= 15; L++) {
+        const unsigned long long m = __ballot(myl[c] == (uint32_t)L);
+        if (myl[c] == (uint32_t)L)
+          rank[c] = cnt[L] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        cnt[L] += (uint32_t)__popcll(m);
       }
-      const bool dist_empty = has_dist && uni(L.dist.empty);
-      // huffmanBlock
-      for (;;) {
-        f.refill();
-        const int v = f.sym(L.lit, L.lfast, kLitBits);
-        if (v < 0) return kCodecCorrupt;
-        if (v < 256) {
-          if (f.olen >= f.cap) return kCodecFull;
-          f.literal((uint32_t)v);
-          continue;
-        }
-        if (f.overrun()) return kCodecEof;
-        if (v == 256) break;
-        int length, nbits;
-        if (v < 265) { length = v - (257 - 3); nbits = 0; }
-        else if (v < 269) { length = v * 2 - (265 * 2 - 11); nbits = 1; }
-        else if (v < 273) { length = v * 4 - (269 * 4 - 19); nbits = 2; }
-        else if (v < 277) { length = v * 8 - (273 * 8 - 35); nbits = 3; }
-        else if (v < 281) { length = v * 16 - (277 * 16 - 67); nbits = 4; }
-        else if (v < 285) { length = v * 32 - (281 * 32 - 131); nbits = 5; }
-        else if (v < 286) { length = 258; nbits = 0; }
-        else return kCodecCorrupt;
-        if (nbits > 0) length += (int)f.take(nbits);
-        f.refill();
-        int dist;
-        if (!has_dist) {
-          dist = (int)rev_bits(f.take(5), 5);
-        } else {
-          if (dist_empty) return kCodecCorrupt;
-          dist = f.sym(L.dist, L.dfast, kDistBits);
-          if (dist < 0) return kCodecCorrupt;
-        }
-        if (dist < 4) {
-          dist++;
-        } else if (dist < 30) {
-          const int nb = (dist - 2) >> 1;
-          const int extra = ((dist & 1) << nb) | (int)f.take(nb);
-          dist = (1 << (nb + 1)) + 1 + extra;
-        } else {
-          return kCodecCorrupt;
-        }
-        if (f.overrun()) return kCodecEof;
-        const uint64_t hist = f.olen < 32768 ? f.olen : 32768;
-        if ((uint64_t)dist > hist) return kCodecCorrupt;
-        if (f.olen + length > f.cap) return kCodecFull;
-        f.copy((uint32_t)dist, (uint32_t)length);
-      }
-    } else {
-      return kCodecCorrupt;
     }
-    if (f.overrun()) return kCodecEof;
-    if (final) break;
   }
-  f.flush_tail();
+  int mn = 0, mx = 0;
+#pragma unroll
+  for (int L = 1; L <= 15; L++)
+    if (cnt[L]) {
+      if (!mn) mn = L;
+      mx = L;
+    }
+  for (int i = l; i < (1 << root); i += 64) tab[i] = (TT)0;
+  if (mx == 0) {
+    wave_lds_sync();
+    return 1;
+  }
+  uint32_t code = 0;
+#pragma unroll
+  for (int L = 1; L <= 15; L++)
+    if (L >= mn && L <= mx) code = (code << 1) + cnt[L];
+  if (code != (1u << mx) && !(code == 1 && mx == 1)) return 2;
+  uint32_t c = 0, o = 0;
+  uint32_t first[16], offs[16];
+  first[0] = offs[0] = 0;
+#pragma unroll
+  for (int L = 1; L <= 15; L++) {
+    c = (c + cnt[L - 1]) << 1;
+    first[L] = c;
+    offs[L] = o;
+    o += cnt[L];
+  }
+  if (l < 16) {
+    uint32_t fc = 0, oc = 0, cc = 0;
+#pragma unroll
+    for (int L = 0; L < 16; L++)
+      if (l == L) {
+        fc = first[L];
+        oc = offs[L];
+        cc = cnt[L];
+      }
+    sl.count[l] = (uint16_t)cc;
+    sl.first[l] = (uint16_t)fc;
+    sl.offs[l] = (uint16_t)oc;
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    if (k * 64 < n) {
+      const uint32_t L = myl[k];
+      if (L) {
+        const uint32_t s = (uint32_t)(k * 64 + l);
+        const uint32_t cd = (uint32_t)sl.first[L] + rank[k];
+        sorted[sl.offs[L] + rank[k]] = (uint16_t)s;
+        const uint32_t rev = __brev(cd) >> (32 - L);
+        if ((int)L <= root) {
+          const TT e = (TT)tab_entry(kind, s, L);
+          for (uint32_t f = rev; f < (1u << root); f += (1u << L)) tab[f] = e;
+        } else {
+          tab[rev & ((1u << root) - 1)] = (TT)kLongMark;
+        }
+      }
+    }
+  }
+  wave_lds_sync();
   return 0;
 }
 
-__global__ void __launch_bounds__(64 * kInflWaves) k_inflate(const uint8_t *__restrict__ span, DevBufs d,
-                                                             const unsigned long long *nblocks, uint64_t nchunks,
-                                                             uint64_t dec_cap) {
-  __shared__ InflLds s_lds[kInflWaves];
-  InflLds &L = s_lds[threadIdx.x >> 6];
+// entry of a code longer than the root table (canonical walk; per lane)
+__device__ __forceinline__ uint32_t slow_walk(const TabSlow &sl, const uint16_t *sorted, uint32_t bits, int root,
+                                              int kind) {
+  for (int L = root + 1; L <= 15; L++) {
+    const uint32_t c = __brev(bits) >> (32 - L);
+    const uint32_t f = sl.first[L], k = sl.count[L];
+    if (c - f < k) return tab_entry(kind, sorted[sl.offs[L] + c - f], (uint32_t)L);
+  }
+  return 0;
+}
+
+// logical compressed dword at byte p (a multiple of 4); bytes at/after n read 0
+__device__ __forceinline__ uint32_t fetch_dword(const CompIn &in, uint64_t p) {
+  if (p >= in.n) return 0u;
+  uint32_t v;
+  if (in.regular) {  // chunk payloads of 32,740 B = 8,185 dwords: a dword never crosses a chunk
+    const uint32_t q = (uint32_t)(p >> 2);
+    const uint32_t jj = q / (kMaxPayload / 4);
+    const uint64_t w = (in.c0 + jj) * (uint64_t)(kChunk / 4) + kChunkHdr / 4 + (q - jj * (kMaxPayload / 4));
+#ifdef RIO_CHECKED
+    if (4 * w + 4 > in.span_bytes) {
+      atomicOr(in.flag, 0x100ull);
+      return 0u;
+    }
+#endif
+    v = reinterpret_cast<const uint32_t *>(in.span)[w];
+  } else {
+    v = in.byte(p) | (in.byte(p + 1) << 8) | (in.byte(p + 2) << 16) | (in.byte(p + 3) << 24);
+  }
+  if (p + 4 > in.n) v &= 0xffffffffu >> (8 * (uint32_t)(p + 4 - in.n));
+  return v;
+}
+
+// Wave-uniform bit reader over one stream (block headers, in escapes): the
+// stream's bytes through two 512 B VGPR windows (lane l holds dwords l and
+// 64+l), read with v_readlane.
+struct TokDec {
+  CompIn in;
+  StreamLds *T;
+  uint32_t c0, c1, n0, n1;
+  uint64_t wbase;
+  uint32_t wi;
+  uint64_t bitbuf;
+  int nb;
+
+  __device__ __forceinline__ uint32_t win_dword(uint64_t b, int k) const {
+    return fetch_dword(in, b + 4 * (uint64_t)(64 * k + lane_id()));
+  }
+  __device__ __forceinline__ void seek(uint64_t bit) {
+    const uint64_t byte = (bit >> 5) << 2;
+    wbase = byte;
+    wi = 0;
+    c0 = win_dword(byte, 0);
+    c1 = win_dword(byte, 1);
+    n0 = win_dword(byte + 512, 0);
+    n1 = win_dword(byte + 512, 1);
+    bitbuf = 0;
+    nb = 0;
+    refill();
+    take((int)(bit & 31));
+  }
+  __device__ __forceinline__ void refill() {
+    if (wi >= 128) {
+      c0 = n0;
+      c1 = n1;
+      wbase += 512;
+      wi -= 128;
+      n0 = win_dword(wbase + 512, 0);
+      n1 = win_dword(wbase + 512, 1);
+    }
+    const uint32_t v = (wi & 64) ? c1 : c0;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane(v, wi & 63);
+    bitbuf |= (uint64_t)w << nb;
+    nb += 32;
+    wi++;
+    // wave-uniform by construction; re-assert it so the state stays in SGPRs
+    bitbuf = uni64(bitbuf);
+    nb = (int)uni((uint32_t)nb);
+    wi = uni(wi);
+    wbase = uni64(wbase);
+  }
+  __device__ __forceinline__ uint32_t take(int k) {
+    const uint32_t v = (uint32_t)(bitbuf & ((1ull << k) - 1));
+    bitbuf >>= k;
+    nb -= k;
+    return v;
+  }
+  __device__ __forceinline__ uint64_t bitpos() const { return 8 * (wbase + 4 * (uint64_t)wi) - (uint64_t)nb; }
+  __device__ __forceinline__ bool overrun() const { return bitpos() > 8 * in.n; }
+};
+
+__device__ __forceinline__ void fixed_tables(StreamLds &T) {
   const int l = lane_id();
-  const uint64_t nb = *nblocks;
-  // one wave per workgroup: the block index is wave-uniform, so the decoder
-  // state derived from it lives in scalar registers (no exec-mask branches)
-  static_assert(kInflWaves == 1, "k_inflate assumes one wave per workgroup");
-  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
-    const uint64_t c0 = uni64(d.blk_c0[b]);
-    const unsigned long long meta = uni64(d.blk_meta[b]);
-    const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
-    // incomplete blocks, and magics that are never untransformed (the header
-    // block is idTransform, registry.go:31; others are errors): nothing decoded
-    if (!(meta & kMetaComplete) || (cls != kMagicPacked && cls != kMagicTrailer)) {
-      if (l == 0) d.blk_out_len[b] = 0;
+  wave_lds_sync();
+  for (int i = l; i < 288; i += 64) T.lens[i] = (uint8_t)(i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8);
+  wave_lds_sync();
+  build_table(T.lens, 288, T.lit, kTokLitRoot, T.ls, T.lsym, kTabLit);
+  for (int i = l; i < 32; i += 64) T.lens[i] = 5;
+  wave_lds_sync();
+  build_table(T.lens, 32, T.dst, kTokDistRoot, T.ds, T.dsym, kTabDist);
+}
+
+// dynamic block header (RFC 1951 §3.2.7; Go inflate.go readHuffman)
+__device__ __forceinline__ int read_dynamic(TokDec &t) {
+  StreamLds &T = *t.T;
+  const int l = lane_id();
+  if (t.nb < 32) t.refill();
+  const uint32_t nlit = t.take(5) + 257, ndist = t.take(5) + 1, nclen = t.take(4) + 4;
+  if (nlit > 286 || ndist > 30) return kCodecCorrupt;
+  wave_lds_sync();
+  if (l < 19) T.cl[l] = 0;
+  wave_lds_sync();
+  for (uint32_t i = 0; i < nclen; i++) {
+    if (t.nb < 32) t.refill();
+    const uint32_t v = t.take(3);
+    if (l == 0) T.cl[kClenOrder[i]] = (uint8_t)v;
+  }
+  wave_lds_sync();
+  if (build_table(T.cl, 19, T.dst, kTokDistRoot, T.ds, T.dsym, kTabClen) != 0) return kCodecCorrupt;
+  const uint32_t n = nlit + ndist;
+  uint32_t i = 0, prev = 0;
+  while (i < n) {
+    if (t.nb < 32) t.refill();
+    const uint32_t e = uni(T.dst[t.bitbuf & ((1u << kTokDistRoot) - 1)]);
+    const uint32_t L = e & 15;
+    if (!L) return kCodecCorrupt;
+    t.take((int)L);
+    const uint32_t x = e >> 16;
+    if (x < 16) {
+      if (l == 0) T.lens[i] = (uint8_t)x;
+      prev = x;
+      i++;
       continue;
     }
-    CompIn in;
-    in.span = span;
-    in.span_bytes = nchunks * (uint64_t)kChunk;
-    in.flag = &d.ctl->out_overflow;
-    in.ck_size = d.ck_size;
-    in.ck_pay = d.ck_pay;
-    in.c0 = c0;
-    in.total = meta & kMetaTotalMask;
-    in.n = uni64(d.blk_len[b]);
-    in.pay0 = uni64(d.ck_pay[c0]);
-    in.regular = (meta & kMetaRegular) != 0;
-    const uint64_t off = uni64(d.blk_dec_off[b]);
-    const uint64_t cap = uni64(d.blk_out_len[b]);  // the bound from k_codec_prepare
-    if (off + cap > dec_cap) {  // the regions need a larger buffer (host retries)
-      if (l == 0) {
-        atomicOr(&d.ctl->out_overflow, 0x40ull);
-        atomicMax(&d.ctl->dec_need, (unsigned long long)(off + cap));
-        d.blk_out_len[b] = 0;
-      }
-      continue;
+    uint32_t rep, b;
+    if (x == 16) {
+      if (i == 0) return kCodecCorrupt;
+      b = prev;
+      rep = 3 + t.take(2);
+    } else if (x == 17) {
+      b = 0;
+      rep = 3 + t.take(3);
+    } else {
+      b = 0;
+      rep = 11 + t.take(7);
     }
-    Fast f;
-    f.in = &in;
-    f.L = &L;
-    f.out = d.dec + off;
-    f.out_room = dec_cap - off;
-    f.cap = cap;
-    f.base = 0;
-    f.pos = 0;
-    f.bitbuf = 0;
-    f.nb = 0;
-    f.olen = 0;
-    f.flushed = 0;
-    f.stage(0);
-    const int err = inflate_fast(f);
-    if (l == 0) {
-      if (err) {  // k_inflate_exact classifies it (Go's lazy byte pulls) or sizes it
-        d.blk_status[b] = kBlkCodec;
-        d.blk_a[b] = kCodecPending;
-        d.blk_b[b] = (unsigned long long)err;
-        d.blk_hdr[b] = f.olen | ((unsigned long long)f.pos << 32);  // where the fast pass stopped (debug)
+    if (i + rep > n) return kCodecCorrupt;
+    for (uint32_t j = l; j < rep; j += 64) T.lens[i + j] = (uint8_t)b;
+    prev = b;
+    i += rep;
+  }
+  wave_lds_sync();
+  if (build_table(T.lens, (int)nlit, T.lit, kTokLitRoot, T.ls, T.lsym, kTabLit) != 0) return kCodecCorrupt;
+  if (build_table(T.lens + nlit, (int)ndist, T.dst, kTokDistRoot, T.ds, T.dsym, kTabDist) == 2) return kCodecCorrupt;
+  return 0;
+}
+
+// stream modes of k_flate_tok
+enum : uint32_t {
+  kVHuff = 0,    // decoding symbols of a fixed / dynamic block
+  kVStored = 1,  // copying a stored block's bytes into literal tokens
+  kVHeader = 2,  // escape: read the next DEFLATE block header
+  kVFinish = 3,  // escape: write the block's result (res)
+  kVNew = 4,     // escape: pick up the next recordio block
+  kVGone = 5,    // no blocks left
+};
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t lane) {
+  return (uint32_t)__builtin_amdgcn_readlane(v, lane);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t lane) {
+  return ((uint64_t)rl32((uint32_t)(v >> 32), lane) << 32) | rl32((uint32_t)v, lane);
+}
+
+__device__ __forceinline__ CompIn make_in(const uint8_t *span, const DevBufs &d, uint64_t nchunks, uint64_t c0,
+                                          uint64_t total, uint64_t n, bool regular) {
+  CompIn in;
+  in.span = span;
+  in.span_bytes = nchunks * (uint64_t)kChunk;
+  in.flag = &d.ctl->out_overflow;
+  in.ck_size = d.ck_size;
+  in.ck_pay = d.ck_pay;
+  in.c0 = c0;
+  in.total = total;
+  in.n = n;
+  in.pay0 = d.ck_pay[c0];
+  in.regular = regular;
+  return in;
+}
+
+__global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ span, DevBufs d,
+                                                  const unsigned long long *nblocks, uint64_t nchunks,
+                                                  uint64_t dec_cap, int round, int last_round) {
+  __shared__ StreamLds S[kVS];
+  const int l = lane_id();
+  const uint32_t g = (uint32_t)l >> 3, j = (uint32_t)l & 7;
+  StreamLds &M = S[g];
+  if (round > 0 && uni64(d.fl_more[round - 1]) == 0) return;
+  const uint64_t nblk = uni64(*nblocks);
+  const uint64_t stride = (uint64_t)gridDim.x * kVS;
+
+  // stream state (the same in the 8 lanes of a group)
+  uint64_t next_b = (uint64_t)blockIdx.x * kVS + g, cur_b = 0;
+  uint32_t mode = kVNew, res = 0;
+  uint32_t bc0 = 0, bn = 0, btot = 0, breg = 0, tcap = 0, cap = 0;  // block
+  uint64_t bitbuf = 0;                                               // bit reader
+  uint32_t nbits = 0, rpos = 0, rhi = 0, nw0 = 0, nw1 = 0;
+  uint32_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0;                       // next 128 B of the ring
+  uint32_t olen = 0, fin = 0, left = 0, fixed_ok = 0;                // decode
+  uint64_t hdrpos = 0;
+  uint32_t nst = 0, nv = 0, pend = 0, npend = 0;                     // tokens
+
+  for (;;) {
+    // ---------------------------------------------------------- escapes
+    unsigned long long esc = __ballot(j == 0 && mode >= kVHeader && mode <= kVNew);
+    while (esc) {
+      const uint32_t gl = (uint32_t)__ffsll((long long)esc) - 1;
+      esc &= esc - 1;
+      const uint32_t gg = gl >> 3;
+      const bool mine = g == gg;
+      StreamLds &G = S[gg];
+      uint32_t sm = rl32(mode, gl);
+      uint64_t sb = rl64(cur_b, gl);
+      uint32_t s_c0 = rl32(bc0, gl), s_n = rl32(bn, gl), s_tot = rl32(btot, gl), s_reg = rl32(breg, gl);
+      uint32_t s_olen = rl32(olen, gl), s_fin = rl32(fin, gl), s_left = rl32(left, gl), s_fixed = rl32(fixed_ok, gl);
+      uint32_t s_nst = rl32(nst, gl);
+      uint64_t s_hdr = rl64(hdrpos, gl);
+      uint64_t s_bit = 32 * (uint64_t)rl32(rpos, gl) - rl32(nbits, gl);
+      uint64_t s_next = rl64(next_b, gl);
+      uint32_t s_tcap = rl32(tcap, gl), s_cap = rl32(cap, gl);
+      bool seek = false, fresh = false;  // fresh: a block ended or began, no pending literals
+      int r = 0;
+      if (sm == kVFinish) {
+        r = (int)rl32(res, gl);
+        FlState *sp = &d.fl[sb];
+        uint32_t stm = kFlDone;
+        if (r == kTokYield || r == kTokDone) {
+          const uint32_t sp_n = rl32(npend, gl);
+          if (sp_n) {  // pending literals (room for one token is kept)
+            if (l == 0) d.tok[(uint64_t)s_c0 * kTokPerChunk + s_nst] = rl32(pend, gl) | (sp_n << 24);
+            s_nst++;
+          }
+          if (r == kTokYield) {
+            const uint32_t vm = rl32(mode, gl);  // unused: the stream's mode before the yield is in s_left/s_fixed
+            (void)vm;
+            stm = s_left ? kFlStored : (s_fixed ? kFlFixed : kFlDynamic);
+            if (last_round) {  // more rounds needed than were launched: the host retries with more
+              if (l == 0) atomicOr(&d.ctl->out_overflow, 0x1000ull);
+              stm = kFlSkip;
+            }
+          }
+        }
+        if (l == 0) {
+          sp->round = (uint32_t)round;
+          sp->ntok = s_nst;
+          if (round == 0) sp->olen2 = 0;
+          if (stm == kFlSkip) {
+            sp->mode = kFlSkip;
+            d.blk_out_len[sb] = 0;
+          } else if (r == kTokDone || r == kTokYield) {
+            sp->mode = stm;
+            sp->olen = s_olen;
+            if (r == kTokYield) {
+              sp->bitpos = s_bit;
+              sp->hdrpos = s_hdr;
+              sp->final_ = s_fin;
+              sp->stored_left = s_left;
+              atomicAdd(&d.fl_more[round], 1ull);
+            }
+          } else {  // k_inflate_exact classifies it (Go's lazy byte pulls) or sizes it
+            sp->bitpos = s_bit;  // where the fast pass stopped and why (RIO_DEBUG)
+            sp->olen = s_olen;
+            sp->pad = (uint32_t)r;
+            sp->mode = kFlError;
+            d.blk_status[sb] = kBlkCodec;
+            d.blk_a[sb] = r == kCodecUnsupported ? (unsigned long long)kCodecUnsupported : kCodecPending;
+            d.blk_b[sb] = (unsigned long long)r;
+            d.blk_out_len[sb] = 0;
+          }
+        }
+        sm = kVNew;
+        r = 0;
+        fresh = true;
       }
-      d.blk_out_len[b] = err ? 0 : f.olen;
+      CompIn in;
+      if (sm == kVNew) {
+        for (;;) {
+          if (s_next >= nblk) {
+            sm = kVGone;
+            break;
+          }
+          sb = s_next;
+          s_next += stride;
+          FlState *sp = &d.fl[sb];
+          const uint64_t c0 = uni64(d.blk_c0[sb]);
+          const unsigned long long meta = uni64(d.blk_meta[sb]);
+          uint32_t stm;
+          if (round == 0) {
+            const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
+            // incomplete blocks, and magics that are never untransformed (the header
+            // block is idTransform, registry.go:31; others are errors): nothing decoded
+            bool skip = !(meta & kMetaComplete) || (cls != kMagicPacked && cls != kMagicTrailer);
+            const uint64_t off = uni64(d.blk_dec_off[sb]), cp = uni64(d.blk_out_len[sb]);
+            if (!skip && off + cp > dec_cap) {  // the regions need a larger buffer (host retries)
+              skip = true;
+              if (l == 0) {
+                atomicOr(&d.ctl->out_overflow, 0x40ull);
+                atomicMax(&d.ctl->dec_need, (unsigned long long)(off + cp));
+              }
+            }
+            if (skip) {
+              if (l == 0) {
+                sp->mode = kFlSkip;
+                sp->round = 0;
+                d.blk_out_len[sb] = 0;
+              }
+              continue;
+            }
+            stm = kFlHeader;
+            s_bit = s_hdr = 0;
+            s_olen = s_fin = s_left = 0;
+          } else {
+            stm = uni(sp->mode);
+            if (stm >= kFlDone) continue;
+            s_bit = uni64(sp->bitpos);
+            s_hdr = uni64(sp->hdrpos);
+            s_olen = (uint32_t)uni64(sp->olen);
+            s_fin = uni(sp->final_);
+            s_left = uni(sp->stored_left);
+          }
+          const uint64_t n = uni64(d.blk_len[sb]);
+          const uint64_t total = meta & kMetaTotalMask;
+          const uint64_t tc = total * (uint64_t)kTokPerChunk;
+          const uint64_t cp = uni64(d.blk_out_len[sb]);
+          s_c0 = (uint32_t)c0;
+          s_n = (uint32_t)n;
+          s_tot = (uint32_t)total;
+          s_reg = (meta & kMetaRegular) != 0;
+          s_tcap = tc > 0xffffff00ull ? 0xffffff00u : (uint32_t)tc;
+          s_cap = cp > 0xfffff000ull ? 0xfffff000u : (uint32_t)cp;
+          s_nst = 0;
+          s_fixed = 0;
+          in = make_in(span, d, nchunks, c0, total, n, s_reg != 0);
+          if (n >= (1ull << 28) || c0 >= (1ull << 32)) {  // beyond the 32-bit stream state of this kernel
+            r = kCodecUnsupported;
+            sm = kVFinish;
+            break;
+          }
+          if (stm == kFlDynamic) {
+            TokDec t;
+            t.in = in;
+            t.T = &G;
+            t.seek(s_hdr);
+            if (read_dynamic(t)) {
+              r = kCodecCorrupt;
+              sm = kVFinish;
+              break;
+            }
+          } else if (stm == kFlFixed) {
+            fixed_tables(G);
+            s_fixed = 1;
+          }
+          sm = stm == kFlHeader ? kVHeader : stm == kFlStored ? kVStored : kVHuff;
+          seek = sm != kVHeader;
+          break;
+        }
+      } else {
+        in = make_in(span, d, nchunks, s_c0, s_tot, s_n, s_reg != 0);
+      }
+      // DEFLATE block headers until a block with content (or the end)
+      while (sm == kVHeader) {
+        TokDec t;
+        t.in = in;
+        t.T = &G;
+        t.seek(s_bit);
+        if (t.nb < 32) t.refill();
+        s_fin = t.take(1);
+        const uint32_t type = t.take(2);
+        if (type == 0) {
+          t.take(t.nb & 7);  // to the byte boundary
+          if (t.nb < 32) t.refill();
+          const uint32_t len = t.take(16), nlen = t.take(16);
+          if ((uint16_t)nlen != (uint16_t)~len) r = kCodecCorrupt;
+          else if (t.bitpos() / 8 + len > in.n) r = kCodecEof;
+          else if (len > s_cap - s_olen) r = kCodecFull;
+          s_left = len;
+          sm = kVStored;
+        } else if (type == 1) {
+          if (!s_fixed) fixed_tables(G);
+          s_fixed = 1;
+          sm = kVHuff;
+        } else if (type == 2) {
+          s_hdr = t.bitpos();
+          r = read_dynamic(t);
+          s_fixed = 0;
+          sm = kVHuff;
+        } else {
+          r = kCodecCorrupt;
+        }
+        if (!r && t.overrun()) r = kCodecEof;
+        s_bit = t.bitpos();
+        if (r) {
+          sm = kVFinish;
+        } else if (sm == kVStored && s_left == 0) {  // empty stored block
+          sm = s_fin ? kVFinish : kVHeader;
+          r = kTokDone;
+        }
+        seek = sm != kVFinish;
+      }
+      // write the stream state back to its lanes
+      if (seek) {  // refill the ring at s_bit: 64 dwords from the dword before it
+        const uint32_t dw = (uint32_t)(s_bit >> 5), base = dw & ~3u;
+        wave_lds_sync();
+        G.ring[(base + l) & (kRingDw - 1)] = fetch_dword(in, 4 * (uint64_t)(base + l));
+        wave_lds_sync();
+        if (mine) {
+          const uint32_t sh = (uint32_t)(s_bit & 31);
+          bitbuf = (uint64_t)(M.ring[dw & (kRingDw - 1)] >> sh);
+          nbits = 32 - sh;
+          rpos = dw + 1;
+          nw0 = M.ring[rpos & (kRingDw - 1)];
+          nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];
+          rhi = base + 64;
+          pf0 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j));
+          pf1 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 1));
+          pf2 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 2));
+          pf3 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 3));
+        }
+      }
+      if (mine) {
+        mode = sm;
+        res = (uint32_t)r;
+        cur_b = sb;
+        next_b = s_next;
+        bc0 = s_c0;
+        bn = s_n;
+        btot = s_tot;
+        breg = s_reg;
+        tcap = s_tcap;
+        cap = s_cap;
+        olen = s_olen;
+        fin = s_fin;
+        left = s_left;
+        fixed_ok = s_fixed;
+        hdrpos = s_hdr;
+        nst = s_nst;
+        if (sm == kVFinish && !seek) {  // (errors keep the bit position for nothing)
+          rpos = (uint32_t)(s_bit >> 5);
+          nbits = 0;
+        }
+        nv = 0;
+        if (fresh) pend = npend = 0;
+      }
+    }
+    if (!__ballot(mode != kVGone)) break;
+
+    // ---------------------------------------------------------- decode steps
+#define RIO_REFILL()                                                 \
+  if (nbits < 32) {                                                  \
+    bitbuf |= (uint64_t)nw0 << nbits;                                \
+    nbits += 32;                                                     \
+    nw0 = nw1;                                                       \
+    rpos++;                                                          \
+    nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];                        \
+  }
+#define RIO_EMIT(t_)                                                 \
+  {                                                                  \
+    if (j == 0) M.tbuf[nv] = (t_);                                   \
+    nv++;                                                            \
+  }
+    for (int step = 0; step < kPass; step++) {
+      if (mode == kVHuff) {
+        if (tcap - nst - nv < 3) {
+          res = (uint32_t)kTokYield;
+          mode = kVFinish;
+        } else {
+          RIO_REFILL();
+          uint32_t e = M.lit[(uint32_t)bitbuf & ((1u << kTokLitRoot) - 1)];
+          uint32_t L = e & 15;
+          if (L == 0 && (e & kEnLenBit)) {
+            e = slow_walk(M.ls, M.lsym, (uint32_t)bitbuf, kTokLitRoot, kTabLit);
+            L = e & 15;
+          }
+          const uint32_t E = (e >> 5) & 7;
+          if (L == 0) {
+            res = kCodecCorrupt;
+            mode = kVFinish;
+          } else if (!(e & kEnLenBit)) {
+            bitbuf >>= L;
+            nbits -= L;
+            if (olen >= cap) {
+              res = kCodecFull;
+              mode = kVFinish;
+            } else {
+              olen++;
+              pend |= (e >> 8) << (8 * npend);
+              if (++npend == 3) {
+                RIO_EMIT(pend | (3u << 24));
+                pend = 0;
+                npend = 0;
+              }
+            }
+          } else if (E == kEobExtra) {
+            bitbuf >>= L;
+            nbits -= L;
+            if (fin) {
+              res = (32 * rpos - nbits > 8 * bn) ? (uint32_t)kCodecEof : (uint32_t)kTokDone;
+              mode = kVFinish;
+            } else {
+              mode = kVHeader;
+            }
+          } else {  // length, then the distance code
+            const uint32_t len = (e >> 8) + 3 + ((uint32_t)(bitbuf >> L) & ((1u << E) - 1));
+            bitbuf >>= (L + E);
+            nbits -= L + E;
+            RIO_REFILL();
+            uint32_t dd = M.dst[(uint32_t)bitbuf & ((1u << kTokDistRoot) - 1)];
+            uint32_t L2 = dd & 15;
+            if (L2 == 0 && (dd & kEnLenBit)) {
+              dd = slow_walk(M.ds, M.dsym, (uint32_t)bitbuf, kTokDistRoot, kTabDist);
+              L2 = dd & 15;
+            }
+            if (L2 == 0) {
+              res = kCodecCorrupt;
+              mode = kVFinish;
+            } else {
+              const uint32_t E2 = (dd >> 8) & 15;
+              const uint32_t dist = (dd >> 16) + ((uint32_t)(bitbuf >> L2) & ((1u << E2) - 1));
+              bitbuf >>= (L2 + E2);
+              nbits -= L2 + E2;
+              const uint32_t hist = olen < 32768u ? olen : 32768u;
+              if (dist > hist) {
+                res = kCodecCorrupt;
+                mode = kVFinish;
+              } else if (len > cap - olen) {
+                res = kCodecFull;
+                mode = kVFinish;
+              } else {
+                if (npend) {
+                  RIO_EMIT(pend | (npend << 24));
+                  pend = 0;
+                  npend = 0;
+                }
+                RIO_EMIT(0x80000000u | ((len - 3) << 16) | (dist - 1));
+                olen += len;
+              }
+            }
+          }
+        }
+      } else if (mode == kVStored) {
+        if (tcap - nst - nv < 3) {
+          res = (uint32_t)kTokYield;
+          mode = kVFinish;
+        } else {
+          RIO_REFILL();
+          if (npend) {  // literals before the stored bytes
+            RIO_EMIT(pend | (npend << 24));
+            pend = 0;
+            npend = 0;
+          }
+          const uint32_t k = left < 3 ? left : 3;
+          const uint32_t v = (uint32_t)bitbuf & (0xffffffffu >> (32 - 8 * k));
+          bitbuf >>= 8 * k;
+          nbits -= 8 * k;
+          RIO_EMIT(v | (k << 24));
+          olen += k;
+          left -= k;
+          if (left == 0) {
+            if (fin) {
+              res = (32 * rpos - nbits > 8 * bn) ? (uint32_t)kCodecEof : (uint32_t)kTokDone;
+              mode = kVFinish;
+            } else {
+              mode = kVHeader;
+            }
+          }
+        }
+      }
+    }
+#undef RIO_REFILL
+#undef RIO_EMIT
+
+    // ---------------------------------------------------------- input pass
+    {
+      uint32_t *tk = d.tok + (uint64_t)bc0 * kTokPerChunk + nst;
+      for (uint32_t k = j; k < nv; k += 8) tk[k] = M.tbuf[k];
+      nst += nv;
+      nv = 0;
+      if (mode <= kVStored) {
+        if (rhi - rpos <= kRingDw - 32) {
+          *reinterpret_cast<uint4 *>(&M.ring[(rhi + 4 * j) & (kRingDw - 1)]) = make_uint4(pf0, pf1, pf2, pf3);
+          rhi += 32;
+          CompIn in = make_in(span, d, nchunks, bc0, btot, bn, breg != 0);
+          pf0 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j));
+          pf1 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 1));
+          pf2 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 2));
+          pf3 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 3));
+        }
+        if (32 * rpos - nbits > 8 * bn + 1024) {  // runaway past the end of the input
+          res = kCodecEof;
+          mode = kVFinish;
+        }
+      }
+      wave_lds_sync();
     }
   }
 }
 
-// The blocks k_inflate failed on: the exact restatement gives the reference's
-// error (and CorruptInputError offset). One wave per failing block, lane 0.
+constexpr int kLzWin = 65536;  // 32 KiB of history + the largest batch (64 x 258 B) + one flush unit
+
+__global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long long *nblocks, int round) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kLzWin];
+  const int l = lane_id();
+  if (round > 0 && uni64(d.fl_more[round - 1]) == 0) return;
+  const uint64_t nb = uni64(*nblocks);
+  constexpr uint32_t M = kLzWin - 1;
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    FlState *sp = &d.fl[b];
+    const uint32_t mode = uni(sp->mode);
+    if (uni(sp->round) != (uint32_t)round || mode == kFlError || mode == kFlSkip) continue;
+    uint64_t olen = uni64(sp->olen2);
+    const uint32_t ntok = uni(sp->ntok);
+    uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
+    const uint32_t *tk = d.tok + uni64(d.blk_c0[b]) * (uint64_t)kTokPerChunk;
+    wave_lds_sync();
+    if (olen > 0) {  // resumed: the history this block has already written
+      const uint64_t h = olen < 32768ull ? olen : 32768ull;
+      for (uint64_t k = l; k < h; k += 64) win[(olen - h + k) & M] = out[olen - h + k];
+      wave_lds_sync();
+    }
+    uint64_t flushed = olen;
+    uint32_t t_next = ((uint32_t)l < ntok) ? tk[l] : 0u;
+    for (uint32_t i0 = 0; i0 < ntok; i0 += 64) {
+      const uint32_t t = t_next;
+      t_next = (i0 + 64 + (uint32_t)l < ntok) ? tk[i0 + 64 + l] : 0u;
+      const bool m = (t >> 31) != 0;
+      const uint32_t len = m ? ((t >> 16) & 0xffu) + 3 : (t >> 24) & 3u;
+      const uint32_t incl = wave_incl_sum(len);
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+      const uint32_t p = incl - len;  // position relative to olen
+      const uint32_t base = (uint32_t)olen;
+      if (!m) {
+        if (len > 0) win[(base + p) & M] = (uint8_t)t;
+        if (len > 1) win[(base + p + 1) & M] = (uint8_t)(t >> 8);
+        if (len > 2) win[(base + p + 2) & M] = (uint8_t)(t >> 16);
+      }
+      const uint32_t dist = (t & 0x7fffu) + 1;
+      const int src_end = (int)p - (int)dist + (int)(len < dist ? len : dist);
+      unsigned long long pend = __ballot(m);
+      while (pend) {
+        // everything before the first unresolved match is final
+        const int R = (int)__builtin_amdgcn_readlane(p, __ffsll((long long)pend) - 1);
+        const bool ready = ((pend >> l) & 1ull) && src_end <= R;
+        if (ready) {
+          const uint32_t s = base + p - dist, q = base + p;
+          uint32_t k = 0;
+          if (dist >= 8) {
+            for (; k + 8 <= len; k += 8) {
+              uint8_t v[8];
+#pragma unroll
+              for (int jj = 0; jj < 8; jj++) v[jj] = win[(s + k + jj) & M];
+#pragma unroll
+              for (int jj = 0; jj < 8; jj++) win[(q + k + jj) & M] = v[jj];
+            }
+          }
+          for (; k < len; k++) win[(q + k) & M] = win[(s + k) & M];
+        }
+        pend &= ~__ballot(ready);
+      }
+      olen += total;
+      if ((olen & ~1023ull) > flushed) {
+        wave_lds_sync();
+        for (uint64_t u0 = flushed & ~1023ull; u0 + 1024 <= olen; u0 += 1024) {
+          const uint4 v = *reinterpret_cast<const uint4 *>(win + ((u0 + 16 * l) & M));
+          *reinterpret_cast<uint4 *>(out + u0 + 16 * l) = v;
+          flushed = u0 + 1024;
+        }
+      }
+    }
+    wave_lds_sync();
+    for (uint64_t k = flushed + l; k < olen; k += 64) out[k] = win[k & M];
+    if (l == 0) {
+      sp->olen2 = olen;
+      if (mode == kFlDone) d.blk_out_len[b] = olen;
+    }
+  }
+}
+
+// The blocks the fast path failed on: the exact restatement gives the
+// reference's error (and CorruptInputError offset). One wave per failing block, lane 0.
 __global__ void __launch_bounds__(64) k_inflate_exact(const uint8_t *__restrict__ span, DevBufs d,
                                                       const unsigned long long *nblocks) {
   __shared__ InflLds L;
@@ -893,11 +1362,21 @@ __global__ void __launch_bounds__(64) k_inflate_exact(const uint8_t *__restrict_
 }
 
 void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
-                    uint64_t nchunks, uint64_t dec_cap, hipStream_t st) {
-  uint64_t g = (max_blocks + kInflWaves - 1) / kInflWaves;
-  if (g > 8192) g = 8192;
-  if (g < 1) g = 1;
-  hipLaunchKernelGGL(k_inflate, dim3((unsigned)g), dim3(64 * kInflWaves), 0, st, span, d, nblocks, nchunks, dec_cap);
+                    uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st) {
+  (void)hipMemsetAsync(d.fl_more, 0, sizeof(unsigned long long) * rounds, st);
+  uint64_t g1 = (max_blocks + kVS - 1) / kVS;
+  const uint64_t r1 = (uint64_t)ncu * 4;  // 4 waves of 8 streams per CU (LDS-bound)
+  if (g1 > r1) g1 = r1;
+  if (g1 < 1) g1 = 1;
+  uint64_t g2 = max_blocks;
+  const uint64_t r2 = (uint64_t)ncu * 2;  // 64 KiB windows: 2 per CU
+  if (g2 > r2) g2 = r2;
+  if (g2 < 1) g2 = 1;
+  for (int r = 0; r < rounds; r++) {
+    hipLaunchKernelGGL(k_flate_tok, dim3((unsigned)g1), dim3(64), 0, st, span, d, nblocks, nchunks,
+                       dec_cap, r, (int)(r == rounds - 1));
+    hipLaunchKernelGGL(k_flate_lz, dim3((unsigned)g2), dim3(64), 0, st, d, nblocks, r);
+  }
   uint64_t ge = (max_blocks + 63) / 64;
   if (ge > 1024) ge = 1024;
   if (ge < 1) ge = 1;

@@ -43,7 +43,8 @@ void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const C
 void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
                           uint32_t factor, hipStream_t st);
 void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks_dev,
-                         uint64_t max_blocks, uint64_t nchunks, int codec, uint64_t dec_cap, hipStream_t st);
+                         uint64_t max_blocks, uint64_t nchunks, int codec, uint64_t dec_cap, int rounds, int ncu,
+                         hipStream_t st);
 }  // namespace rio
 
 using namespace rio;
@@ -81,6 +82,7 @@ struct rio_ctx {
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
   uint64_t side_cap = 0, item_cap = 0, dec_cap = 0;
   uint32_t dec_factor = 8;  // first-attempt decode-region bound: compressed bytes x this
+  int fl_rounds = kFlRounds;  // flate Huffman/copy rounds per span (doubled if a block needs more)
   DevBufs d{};
   unsigned long long *nblocks_dev = nullptr;
   uint8_t *d_span = nullptr;  // staging for host spans (lazy)
@@ -123,7 +125,7 @@ static int alloc_bufs(rio_ctx *c) {
   if (dalloc(&d.blk_c0, nb) || dalloc(&d.blk_meta, nb) || dalloc(&d.blk_len, nb) || dalloc(&d.blk_nitems, nb) ||
       dalloc(&d.blk_hdr, nb) || dalloc(&d.blk_item_base, nb + 1) || dalloc(&d.blk_status, nb) ||
       dalloc(&d.blk_a, nb) || dalloc(&d.blk_b, nb) || dalloc(&d.blk_out_len, nb) || dalloc(&d.blk_dec_off, nb + 1) ||
-      dalloc(&d.blk_need, nb))
+      dalloc(&d.blk_need, nb) || dalloc(&d.fl, nb))
     return -1;
   if (dalloc(&d.scan_tmp, (n + 2047) / 2048 + 16) || dalloc(&d.strad, n)) return -1;
   if (dalloc(&d.item_off, c->item_cap) || dalloc(&d.item_len, c->item_cap) || dalloc(&d.side, c->side_cap))
@@ -135,7 +137,7 @@ static void free_all(rio_ctx *c) {
   DevBufs &d = c->d;
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.item_off, d.item_len, d.side,
-                d.strad, d.scan_tmp, d.dec, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
+                d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span};
   for (void *p : ps)
     if (p) hipFree(p);
@@ -175,7 +177,7 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   HIP_OK(hipEventCreateWithFlags(&c->evB, hipEventDisableTiming));
   if (alloc_bufs(c)) return -1;
   DevBufs &d = c->d;
-  if (dalloc(&d.ctl, 1) || dalloc(&c->nblocks_dev, 2)) return -1;
+  if (dalloc(&d.ctl, 1) || dalloc(&c->nblocks_dev, 2) || dalloc(&d.fl_more, 64)) return -1;
   // CRC tables
   std::vector<uint32_t> fold(kFoldWords), mul(kMulTables * 1024), fa(kMaxPayload + 1), fb(kMaxPayload + 1);
   build_crc_tables(fold.data(), mul.data(), fa.data(), fb.data());
@@ -219,6 +221,15 @@ static int ensure_dec(rio_ctx *c, uint64_t need) {
   return 0;
 }
 
+// flate token regions: kTokPerChunk u32 per chunk of the span
+static int ensure_tok(rio_ctx *c, uint64_t nchunks) {
+  const uint64_t need = nchunks * (uint64_t)kTokPerChunk;
+  if (c->d.tok_cap >= need) return 0;
+  if (dalloc(&c->d.tok, need)) return -1;
+  c->d.tok_cap = need;
+  return 0;
+}
+
 // Enqueue the full pipeline for `nchunks` whole chunks at device span `span`.
 static int ensure_side(rio_ctx *c, uint64_t need) {
   if (c->side_cap >= need) return 0;
@@ -252,8 +263,9 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   if (codec != RIO_CODEC_NONE && nchunks > 0) {
     // decode regions: factor x the compressed bytes per block (+4 KiB each)
     if (ensure_dec(c, (uint64_t)c->dec_factor * nchunks * kChunk + nchunks * 4352ull)) return -1;
+    if (codec == RIO_CODEC_FLATE && ensure_tok(c, nchunks)) return -1;
     launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
-    launch_codec_decode(span, d, c->nblocks_dev, max_blocks, nchunks, codec, c->dec_cap, st);
+    launch_codec_decode(span, d, c->nblocks_dev, max_blocks, nchunks, codec, c->dec_cap, c->fl_rounds, c->ncu, st);
     c->last_had_dec = true;
   }
   HIP_OK(hipEventRecord(c->ev[kEvDec], st));
@@ -387,6 +399,8 @@ static void debug_dump(rio_ctx *c) {
     hipMemcpy(hd.data(), c->d.blk_hdr, 8 * nb, hipMemcpyDeviceToHost);
   }
   fprintf(stderr, "rio debug: nblocks=%llu overflow=%llu\n", nb, (unsigned long long)c->h_ctl->out_overflow);
+  std::vector<FlState> fl(nb);
+  if (nb && c->d.fl) hipMemcpy(fl.data(), c->d.fl, sizeof(FlState) * nb, hipMemcpyDeviceToHost);
   int shown = 0;
   for (uint64_t b = 0; b < nb && shown < 24; b++) {
     if (b >= 4 && st[b] == 0) continue;
@@ -395,6 +409,9 @@ static void debug_dump(rio_ctx *c) {
             "  blk %llu c0=%llu status=%llu meta=%llx len=%llu out_len=%llu dec_off=%llu nitems=%llu base=%llu "
             "a=%llu b=%llu hdr=%llx\n",
             (unsigned long long)b, a[b], st[b], me[b], bl[b], ol[b], doff[b], ni[b], ib[b], ea[b], eb[b], hd[b]);
+    if (c->d.fl)
+      fprintf(stderr, "    fl: mode=%u round=%u ntok=%u olen=%llu olen2=%llu bitpos=%llu hdrpos=%llu fast_err=%d\n", fl[b].mode,
+              fl[b].round, fl[b].ntok, fl[b].olen, fl[b].olen2, fl[b].bitpos, fl[b].hdrpos, (int)fl[b].pad);
   }
 }
 
@@ -421,6 +438,8 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
     // decode regions: blocks that overflowed theirs carry their exact size (blk_need)
     // into the next attempt; a buffer too small for all regions grows to fit
     if (codec != RIO_CODEC_NONE && (c->h_ctl->out_overflow & 0x40) && ensure_dec(c, c->h_ctl->dec_need)) return -1;
+    // a flate block needed more Huffman/copy rounds than were launched
+    if ((c->h_ctl->out_overflow & 0x1000) && c->fl_rounds < 64) c->fl_rounds = c->fl_rounds * 2 > 64 ? 64 : c->fl_rounds * 2;
   }
   if (getenv("RIO_DEBUG")) debug_dump(c);
   float ms = 0;

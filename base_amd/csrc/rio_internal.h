@@ -98,6 +98,30 @@ constexpr int kMetaClsShift = 32;                             // MagicClass (8 b
 constexpr unsigned long long kMetaRegular = 1ull << 40;       // every chunk but the last is full
 constexpr unsigned long long kMetaComplete = 1ull << 41;      // all chunks inside the span
 
+// Two-pass flate decode (codec_flate.hip): per-block state handed from the
+// Huffman pass (k_flate_tok, writes LZ77 tokens) to the copy pass (k_flate_lz,
+// 32 KiB LDS window) and kept across rounds when a block's token region fills.
+enum FlMode : uint32_t {
+  kFlHeader = 0,   // next: a DEFLATE block header (BFINAL, BTYPE)
+  kFlFixed = 1,    // inside a fixed-Huffman block
+  kFlDynamic = 2,  // inside a dynamic-Huffman block (tables rebuilt from hdrpos on resume)
+  kFlStored = 3,   // inside a stored block, stored_left bytes to go
+  kFlDone = 4,     // final block decoded
+  kFlError = 5,    // decode failed (k_inflate_exact classifies it)
+  kFlSkip = 6,     // not decoded (incomplete block, header magic, region overflow)
+};
+struct FlState {
+  unsigned long long bitpos;  // logical bit offset of the next symbol / header
+  unsigned long long hdrpos;  // kFlDynamic: bit offset of the block's HLIT field
+  unsigned long long olen;    // output bytes of all tokens so far
+  unsigned long long olen2;   // output bytes the copy pass has written
+  uint32_t mode, final_;      // FlMode; the current DEFLATE block has BFINAL set
+  uint32_t ntok, round;       // tokens written in `round`
+  uint32_t stored_left, pad;
+};
+constexpr int kFlRounds = 6;          // Huffman/copy rounds launched per span
+constexpr int kTokPerChunk = kChunk;  // token region: 32,768 u32 per chunk of the block
+
 // Device arrays of one context (capacities fixed at rio_open, grown on demand).
 struct DevBufs {
   // per chunk
@@ -127,6 +151,10 @@ struct DevBufs {
   unsigned long long *scan_tmp;  // tile partials
   uint8_t *dec;                  // decoded blocks (compressed codecs)
   uint64_t dec_cap;              // bytes at dec
+  FlState *fl;                   // per block (flate)
+  uint32_t *tok;                 // flate tokens: block b's region starts at blk_c0[b] * kTokPerChunk
+  uint64_t tok_cap;              // u32 entries at tok
+  unsigned long long *fl_more;   // per round: blocks whose token region filled (kFlRounds)
   Ctl *ctl;
   // CRC tables (constant)
   uint32_t *crc_fold;   // 4 x 256 fold tables, each replicated x32 (bank-private copies)
