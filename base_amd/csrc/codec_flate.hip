@@ -516,14 +516,15 @@ __device__ __forceinline__ uint32_t tab_entry(int kind, uint32_t s, uint32_t len
   return len | (s << 16);
 }
 
-// canonical code data for codes longer than the root table
+// canonical code data for codes longer than the root table: per code length,
+// first code (15:0), count (31:16), index of its first entry in canonical order (47:32)
 struct TabSlow {
-  uint16_t count[16], first[16], offs[16];
+  uint64_t fco[16];
 };
 
 constexpr int kVS = 8;         // streams per wave
 constexpr int kRingDw = 128;   // input ring per stream (dwords)
-constexpr int kTbuf = 16;      // tokens buffered per stream between input passes
+constexpr int kTbuf = 36;      // tokens buffered per stream between input passes (2 per step, hot + full, + 1 slack)
 constexpr int kPass = 8;       // decode steps between input passes
 
 struct __attribute__((aligned(16))) StreamLds {
@@ -531,7 +532,8 @@ struct __attribute__((aligned(16))) StreamLds {
   uint32_t tbuf[kTbuf];
   uint32_t dst[1 << kTokDistRoot];  // also the code-length table while a header is read
   uint16_t lit[1 << kTokLitRoot];
-  uint16_t lsym[288], dsym[32];     // symbols in canonical order
+  uint32_t dent[32];                // distance entries in canonical order (code length 0)
+  uint16_t lent[288];               // literal/length entries in canonical order (code length 0)
   TabSlow ls, ds;
   uint8_t lens[320];
   uint8_t cl[24];
@@ -544,8 +546,8 @@ struct __attribute__((aligned(16))) StreamLds {
 // Ranks within a length come from ballots, so every lane places its own
 // symbol; entries of codes up to `root` bits are replicated by their lanes.
 template <class TT>
-__device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, int root, TabSlow &sl,
-                                           uint16_t *sorted, int kind) {
+__device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, int root, TabSlow &sl, TT *sorted,
+                                           int kind) {
   const int l = lane_id();
   uint32_t cnt[16];
 #pragma unroll
@@ -603,9 +605,7 @@ __device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, 
         oc = offs[L];
         cc = cnt[L];
       }
-    sl.count[l] = (uint16_t)cc;
-    sl.first[l] = (uint16_t)fc;
-    sl.offs[l] = (uint16_t)oc;
+    sl.fco[l] = (uint64_t)(fc & 0xffffu) | ((uint64_t)cc << 16) | ((uint64_t)oc << 32);
   }
   wave_lds_sync();
 #pragma unroll
@@ -614,13 +614,14 @@ __device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, 
       const uint32_t L = myl[k];
       if (L) {
         const uint32_t s = (uint32_t)(k * 64 + l);
-        const uint32_t cd = (uint32_t)sl.first[L] + rank[k];
-        sorted[sl.offs[L] + rank[k]] = (uint16_t)s;
+        const uint64_t fco = sl.fco[L];
+        const uint32_t cd = (uint32_t)(fco & 0xffffu) + rank[k];
         const uint32_t rev = __brev(cd) >> (32 - L);
         if ((int)L <= root) {
           const TT e = (TT)tab_entry(kind, s, L);
           for (uint32_t f = rev; f < (1u << root); f += (1u << L)) tab[f] = e;
         } else {
+          sorted[(uint32_t)(fco >> 32) + rank[k]] = (TT)tab_entry(kind, s, 0);
           tab[rev & ((1u << root) - 1)] = (TT)kLongMark;
         }
       }
@@ -630,15 +631,27 @@ __device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, 
   return 0;
 }
 
-// entry of a code longer than the root table (canonical walk; per lane)
-__device__ __forceinline__ uint32_t slow_walk(const TabSlow &sl, const uint16_t *sorted, uint32_t bits, int root,
-                                              int kind) {
-  for (int L = root + 1; L <= 15; L++) {
-    const uint32_t c = __brev(bits) >> (32 - L);
-    const uint32_t f = sl.first[L], k = sl.count[L];
-    if (c - f < k) return tab_entry(kind, sorted[sl.offs[L] + c - f], (uint32_t)L);
+// entry of a code longer than the root table (canonical walk; per lane): the
+// canonical data of every longer length is read at once, then one entry
+template <int kRoot, class TT>
+__device__ __forceinline__ uint32_t slow_walk(const TabSlow &sl, const TT *sorted, uint32_t bits) {
+  constexpr int kN = 15 - kRoot;
+  uint64_t f[kN];
+#pragma unroll
+  for (int i = 0; i < kN; i++) f[i] = sl.fco[kRoot + 1 + i];
+  const uint32_t rb = __brev(bits);
+  uint32_t idx = 0xffffffffu, len = 0;
+#pragma unroll
+  for (int i = kN - 1; i >= 0; i--) {  // the shortest match wins (codes are prefix-free)
+    const uint32_t L = kRoot + 1 + i;
+    const uint32_t c = rb >> (32 - L);
+    const uint32_t d = c - (uint32_t)(f[i] & 0xffffu);
+    if (d < (uint32_t)((f[i] >> 16) & 0xffffu)) {
+      idx = (uint32_t)(f[i] >> 32) + d;
+      len = L;
+    }
   }
-  return 0;
+  return idx == 0xffffffffu ? 0u : ((uint32_t)sorted[idx] | len);
 }
 
 // logical compressed dword at byte p (a multiple of 4); bytes at/after n read 0
@@ -726,10 +739,10 @@ __device__ __forceinline__ void fixed_tables(StreamLds &T) {
   wave_lds_sync();
   for (int i = l; i < 288; i += 64) T.lens[i] = (uint8_t)(i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8);
   wave_lds_sync();
-  build_table(T.lens, 288, T.lit, kTokLitRoot, T.ls, T.lsym, kTabLit);
+  build_table(T.lens, 288, T.lit, kTokLitRoot, T.ls, T.lent, kTabLit);
   for (int i = l; i < 32; i += 64) T.lens[i] = 5;
   wave_lds_sync();
-  build_table(T.lens, 32, T.dst, kTokDistRoot, T.ds, T.dsym, kTabDist);
+  build_table(T.lens, 32, T.dst, kTokDistRoot, T.ds, T.dent, kTabDist);
 }
 
 // dynamic block header (RFC 1951 §3.2.7; Go inflate.go readHuffman)
@@ -748,7 +761,7 @@ __device__ __forceinline__ int read_dynamic(TokDec &t) {
     if (l == 0) T.cl[kClenOrder[i]] = (uint8_t)v;
   }
   wave_lds_sync();
-  if (build_table(T.cl, 19, T.dst, kTokDistRoot, T.ds, T.dsym, kTabClen) != 0) return kCodecCorrupt;
+  if (build_table(T.cl, 19, T.dst, kTokDistRoot, T.ds, T.dent, kTabClen) != 0) return kCodecCorrupt;
   const uint32_t n = nlit + ndist;
   uint32_t i = 0, prev = 0;
   while (i < n) {
@@ -782,8 +795,8 @@ __device__ __forceinline__ int read_dynamic(TokDec &t) {
     i += rep;
   }
   wave_lds_sync();
-  if (build_table(T.lens, (int)nlit, T.lit, kTokLitRoot, T.ls, T.lsym, kTabLit) != 0) return kCodecCorrupt;
-  if (build_table(T.lens + nlit, (int)ndist, T.dst, kTokDistRoot, T.ds, T.dsym, kTabDist) == 2) return kCodecCorrupt;
+  if (build_table(T.lens, (int)nlit, T.lit, kTokLitRoot, T.ls, T.lent, kTabLit) != 0) return kCodecCorrupt;
+  if (build_table(T.lens + nlit, (int)ndist, T.dst, kTokDistRoot, T.ds, T.dent, kTabDist) == 2) return kCodecCorrupt;
   return 0;
 }
 
@@ -1086,7 +1099,71 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
     }
     if (!__ballot(mode != kVGone)) break;
 
-    // ---------------------------------------------------------- decode steps
+    // ---------------------------------------------------------- hot steps
+    // The common case, branch-light: a stream decoding a Huffman block with
+    // room for this pass's tokens decodes one literal or one match per step.
+    // The step starts with >= 32 bits in the buffer, and the two ring words
+    // after them (nw0, nw1) were requested at the end of the previous step,
+    // so no refill waits on LDS. Anything else -- a code longer than the root
+    // table, end of block, a corrupt or oversized symbol -- leaves the state
+    // untouched and the stream to the full step below.
+    if (mode == kVHuff && nbits < 32) {  // the hot step starts with >= 32 bits
+      bitbuf |= (uint64_t)nw0 << nbits;
+      nbits += 32;
+      rpos++;
+      nw0 = M.ring[rpos & (kRingDw - 1)];
+      nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];
+    }
+    const bool hot0 = mode == kVHuff && tcap - nst - nv >= 2 * kPass + 3;
+    bool cold = !hot0;
+    if (__ballot(hot0)) {
+      for (int step = 0; step < kPass; step++) {
+        if (!cold) {
+          uint32_t e = M.lit[(uint32_t)bitbuf & ((1u << kTokLitRoot) - 1)];
+          if ((e & 15) == 0 && (e & kEnLenBit)) e = slow_walk<kTokLitRoot>(M.ls, M.lent, (uint32_t)bitbuf);
+          const uint32_t L = e & 15, isl = (e >> 4) & 1, E = (e >> 5) & 7;
+          const uint32_t len = (e >> 8) + 3 + ((uint32_t)(bitbuf >> L) & ((1u << E) - 1));
+          uint64_t b1 = bitbuf >> (L + E);
+          uint32_t n1 = nbits - (L + E);
+          const bool m1 = n1 < 32;
+          b1 |= m1 ? ((uint64_t)nw0 << n1) : 0ull;
+          n1 += m1 ? 32u : 0u;
+          uint32_t dd = M.dst[(uint32_t)b1 & ((1u << kTokDistRoot) - 1)];
+          if (isl && (dd & 15) == 0 && (dd & kEnLenBit)) dd = slow_walk<kTokDistRoot>(M.ds, M.dent, (uint32_t)b1);
+          const uint32_t L2 = dd & 15, E2 = (dd >> 8) & 15;
+          const uint32_t dist = (dd >> 16) + ((uint32_t)(b1 >> L2) & ((1u << E2) - 1));
+          const uint32_t c2 = isl ? L2 + E2 : 0u;
+          uint64_t b2 = b1 >> c2;
+          uint32_t n2 = n1 - c2;
+          const bool m2 = n2 < 32;
+          b2 |= m2 ? ((uint64_t)(m1 ? nw1 : nw0) << n2) : 0ull;
+          n2 += m2 ? 32u : 0u;
+          const uint32_t hist = olen < 32768u ? olen : 32768u;
+          const bool ok = L != 0 && (isl ? (E != kEobExtra && L2 != 0 && dist <= hist && len <= cap - olen)
+                                         : olen < cap);
+          // tokens: a full literal triple, or the pending literals then the match
+          const uint32_t lt = pend | ((e >> 8) << (8 * npend)), ln = npend + 1;
+          const bool c1 = isl ? npend != 0 : ln == 3;
+          const uint32_t t2 = 0x80000000u | ((len - 3) << 16) | (dist - 1);
+          const uint32_t t1 = isl ? (pend | (npend << 24)) : (lt | (3u << 24));
+          M.tbuf[nv] = c1 ? t1 : t2;  // (a failed step's writes sit past nv)
+          M.tbuf[nv + 1] = t2;
+          const bool clr = isl || c1;
+          bitbuf = ok ? b2 : bitbuf;
+          nbits = ok ? n2 : nbits;
+          rpos += ok ? (m1 ? 1u : 0u) + (m2 ? 1u : 0u) : 0u;
+          nv += ok ? (c1 ? 1u : 0u) + isl : 0u;
+          pend = ok ? (clr ? 0u : lt) : pend;
+          npend = ok ? (clr ? 0u : ln) : npend;
+          olen += ok ? (isl ? len : 1u) : 0u;
+          cold = !ok;
+          nw0 = M.ring[rpos & (kRingDw - 1)];
+          nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];
+        }
+      }
+    }
+
+    // ---------------------------------------------------------- full steps
 #define RIO_REFILL()                                                 \
   if (nbits < 32) {                                                  \
     bitbuf |= (uint64_t)nw0 << nbits;                                \
@@ -1100,8 +1177,9 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
     if (j == 0) M.tbuf[nv] = (t_);                                   \
     nv++;                                                            \
   }
-    for (int step = 0; step < kPass; step++) {
-      if (mode == kVHuff) {
+    for (int step = 0; step < kPass && __ballot(cold && mode <= kVStored); step++) {
+      if (!cold) {
+      } else if (mode == kVHuff) {
         if (tcap - nst - nv < 3) {
           res = (uint32_t)kTokYield;
           mode = kVFinish;
@@ -1110,7 +1188,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           uint32_t e = M.lit[(uint32_t)bitbuf & ((1u << kTokLitRoot) - 1)];
           uint32_t L = e & 15;
           if (L == 0 && (e & kEnLenBit)) {
-            e = slow_walk(M.ls, M.lsym, (uint32_t)bitbuf, kTokLitRoot, kTabLit);
+            e = slow_walk<kTokLitRoot>(M.ls, M.lent, (uint32_t)bitbuf);
             L = e & 15;
           }
           const uint32_t E = (e >> 5) & 7;
@@ -1149,7 +1227,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
             uint32_t dd = M.dst[(uint32_t)bitbuf & ((1u << kTokDistRoot) - 1)];
             uint32_t L2 = dd & 15;
             if (L2 == 0 && (dd & kEnLenBit)) {
-              dd = slow_walk(M.ds, M.dsym, (uint32_t)bitbuf, kTokDistRoot, kTabDist);
+              dd = slow_walk<kTokDistRoot>(M.ds, M.dent, (uint32_t)bitbuf);
               L2 = dd & 15;
             }
             if (L2 == 0) {
@@ -1212,11 +1290,9 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
 #undef RIO_EMIT
 
     // ---------------------------------------------------------- input pass
+    // (the ring takes the prefetched words first: the loads were issued a
+    // pass ago, and no store issued since may sit in front of them in vmcnt)
     {
-      uint32_t *tk = d.tok + (uint64_t)bc0 * kTokPerChunk + nst;
-      for (uint32_t k = j; k < nv; k += 8) tk[k] = M.tbuf[k];
-      nst += nv;
-      nv = 0;
       if (mode <= kVStored) {
         if (rhi - rpos <= kRingDw - 32) {
           *reinterpret_cast<uint4 *>(&M.ring[(rhi + 4 * j) & (kRingDw - 1)]) = make_uint4(pf0, pf1, pf2, pf3);
@@ -1232,15 +1308,31 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           mode = kVFinish;
         }
       }
+      uint32_t *tk = d.tok + (uint64_t)bc0 * kTokPerChunk + nst;
+      for (uint32_t k = j; k < nv; k += 8) tk[k] = M.tbuf[k];
+      nst += nv;
+      nv = 0;
       wave_lds_sync();
     }
   }
 }
 
-constexpr int kLzWin = 65536;  // 32 KiB of history + the largest batch (64 x 258 B) + one flush unit
+constexpr int kLzWin = 65536;  // 32 KiB of history + up to 32 KiB written but not yet flushed
+constexpr int kLzSuper = 16;   // batches of 64 tokens staged in LDS per super-batch
+
+// write the completed 1 KiB units of [flushed, olen) to HBM, 16 B per lane
+__device__ __forceinline__ void lz_flush_units(const uint8_t *win, uint8_t *out, uint64_t &flushed, uint64_t olen) {
+  const int l = lane_id();
+  for (uint64_t u0 = flushed & ~1023ull; u0 + 1024 <= olen; u0 += 1024) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(win + ((u0 + 16 * l) & (kLzWin - 1)));
+    *reinterpret_cast<uint4 *>(out + u0 + 16 * l) = v;
+    flushed = u0 + 1024;
+  }
+}
 
 __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long long *nblocks, int round) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kLzWin];
+  __shared__ uint32_t tbuf[64 * kLzSuper];
   const int l = lane_id();
   if (round > 0 && uni64(d.fl_more[round - 1]) == 0) return;
   const uint64_t nb = uni64(*nblocks);
@@ -1260,55 +1352,97 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
       wave_lds_sync();
     }
     uint64_t flushed = olen;
-    uint32_t t_next = ((uint32_t)l < ntok) ? tk[l] : 0u;
-    for (uint32_t i0 = 0; i0 < ntok; i0 += 64) {
-      const uint32_t t = t_next;
-      t_next = (i0 + 64 + (uint32_t)l < ntok) ? tk[i0 + 64 + l] : 0u;
-      const bool m = (t >> 31) != 0;
-      const uint32_t len = m ? ((t >> 16) & 0xffu) + 3 : (t >> 24) & 3u;
-      const uint32_t incl = wave_incl_sum(len);
-      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-      const uint32_t p = incl - len;  // position relative to olen
-      const uint32_t base = (uint32_t)olen;
-      if (!m) {
-        if (len > 0) win[(base + p) & M] = (uint8_t)t;
-        if (len > 1) win[(base + p + 1) & M] = (uint8_t)(t >> 8);
-        if (len > 2) win[(base + p + 2) & M] = (uint8_t)(t >> 16);
-      }
-      const uint32_t dist = (t & 0x7fffu) + 1;
-      const int src_end = (int)p - (int)dist + (int)(len < dist ? len : dist);
-      unsigned long long pend = __ballot(m);
-      while (pend) {
-        // everything before the first unresolved match is final
-        const int R = (int)__builtin_amdgcn_readlane(p, __ffsll((long long)pend) - 1);
-        const bool ready = ((pend >> l) & 1ull) && src_end <= R;
-        if (ready) {
-          const uint32_t s = base + p - dist, q = base + p;
-          uint32_t k = 0;
-          if (dist >= 8) {
-            for (; k + 8 <= len; k += 8) {
-              uint8_t v[8];
+    // Tokens stream through LDS one super-batch (1,024 tokens) at a time; the
+    // next super-batch is loaded into registers while this one is decoded, and
+    // completed output is flushed just before those loads are issued, so no
+    // load ever waits behind a recent store (vmcnt is in order).
+    uint32_t pre[kLzSuper];
 #pragma unroll
-              for (int jj = 0; jj < 8; jj++) v[jj] = win[(s + k + jj) & M];
+    for (int q = 0; q < kLzSuper; q++) pre[q] = (64u * q + (uint32_t)l < ntok) ? tk[64 * q + l] : 0u;
+    for (uint32_t s0 = 0; s0 < ntok; s0 += 64 * kLzSuper) {
+      wave_lds_sync();
 #pragma unroll
-              for (int jj = 0; jj < 8; jj++) win[(q + k + jj) & M] = v[jj];
+      for (int q = 0; q < kLzSuper; q++) tbuf[64 * q + l] = pre[q];
+      lz_flush_units(win, out, flushed, olen);
+      const uint32_t s1 = s0 + 64 * kLzSuper;
+#pragma unroll
+      for (int q = 0; q < kLzSuper; q++) pre[q] = (s1 + 64u * q + (uint32_t)l < ntok) ? tk[s1 + 64 * q + l] : 0u;
+      wave_lds_sync();
+      const uint32_t nbat = (ntok - s0 + 63) / 64 < (uint32_t)kLzSuper ? (ntok - s0 + 63) / 64 : (uint32_t)kLzSuper;
+      for (uint32_t bi = 0; bi < nbat; bi++) {
+        const uint32_t t = (s0 + 64 * bi + (uint32_t)l < ntok) ? tbuf[64 * bi + l] : 0u;
+        const bool m = (t >> 31) != 0;
+        const uint32_t len = m ? ((t >> 16) & 0xffu) + 3 : (t >> 24) & 3u;
+        const uint32_t incl = wave_incl_sum_dpp(len);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+        const uint32_t p = incl - len;  // position relative to olen
+        const uint32_t base = (uint32_t)olen;
+        if (!m) {
+          if (len > 0) win[(base + p) & M] = (uint8_t)t;
+          if (len > 1) win[(base + p + 1) & M] = (uint8_t)(t >> 8);
+          if (len > 2) win[(base + p + 2) & M] = (uint8_t)(t >> 16);
+        }
+        const uint32_t dist = (t & 0x7fffu) + 1;
+        const int src_end = (int)p - (int)dist + (int)(len < dist ? len : dist);
+        const unsigned long long mm = __ballot(m);
+        if (mm) {
+          // one parallel round: every match whose source ends before the batch's
+          // first match (its own lane copies it, 8 bytes per LDS round trip) ...
+          const int R = (int)__builtin_amdgcn_readlane(p, __ffsll((long long)mm) - 1);
+          const bool ready = m && src_end <= R;
+          if (ready) {
+            const uint32_t sa = base + p - dist, q = base + p;
+            if (dist >= 8 || len <= dist) {  // no byte of an 8-byte piece depends on another
+              for (uint32_t k = 0; k < len; k += 8) {
+                const uint32_t a0 = (sa + k) & M, d0 = (q + k) & M;
+                uint8_t v[8];
+                if (a0 + 8 <= (uint32_t)kLzWin) {
+#pragma unroll
+                  for (int jj = 0; jj < 8; jj++) v[jj] = win[a0 + jj];
+                } else {
+#pragma unroll
+                  for (int jj = 0; jj < 8; jj++) v[jj] = win[(a0 + jj) & M];
+                }
+                if (d0 + 8 <= (uint32_t)kLzWin && k + 8 <= len) {
+#pragma unroll
+                  for (int jj = 0; jj < 8; jj++) win[d0 + jj] = v[jj];
+                } else {
+#pragma unroll
+                  for (int jj = 0; jj < 8; jj++)
+                    if (k + jj < len) win[(d0 + jj) & M] = v[jj];
+                }
+              }
+            } else {  // overlapping run: byte by byte, each byte reads one written before it
+              for (uint32_t k = 0; k < len; k++) win[(q + k) & M] = win[(sa + k) & M];
             }
           }
-          for (; k < len; k++) win[(q + k) & M] = win[(s + k) & M];
+          // ... then the rest (sources inside this batch) in order, each copied by
+          // the whole wave: every byte it reads precedes it and is final by then
+          unsigned long long rem = mm & ~__ballot(ready);
+          while (rem) {
+            const int f = __ffsll((long long)rem) - 1;
+            rem &= rem - 1;
+            const uint32_t P = base + (uint32_t)__builtin_amdgcn_readlane(p, f);
+            const uint32_t D = (uint32_t)__builtin_amdgcn_readlane(dist, f);
+            const uint32_t N = (uint32_t)__builtin_amdgcn_readlane(len, f);
+            for (uint32_t k0 = 0; k0 < N; k0 += 64) {
+              const uint32_t k = k0 + (uint32_t)l;
+              const uint32_t kk = D >= N ? k : k % D;
+              const uint8_t v = k < N ? win[(P - D + kk) & M] : 0;
+              if (k < N) win[(P + k) & M] = v;
+            }
+          }
         }
-        pend &= ~__ballot(ready);
-      }
-      olen += total;
-      if ((olen & ~1023ull) > flushed) {
-        wave_lds_sync();
-        for (uint64_t u0 = flushed & ~1023ull; u0 + 1024 <= olen; u0 += 1024) {
-          const uint4 v = *reinterpret_cast<const uint4 *>(win + ((u0 + 16 * l) & M));
-          *reinterpret_cast<uint4 *>(out + u0 + 16 * l) = v;
-          flushed = u0 + 1024;
+        olen += total;
+        // a write at x replaces x - 64 KiB: keep the unflushed part under 32 KiB
+        if (olen - flushed > 32768 - 1024) {
+          wave_lds_sync();
+          lz_flush_units(win, out, flushed, olen);
         }
       }
     }
     wave_lds_sync();
+    lz_flush_units(win, out, flushed, olen);
     for (uint64_t k = flushed + l; k < olen; k += 64) out[k] = win[k & M];
     if (l == 0) {
       sp->olen2 = olen;

@@ -30,6 +30,18 @@ __device__ __forceinline__ T wave_incl_sum(T v) {
   return v;
 }
 
+// inclusive prefix sum of a u32 over the wave with DPP: row shifts inside
+// each 16-lane row, then the row broadcasts (GFX9 row_bcast:15 / row_bcast:31)
+__device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
 template <class T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
