@@ -859,6 +859,9 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
     // ---------------------------------------------------------- escapes
     unsigned long long esc = __ballot(j == 0 && mode >= kVHeader && mode <= kVNew);
     while (esc) {
+#ifdef RIO_FLSTAT
+      if (l == 0) atomicAdd(&d.ctl->flstat_esc, 1ull);
+#endif
       const uint32_t gl = (uint32_t)__ffsll((long long)esc) - 1;
       esc &= esc - 1;
       const uint32_t gg = gl >> 3;
@@ -1164,6 +1167,12 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
     }
 
     // ---------------------------------------------------------- full steps
+#ifdef RIO_FLSTAT
+    if (l == 0) {
+      atomicAdd(&d.ctl->pad[0], 1ull);
+      if (__ballot(cold && mode <= kVStored)) atomicAdd(&d.ctl->pad[1], 1ull);
+    }
+#endif
 #define RIO_REFILL()                                                 \
   if (nbits < 32) {                                                  \
     bitbuf |= (uint64_t)nw0 << nbits;                                \
@@ -1317,6 +1326,15 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
   }
 }
 
+// k mod d for k < 2^20, d >= 1 (float reciprocal, one correction step)
+__device__ __forceinline__ uint32_t umod_small(uint32_t k, uint32_t d) {
+  uint32_t q = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)d));
+  int32_t r = (int32_t)(k - q * d);
+  if (r < 0) r += (int32_t)d;
+  if (r >= (int32_t)d) r -= (int32_t)d;
+  return (uint32_t)r;
+}
+
 constexpr int kLzWin = 65536;  // 32 KiB of history + up to 32 KiB written but not yet flushed
 constexpr int kLzSuper = 16;   // batches of 64 tokens staged in LDS per super-batch
 
@@ -1389,7 +1407,7 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
           // one parallel round: every match whose source ends before the batch's
           // first match (its own lane copies it, 8 bytes per LDS round trip) ...
           const int R = (int)__builtin_amdgcn_readlane(p, __ffsll((long long)mm) - 1);
-          const bool ready = m && src_end <= R;
+          const bool ready = m && src_end <= R && len <= 16;
           if (ready) {
             const uint32_t sa = base + p - dist, q = base + p;
             if (dist >= 8 || len <= dist) {  // no byte of an 8-byte piece depends on another
@@ -1416,8 +1434,9 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
               for (uint32_t k = 0; k < len; k++) win[(q + k) & M] = win[(sa + k) & M];
             }
           }
-          // ... then the rest (sources inside this batch) in order, each copied by
-          // the whole wave: every byte it reads precedes it and is final by then
+          // ... then the rest (sources inside this batch, or longer than 16 B) in
+          // order, each copied by the whole wave: every byte it reads precedes it
+          // and is final by then
           unsigned long long rem = mm & ~__ballot(ready);
           while (rem) {
             const int f = __ffsll((long long)rem) - 1;
@@ -1427,7 +1446,7 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
             const uint32_t N = (uint32_t)__builtin_amdgcn_readlane(len, f);
             for (uint32_t k0 = 0; k0 < N; k0 += 64) {
               const uint32_t k = k0 + (uint32_t)l;
-              const uint32_t kk = D >= N ? k : k % D;
+              const uint32_t kk = D >= N ? k : umod_small(k, D);
               const uint8_t v = k < N ? win[(P - D + kk) & M] : 0;
               if (k < N) win[(P + k) & M] = v;
             }

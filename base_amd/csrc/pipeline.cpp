@@ -249,7 +249,8 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   HIP_OK(hipEventRecord(c->ev[kEvStart], st));
   // control words are min-reduced: reset to ~0 (out_overflow to 0)
   HIP_OK(hipMemsetAsync(d.ctl, 0xff, 4 * sizeof(unsigned long long), st));
-  HIP_OK(hipMemsetAsync(&d.ctl->out_overflow, 0, 2 * sizeof(unsigned long long), st));  // + dec_need
+  HIP_OK(hipMemsetAsync(&d.ctl->out_overflow, 0, 4 * sizeof(unsigned long long), st));  // + dec_need, pad
+  HIP_OK(hipMemsetAsync(&d.ctl->flstat_esc, 0, sizeof(unsigned long long), st));
   if (attempt == 0 && codec != RIO_CODEC_NONE && nchunks > 0)
     HIP_OK(hipMemsetAsync(d.blk_need, 0, nchunks * sizeof(unsigned long long), st));
   HIP_OK(hipMemsetAsync(c->nblocks_dev, 0, 2 * sizeof(unsigned long long), st));
@@ -398,7 +399,9 @@ static void debug_dump(rio_ctx *c) {
     hipMemcpy(eb.data(), c->d.blk_b, 8 * nb, hipMemcpyDeviceToHost);
     hipMemcpy(hd.data(), c->d.blk_hdr, 8 * nb, hipMemcpyDeviceToHost);
   }
-  fprintf(stderr, "rio debug: nblocks=%llu overflow=%llu\n", nb, (unsigned long long)c->h_ctl->out_overflow);
+  fprintf(stderr, "rio debug: nblocks=%llu overflow=%llu flstat passes=%llu full=%llu esc=%llu\n", nb,
+          (unsigned long long)c->h_ctl->out_overflow, (unsigned long long)c->h_ctl->pad[0],
+          (unsigned long long)c->h_ctl->pad[1], (unsigned long long)c->h_ctl->flstat_esc);
   std::vector<FlState> fl(nb);
   if (nb && c->d.fl) hipMemcpy(fl.data(), c->d.fl, sizeof(FlState) * nb, hipMemcpyDeviceToHost);
   int shown = 0;

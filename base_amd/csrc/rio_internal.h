@@ -62,7 +62,7 @@ struct Ctl {
   unsigned long long first_incomplete;   // min c0 of a block extending past the span
   unsigned long long out_overflow;       // nonzero if side/items exceeded capacity
   unsigned long long dec_need;           // decode regions' total size (when it exceeds dec_cap)
-  unsigned long long pad[2];
+  unsigned long long pad[2];             // (RIO_FLSTAT builds: flate pass counters)
   // filled by k_resolve
   unsigned long long stop_key;
   unsigned long long n_valid_blocks;
@@ -79,6 +79,7 @@ struct Ctl {
   unsigned long long blk_status, blk_a, blk_b, blk_c0, blk_payload;
   unsigned long long consumed_chunks;
   unsigned long long mag_cur, mag_prev, mag_blk;  // little-endian magic bytes
+  unsigned long long flstat_esc;                  // (RIO_FLSTAT builds: flate escapes)
 };
 
 constexpr unsigned long long kNone = ~0ull;
