@@ -479,8 +479,9 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
 // Table entries. Literal/length (u16): code length (3:0; 0 = not decodable
 // from the root), bit 4 set for a length or end-of-block, length extra bits
 // (7:5; 7 = end-of-block), literal byte or length base - 3 (15:8).
-// Distance (u32): code length (3:0), extra bits (11:8), base (31:16).
-// Code-length alphabet (u32): code length (3:0), symbol (31:16).
+// Distance (u16): code length (3:0), symbol (12:8); base and extra bits
+// follow from the symbol (dist_sym). Code-length alphabet (u16): code
+// length (3:0), symbol (12:8).
 // Code length 0 with bit 4 set (kLongMark) marks a code longer than the root
 // (canonical walk); an all-zero entry is a bit pattern no code has or a
 // symbol DEFLATE never assigns (literal/length 286-287, distance 30-31):
@@ -490,7 +491,10 @@ constexpr uint32_t kLongMark = kEnLenBit;
 constexpr uint32_t kEobExtra = 7;
 enum : int { kTabLit = 0, kTabDist = 1, kTabClen = 2 };
 enum : int { kTokDone = 0, kTokYield = -1 };
-constexpr int kTokLitRoot = 10;
+#ifndef RIO_LIT_ROOT
+#define RIO_LIT_ROOT 10
+#endif
+constexpr int kTokLitRoot = RIO_LIT_ROOT;  // literal/length root table bits
 constexpr int kTokDistRoot = 8;
 
 // RFC 1951 §3.2.5 length / distance bases and extra bits
@@ -510,31 +514,31 @@ __device__ __forceinline__ uint32_t tab_entry(int kind, uint32_t s, uint32_t len
     return 0;
   }
   if (kind == kTabDist) {
-    if (s < 30) return len | ((uint32_t)kDistExtra[s] << 8) | ((uint32_t)kDistBase[s] << 16);
-    return 0;
+    return s < 30 ? len | (s << 8) : 0u;
   }
-  return len | (s << 16);
+  return len | (s << 8);
 }
 
-// canonical code data for codes longer than the root table: per code length,
-// first code (15:0), count (31:16), index of its first entry in canonical order (47:32)
-struct TabSlow {
-  uint64_t fco[16];
-};
-
 constexpr int kVS = 8;         // streams per wave
-constexpr int kRingDw = 128;   // input ring per stream (dwords)
+constexpr int kRingDw = 64;    // input ring per stream (dwords)
 constexpr int kTbuf = 36;      // tokens buffered per stream between input passes (2 per step, hot + full, + 1 slack)
 constexpr int kPass = 8;       // decode steps between input passes
 
+// Canonical code data per code length (first code 15:0, count 31:16, index
+// of its first entry in canonical order 47:32); streams keep the lengths
+// longer than their root tables, for the canonical walk.
 struct __attribute__((aligned(16))) StreamLds {
   uint32_t ring[kRingDw];
   uint32_t tbuf[kTbuf];
-  uint32_t dst[1 << kTokDistRoot];  // also the code-length table while a header is read
+  uint64_t lfco[15 - kTokLitRoot], dfco[15 - kTokDistRoot];
   uint16_t lit[1 << kTokLitRoot];
-  uint32_t dent[32];                // distance entries in canonical order (code length 0)
-  uint16_t lent[288];               // literal/length entries in canonical order (code length 0)
-  TabSlow ls, ds;
+  uint16_t dst[1 << kTokDistRoot];  // also the code-length table while a header is read
+  uint16_t lent[288], dent[32];     // entries of codes longer than the root, canonical order (code length 0)
+};
+// per wave: scratch of the header reads and table builds (escapes work on
+// one stream at a time)
+struct WaveLds {
+  uint64_t fco[16];
   uint8_t lens[320];
   uint8_t cl[24];
 };
@@ -546,8 +550,8 @@ struct __attribute__((aligned(16))) StreamLds {
 // Ranks within a length come from ballots, so every lane places its own
 // symbol; entries of codes up to `root` bits are replicated by their lanes.
 template <class TT>
-__device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, int root, TabSlow &sl, TT *sorted,
-                                           int kind) {
+__device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, int root, uint64_t *sfco,
+                                           uint64_t *lfco, TT *sorted, int kind) {
   const int l = lane_id();
   uint32_t cnt[16];
 #pragma unroll
@@ -605,7 +609,9 @@ __device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, 
         oc = offs[L];
         cc = cnt[L];
       }
-    sl.fco[l] = (uint64_t)(fc & 0xffffu) | ((uint64_t)cc << 16) | ((uint64_t)oc << 32);
+    const uint64_t v = (uint64_t)(fc & 0xffffu) | ((uint64_t)cc << 16) | ((uint64_t)oc << 32);
+    sfco[l] = v;
+    if (l > root) lfco[l - root - 1] = v;
   }
   wave_lds_sync();
 #pragma unroll
@@ -614,7 +620,7 @@ __device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, 
       const uint32_t L = myl[k];
       if (L) {
         const uint32_t s = (uint32_t)(k * 64 + l);
-        const uint64_t fco = sl.fco[L];
+        const uint64_t fco = sfco[L];
         const uint32_t cd = (uint32_t)(fco & 0xffffu) + rank[k];
         const uint32_t rev = __brev(cd) >> (32 - L);
         if ((int)L <= root) {
@@ -634,11 +640,11 @@ __device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, 
 // entry of a code longer than the root table (canonical walk; per lane): the
 // canonical data of every longer length is read at once, then one entry
 template <int kRoot, class TT>
-__device__ __forceinline__ uint32_t slow_walk(const TabSlow &sl, const TT *sorted, uint32_t bits) {
+__device__ __forceinline__ uint32_t slow_walk(const uint64_t *lfco, const TT *sorted, uint32_t bits) {
   constexpr int kN = 15 - kRoot;
   uint64_t f[kN];
 #pragma unroll
-  for (int i = 0; i < kN; i++) f[i] = sl.fco[kRoot + 1 + i];
+  for (int i = 0; i < kN; i++) f[i] = lfco[i];
   const uint32_t rb = __brev(bits);
   uint32_t idx = 0xffffffffu, len = 0;
 #pragma unroll
@@ -652,6 +658,12 @@ __device__ __forceinline__ uint32_t slow_walk(const TabSlow &sl, const TT *sorte
     }
   }
   return idx == 0xffffffffu ? 0u : ((uint32_t)sorted[idx] | len);
+}
+
+// distance base and extra bits of distance symbol s < 30 (RFC 1951 §3.2.5)
+__device__ __forceinline__ uint32_t dist_base(uint32_t s, uint32_t &extra) {
+  extra = s < 4 ? 0u : (s >> 1) - 1;
+  return s < 4 ? s + 1 : ((2u + (s & 1)) << extra) + 1;
 }
 
 // logical compressed dword at byte p (a multiple of 4); bytes at/after n read 0
@@ -682,6 +694,7 @@ __device__ __forceinline__ uint32_t fetch_dword(const CompIn &in, uint64_t p) {
 struct TokDec {
   CompIn in;
   StreamLds *T;
+  WaveLds *W;
   uint32_t c0, c1, n0, n1;
   uint64_t wbase;
   uint32_t wi;
@@ -734,34 +747,35 @@ struct TokDec {
   __device__ __forceinline__ bool overrun() const { return bitpos() > 8 * in.n; }
 };
 
-__device__ __forceinline__ void fixed_tables(StreamLds &T) {
+__device__ __forceinline__ void fixed_tables(StreamLds &T, WaveLds &W) {
   const int l = lane_id();
   wave_lds_sync();
-  for (int i = l; i < 288; i += 64) T.lens[i] = (uint8_t)(i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8);
+  for (int i = l; i < 288; i += 64) W.lens[i] = (uint8_t)(i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8);
   wave_lds_sync();
-  build_table(T.lens, 288, T.lit, kTokLitRoot, T.ls, T.lent, kTabLit);
-  for (int i = l; i < 32; i += 64) T.lens[i] = 5;
+  build_table(W.lens, 288, T.lit, kTokLitRoot, W.fco, T.lfco, T.lent, kTabLit);
+  for (int i = l; i < 32; i += 64) W.lens[i] = 5;
   wave_lds_sync();
-  build_table(T.lens, 32, T.dst, kTokDistRoot, T.ds, T.dent, kTabDist);
+  build_table(W.lens, 32, T.dst, kTokDistRoot, W.fco, T.dfco, T.dent, kTabDist);
 }
 
 // dynamic block header (RFC 1951 §3.2.7; Go inflate.go readHuffman)
 __device__ __forceinline__ int read_dynamic(TokDec &t) {
   StreamLds &T = *t.T;
+  WaveLds &W = *t.W;
   const int l = lane_id();
   if (t.nb < 32) t.refill();
   const uint32_t nlit = t.take(5) + 257, ndist = t.take(5) + 1, nclen = t.take(4) + 4;
   if (nlit > 286 || ndist > 30) return kCodecCorrupt;
   wave_lds_sync();
-  if (l < 19) T.cl[l] = 0;
+  if (l < 19) W.cl[l] = 0;
   wave_lds_sync();
   for (uint32_t i = 0; i < nclen; i++) {
     if (t.nb < 32) t.refill();
     const uint32_t v = t.take(3);
-    if (l == 0) T.cl[kClenOrder[i]] = (uint8_t)v;
+    if (l == 0) W.cl[kClenOrder[i]] = (uint8_t)v;
   }
   wave_lds_sync();
-  if (build_table(T.cl, 19, T.dst, kTokDistRoot, T.ds, T.dent, kTabClen) != 0) return kCodecCorrupt;
+  if (build_table(W.cl, 19, T.dst, kTokDistRoot, W.fco, T.dfco, T.dent, kTabClen) != 0) return kCodecCorrupt;
   const uint32_t n = nlit + ndist;
   uint32_t i = 0, prev = 0;
   while (i < n) {
@@ -770,9 +784,9 @@ __device__ __forceinline__ int read_dynamic(TokDec &t) {
     const uint32_t L = e & 15;
     if (!L) return kCodecCorrupt;
     t.take((int)L);
-    const uint32_t x = e >> 16;
+    const uint32_t x = e >> 8;
     if (x < 16) {
-      if (l == 0) T.lens[i] = (uint8_t)x;
+      if (l == 0) W.lens[i] = (uint8_t)x;
       prev = x;
       i++;
       continue;
@@ -790,13 +804,14 @@ __device__ __forceinline__ int read_dynamic(TokDec &t) {
       rep = 11 + t.take(7);
     }
     if (i + rep > n) return kCodecCorrupt;
-    for (uint32_t j = l; j < rep; j += 64) T.lens[i + j] = (uint8_t)b;
+    for (uint32_t j = l; j < rep; j += 64) W.lens[i + j] = (uint8_t)b;
     prev = b;
     i += rep;
   }
   wave_lds_sync();
-  if (build_table(T.lens, (int)nlit, T.lit, kTokLitRoot, T.ls, T.lent, kTabLit) != 0) return kCodecCorrupt;
-  if (build_table(T.lens + nlit, (int)ndist, T.dst, kTokDistRoot, T.ds, T.dent, kTabDist) == 2) return kCodecCorrupt;
+  if (build_table(W.lens, (int)nlit, T.lit, kTokLitRoot, W.fco, T.lfco, T.lent, kTabLit) != 0) return kCodecCorrupt;
+  if (build_table(W.lens + nlit, (int)ndist, T.dst, kTokDistRoot, W.fco, T.dfco, T.dent, kTabDist) == 2)
+    return kCodecCorrupt;
   return 0;
 }
 
@@ -837,6 +852,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
                                                   const unsigned long long *nblocks, uint64_t nchunks,
                                                   uint64_t dec_cap, int round, int last_round) {
   __shared__ StreamLds S[kVS];
+  __shared__ WaveLds W;
   const int l = lane_id();
   const uint32_t g = (uint32_t)l >> 3, j = (uint32_t)l & 7;
   StreamLds &M = S[g];
@@ -998,6 +1014,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
             TokDec t;
             t.in = in;
             t.T = &G;
+            t.W = &W;
             t.seek(s_hdr);
             if (read_dynamic(t)) {
               r = kCodecCorrupt;
@@ -1005,7 +1022,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
               break;
             }
           } else if (stm == kFlFixed) {
-            fixed_tables(G);
+            fixed_tables(G, W);
             s_fixed = 1;
           }
           sm = stm == kFlHeader ? kVHeader : stm == kFlStored ? kVStored : kVHuff;
@@ -1020,6 +1037,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
         TokDec t;
         t.in = in;
         t.T = &G;
+        t.W = &W;
         t.seek(s_bit);
         if (t.nb < 32) t.refill();
         s_fin = t.take(1);
@@ -1034,7 +1052,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           s_left = len;
           sm = kVStored;
         } else if (type == 1) {
-          if (!s_fixed) fixed_tables(G);
+          if (!s_fixed) fixed_tables(G, W);
           s_fixed = 1;
           sm = kVHuff;
         } else if (type == 2) {
@@ -1056,10 +1074,10 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
         seek = sm != kVFinish;
       }
       // write the stream state back to its lanes
-      if (seek) {  // refill the ring at s_bit: 64 dwords from the dword before it
+      if (seek) {  // refill the ring at s_bit: 32 dwords from the 16 B boundary before it
         const uint32_t dw = (uint32_t)(s_bit >> 5), base = dw & ~3u;
         wave_lds_sync();
-        G.ring[(base + l) & (kRingDw - 1)] = fetch_dword(in, 4 * (uint64_t)(base + l));
+        if (l < 32) G.ring[(base + l) & (kRingDw - 1)] = fetch_dword(in, 4 * (uint64_t)(base + l));
         wave_lds_sync();
         if (mine) {
           const uint32_t sh = (uint32_t)(s_bit & 31);
@@ -1068,7 +1086,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           rpos = dw + 1;
           nw0 = M.ring[rpos & (kRingDw - 1)];
           nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];
-          rhi = base + 64;
+          rhi = base + 32;
           pf0 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j));
           pf1 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 1));
           pf2 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 2));
@@ -1123,7 +1141,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
       for (int step = 0; step < kPass; step++) {
         if (!cold) {
           uint32_t e = M.lit[(uint32_t)bitbuf & ((1u << kTokLitRoot) - 1)];
-          if ((e & 15) == 0 && (e & kEnLenBit)) e = slow_walk<kTokLitRoot>(M.ls, M.lent, (uint32_t)bitbuf);
+          if ((e & 15) == 0 && (e & kEnLenBit)) e = slow_walk<kTokLitRoot>(M.lfco, M.lent, (uint32_t)bitbuf);
           const uint32_t L = e & 15, isl = (e >> 4) & 1, E = (e >> 5) & 7;
           const uint32_t len = (e >> 8) + 3 + ((uint32_t)(bitbuf >> L) & ((1u << E) - 1));
           uint64_t b1 = bitbuf >> (L + E);
@@ -1132,9 +1150,10 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           b1 |= m1 ? ((uint64_t)nw0 << n1) : 0ull;
           n1 += m1 ? 32u : 0u;
           uint32_t dd = M.dst[(uint32_t)b1 & ((1u << kTokDistRoot) - 1)];
-          if (isl && (dd & 15) == 0 && (dd & kEnLenBit)) dd = slow_walk<kTokDistRoot>(M.ds, M.dent, (uint32_t)b1);
-          const uint32_t L2 = dd & 15, E2 = (dd >> 8) & 15;
-          const uint32_t dist = (dd >> 16) + ((uint32_t)(b1 >> L2) & ((1u << E2) - 1));
+          if (isl && (dd & 15) == 0 && (dd & kEnLenBit)) dd = slow_walk<kTokDistRoot>(M.dfco, M.dent, (uint32_t)b1);
+          const uint32_t L2 = dd & 15;
+          uint32_t E2;
+          const uint32_t dist = dist_base((dd >> 8) & 31, E2) + ((uint32_t)(b1 >> L2) & ((1u << E2) - 1));
           const uint32_t c2 = isl ? L2 + E2 : 0u;
           uint64_t b2 = b1 >> c2;
           uint32_t n2 = n1 - c2;
@@ -1197,7 +1216,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           uint32_t e = M.lit[(uint32_t)bitbuf & ((1u << kTokLitRoot) - 1)];
           uint32_t L = e & 15;
           if (L == 0 && (e & kEnLenBit)) {
-            e = slow_walk<kTokLitRoot>(M.ls, M.lent, (uint32_t)bitbuf);
+            e = slow_walk<kTokLitRoot>(M.lfco, M.lent, (uint32_t)bitbuf);
             L = e & 15;
           }
           const uint32_t E = (e >> 5) & 7;
@@ -1236,15 +1255,15 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
             uint32_t dd = M.dst[(uint32_t)bitbuf & ((1u << kTokDistRoot) - 1)];
             uint32_t L2 = dd & 15;
             if (L2 == 0 && (dd & kEnLenBit)) {
-              dd = slow_walk<kTokDistRoot>(M.ds, M.dent, (uint32_t)bitbuf);
+              dd = slow_walk<kTokDistRoot>(M.dfco, M.dent, (uint32_t)bitbuf);
               L2 = dd & 15;
             }
             if (L2 == 0) {
               res = kCodecCorrupt;
               mode = kVFinish;
             } else {
-              const uint32_t E2 = (dd >> 8) & 15;
-              const uint32_t dist = (dd >> 16) + ((uint32_t)(bitbuf >> L2) & ((1u << E2) - 1));
+              uint32_t E2;
+              const uint32_t dist = dist_base((dd >> 8) & 31, E2) + ((uint32_t)(bitbuf >> L2) & ((1u << E2) - 1));
               bitbuf >>= (L2 + E2);
               nbits -= L2 + E2;
               const uint32_t hist = olen < 32768u ? olen : 32768u;
@@ -1335,14 +1354,30 @@ __device__ __forceinline__ uint32_t umod_small(uint32_t k, uint32_t d) {
   return (uint32_t)r;
 }
 
-constexpr int kLzWin = 65536;  // 32 KiB of history + up to 32 KiB written but not yet flushed
-constexpr int kLzSuper = 16;   // batches of 64 tokens staged in LDS per super-batch
+// Copy-pass window: a ring of 48 KiB = the 32 KiB DEFLATE history + one batch
+// (at most 16 KiB; a longer batch is split in two halves), flushed after
+// every batch: a write at x replaces x - 48 KiB, which is flushed and older
+// than any source of the batch.
+constexpr uint32_t kLzWin = 49152;
+constexpr uint32_t kLzSpan = kLzWin - 32768;
+constexpr int kLzSuper = 16;  // batches of 64 tokens staged in LDS per super-batch
+
+// x mod 49152 (= 3 * 2^14) for any u32 x
+__device__ __forceinline__ uint32_t lz_slot(uint32_t x) {
+  const uint32_t q = ((x >> 14) * 43691u) >> 17;  // (x >> 14) / 3
+  return x - q * kLzWin;
+}
+__device__ __forceinline__ uint32_t lz_next(uint32_t slot, uint32_t k) {  // slot + k (k < kLzWin), wrapped
+  const uint32_t r = slot + k;
+  return r >= kLzWin ? r - kLzWin : r;
+}
 
 // write the completed 1 KiB units of [flushed, olen) to HBM, 16 B per lane
+// (a unit never wraps: 49152 is a multiple of 1024)
 __device__ __forceinline__ void lz_flush_units(const uint8_t *win, uint8_t *out, uint64_t &flushed, uint64_t olen) {
   const int l = lane_id();
   for (uint64_t u0 = flushed & ~1023ull; u0 + 1024 <= olen; u0 += 1024) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(win + ((u0 + 16 * l) & (kLzWin - 1)));
+    const uint4 v = *reinterpret_cast<const uint4 *>(win + lz_slot((uint32_t)u0) + 16 * l);
     *reinterpret_cast<uint4 *>(out + u0 + 16 * l) = v;
     flushed = u0 + 1024;
   }
@@ -1354,7 +1389,6 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
   const int l = lane_id();
   if (round > 0 && uni64(d.fl_more[round - 1]) == 0) return;
   const uint64_t nb = uni64(*nblocks);
-  constexpr uint32_t M = kLzWin - 1;
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     FlState *sp = &d.fl[b];
     const uint32_t mode = uni(sp->mode);
@@ -1366,14 +1400,12 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
     wave_lds_sync();
     if (olen > 0) {  // resumed: the history this block has already written
       const uint64_t h = olen < 32768ull ? olen : 32768ull;
-      for (uint64_t k = l; k < h; k += 64) win[(olen - h + k) & M] = out[olen - h + k];
+      for (uint64_t k = l; k < h; k += 64) win[lz_slot((uint32_t)(olen - h + k))] = out[olen - h + k];
       wave_lds_sync();
     }
     uint64_t flushed = olen;
     // Tokens stream through LDS one super-batch (1,024 tokens) at a time; the
-    // next super-batch is loaded into registers while this one is decoded, and
-    // completed output is flushed just before those loads are issued, so no
-    // load ever waits behind a recent store (vmcnt is in order).
+    // next super-batch is loaded into registers while this one is decoded.
     uint32_t pre[kLzSuper];
 #pragma unroll
     for (int q = 0; q < kLzSuper; q++) pre[q] = (64u * q + (uint32_t)l < ntok) ? tk[64 * q + l] : 0u;
@@ -1381,88 +1413,96 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
       wave_lds_sync();
 #pragma unroll
       for (int q = 0; q < kLzSuper; q++) tbuf[64 * q + l] = pre[q];
-      lz_flush_units(win, out, flushed, olen);
       const uint32_t s1 = s0 + 64 * kLzSuper;
 #pragma unroll
       for (int q = 0; q < kLzSuper; q++) pre[q] = (s1 + 64u * q + (uint32_t)l < ntok) ? tk[s1 + 64 * q + l] : 0u;
       wave_lds_sync();
       const uint32_t nbat = (ntok - s0 + 63) / 64 < (uint32_t)kLzSuper ? (ntok - s0 + 63) / 64 : (uint32_t)kLzSuper;
       for (uint32_t bi = 0; bi < nbat; bi++) {
-        const uint32_t t = (s0 + 64 * bi + (uint32_t)l < ntok) ? tbuf[64 * bi + l] : 0u;
-        const bool m = (t >> 31) != 0;
-        const uint32_t len = m ? ((t >> 16) & 0xffu) + 3 : (t >> 24) & 3u;
-        const uint32_t incl = wave_incl_sum_dpp(len);
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-        const uint32_t p = incl - len;  // position relative to olen
-        const uint32_t base = (uint32_t)olen;
-        if (!m) {
-          if (len > 0) win[(base + p) & M] = (uint8_t)t;
-          if (len > 1) win[(base + p + 1) & M] = (uint8_t)(t >> 8);
-          if (len > 2) win[(base + p + 2) & M] = (uint8_t)(t >> 16);
-        }
-        const uint32_t dist = (t & 0x7fffu) + 1;
-        const int src_end = (int)p - (int)dist + (int)(len < dist ? len : dist);
-        const unsigned long long mm = __ballot(m);
-        if (mm) {
-          // one parallel round: every match whose source ends before the batch's
-          // first match (its own lane copies it, 8 bytes per LDS round trip) ...
-          const int R = (int)__builtin_amdgcn_readlane(p, __ffsll((long long)mm) - 1);
-          const bool ready = m && src_end <= R && len <= 16;
-          if (ready) {
-            const uint32_t sa = base + p - dist, q = base + p;
-            if (dist >= 8 || len <= dist) {  // no byte of an 8-byte piece depends on another
-              for (uint32_t k = 0; k < len; k += 8) {
-                const uint32_t a0 = (sa + k) & M, d0 = (q + k) & M;
-                uint8_t v[8];
-                if (a0 + 8 <= (uint32_t)kLzWin) {
+        const uint32_t t0 = (s0 + 64 * bi + (uint32_t)l < ntok) ? tbuf[64 * bi + l] : 0u;
+        const uint32_t len0 = (t0 >> 31) ? ((t0 >> 16) & 0xffu) + 3 : (t0 >> 24) & 3u;
+        // a batch spanning more than kLzSpan bytes (long matches) goes in two halves
+        const uint32_t all = (uint32_t)__builtin_amdgcn_readlane(wave_incl_sum_dpp(len0), 63);
+        const int halves = all > kLzSpan ? 2 : 1;
+        for (int h = 0; h < halves; h++) {
+          const bool mine = halves == 1 || ((l < 32) == (h == 0));
+          const uint32_t t = mine ? t0 : 0u;
+          const bool m = (t >> 31) != 0;
+          const uint32_t len = mine ? len0 : 0u;
+          const uint32_t incl = wave_incl_sum_dpp(len);
+          const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+          const uint32_t p = incl - len;  // position relative to olen
+          const uint32_t base = (uint32_t)olen;
+          const uint32_t q0 = lz_slot(base + p);  // the token's first output slot
+          if (!m) {
+            if (len > 0) win[q0] = (uint8_t)t;
+            if (len > 1) win[lz_next(q0, 1)] = (uint8_t)(t >> 8);
+            if (len > 2) win[lz_next(q0, 2)] = (uint8_t)(t >> 16);
+          }
+          const uint32_t dist = (t & 0x7fffu) + 1;
+          const int src_end = (int)p - (int)dist + (int)(len < dist ? len : dist);
+          const unsigned long long mm = __ballot(m);
+          if (mm) {
+            // one parallel round: every short match whose source ends before the
+            // batch's first match, copied by its own lane 8 bytes at a time ...
+            const int R = (int)__builtin_amdgcn_readlane(p, __ffsll((long long)mm) - 1);
+            const bool ready = m && src_end <= R && len <= 16;
+            if (ready) {
+              const uint32_t a0 = lz_slot(base + p - dist);
+              if (dist >= 8 || len <= dist) {  // no byte of an 8-byte piece depends on another
+                for (uint32_t k = 0; k < len; k += 8) {
+                  const uint32_t sa = lz_next(a0, k), da = lz_next(q0, k);
+                  uint8_t v[8];
+                  if (sa + 8 <= kLzWin) {
 #pragma unroll
-                  for (int jj = 0; jj < 8; jj++) v[jj] = win[a0 + jj];
-                } else {
+                    for (int jj = 0; jj < 8; jj++) v[jj] = win[sa + jj];
+                  } else {
 #pragma unroll
-                  for (int jj = 0; jj < 8; jj++) v[jj] = win[(a0 + jj) & M];
+                    for (int jj = 0; jj < 8; jj++) v[jj] = win[lz_next(sa, jj)];
+                  }
+                  if (da + 8 <= kLzWin && k + 8 <= len) {
+#pragma unroll
+                    for (int jj = 0; jj < 8; jj++) win[da + jj] = v[jj];
+                  } else {
+#pragma unroll
+                    for (int jj = 0; jj < 8; jj++)
+                      if (k + jj < len) win[lz_next(da, jj)] = v[jj];
+                  }
                 }
-                if (d0 + 8 <= (uint32_t)kLzWin && k + 8 <= len) {
-#pragma unroll
-                  for (int jj = 0; jj < 8; jj++) win[d0 + jj] = v[jj];
-                } else {
-#pragma unroll
-                  for (int jj = 0; jj < 8; jj++)
-                    if (k + jj < len) win[(d0 + jj) & M] = v[jj];
-                }
+              } else {  // overlapping run: byte by byte, each byte reads one written before it
+                for (uint32_t k = 0; k < len; k++) win[lz_next(q0, k)] = win[lz_next(a0, k)];
               }
-            } else {  // overlapping run: byte by byte, each byte reads one written before it
-              for (uint32_t k = 0; k < len; k++) win[(q + k) & M] = win[(sa + k) & M];
+            }
+            // ... then the rest (sources inside this batch, or longer than 16 B) in
+            // order, each copied by the whole wave: every byte it reads precedes it
+            // and is final by then
+            unsigned long long rem = mm & ~__ballot(ready);
+            while (rem) {
+              const int f = __ffsll((long long)rem) - 1;
+              rem &= rem - 1;
+              const uint32_t P = base + (uint32_t)__builtin_amdgcn_readlane(p, f);
+              const uint32_t D = (uint32_t)__builtin_amdgcn_readlane(dist, f);
+              const uint32_t N = (uint32_t)__builtin_amdgcn_readlane(len, f);
+              const uint32_t sa = lz_slot(P - D), da = lz_slot(P);
+              for (uint32_t k0 = 0; k0 < N; k0 += 64) {
+                const uint32_t k = k0 + (uint32_t)l;
+                const uint32_t kk = D >= N ? k : umod_small(k, D);
+                const uint8_t v = k < N ? win[lz_next(sa, kk)] : 0;
+                if (k < N) win[lz_next(da, k)] = v;
+              }
             }
           }
-          // ... then the rest (sources inside this batch, or longer than 16 B) in
-          // order, each copied by the whole wave: every byte it reads precedes it
-          // and is final by then
-          unsigned long long rem = mm & ~__ballot(ready);
-          while (rem) {
-            const int f = __ffsll((long long)rem) - 1;
-            rem &= rem - 1;
-            const uint32_t P = base + (uint32_t)__builtin_amdgcn_readlane(p, f);
-            const uint32_t D = (uint32_t)__builtin_amdgcn_readlane(dist, f);
-            const uint32_t N = (uint32_t)__builtin_amdgcn_readlane(len, f);
-            for (uint32_t k0 = 0; k0 < N; k0 += 64) {
-              const uint32_t k = k0 + (uint32_t)l;
-              const uint32_t kk = D >= N ? k : umod_small(k, D);
-              const uint8_t v = k < N ? win[(P - D + kk) & M] : 0;
-              if (k < N) win[(P + k) & M] = v;
-            }
+          olen += total;
+          if ((olen & ~1023ull) > flushed) {
+            wave_lds_sync();
+            lz_flush_units(win, out, flushed, olen);
           }
-        }
-        olen += total;
-        // a write at x replaces x - 64 KiB: keep the unflushed part under 32 KiB
-        if (olen - flushed > 32768 - 1024) {
-          wave_lds_sync();
-          lz_flush_units(win, out, flushed, olen);
         }
       }
     }
     wave_lds_sync();
     lz_flush_units(win, out, flushed, olen);
-    for (uint64_t k = flushed + l; k < olen; k += 64) out[k] = win[k & M];
+    for (uint64_t k = flushed + l; k < olen; k += 64) out[k] = win[lz_slot((uint32_t)k)];
     if (l == 0) {
       sp->olen2 = olen;
       if (mode == kFlDone) d.blk_out_len[b] = olen;
@@ -1518,11 +1558,12 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
                     uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st) {
   (void)hipMemsetAsync(d.fl_more, 0, sizeof(unsigned long long) * rounds, st);
   uint64_t g1 = (max_blocks + kVS - 1) / kVS;
-  const uint64_t r1 = (uint64_t)ncu * 4;  // 4 waves of 8 streams per CU (LDS-bound)
+  // resident waves of 8 streams per CU: LDS-bound
+  const uint64_t r1 = (uint64_t)ncu * (163840 / (sizeof(StreamLds) * kVS + sizeof(WaveLds)));
   if (g1 > r1) g1 = r1;
   if (g1 < 1) g1 = 1;
   uint64_t g2 = max_blocks;
-  const uint64_t r2 = (uint64_t)ncu * 2;  // 64 KiB windows: 2 per CU
+  const uint64_t r2 = (uint64_t)ncu * 3;  // 48 KiB windows: 3 per CU
   if (g2 > r2) g2 = r2;
   if (g2 < 1) g2 = 1;
   for (int r = 0; r < rounds; r++) {
