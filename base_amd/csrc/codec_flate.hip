@@ -994,7 +994,8 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           }
           const uint64_t n = uni64(d.blk_len[sb]);
           const uint64_t total = meta & kMetaTotalMask;
-          const uint64_t tc = total * (uint64_t)kTokPerChunk;
+          uint64_t tc = total * (uint64_t)kTokPerChunk;
+          if (d.tok_limit && d.tok_limit < tc) tc = d.tok_limit < 64 ? 64 : d.tok_limit;
           const uint64_t cp = uni64(d.blk_out_len[sb]);
           s_c0 = (uint32_t)c0;
           s_n = (uint32_t)n;
@@ -1561,6 +1562,7 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
   // resident waves of 8 streams per CU: LDS-bound
   const uint64_t r1 = (uint64_t)ncu * (163840 / (sizeof(StreamLds) * kVS + sizeof(WaveLds)));
   if (g1 > r1) g1 = r1;
+  if (d.fl_grid && g1 > d.fl_grid) g1 = d.fl_grid;
   if (g1 < 1) g1 = 1;
   uint64_t g2 = max_blocks;
   const uint64_t r2 = (uint64_t)ncu * 3;  // 48 KiB windows: 3 per CU

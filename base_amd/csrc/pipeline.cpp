@@ -160,6 +160,11 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   HIP_OK(hipGetDeviceProperties(&prop, c->device));
   c->ncu = prop.multiProcessorCount;
   if (const char *f = getenv("RIO_KERNEL_FLAGS")) c->kernel_flags = atoi(f);
+  // test hook: a small flate token region per block and round forces the
+  // yield / resume path across rounds (and the host retry with more rounds)
+  if (const char *f = getenv("RIO_FL_TOKCAP")) c->d.tok_limit = strtoull(f, nullptr, 10);
+  // test hook: few Huffman-pass waves, so every stream decodes many blocks
+  if (const char *f = getenv("RIO_FL_GRID")) c->d.fl_grid = strtoull(f, nullptr, 10);
   uint64_t span = (cfg && cfg->max_span_bytes) ? cfg->max_span_bytes : (256ull << 20);
   span = (span + kChunk - 1) / kChunk * kChunk;
   c->max_span = span;

@@ -155,6 +155,8 @@ struct DevBufs {
   FlState *fl;                   // per block (flate)
   uint32_t *tok;                 // flate tokens: block b's region starts at blk_c0[b] * kTokPerChunk
   uint64_t tok_cap;              // u32 entries at tok
+  uint64_t tok_limit;            // tokens per block and round (0: the whole region; RIO_FL_TOKCAP, tests)
+  uint64_t fl_grid;              // Huffman-pass workgroups (0: all resident; RIO_FL_GRID, tests)
   unsigned long long *fl_more;   // per round: blocks whose token region filled (kFlRounds)
   Ctl *ctl;
   // CRC tables (constant)
