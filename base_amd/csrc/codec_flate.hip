@@ -479,9 +479,9 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
 // Table entries. Literal/length (u16): code length (3:0; 0 = not decodable
 // from the root), bit 4 set for a length or end-of-block, length extra bits
 // (7:5; 7 = end-of-block), literal byte or length base - 3 (15:8).
-// Distance (u16): code length (3:0), symbol (12:8); base and extra bits
-// follow from the symbol (dist_sym). Code-length alphabet (u16): code
-// length (3:0), symbol (12:8).
+// Distance (u16): code length (3:0), m (6:5), extra bits (10:7), with
+// base = (m << extra) + 1. Code-length alphabet (u16): code length (3:0),
+// symbol (12:8).
 // Code length 0 with bit 4 set (kLongMark) marks a code longer than the root
 // (canonical walk); an all-zero entry is a bit pattern no code has or a
 // symbol DEFLATE never assigns (literal/length 286-287, distance 30-31):
@@ -492,7 +492,7 @@ constexpr uint32_t kEobExtra = 7;
 enum : int { kTabLit = 0, kTabDist = 1, kTabClen = 2 };
 enum : int { kTokDone = 0, kTokYield = -1 };
 #ifndef RIO_LIT_ROOT
-#define RIO_LIT_ROOT 10
+#define RIO_LIT_ROOT 9
 #endif
 constexpr int kTokLitRoot = RIO_LIT_ROOT;  // literal/length root table bits
 constexpr int kTokDistRoot = 8;
@@ -513,15 +513,28 @@ __device__ __forceinline__ uint32_t tab_entry(int kind, uint32_t s, uint32_t len
       return len | kEnLenBit | ((uint32_t)kLenExtra[s - 257] << 5) | ((uint32_t)(kLenBase[s - 257] - 3) << 8);
     return 0;
   }
-  if (kind == kTabDist) {
-    return s < 30 ? len | (s << 8) : 0u;
+  if (kind == kTabDist) {  // base = (m << extra) + 1
+    if (s >= 30) return 0u;
+    const uint32_t m = s < 4 ? s : 2u | (s & 1), ex = s < 4 ? 0u : (s >> 1) - 1;
+    return len | (m << 5) | (ex << 7);
   }
   return len | (s << 8);
 }
 
-constexpr int kVS = 8;         // streams per wave
-constexpr int kRingDw = 64;    // input ring per stream (dwords)
-constexpr int kTbuf = 36;      // tokens buffered per stream between input passes (2 per step, hot + full, + 1 slack)
+#ifndef RIO_FL_LANES
+#define RIO_FL_LANES 8
+#endif
+constexpr int kVG = RIO_FL_LANES;  // lanes per stream (its state is the same in all of them)
+constexpr int kVS = 64 / kVG;      // streams per wave
+constexpr int kPf = 16 / kVG;      // prefetched ring dwords per lane (16 per stream)
+// Input ring per stream: 32 dwords, refilled with 16 (a 2-dword prefetch per
+// lane) whenever at most 16 are left. A pass decodes at most kPass symbols,
+// <= 48 bits = 1.5 dwords each, so at most 12 dwords: a ring that starts a
+// pass with >= 14 dwords never runs dry (the two ahead of rpos stay valid),
+// and after the refill it holds >= 17 again (18 after a seek). A refill
+// replaces dwords [rhi - 32, rhi - 16), all consumed.
+constexpr int kRingDw = 32;
+constexpr int kTbuf = 10;      // tokens per stream per pass: 1 per step + 2 slack (a failed hot step's write)
 constexpr int kPass = 8;       // decode steps between input passes
 
 // Canonical code data per code length (first code 15:0, count 31:16, index
@@ -658,12 +671,6 @@ __device__ __forceinline__ uint32_t slow_walk(const uint64_t *lfco, const TT *so
     }
   }
   return idx == 0xffffffffu ? 0u : ((uint32_t)sorted[idx] | len);
-}
-
-// distance base and extra bits of distance symbol s < 30 (RFC 1951 §3.2.5)
-__device__ __forceinline__ uint32_t dist_base(uint32_t s, uint32_t &extra) {
-  extra = s < 4 ? 0u : (s >> 1) - 1;
-  return s < 4 ? s + 1 : ((2u + (s & 1)) << extra) + 1;
 }
 
 // logical compressed dword at byte p (a multiple of 4); bytes at/after n read 0
@@ -854,22 +861,27 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
   __shared__ StreamLds S[kVS];
   __shared__ WaveLds W;
   const int l = lane_id();
-  const uint32_t g = (uint32_t)l >> 3, j = (uint32_t)l & 7;
+  const uint32_t g = (uint32_t)l / kVG, j = (uint32_t)l % kVG;
   StreamLds &M = S[g];
   if (round > 0 && uni64(d.fl_more[round - 1]) == 0) return;
   const uint64_t nblk = uni64(*nblocks);
   const uint64_t stride = (uint64_t)gridDim.x * kVS;
 
-  // stream state (the same in the 8 lanes of a group)
+  // stream state (the same in the kVG lanes of a group)
   uint64_t next_b = (uint64_t)blockIdx.x * kVS + g, cur_b = 0;
   uint32_t mode = kVNew, res = 0;
   uint32_t bc0 = 0, bn = 0, btot = 0, breg = 0, tcap = 0, cap = 0;  // block
-  uint64_t bitbuf = 0;                                               // bit reader
-  uint32_t nbits = 0, rpos = 0, rhi = 0, nw0 = 0, nw1 = 0;
-  uint32_t pf0 = 0, pf1 = 0, pf2 = 0, pf3 = 0;                       // next 128 B of the ring
-  uint32_t olen = 0, fin = 0, left = 0, fixed_ok = 0;                // decode
+  // bit reader: stream dwords rpos-2 (lo) and rpos-1 (hi), bit offset o < 32
+  // into lo; nw0 / nw1 = ring dwords rpos, rpos+1 (requested one step ahead).
+  // The 32-bit window at the read position is alignbit(hi, lo, o): >= 33
+  // valid bits, enough for any code plus its extra bits.
+  uint32_t lo = 0, hi = 0, o = 0, rpos = 0, rhi = 0, nw0 = 0, nw1 = 0;
+  uint32_t pf[kPf];  // next 64 B of the ring
+#pragma unroll
+  for (int i = 0; i < kPf; i++) pf[i] = 0;
+  uint32_t olen = 0, fin = 0, left = 0, fixed_ok = 0;  // decode
   uint64_t hdrpos = 0;
-  uint32_t nst = 0, nv = 0, pend = 0, npend = 0;                     // tokens
+  uint32_t nst = 0, nv = 0;  // tokens stored / buffered in tbuf
 
   for (;;) {
     // ---------------------------------------------------------- escapes
@@ -880,7 +892,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
 #endif
       const uint32_t gl = (uint32_t)__ffsll((long long)esc) - 1;
       esc &= esc - 1;
-      const uint32_t gg = gl >> 3;
+      const uint32_t gg = gl / kVG;
       const bool mine = g == gg;
       StreamLds &G = S[gg];
       uint32_t sm = rl32(mode, gl);
@@ -889,29 +901,20 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
       uint32_t s_olen = rl32(olen, gl), s_fin = rl32(fin, gl), s_left = rl32(left, gl), s_fixed = rl32(fixed_ok, gl);
       uint32_t s_nst = rl32(nst, gl);
       uint64_t s_hdr = rl64(hdrpos, gl);
-      uint64_t s_bit = 32 * (uint64_t)rl32(rpos, gl) - rl32(nbits, gl);
+      uint64_t s_bit = 32 * ((uint64_t)rl32(rpos, gl) - 2) + rl32(o, gl);
       uint64_t s_next = rl64(next_b, gl);
       uint32_t s_tcap = rl32(tcap, gl), s_cap = rl32(cap, gl);
-      bool seek = false, fresh = false;  // fresh: a block ended or began, no pending literals
+      bool seek = false;
       int r = 0;
       if (sm == kVFinish) {
         r = (int)rl32(res, gl);
         FlState *sp = &d.fl[sb];
         uint32_t stm = kFlDone;
-        if (r == kTokYield || r == kTokDone) {
-          const uint32_t sp_n = rl32(npend, gl);
-          if (sp_n) {  // pending literals (room for one token is kept)
-            if (l == 0) d.tok[(uint64_t)s_c0 * kTokPerChunk + s_nst] = rl32(pend, gl) | (sp_n << 24);
-            s_nst++;
-          }
-          if (r == kTokYield) {
-            const uint32_t vm = rl32(mode, gl);  // unused: the stream's mode before the yield is in s_left/s_fixed
-            (void)vm;
-            stm = s_left ? kFlStored : (s_fixed ? kFlFixed : kFlDynamic);
-            if (last_round) {  // more rounds needed than were launched: the host retries with more
-              if (l == 0) atomicOr(&d.ctl->out_overflow, 0x1000ull);
-              stm = kFlSkip;
-            }
+        if (r == kTokYield) {
+          stm = s_left ? kFlStored : (s_fixed ? kFlFixed : kFlDynamic);
+          if (last_round) {  // more rounds needed than were launched: the host retries with more
+            if (l == 0) atomicOr(&d.ctl->out_overflow, 0x1000ull);
+            stm = kFlSkip;
           }
         }
         if (l == 0) {
@@ -944,7 +947,6 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
         }
         sm = kVNew;
         r = 0;
-        fresh = true;
       }
       CompIn in;
       if (sm == kVNew) {
@@ -1081,17 +1083,15 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
         if (l < 32) G.ring[(base + l) & (kRingDw - 1)] = fetch_dword(in, 4 * (uint64_t)(base + l));
         wave_lds_sync();
         if (mine) {
-          const uint32_t sh = (uint32_t)(s_bit & 31);
-          bitbuf = (uint64_t)(M.ring[dw & (kRingDw - 1)] >> sh);
-          nbits = 32 - sh;
-          rpos = dw + 1;
+          lo = M.ring[dw & (kRingDw - 1)];
+          hi = M.ring[(dw + 1) & (kRingDw - 1)];
+          o = (uint32_t)(s_bit & 31);
+          rpos = dw + 2;
           nw0 = M.ring[rpos & (kRingDw - 1)];
           nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];
           rhi = base + 32;
-          pf0 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j));
-          pf1 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 1));
-          pf2 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 2));
-          pf3 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 3));
+#pragma unroll
+          for (int i = 0; i < kPf; i++) pf[i] = fetch_dword(in, 4 * (uint64_t)(rhi + kPf * j + i));
         }
       }
       if (mine) {
@@ -1111,12 +1111,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
         fixed_ok = s_fixed;
         hdrpos = s_hdr;
         nst = s_nst;
-        if (sm == kVFinish && !seek) {  // (errors keep the bit position for nothing)
-          rpos = (uint32_t)(s_bit >> 5);
-          nbits = 0;
-        }
         nv = 0;
-        if (fresh) pend = npend = 0;
       }
     }
     if (!__ballot(mode != kVGone)) break;
@@ -1124,62 +1119,47 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
     // ---------------------------------------------------------- hot steps
     // The common case, branch-light: a stream decoding a Huffman block with
     // room for this pass's tokens decodes one literal or one match per step.
-    // The step starts with >= 32 bits in the buffer, and the two ring words
-    // after them (nw0, nw1) were requested at the end of the previous step,
-    // so no refill waits on LDS. Anything else -- a code longer than the root
-    // table, end of block, a corrupt or oversized symbol -- leaves the state
-    // untouched and the stream to the full step below.
-    if (mode == kVHuff && nbits < 32) {  // the hot step starts with >= 32 bits
-      bitbuf |= (uint64_t)nw0 << nbits;
-      nbits += 32;
-      rpos++;
-      nw0 = M.ring[rpos & (kRingDw - 1)];
-      nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];
-    }
-    const bool hot0 = mode == kVHuff && tcap - nst - nv >= 2 * kPass + 3;
+    // Anything else -- end of block, a corrupt or oversized symbol -- leaves
+    // the state untouched and the stream to the full step below.
+    const bool hot0 = mode == kVHuff && tcap - nst - nv >= kPass + 3;
     bool cold = !hot0;
+    uint32_t hs = 0;  // hot steps taken: a pass decodes at most kPass symbols
     if (__ballot(hot0)) {
       for (int step = 0; step < kPass; step++) {
         if (!cold) {
-          uint32_t e = M.lit[(uint32_t)bitbuf & ((1u << kTokLitRoot) - 1)];
-          if ((e & 15) == 0 && (e & kEnLenBit)) e = slow_walk<kTokLitRoot>(M.lfco, M.lent, (uint32_t)bitbuf);
+          hs++;
+          const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, o);
+          uint32_t e = M.lit[w & ((1u << kTokLitRoot) - 1)];
+          if ((e & 15) == 0 && (e & kEnLenBit)) e = slow_walk<kTokLitRoot>(M.lfco, M.lent, w);
           const uint32_t L = e & 15, isl = (e >> 4) & 1, E = (e >> 5) & 7;
-          const uint32_t len = (e >> 8) + 3 + ((uint32_t)(bitbuf >> L) & ((1u << E) - 1));
-          uint64_t b1 = bitbuf >> (L + E);
-          uint32_t n1 = nbits - (L + E);
-          const bool m1 = n1 < 32;
-          b1 |= m1 ? ((uint64_t)nw0 << n1) : 0ull;
-          n1 += m1 ? 32u : 0u;
-          uint32_t dd = M.dst[(uint32_t)b1 & ((1u << kTokDistRoot) - 1)];
-          if (isl && (dd & 15) == 0 && (dd & kEnLenBit)) dd = slow_walk<kTokDistRoot>(M.dfco, M.dent, (uint32_t)b1);
-          const uint32_t L2 = dd & 15;
-          uint32_t E2;
-          const uint32_t dist = dist_base((dd >> 8) & 31, E2) + ((uint32_t)(b1 >> L2) & ((1u << E2) - 1));
-          const uint32_t c2 = isl ? L2 + E2 : 0u;
-          uint64_t b2 = b1 >> c2;
-          uint32_t n2 = n1 - c2;
-          const bool m2 = n2 < 32;
-          b2 |= m2 ? ((uint64_t)(m1 ? nw1 : nw0) << n2) : 0ull;
-          n2 += m2 ? 32u : 0u;
+          const uint32_t len = (e >> 8) + 3 + __builtin_amdgcn_ubfe(w, L, E);
+          uint32_t o1 = o + L + E;
+          const bool a1 = o1 >= 32;
+          const uint32_t lo1 = a1 ? hi : lo, hi1 = a1 ? nw0 : hi;
+          o1 -= a1 ? 32u : 0u;
+          const uint32_t w2 = __builtin_amdgcn_alignbit(hi1, lo1, o1);
+          uint32_t dd = M.dst[w2 & ((1u << kTokDistRoot) - 1)];
+          if (isl && (dd & 15) == 0 && (dd & kEnLenBit)) dd = slow_walk<kTokDistRoot>(M.dfco, M.dent, w2);
+          const uint32_t L2 = dd & 15, E2 = (dd >> 7) & 15;
+          const uint32_t dist = (((dd >> 5) & 3) << E2) + 1 + __builtin_amdgcn_ubfe(w2, L2, E2);
+          uint32_t o2 = o1 + (isl ? L2 + E2 : 0u);
+          const bool a2 = o2 >= 32;
+          const uint32_t lo2 = a2 ? hi1 : lo1, hi2 = a2 ? (a1 ? nw1 : nw0) : hi1;
+          o2 -= a2 ? 32u : 0u;
           const uint32_t hist = olen < 32768u ? olen : 32768u;
           const bool ok = L != 0 && (isl ? (E != kEobExtra && L2 != 0 && dist <= hist && len <= cap - olen)
                                          : olen < cap);
-          // tokens: a full literal triple, or the pending literals then the match
-          const uint32_t lt = pend | ((e >> 8) << (8 * npend)), ln = npend + 1;
-          const bool c1 = isl ? npend != 0 : ln == 3;
-          const uint32_t t2 = 0x80000000u | ((len - 3) << 16) | (dist - 1);
-          const uint32_t t1 = isl ? (pend | (npend << 24)) : (lt | (3u << 24));
-          M.tbuf[nv] = c1 ? t1 : t2;  // (a failed step's writes sit past nv)
-          M.tbuf[nv + 1] = t2;
-          const bool clr = isl || c1;
-          bitbuf = ok ? b2 : bitbuf;
-          nbits = ok ? n2 : nbits;
-          rpos += ok ? (m1 ? 1u : 0u) + (m2 ? 1u : 0u) : 0u;
-          nv += ok ? (c1 ? 1u : 0u) + isl : 0u;
-          pend = ok ? (clr ? 0u : lt) : pend;
-          npend = ok ? (clr ? 0u : ln) : npend;
-          olen += ok ? (isl ? len : 1u) : 0u;
-          cold = !ok;
+          M.tbuf[nv] = isl ? (0x80000000u | ((len - 3) << 16) | (dist - 1)) : ((e >> 8) | (1u << 24));
+          if (ok) {
+            lo = lo2;
+            hi = hi2;
+            o = o2;
+            rpos += (a1 ? 1u : 0u) + (a2 ? 1u : 0u);
+            nv++;
+            olen += isl ? len : 1u;
+          } else {
+            cold = true;
+          }
           nw0 = M.ring[rpos & (kRingDw - 1)];
           nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];
         }
@@ -1193,80 +1173,67 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
       if (__ballot(cold && mode <= kVStored)) atomicAdd(&d.ctl->pad[1], 1ull);
     }
 #endif
-#define RIO_REFILL()                                                 \
-  if (nbits < 32) {                                                  \
-    bitbuf |= (uint64_t)nw0 << nbits;                                \
-    nbits += 32;                                                     \
-    nw0 = nw1;                                                       \
-    rpos++;                                                          \
-    nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];                        \
+#define RIO_ADV(c_)                                    \
+  {                                                    \
+    o += (c_);                                         \
+    if (o >= 32) {                                     \
+      lo = hi;                                         \
+      hi = nw0;                                        \
+      nw0 = nw1;                                       \
+      rpos++;                                          \
+      nw1 = M.ring[(rpos + 1) & (kRingDw - 1)];        \
+      o -= 32;                                         \
+    }                                                  \
   }
-#define RIO_EMIT(t_)                                                 \
-  {                                                                  \
-    if (j == 0) M.tbuf[nv] = (t_);                                   \
-    nv++;                                                            \
+#define RIO_EMIT(t_)                                   \
+  {                                                    \
+    M.tbuf[nv] = (t_);                                 \
+    nv++;                                              \
   }
-    for (int step = 0; step < kPass && __ballot(cold && mode <= kVStored); step++) {
-      if (!cold) {
+    for (uint32_t step = 0; step < kPass && __ballot(cold && mode <= kVStored && step + hs < kPass); step++) {
+      if (!cold || step + hs >= kPass) {
       } else if (mode == kVHuff) {
         if (tcap - nst - nv < 3) {
           res = (uint32_t)kTokYield;
           mode = kVFinish;
         } else {
-          RIO_REFILL();
-          uint32_t e = M.lit[(uint32_t)bitbuf & ((1u << kTokLitRoot) - 1)];
-          uint32_t L = e & 15;
-          if (L == 0 && (e & kEnLenBit)) {
-            e = slow_walk<kTokLitRoot>(M.lfco, M.lent, (uint32_t)bitbuf);
-            L = e & 15;
-          }
-          const uint32_t E = (e >> 5) & 7;
+          const uint32_t w = __builtin_amdgcn_alignbit(hi, lo, o);
+          uint32_t e = M.lit[w & ((1u << kTokLitRoot) - 1)];
+          if ((e & 15) == 0 && (e & kEnLenBit)) e = slow_walk<kTokLitRoot>(M.lfco, M.lent, w);
+          const uint32_t L = e & 15, E = (e >> 5) & 7;
           if (L == 0) {
             res = kCodecCorrupt;
             mode = kVFinish;
           } else if (!(e & kEnLenBit)) {
-            bitbuf >>= L;
-            nbits -= L;
+            RIO_ADV(L);
             if (olen >= cap) {
               res = kCodecFull;
               mode = kVFinish;
             } else {
+              RIO_EMIT((e >> 8) | (1u << 24));
               olen++;
-              pend |= (e >> 8) << (8 * npend);
-              if (++npend == 3) {
-                RIO_EMIT(pend | (3u << 24));
-                pend = 0;
-                npend = 0;
-              }
             }
           } else if (E == kEobExtra) {
-            bitbuf >>= L;
-            nbits -= L;
+            RIO_ADV(L);
             if (fin) {
-              res = (32 * rpos - nbits > 8 * bn) ? (uint32_t)kCodecEof : (uint32_t)kTokDone;
+              res = (32 * (rpos - 2) + o > 8 * bn) ? (uint32_t)kCodecEof : (uint32_t)kTokDone;
               mode = kVFinish;
             } else {
               mode = kVHeader;
             }
           } else {  // length, then the distance code
-            const uint32_t len = (e >> 8) + 3 + ((uint32_t)(bitbuf >> L) & ((1u << E) - 1));
-            bitbuf >>= (L + E);
-            nbits -= L + E;
-            RIO_REFILL();
-            uint32_t dd = M.dst[(uint32_t)bitbuf & ((1u << kTokDistRoot) - 1)];
-            uint32_t L2 = dd & 15;
-            if (L2 == 0 && (dd & kEnLenBit)) {
-              dd = slow_walk<kTokDistRoot>(M.dfco, M.dent, (uint32_t)bitbuf);
-              L2 = dd & 15;
-            }
+            const uint32_t len = (e >> 8) + 3 + __builtin_amdgcn_ubfe(w, L, E);
+            RIO_ADV(L + E);
+            const uint32_t w2 = __builtin_amdgcn_alignbit(hi, lo, o);
+            uint32_t dd = M.dst[w2 & ((1u << kTokDistRoot) - 1)];
+            if ((dd & 15) == 0 && (dd & kEnLenBit)) dd = slow_walk<kTokDistRoot>(M.dfco, M.dent, w2);
+            const uint32_t L2 = dd & 15, E2 = (dd >> 7) & 15;
             if (L2 == 0) {
               res = kCodecCorrupt;
               mode = kVFinish;
             } else {
-              uint32_t E2;
-              const uint32_t dist = dist_base((dd >> 8) & 31, E2) + ((uint32_t)(bitbuf >> L2) & ((1u << E2) - 1));
-              bitbuf >>= (L2 + E2);
-              nbits -= L2 + E2;
+              const uint32_t dist = (((dd >> 5) & 3) << E2) + 1 + __builtin_amdgcn_ubfe(w2, L2, E2);
+              RIO_ADV(L2 + E2);
               const uint32_t hist = olen < 32768u ? olen : 32768u;
               if (dist > hist) {
                 res = kCodecCorrupt;
@@ -1275,38 +1242,26 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
                 res = kCodecFull;
                 mode = kVFinish;
               } else {
-                if (npend) {
-                  RIO_EMIT(pend | (npend << 24));
-                  pend = 0;
-                  npend = 0;
-                }
                 RIO_EMIT(0x80000000u | ((len - 3) << 16) | (dist - 1));
                 olen += len;
               }
             }
           }
         }
-      } else if (mode == kVStored) {
+      } else if (mode == kVStored) {  // stored bytes become literal tokens, 3 at a time
         if (tcap - nst - nv < 3) {
           res = (uint32_t)kTokYield;
           mode = kVFinish;
         } else {
-          RIO_REFILL();
-          if (npend) {  // literals before the stored bytes
-            RIO_EMIT(pend | (npend << 24));
-            pend = 0;
-            npend = 0;
-          }
           const uint32_t k = left < 3 ? left : 3;
-          const uint32_t v = (uint32_t)bitbuf & (0xffffffffu >> (32 - 8 * k));
-          bitbuf >>= 8 * k;
-          nbits -= 8 * k;
+          const uint32_t v = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, o), 0, 8 * k);
+          RIO_ADV(8 * k);
           RIO_EMIT(v | (k << 24));
           olen += k;
           left -= k;
           if (left == 0) {
             if (fin) {
-              res = (32 * rpos - nbits > 8 * bn) ? (uint32_t)kCodecEof : (uint32_t)kTokDone;
+              res = (32 * (rpos - 2) + o > 8 * bn) ? (uint32_t)kCodecEof : (uint32_t)kTokDone;
               mode = kVFinish;
             } else {
               mode = kVHeader;
@@ -1315,7 +1270,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
         }
       }
     }
-#undef RIO_REFILL
+#undef RIO_ADV
 #undef RIO_EMIT
 
     // ---------------------------------------------------------- input pass
@@ -1323,22 +1278,28 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
     // pass ago, and no store issued since may sit in front of them in vmcnt)
     {
       if (mode <= kVStored) {
-        if (rhi - rpos <= kRingDw - 32) {
-          *reinterpret_cast<uint4 *>(&M.ring[(rhi + 4 * j) & (kRingDw - 1)]) = make_uint4(pf0, pf1, pf2, pf3);
-          rhi += 32;
+        if (rhi - rpos <= kRingDw - 16) {
+          uint32_t *rw = &M.ring[(rhi + kPf * j) & (kRingDw - 1)];
+          if (kPf == 4) {
+            *reinterpret_cast<uint4 *>(rw) = make_uint4(pf[0], pf[1 % kPf], pf[2 % kPf], pf[3 % kPf]);
+          } else if (kPf == 2) {
+            *reinterpret_cast<uint2 *>(rw) = make_uint2(pf[0], pf[1 % kPf]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < kPf; i++) rw[i] = pf[i];
+          }
+          rhi += 16;
           CompIn in = make_in(span, d, nchunks, bc0, btot, bn, breg != 0);
-          pf0 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j));
-          pf1 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 1));
-          pf2 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 2));
-          pf3 = fetch_dword(in, 4 * (uint64_t)(rhi + 4 * j + 3));
+#pragma unroll
+          for (int i = 0; i < kPf; i++) pf[i] = fetch_dword(in, 4 * (uint64_t)(rhi + kPf * j + i));
         }
-        if (32 * rpos - nbits > 8 * bn + 1024) {  // runaway past the end of the input
+        if (32 * (rpos - 2) + o > 8 * bn + 1024) {  // runaway past the end of the input
           res = kCodecEof;
           mode = kVFinish;
         }
       }
       uint32_t *tk = d.tok + (uint64_t)bc0 * kTokPerChunk + nst;
-      for (uint32_t k = j; k < nv; k += 8) tk[k] = M.tbuf[k];
+      for (uint32_t k = j; k < nv; k += kVG) tk[k] = M.tbuf[k];
       nst += nv;
       nv = 0;
       wave_lds_sync();

@@ -454,7 +454,8 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
   hipEventElapsedTime(&ms, c->ev[kEvStart], c->ev[kEvEnd]);
   if (collect(c, report_span, file_off, codec, mode, nbytes, out, to_host)) return -1;
   out->kernel_ms = ms;
-  if (c->h_ctl->out_overflow && out->stop != RIO_STOP_ERROR) {
+  if (c->h_ctl->out_overflow) {  // still short after the retries: report that, not what it garbled
+    memset(&out->err, 0, sizeof(out->err));
     rio_set_error(&out->err, RIO_ERR_CAPACITY, file_off, "output capacity exceeded");
     out->stop = RIO_STOP_ERROR;
   }

@@ -111,10 +111,10 @@ def test_many_blocks_per_stream(gpu_lib):
     assert err == "" and items == recs
 
 
-@pytest.mark.parametrize("cap", [64, 300, 2000])
+@pytest.mark.parametrize("cap", [128, 300, 2000])
 def test_token_region_yield_and_resume(gpu_lib, cap):
     # a small token region per round: blocks yield and resume across rounds;
-    # at 64 tokens a block needs more than the 6 launched rounds and the host
+    # at 128 tokens a block needs more than the 6 launched rounds and the host
     # retries with more
     recs = mixed_records(cap, 300)
     data = write(recs, 6, "go", max_items=50)
@@ -136,6 +136,20 @@ def test_c3_like_fastq(ctx):
     for first in range(0, nrec, 1024):
         want.extend(c3_data.records(first, min(1024, nrec - first)))
     assert err == "" and items == want
+
+
+def test_rounds_exhausted_is_a_capacity_error(gpu_lib):
+    # more rounds than the host will ever launch (64): a capacity error, never
+    # a decode error or garbled records
+    rng = random.Random(3)
+    recs = [bytes(rng.getrandbits(8) for _ in range(30000))]  # stored: ~10k tokens
+    data = write(recs, 6, "go")
+    c = make_ctx({"RIO_FL_TOKCAP": 64})
+    try:
+        items, err = scan_all(data, c)
+    finally:
+        c.close()
+    assert items == [] and "capacity" in err
 
 
 def test_corrupt_streams_match_oracle(ctx, oracle):
