@@ -1316,17 +1316,17 @@ __device__ __forceinline__ uint32_t umod_small(uint32_t k, uint32_t d) {
   return (uint32_t)r;
 }
 
-// Copy-pass window: a ring of 48 KiB = the 32 KiB DEFLATE history + one batch
-// (at most 16 KiB; a longer batch is split in two halves), flushed after
-// every batch: a write at x replaces x - 48 KiB, which is flushed and older
-// than any source of the batch.
-constexpr uint32_t kLzWin = 49152;
+// Copy-pass window: a ring of 36 KiB = the 32 KiB DEFLATE history + one batch
+// of at most 4 KiB (a wider batch -- long matches -- goes in 8 parts of 8
+// tokens, <= 2,064 B each), flushed after every batch: a write at x replaces
+// x - 36 KiB, which is flushed and older than any source of the batch.
+constexpr uint32_t kLzWin = 36864;
 constexpr uint32_t kLzSpan = kLzWin - 32768;
-constexpr int kLzSuper = 16;  // batches of 64 tokens staged in LDS per super-batch
+constexpr int kLzSuper = 4;  // batches of 64 tokens staged in LDS per super-batch
 
-// x mod 49152 (= 3 * 2^14) for any u32 x
+// x mod 36864 (= 9 * 2^12) for any u32 x
 __device__ __forceinline__ uint32_t lz_slot(uint32_t x) {
-  const uint32_t q = ((x >> 14) * 43691u) >> 17;  // (x >> 14) / 3
+  const uint32_t q = __umulhi(x >> 12, 0x1C71C71Du);  // (x >> 12) / 9, exact below 2^20
   return x - q * kLzWin;
 }
 __device__ __forceinline__ uint32_t lz_next(uint32_t slot, uint32_t k) {  // slot + k (k < kLzWin), wrapped
@@ -1366,7 +1366,7 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
       wave_lds_sync();
     }
     uint64_t flushed = olen;
-    // Tokens stream through LDS one super-batch (1,024 tokens) at a time; the
+    // Tokens stream through LDS one super-batch (256 tokens) at a time; the
     // next super-batch is loaded into registers while this one is decoded.
     uint32_t pre[kLzSuper];
 #pragma unroll
@@ -1383,11 +1383,11 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
       for (uint32_t bi = 0; bi < nbat; bi++) {
         const uint32_t t0 = (s0 + 64 * bi + (uint32_t)l < ntok) ? tbuf[64 * bi + l] : 0u;
         const uint32_t len0 = (t0 >> 31) ? ((t0 >> 16) & 0xffu) + 3 : (t0 >> 24) & 3u;
-        // a batch spanning more than kLzSpan bytes (long matches) goes in two halves
+        // a batch spanning more than kLzSpan bytes (long matches) goes in 8 parts
         const uint32_t all = (uint32_t)__builtin_amdgcn_readlane(wave_incl_sum_dpp(len0), 63);
-        const int halves = all > kLzSpan ? 2 : 1;
-        for (int h = 0; h < halves; h++) {
-          const bool mine = halves == 1 || ((l < 32) == (h == 0));
+        const int parts = all > kLzSpan ? 8 : 1;
+        for (int h = 0; h < parts; h++) {
+          const bool mine = parts == 1 || (l >> 3) == h;
           const uint32_t t = mine ? t0 : 0u;
           const bool m = (t >> 31) != 0;
           const uint32_t len = mine ? len0 : 0u;
@@ -1526,7 +1526,7 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
   if (d.fl_grid && g1 > d.fl_grid) g1 = d.fl_grid;
   if (g1 < 1) g1 = 1;
   uint64_t g2 = max_blocks;
-  const uint64_t r2 = (uint64_t)ncu * 3;  // 48 KiB windows: 3 per CU
+  const uint64_t r2 = (uint64_t)ncu * 4;  // 36 KiB windows: 4 per CU
   if (g2 > r2) g2 = r2;
   if (g2 < 1) g2 = 1;
   for (int r = 0; r < rounds; r++) {
