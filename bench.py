@@ -110,6 +110,30 @@ def cpu_baseline(data: bytes, budget_s: float = 10.0):
                       f"(oracle/scanner.c) single thread on {cpu}; the Go reference cannot be built here"}
 
 
+def c3_flate(args, local, world, dist):
+    """BASELINE.json configs[2] beside the headline: ~10 GiB of FASTQ-like records in
+    flate blocks (1,024 records per block) per GPU, device-resident, one pass =
+    chunk CRC + two-pass DEFLATE decode + packed unpack (tools/bench_flate.py).
+    Whole-job GiB/s of compressed input over the max time across ranks."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_flate
+    r = bench_flate.run_c3(replicas=args.flate_replicas, steps=max(2, min(args.steps, 5)), warmup=1,
+                           device=local, check=True)
+    if dist is not None:
+        t = torch.tensor([r["ms_per_step"]], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+        r["value"] = round(r["config"]["span_bytes"] * world / (ms * 1e-3) / 2 ** 30, 2)
+        r["ms_per_step"] = round(ms, 3)
+    r["n_gpus"] = world
+    r["target_GiBs"] = 40.0  # BASELINE.json north_star: >= 40 GiB/s compressed-in on flate at 1 GPU
+    # HBM roofline of the decode pipeline: compressed bytes read + decoded bytes written
+    moved = (r["config"]["span_bytes"] + r["config"]["records_bytes"]) * world
+    r["hbm_frac"] = round(moved / (r["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,6 +141,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--replicas", type=int, default=REPLICAS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-flate", action="store_true", help="skip the C3 flate measurement (configs[2])")
+    ap.add_argument("--flate-replicas", type=int, default=80)
     args = ap.parse_args()
 
     import torch
@@ -213,11 +239,15 @@ def main():
                       "parallelism": f"{world} GPU(s), independent replica sets",
                       "bytes_in_per_gpu": span_len},
            "roofline": roof}
+    ctx.close()
+    del dev
+    torch.cuda.empty_cache()
+    if not args.no_flate:
+        out["c3_flate"] = c3_flate(args, local, world, dist)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 

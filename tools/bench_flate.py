@@ -22,46 +22,41 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--base-mib", type=int, default=128)
-    ap.add_argument("--replicas", type=int, default=80)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--per-block", type=int, default=1024)
-    args = ap.parse_args()
-
+def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=0, check=True):
+    """The C3 workload on cuda:`device`; returns the measurement dict (no print)."""
     import torch
     import c3_data
     from base_amd.recordio import gpu
 
     t0 = time.perf_counter()
-    data, nrec, rec_bytes = c3_data.make_file(args.base_mib << 20, args.per_block, workers=16)
+    data, nrec, rec_bytes = c3_data.make_file(base_mib << 20, per_block, workers=16)
     gen_s = time.perf_counter() - t0
     CH = 32768
     body = data[CH:]
-    total = CH + args.replicas * len(body)
-    dev = torch.empty(total, dtype=torch.uint8, device="cuda:0")
+    total = CH + replicas * len(body)
+    dev = torch.empty(total, dtype=torch.uint8, device=f"cuda:{device}")
     dev[:len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
-    for r in range(1, args.replicas):
+    for r in range(1, replicas):
         dev[CH + r * len(body):CH + (r + 1) * len(body)].copy_(dev[CH:len(data)])
     torch.cuda.synchronize()
 
-    # parity on the base file (device path, views into the decoded blocks)
-    ctx1 = gpu.Context(0, max_span_bytes=len(body) + CH)
-    b = ctx1.scan_device(dev.data_ptr() + CH, len(body), file_off=CH, is_file_end=True, codec=gpu.RIO_CODEC_FLATE)
-    assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
-    items = gpu.device_batch_items(b, body)
-    h_got = hashlib.sha256(b"".join(items)).hexdigest()
-    want = []
-    for first in range(0, nrec, args.per_block):
-        want.extend(c3_data.records(first, min(args.per_block, nrec - first)))
-    h_want = hashlib.sha256(b"".join(want)).hexdigest()
-    parity = (len(items) == nrec and h_got == h_want and [len(x) for x in items] == [len(x) for x in want])
-    ctx1.close()
+    parity = None
+    if check:  # the base file's items (device path, views into the decoded blocks)
+        ctx1 = gpu.Context(device, max_span_bytes=len(body) + CH)
+        b = ctx1.scan_device(dev.data_ptr() + CH, len(body), file_off=CH, is_file_end=True,
+                             codec=gpu.RIO_CODEC_FLATE)
+        assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
+        items = gpu.device_batch_items(b, body)
+        h_got = hashlib.sha256(b"".join(items)).hexdigest()
+        want = []
+        for first in range(0, nrec, per_block):
+            want.extend(c3_data.records(first, min(per_block, nrec - first)))
+        h_want = hashlib.sha256(b"".join(want)).hexdigest()
+        parity = (len(items) == nrec and h_got == h_want and [len(x) for x in items] == [len(x) for x in want])
+        ctx1.close()
 
     span_len = total - CH
-    ctx = gpu.Context(0, max_span_bytes=total, max_items=nrec * args.replicas + 1024)
+    ctx = gpu.Context(device, max_span_bytes=total, max_items=nrec * replicas + 1024)
     ptr = dev.data_ptr() + CH
 
     def step():
@@ -70,21 +65,24 @@ def main():
 
     bb = step()
     assert bb.stop == gpu.RIO_STOP_EOF and bb.err.code == 0, bb.err.msg
-    assert bb.n_items == nrec * args.replicas
-    for _ in range(args.warmup):
+    assert bb.n_items == nrec * replicas
+    for _ in range(warmup):
         step()
     stages = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
         stages.append(ctx.stage_times())
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.steps
+    dt = (time.perf_counter() - t0) / steps
     import numpy as np
     st = np.mean(np.array(stages), axis=0)
-    out_bytes = rec_bytes * args.replicas
-    print(json.dumps({
+    out_bytes = rec_bytes * replicas
+    ctx.close()
+    del dev
+    torch.cuda.empty_cache()
+    return {
         "metric": "recordio scan GiB/s device-resident (compressed in), flate",
         "value": round(span_len / dt / 2 ** 30, 2), "unit": "GiB/s",
         "out_GiBs": round(out_bytes / dt / 2 ** 30, 2),
@@ -92,11 +90,22 @@ def main():
         "stage_ms": {"parse": round(st[0], 3), "decode": round(st[1], 3), "crc": round(st[2], 3),
                      "meta": round(st[3], 3), "total": round(st[4], 3)},
         "decode_in_GiBs": round(span_len / (st[1] * 1e-3) / 2 ** 30, 2) if st[1] > 0 else None,
-        "config": {"workload": "C3-like flate FASTQ, %d records/block" % args.per_block,
+        "config": {"workload": "C3-like flate FASTQ, %d records/block" % per_block,
                    "base_file_bytes": len(data), "base_records": nrec, "base_record_bytes": rec_bytes,
-                   "replicas": args.replicas, "span_bytes": span_len, "gen_s": round(gen_s, 1)},
-        "parity": parity}), flush=True)
-    ctx.close()
+                   "replicas": replicas, "span_bytes": span_len, "records_bytes": out_bytes,
+                   "gen_s": round(gen_s, 1)},
+        "parity": parity}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--base-mib", type=int, default=128)
+    ap.add_argument("--replicas", type=int, default=80)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--per-block", type=int, default=1024)
+    args = ap.parse_args()
+    print(json.dumps(run_c3(args.base_mib, args.replicas, args.steps, args.warmup, args.per_block)), flush=True)
 
 
 if __name__ == "__main__":
