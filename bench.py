@@ -118,8 +118,9 @@ def c3_flate(args, local, world, dist):
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_flate
+    cpu_s = 8.0 if (world == 1 and not args.no_cpu_baseline) else 0.0
     r = bench_flate.run_c3(replicas=args.flate_replicas, steps=max(2, min(args.steps, 5)), warmup=1,
-                           device=local, check=True)
+                           device=local, check=True, cpu_s=cpu_s)
     if dist is not None:
         t = torch.tensor([r["ms_per_step"]], device=f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

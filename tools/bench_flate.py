@@ -22,7 +22,27 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=0, check=True):
+def cpu_baseline_c3(data: bytes, nrec: int, budget_s: float = 8.0):
+    """The C oracle (oracle/scanner.c + oracle/inflate.c: recordio.NewScanner's loop
+    with Go-semantics inflate) on one host core over the C3 base file."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    O.build()
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        n, _ = O.scan_count(data)
+        assert n == nrec, (n, nrec)
+        passes += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(passes * len(data) / dt / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": "%d x C3 base file (%d B compressed, %d records), C oracle single thread; "
+                      "the Go reference cannot be built here" % (passes, len(data), nrec)}
+
+
+def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0):
     """The C3 workload on cuda:`device`; returns the measurement dict (no print)."""
     import torch
     import c3_data
@@ -82,6 +102,7 @@ def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=
     ctx.close()
     del dev
     torch.cuda.empty_cache()
+    cpu = cpu_baseline_c3(data, nrec, cpu_s) if cpu_s > 0 else None
     return {
         "metric": "recordio scan GiB/s device-resident (compressed in), flate",
         "value": round(span_len / dt / 2 ** 30, 2), "unit": "GiB/s",
@@ -94,7 +115,7 @@ def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=
                    "base_file_bytes": len(data), "base_records": nrec, "base_record_bytes": rec_bytes,
                    "replicas": replicas, "span_bytes": span_len, "records_bytes": out_bytes,
                    "gen_s": round(gen_s, 1)},
-        "parity": parity}
+        "parity": parity, "cpu_baseline": cpu}
 
 
 def main():
