@@ -1,6 +1,7 @@
 // Compressed-codec stages (flate / zstd) of the span pipeline: sizing of the
-// per-block decode regions and decoder dispatch (codec_flate.hip). Decoded
-// blocks stay where they were decoded; items are views into them.
+// per-block decode regions and decoder dispatch (codec_flate.hip,
+// codec_zstd.hip). Decoded blocks stay where they were decoded; items are
+// views into them.
 #include <hip/hip_runtime.h>
 #include <inttypes.h>
 #include <stdio.h>
@@ -38,6 +39,8 @@ void launch_block_scan(const unsigned long long *in, unsigned long long *out, un
                        const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
                     uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st);
+void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
+                 uint64_t dec_cap, uint64_t grid, hipStream_t st);
 
 static unsigned grid_blocks(uint64_t n) {
   uint64_t g = (n + 255) / 256;
@@ -59,8 +62,24 @@ void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned l
     launch_inflate(span, d, nblocks_dev, max_blocks, nchunks, dec_cap, rounds, ncu, st);
     return;
   }
+  if (codec == RIO_CODEC_ZSTD && d.zlit) {
+    launch_zstd(span, d, nblocks_dev, max_blocks, dec_cap, d.zlit_waves, st);
+    return;
+  }
   hipLaunchKernelGGL(k_codec_unsupported, dim3(grid_blocks(max_blocks)), dim3(256), 0, st, d, nblocks_dev);
 }
+
+// libzstd's error names (ZSTD_getErrorName) for codec_zstd.hip's ZErr codes
+static const char *const kZstdErrNames[] = {
+    "",
+    "Src size is incorrect",
+    "Unknown frame descriptor",
+    "Corrupted block detected",
+    "Restored data doesn't match checksum",
+    "Dictionary mismatch",
+    "Frame requires too much memory for decoding",
+    "Unsupported frame parameter",
+};
 
 void codec_error_text(uint64_t code, uint64_t off, uint64_t file_off, rio_error *e) {
   switch (code) {
@@ -74,7 +93,10 @@ void codec_error_text(uint64_t code, uint64_t off, uint64_t file_off, rio_error 
     rio_set_error(e, RIO_ERR_ZSTD_EMPTY, file_off, "Bytes slice is empty");
     break;
   case kCodecZstd:
-    rio_set_error(e, RIO_ERR_ZSTD, file_off, "zstd: error %" PRIu64, off);
+    if (off >= 1 && off < sizeof(kZstdErrNames) / sizeof(kZstdErrNames[0]))
+      rio_set_error(e, RIO_ERR_ZSTD, file_off, "%s", kZstdErrNames[off]);
+    else
+      rio_set_error(e, RIO_ERR_ZSTD, file_off, "Corrupted block detected");
     break;
   default:
     rio_set_error(e, RIO_ERR_ARG, file_off, "codec not supported by this build");

@@ -42,15 +42,6 @@ struct InflLds {
   uint16_t offs[kMaxBits + 2];
 };
 
-// wave-uniform value (LDS loads are per lane; this makes them scalar)
-// (the builtin returns int: widen through uint32_t, never sign-extend)
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint64_t uni64(uint64_t v) {
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // ---------------------------------------------------------------- tables
 __device__ __forceinline__ uint32_t rev_bits(uint32_t code, int len) { return __brev(code) >> (32 - len); }
 

@@ -11,6 +11,15 @@ namespace rio {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// wave-uniform value (LDS loads are per lane; this makes them scalar)
+// (the builtin returns int: widen through uint32_t, never sign-extend)
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // lane j's value, as a wave-uniform (scalar) value
 __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int j) {
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, j);

@@ -158,6 +158,8 @@ struct DevBufs {
   uint64_t tok_limit;            // tokens per block and round (0: the whole region; RIO_FL_TOKCAP, tests)
   uint64_t fl_grid;              // Huffman-pass workgroups (0: all resident; RIO_FL_GRID, tests)
   unsigned long long *fl_more;   // per round: blocks whose token region filled (kFlRounds)
+  uint8_t *zlit;                 // zstd: one literal buffer per decoder wave (codec_zstd.hip)
+  uint64_t zlit_waves;           // decoder waves zlit holds buffers for
   Ctl *ctl;
   // CRC tables (constant)
   uint32_t *crc_fold;   // 4 x 256 fold tables, each replicated x32 (bank-private copies)
@@ -165,6 +167,10 @@ struct DevBufs {
   uint32_t *crc_fix_a;  // per payload size: ~0 shifted over 16+size bytes
   uint32_t *crc_fix_b;  // per payload size: x^(-8*pad)
 };
+
+// zstd decoder sizing (codec_zstd.hip)
+uint64_t zstd_grid(int ncu);             // decoder waves launched
+uint64_t zstd_lit_bytes(uint64_t grid);  // literal buffers for that many waves
 
 // Kernel argument blocks (kernels.hip, codec.hip; filled by pipeline.cpp).
 struct ParseArgs {

@@ -13,9 +13,8 @@ from conftest import golden_bytes, oracle_has_zstd
 
 pytestmark = pytest.mark.gpu
 
-# codecs with a GPU decoder in this build (zstd: oracle restated, GPU decoder
-# next -- DESIGN.md §7); RIO_TEST_CODECS overrides
-DEFAULT_CODECS = "none,flate"
+# codecs with a GPU decoder in this build; RIO_TEST_CODECS overrides
+DEFAULT_CODECS = "none,flate,zstd"
 
 
 def sha(items):
@@ -264,8 +263,8 @@ def test_device_path_views(oracle):
 
 
 def test_unsupported_codec_fails_loudly(gpu_ctx):
-    """Until the zstd GPU decoder lands, a zstd block is an error -- never a CPU
-    fallback and never silent data."""
+    """With a codec excluded from the build under test (RIO_TEST_CODECS), a zstd
+    block is an error -- never a CPU fallback and never silent data."""
     if "zstd" in os.environ.get("RIO_TEST_CODECS", DEFAULT_CODECS).split(","):
         pytest.skip("zstd decoder under test")
     from base_amd.recordio.codecs import have_zstd

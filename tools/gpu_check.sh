@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-export RIO_TEST_CODECS="${RIO_TEST_CODECS:-none,flate}"
+export RIO_TEST_CODECS="${RIO_TEST_CODECS:-none,flate,zstd}"
 
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 tmo=$2
