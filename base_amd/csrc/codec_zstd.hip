@@ -760,35 +760,58 @@ __device__ int64_t z_decode_frame(ZFrame &z, ZLds &L, int64_t in, int64_t n) {
   return pos;
 }
 
-// the frames' declared content sizes (the retry's region when a block
-// outgrew its first bound); -1 if a frame declares none
-__device__ int64_t z_declared_size(const uint8_t *src, int64_t n) {
+// An upper bound of the block's decoded size from its frame and block headers
+// alone (the retry's region when a block outgrew its first bound): raw and RLE
+// blocks regenerate exactly their size, a compressed block at most
+// min(window, 128 KiB). -1 if the headers do not parse (then the block's
+// decode error is what the retry reports).
+__device__ int64_t z_size_bound(const uint8_t *src, int64_t n) {
   int64_t pos = 0, total = 0;
-  int frames = 0;
-  while (pos < n && frames < 64) {
-    if (n - pos < 8) return -1;
+  while (pos < n) {
+    if (n - pos < 4) return -1;
     const uint32_t magic = zrd32(src, pos);
     if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
+      if (n - pos < 8) return -1;
       pos += 8 + (int64_t)zrd32(src, pos + 4);
       continue;
     }
-    if (magic != kZMagic) return -1;
+    if (magic != kZMagic || n - pos < 5) return -1;
     const int fhd = src[pos + 4];
-    const int fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, did_flag = fhd & 3;
+    const int fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, checksum = (fhd >> 2) & 1, did_flag = fhd & 3;
     const int did_len = did_flag == 0 ? 0 : did_flag == 1 ? 1 : did_flag == 2 ? 2 : 4;
-    const int64_t p = pos + 5 + (single ? 0 : 1) + did_len;
     const int fcs_len = fcs_flag == 0 ? (single ? 1 : 0) : (fcs_flag == 1 ? 2 : (fcs_flag == 2 ? 4 : 8));
-    if (fcs_len == 0 || p + fcs_len > n) return -1;
-    int64_t fcs;
-    if (fcs_len == 1) fcs = src[p];
-    else if (fcs_len == 2) fcs = zrd16(src, p) + 256;
-    else if (fcs_len == 4) fcs = zrd32(src, p);
-    else fcs = (int64_t)(zrd32(src, p) | ((uint64_t)zrd32(src, p + 4) << 32));
-    total += fcs;
-    frames++;
-    // the next frame's offset needs this frame decoded: one declared size
-    // is enough for a single-frame block; more frames grow on the next retry
-    return total;
+    int64_t p = pos + 5;
+    uint64_t window = 0;
+    if (!single) {
+      if (p >= n) return -1;
+      const int wd = src[p++];
+      const int wlog = 10 + (wd >> 3);
+      if (wlog > 31) return -1;
+      window = (1ull << wlog) + ((1ull << wlog) / 8) * (uint64_t)(wd & 7);
+    }
+    p += did_len;
+    if (p + fcs_len > n) return -1;
+    if (single) {
+      if (fcs_len == 1) window = src[p];
+      else if (fcs_len == 2) window = zrd16(src, p) + 256;
+      else if (fcs_len == 4) window = zrd32(src, p);
+      else window = zrd32(src, p) | ((uint64_t)zrd32(src, p + 4) << 32);
+    }
+    p += fcs_len;
+    const int64_t block_max = window < (uint64_t)kZBlockMax ? (int64_t)window : kZBlockMax;
+    for (;;) {
+      if (p + 3 > n) return -1;
+      const uint32_t bh = zrd24(src, p);
+      p += 3;
+      const int type = (bh >> 1) & 3;
+      const int64_t size = bh >> 3;
+      if (type == 3) return -1;
+      total += type == 2 ? block_max : size;
+      p += type == 1 ? 1 : size;
+      if (p > n) return -1;
+      if (bh & 1) break;
+    }
+    pos = p + (checksum ? 4 : 0);
   }
   return total;
 }
@@ -881,7 +904,7 @@ __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, D
       }
       olen = z.olen;
       if (zerr == kZFull) {  // size the retry from the declared content size
-        int64_t need = z_declared_size(z.src, (int64_t)n);
+        int64_t need = z_size_bound(z.src, (int64_t)n);
         if (need <= (int64_t)cap) need = 4 * (int64_t)cap + 4096;
         if (l == 0) {
           d.blk_need[b] = (unsigned long long)need;

@@ -68,6 +68,41 @@ def zstd_compress(data: bytes, level: int = 5) -> bytes:
     return dst.raw[:n]
 
 
+def zstd_compress_ex(data: bytes, level: int = 5, checksum: bool = False, content_size: bool = True,
+                     window_log: int = 0) -> bytes:
+    """One frame with explicit frame parameters (ZSTD_compress2 over a CCtx):
+    the content checksum (XXH64), the content-size field and the window log.
+    Test helper: the recordio writer itself uses zstd_compress."""
+    lib = _libzstd()
+    if not hasattr(lib, "_cctx_ready"):
+        lib.ZSTD_createCCtx.restype = ctypes.c_void_p
+        lib.ZSTD_freeCCtx.argtypes = [ctypes.c_void_p]
+        lib.ZSTD_CCtx_setParameter.restype = ctypes.c_size_t
+        lib.ZSTD_CCtx_setParameter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        lib.ZSTD_compress2.restype = ctypes.c_size_t
+        lib.ZSTD_compress2.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                       ctypes.c_size_t]
+        lib._cctx_ready = True
+    cctx = lib.ZSTD_createCCtx()
+    try:
+        # zstd.h: ZSTD_c_compressionLevel 100, windowLog 101, contentSizeFlag 200, checksumFlag 201
+        params = [(100, level if level >= 0 else 5), (200, int(content_size)), (201, int(checksum))]
+        if window_log:
+            params.append((101, window_log))
+        for k, v in params:
+            if lib.ZSTD_isError(lib.ZSTD_CCtx_setParameter(cctx, k, v)):
+                raise RuntimeError("ZSTD_CCtx_setParameter(%d, %d) failed" % (k, v))
+        src = bytes(data)
+        cap = lib.ZSTD_compressBound(len(src))
+        dst = ctypes.create_string_buffer(cap)
+        n = lib.ZSTD_compress2(cctx, dst, cap, src, len(src))
+        if lib.ZSTD_isError(n):
+            raise RuntimeError("ZSTD_compress2 failed")
+        return dst.raw[:n]
+    finally:
+        lib.ZSTD_freeCCtx(cctx)
+
+
 def zstd_decompress_ref(data: bytes, cap: int) -> bytes:
     """libzstd decode (test/fixture helper only)."""
     lib = _libzstd()
@@ -114,4 +149,4 @@ def have_zstd() -> bool:
 
 
 __all__ = ["flate_compress", "zstd_compress", "make_compressor", "parse_transformer",
-           "have_zstd", "zstd_version", "zstd_decompress_ref"]
+           "have_zstd", "zstd_version", "zstd_decompress_ref", "zstd_compress_ex"]

@@ -263,14 +263,10 @@ def test_device_path_views(oracle):
 
 
 def test_unsupported_codec_fails_loudly(gpu_ctx):
-    """With a codec excluded from the build under test (RIO_TEST_CODECS), a zstd
-    block is an error -- never a CPU fallback and never silent data."""
-    if "zstd" in os.environ.get("RIO_TEST_CODECS", DEFAULT_CODECS).split(","):
-        pytest.skip("zstd decoder under test")
-    from base_amd.recordio.codecs import have_zstd
-    from base_amd.recordio.writer import write_file, WriterOpts
-    if not have_zstd():
-        pytest.skip("libzstd not present to write the fixture")
-    data = write_file([b"a" * 100] * 10, WriterOpts(Transformers=["zstd"]))
+    """A transformer this build has no decoder for is an error -- never a CPU
+    fallback and never silent data (registry.go:54-64: "Transformer %s not found")."""
+    from base_amd.recordio.writer import write_file
+    # the body is written untransformed; the header names an unknown codec
+    data = write_file([b"a" * 100] * 10, header=[("transformer", "snappy")])
     _, items, _, err, e = gpu_scan(data, gpu_ctx, read_trailer=False)
-    assert items == [] and e is not None and "not supported" in err
+    assert items == [] and e is not None and err == "Transformer snappy not found"

@@ -42,15 +42,15 @@ def cpu_baseline_c3(data: bytes, nrec: int, budget_s: float = 8.0):
                       "the Go reference cannot be built here" % (passes, len(data), nrec)}
 
 
-def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0):
-    """The C3 workload on cuda:`device`; returns the measurement dict (no print)."""
+def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, warmup, device=0, check=True):
+    """One compressed workload on cuda:`device`: the base file `data` copied to
+    HBM, its body replicated `replicas` times; one step = the scan pipeline over
+    the whole device-resident span. Parity: the base file's items (device path)
+    against want_fn() by SHA-256 and lengths. Returns the measurement dict."""
+    import numpy as np
     import torch
-    import c3_data
     from base_amd.recordio import gpu
 
-    t0 = time.perf_counter()
-    data, nrec, rec_bytes = c3_data.make_file(base_mib << 20, per_block, workers=16)
-    gen_s = time.perf_counter() - t0
     CH = 32768
     body = data[CH:]
     total = CH + replicas * len(body)
@@ -63,14 +63,11 @@ def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=
     parity = None
     if check:  # the base file's items (device path, views into the decoded blocks)
         ctx1 = gpu.Context(device, max_span_bytes=len(body) + CH)
-        b = ctx1.scan_device(dev.data_ptr() + CH, len(body), file_off=CH, is_file_end=True,
-                             codec=gpu.RIO_CODEC_FLATE)
+        b = ctx1.scan_device(dev.data_ptr() + CH, len(body), file_off=CH, is_file_end=True, codec=codec)
         assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
         items = gpu.device_batch_items(b, body)
+        want = want_fn()
         h_got = hashlib.sha256(b"".join(items)).hexdigest()
-        want = []
-        for first in range(0, nrec, per_block):
-            want.extend(c3_data.records(first, min(per_block, nrec - first)))
         h_want = hashlib.sha256(b"".join(want)).hexdigest()
         parity = (len(items) == nrec and h_got == h_want and [len(x) for x in items] == [len(x) for x in want])
         ctx1.close()
@@ -80,7 +77,7 @@ def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=
     ptr = dev.data_ptr() + CH
 
     def step():
-        ctx.scan_device_async(ptr, span_len, CH, gpu.RIO_CODEC_FLATE)
+        ctx.scan_device_async(ptr, span_len, CH, codec)
         return ctx.sync()
 
     bb = step()
@@ -96,26 +93,44 @@ def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=
         stages.append(ctx.stage_times())
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
-    import numpy as np
     st = np.mean(np.array(stages), axis=0)
     out_bytes = rec_bytes * replicas
     ctx.close()
     del dev
     torch.cuda.empty_cache()
-    cpu = cpu_baseline_c3(data, nrec, cpu_s) if cpu_s > 0 else None
     return {
-        "metric": "recordio scan GiB/s device-resident (compressed in), flate",
         "value": round(span_len / dt / 2 ** 30, 2), "unit": "GiB/s",
         "out_GiBs": round(out_bytes / dt / 2 ** 30, 2),
         "ms_per_step": round(dt * 1e3, 3),
         "stage_ms": {"parse": round(st[0], 3), "decode": round(st[1], 3), "crc": round(st[2], 3),
                      "meta": round(st[3], 3), "total": round(st[4], 3)},
         "decode_in_GiBs": round(span_len / (st[1] * 1e-3) / 2 ** 30, 2) if st[1] > 0 else None,
-        "config": {"workload": "C3-like flate FASTQ, %d records/block" % per_block,
-                   "base_file_bytes": len(data), "base_records": nrec, "base_record_bytes": rec_bytes,
-                   "replicas": replicas, "span_bytes": span_len, "records_bytes": out_bytes,
-                   "gen_s": round(gen_s, 1)},
-        "parity": parity, "cpu_baseline": cpu}
+        "config": {"workload": workload, "base_file_bytes": len(data), "base_records": nrec,
+                   "base_record_bytes": rec_bytes, "replicas": replicas, "span_bytes": span_len,
+                   "records_bytes": out_bytes},
+        "parity": parity}
+
+
+def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0):
+    """The C3 workload on cuda:`device`; returns the measurement dict (no print)."""
+    import c3_data
+    from base_amd.recordio import gpu
+
+    t0 = time.perf_counter()
+    data, nrec, rec_bytes = c3_data.make_file(base_mib << 20, per_block, workers=16)
+    gen_s = time.perf_counter() - t0
+
+    def want():
+        w = []
+        for first in range(0, nrec, per_block):
+            w.extend(c3_data.records(first, min(per_block, nrec - first)))
+        return w
+
+    res = measure(data, nrec, rec_bytes, want, gpu.RIO_CODEC_FLATE,
+                  "C3-like flate FASTQ, %d records/block" % per_block, replicas, steps, warmup, device, check)
+    res["config"]["gen_s"] = round(gen_s, 1)
+    res["cpu_baseline"] = cpu_baseline_c3(data, nrec, cpu_s) if cpu_s > 0 else None
+    return dict({"metric": "recordio scan GiB/s device-resident (compressed in), flate"}, **res)
 
 
 def main():

@@ -1,0 +1,71 @@
+"""Zstd workload (BASELINE.json configs[3]) on one MI355X.
+
+A zstd recordio file (tools/c4_data.py: record sizes log-uniform 64 B-64 KiB,
+>= 1 MiB blocks, level 5) is built on the host, copied to HBM and its body
+replicated to ~10 GiB of records; one step = the scan pipeline over the whole
+device-resident span (chunk CRC + zstd decode + packed unpack). Parity: the base
+file's items against the generator's records. Prints one JSON line.
+
+  python tools/bench_zstd.py [--base-mib 128] [--replicas 80] [--steps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def cpu_baseline_c4(data: bytes, nrec: int, budget_s: float = 8.0):
+    """The C oracle (oracle/scanner.c + oracle/zstd_dec.c: recordio.NewScanner's
+    loop with an RFC 8878 restatement of ZSTD_decompress) on one host core."""
+    from oracle import oracle as O
+    O.build()
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        n, _ = O.scan_count(data)
+        assert n == nrec, (n, nrec)
+        passes += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(passes * len(data) / dt / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": "%d x C4 base file (%d B compressed, %d records), C oracle single thread; "
+                      "the Go reference (DataDog/zstd = libzstd) cannot be built here" % (passes, len(data), nrec)}
+
+
+def run_c4(base_mib=128, replicas=80, steps=5, warmup=1, device=0, check=True, cpu_s=0.0):
+    import bench_flate
+    import c4_data
+    from base_amd.recordio import gpu
+
+    t0 = time.perf_counter()
+    data, nblk, nrec, rec_bytes = c4_data.make_file(base_mib << 20, workers=16)
+    gen_s = time.perf_counter() - t0
+    res = bench_flate.measure(data, nrec, rec_bytes, lambda: c4_data.all_records(nblk), gpu.RIO_CODEC_ZSTD,
+                              "C4-like zstd level 5, records 64 B-64 KiB log-uniform, 1 MiB blocks",
+                              replicas, steps, warmup, device, check)
+    res["config"]["gen_s"] = round(gen_s, 1)
+    res["cpu_baseline"] = cpu_baseline_c4(data, nrec, cpu_s) if cpu_s > 0 else None
+    return dict({"metric": "recordio scan GiB/s device-resident (compressed in), zstd"}, **res)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--base-mib", type=int, default=128)
+    ap.add_argument("--replicas", type=int, default=80)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cpu-s", type=float, default=0.0)
+    args = ap.parse_args()
+    print(json.dumps(run_c4(args.base_mib, args.replicas, args.steps, args.warmup, cpu_s=args.cpu_s)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
