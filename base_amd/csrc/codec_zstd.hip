@@ -58,10 +58,33 @@ __constant__ int16_t kLLDef[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 
                                    2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
 __constant__ int16_t kMLDef[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
                                    1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+// (base | extra bits << 24) per code: one scalar load each in the sequence loop
+// (a byte table would be a vector load whose wait drains every load in flight)
+struct ZCodes {
+  uint32_t ll[36], ml[53];
+};
+__constant__ ZCodes kZCodes = {
+    {0 | 0u << 24,      1 | 0u << 24,      2 | 0u << 24,      3 | 0u << 24,      4 | 0u << 24,      5 | 0u << 24,
+     6 | 0u << 24,      7 | 0u << 24,      8 | 0u << 24,      9 | 0u << 24,      10 | 0u << 24,     11 | 0u << 24,
+     12 | 0u << 24,     13 | 0u << 24,     14 | 0u << 24,     15 | 0u << 24,     16 | 1u << 24,     18 | 1u << 24,
+     20 | 1u << 24,     22 | 1u << 24,     24 | 2u << 24,     28 | 2u << 24,     32 | 3u << 24,     40 | 3u << 24,
+     48 | 4u << 24,     64 | 6u << 24,     128 | 7u << 24,    256 | 8u << 24,    512 | 9u << 24,    1024 | 10u << 24,
+     2048 | 11u << 24,  4096 | 12u << 24,  8192 | 13u << 24,  16384 | 14u << 24, 32768 | 15u << 24, 65536 | 16u << 24},
+    {3 | 0u << 24,     4 | 0u << 24,     5 | 0u << 24,     6 | 0u << 24,     7 | 0u << 24,     8 | 0u << 24,
+     9 | 0u << 24,     10 | 0u << 24,    11 | 0u << 24,    12 | 0u << 24,    13 | 0u << 24,    14 | 0u << 24,
+     15 | 0u << 24,    16 | 0u << 24,    17 | 0u << 24,    18 | 0u << 24,    19 | 0u << 24,    20 | 0u << 24,
+     21 | 0u << 24,    22 | 0u << 24,    23 | 0u << 24,    24 | 0u << 24,    25 | 0u << 24,    26 | 0u << 24,
+     27 | 0u << 24,    28 | 0u << 24,    29 | 0u << 24,    30 | 0u << 24,    31 | 0u << 24,    32 | 0u << 24,
+     33 | 0u << 24,    34 | 0u << 24,    35 | 1u << 24,    37 | 1u << 24,    39 | 1u << 24,    41 | 1u << 24,
+     43 | 2u << 24,    47 | 2u << 24,    51 | 3u << 24,    59 | 3u << 24,    67 | 4u << 24,    83 | 4u << 24,
+     99 | 5u << 24,    131 | 7u << 24,   259 | 8u << 24,   515 | 9u << 24,   1027 | 10u << 24, 2051 | 11u << 24,
+     4099 | 12u << 24, 8195 | 13u << 24, 16387 | 14u << 24, 32771 | 15u << 24, 65539 | 16u << 24}};
+
 // 29 predefined offset codes; 29..31 (the table's max_sym) have count 0
 __constant__ int16_t kOFDef[32] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
                                    1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, 0, 0, 0};
 
+constexpr int kZDesc = 512;  // staged description bytes (an NCount needs < 100, a Huffman tree < 129)
 struct ZLds {
   uint32_t ll[1 << 9], ml[1 << 9], of[1 << 8];  // FSE cells: sym | nbits << 8 | base << 16
   uint32_t wt[1 << 6];                           // FSE table of Huffman weights
@@ -70,6 +93,12 @@ struct ZLds {
   uint16_t next[64];
   uint8_t w[256];
   int32_t res[12];  // lane 0's results, broadcast
+  uint32_t sring[128];      // the sequence bitstream, two 256 B blocks (ZSeqBr)
+  uint64_t ll2[1 << 9], ml2[1 << 9];  // ll / ml cells | (code base | extra bits << 24) << 32 (fast path)
+  uint8_t hout[4][256];     // Huffman streams' decoded literals, flushed 256 at a time
+  // table descriptions (FSE NCount, Huffman tree) staged from HBM by the whole
+  // wave: lane 0's serial bit walks over them then cost LDS, not HBM, latency
+  uint32_t desc[kZDesc / 4 + 4];
 };
 
 __device__ __forceinline__ void zsync() {
@@ -127,15 +156,14 @@ __device__ __forceinline__ bool bwd_init(ZBwd &r, const uint8_t *src, int64_t st
   return true;
 }
 
-// forward (FSE table descriptions): bits past byte n read as zero
+// forward (FSE table descriptions): bits past byte n read as zero; p is a
+// staged description (ZLds::desc), zero-padded, nb <= 16
 __device__ __forceinline__ uint32_t fwd_peek(const uint8_t *p, int64_t n, uint64_t pos, int nb) {
+  const uint64_t B = pos >> 3;
   uint32_t v = 0;
-  for (int i = 0; i < nb; i++) {
-    const uint64_t b = pos + i;
-    const uint32_t bit = (int64_t)(b >> 3) < n ? (p[b >> 3] >> (b & 7)) & 1u : 0u;
-    v |= bit << i;
-  }
-  return v;
+#pragma unroll
+  for (int i = 0; i < 4; i++) v |= (int64_t)(B + i) < n ? (uint32_t)p[B + i] << (8 * i) : 0u;
+  return (v >> (pos & 7)) & ((1u << nb) - 1u);
 }
 
 // ---------------------------------------------------------------- FSE
@@ -303,18 +331,163 @@ __device__ int z_huf_read(ZLds &L, int *max_bits_out, const uint8_t *src, int64_
   return (int)used;
 }
 
-// one Huffman stream -> out[0, count); true iff it decodes exactly (oracle huf_stream)
-__device__ bool z_huf_stream(const ZLds &L, int max_bits, const uint8_t *src, int64_t start, int64_t n, uint8_t *out,
-                             int64_t count) {
-  ZBwd r;
-  if (!bwd_init(r, src, start, n)) return false;
-  for (int64_t i = 0; i < count; i++) {
-    const uint32_t e = L.huf[r.peek(max_bits)];
-    out[i] = (uint8_t)(e >> 4);
-    r.read((int)(e & 15));
-    if (r.bit < 0) return false;
+// Backward bit reader for the hot loops (Huffman literal streams, the sequence
+// bitstream): remaining bits are [lo, bit) of the dword array w (w = the
+// stream's first byte rounded down to 4; bits below lo read as zero). The
+// window is dwords q (c0) and q+1 (c1); the next 4 dwords down are in flight
+// (pf[0] = dword q-1 ...) so that stepping down does not wait on memory.
+// U: the state is wave-uniform (every lane walks the same stream): a dword is
+// made scalar only when it enters the window, never at its load (that would
+// wait for the load right there).
+template <bool U>
+struct ZBrT {
+  static constexpr int kPf = 4;
+  const uint32_t *w;
+  int32_t bit, lo, q;
+  uint32_t c0, c1, pf[kPf];
+  __device__ __forceinline__ uint32_t ld(int32_t i) const { return i >= 0 ? w[i] : 0u; }
+  __device__ __forceinline__ uint32_t mk(uint32_t v) const { return U ? uni(v) : v; }
+  // false: empty stream or no end marker in its last byte
+  __device__ __forceinline__ bool init(const uint8_t *src, int64_t start, int64_t n) {
+    if (n <= 0) return false;
+    const uint32_t last = src[start + n - 1];
+    if (last == 0) return false;
+    w = reinterpret_cast<const uint32_t *>(src + (start & ~3ll));
+    lo = 8 * (int32_t)(start & 3);
+    bit = lo + 8 * (int32_t)n - (8 - highbit(last));
+    q = INT32_MIN;
+    return true;
   }
-  return r.bit == 0;
+  __device__ __forceinline__ void seek(int32_t b) {
+    const int32_t qq = b >> 5;
+    if (qq != q) {
+      if (qq == q - 1) {
+        c1 = c0;
+        c0 = mk(pf[0]);
+#pragma unroll
+        for (int i = 0; i + 1 < kPf; i++) pf[i] = pf[i + 1];
+        pf[kPf - 1] = ld(qq - kPf);
+      } else {
+        c0 = mk(ld(qq));
+        c1 = mk(ld(qq + 1));
+#pragma unroll
+        for (int i = 0; i < kPf; i++) pf[i] = ld(qq - 1 - i);
+      }
+      q = qq;
+    }
+  }
+  // bits [b, b + nb), nb <= 32
+  __device__ __forceinline__ uint32_t get(int32_t b, int nb) {
+    seek(b);
+    uint32_t v = __builtin_amdgcn_alignbit(c1, c0, (uint32_t)b & 31u);
+    v &= nb >= 32 ? ~0u : ((1u << nb) - 1u);
+    if (b < lo) v = (lo - b >= nb) ? 0u : (v & (~0u << (lo - b)));
+    return v;
+  }
+  __device__ __forceinline__ uint32_t read(int nb) {
+    bit -= nb;
+    return get(bit, nb);
+  }
+  __device__ __forceinline__ bool overrun() const { return bit < lo; }
+  __device__ __forceinline__ bool exact() const { return bit == lo; }
+};
+using ZBr = ZBrT<false>;
+
+// The sequence bitstream reader (wave-uniform): the stream moves through LDS
+// in 256 B blocks, two resident (block B in ring slot B & 1). Every lane
+// loads one dword of the block after next when a block is entered, and stores
+// it into LDS when that block is entered in turn, so the only wait on memory
+// is for a load issued ~80 sequences earlier.
+struct ZSeqBr {
+  const uint32_t *w;
+  uint32_t *ring;
+  int32_t bit, lo, q, inst;  // inst: the lowest block in LDS
+  uint32_t c0, c1, pre;      // window dwords q, q+1 (scalar); this lane's dword of block inst-1
+  __device__ __forceinline__ uint32_t ld(int32_t i) const { return i >= 0 ? w[i] : 0u; }
+  __device__ bool init(const uint8_t *src, int64_t start, int64_t n, uint32_t *lds_ring) {
+    if (n <= 0) return false;
+    const uint32_t last = src[start + n - 1];
+    if (last == 0) return false;
+    const int l = lane_id();
+    w = reinterpret_cast<const uint32_t *>(src + (start & ~3ll));
+    ring = lds_ring;
+    lo = 8 * (int32_t)(start & 3);
+    bit = lo + 8 * (int32_t)n - (8 - highbit(last));
+    const int32_t top = ((bit - 1) >> 5) >> 6;  // block of the highest stream dword
+    zsync();
+    ring[(top & 1) * 64 + l] = ld(top * 64 + l);
+    ring[((top - 1) & 1) * 64 + l] = ld((top - 1) * 64 + l);
+    pre = ld((top - 2) * 64 + l);
+    inst = top - 1;
+    q = INT32_MIN;
+    zsync();
+    return true;
+  }
+  __device__ __forceinline__ void seek(int32_t b) {
+    const int32_t qq = b >> 5;
+    if (qq != q) {
+      if ((qq >> 6) < inst) {  // entering block inst-1 (one dword down at a time)
+        zsync();
+        ring[((inst - 1) & 1) * 64 + lane_id()] = pre;
+        zsync();
+        inst--;
+        pre = ld((inst - 1) * 64 + lane_id());
+      }
+      if (qq == q - 1) {
+        c1 = c0;
+      } else {
+        c1 = uni(ring[(qq + 1) & 127]);
+      }
+      c0 = uni(ring[qq & 127]);
+      q = qq;
+    }
+  }
+  __device__ __forceinline__ uint32_t read(int nb) {  // nb <= 32
+    bit -= nb;
+    const int32_t b = bit;
+    seek(b);
+    uint32_t v = __builtin_amdgcn_alignbit(c1, c0, (uint32_t)b & 31u);
+    v &= nb >= 32 ? ~0u : ((1u << nb) - 1u);
+    if (b < lo) v = (lo - b >= nb) ? 0u : (v & (~0u << (lo - b)));
+    return v;
+  }
+  __device__ __forceinline__ bool overrun() const { return bit < lo; }
+  __device__ __forceinline__ bool exact() const { return bit == lo; }
+};
+
+// Huffman literal streams (oracle huf_stream): lane t < ns decodes stream t
+// (bytes [st, st + sn) of src) into out + t * seg, cnt symbols; true iff every
+// stream decodes exactly. A read below a stream's start only ever lowers
+// `bit`, so the final exact-consumption check also catches an overrun
+// mid-stream. The decoded bytes go to LDS and are written out by the whole
+// wave every 256 symbols: the decode loop issues no stores, so its input
+// prefetch is never held up behind them.
+__device__ bool z_huf_streams(ZLds &L, int max_bits, const uint8_t *src, int64_t st, int64_t sn, int ns, uint8_t *out,
+                              int64_t seg, int64_t cnt) {
+  const int l = lane_id();
+  ZBr r;
+  bool ok = true;
+  if (l < ns) ok = r.init(src, st, sn);
+  const int64_t seg_max = (int64_t)uni((uint32_t)(ns == 1 ? cnt : seg));
+  for (int64_t i0 = 0; i0 < seg_max; i0 += 256) {
+    if (l < ns && ok) {
+      const int64_t m = cnt - i0 < 256 ? cnt - i0 : 256;
+      for (int64_t j = 0; j < m; j++) {
+        const uint32_t e = L.huf[r.get(r.bit - max_bits, max_bits)];
+        L.hout[l][j] = (uint8_t)(e >> 4);
+        r.bit -= (int32_t)(e & 15);
+      }
+    }
+    zsync();
+    for (int k = l; k < 256 * ns; k += 64) {
+      const int t = k >> 8, j = k & 255;
+      const int64_t ct = (int64_t)__builtin_amdgcn_readlane((int)cnt, t);
+      if (i0 + j < ct) out[t * seg + i0 + j] = L.hout[t][j];
+    }
+    zsync();
+  }
+  if (l < ns && ok) ok = r.exact();
+  return __ballot(l < ns && !ok) == 0;
 }
 
 // ---------------------------------------------------------------- sequence tables
@@ -352,13 +525,25 @@ __device__ int z_seq_table(uint32_t *t, uint16_t *next, int16_t *norm, int *have
 // ---------------------------------------------------------------- frame state
 struct ZFrame {
   const uint8_t *src;  // flattened compressed block
-  uint8_t *out;        // decode region
-  int64_t cap, olen, frame_start;
-  uint8_t *lit;        // this wave's literal buffer
+  uint8_t *out;        // decode region (serial path)
+  int64_t cap, olen, frame_start;  // olen: output bytes so far (whole recordio block)
+  uint8_t *lit;        // the current zstd block's literals
   int max_bits, have_huf, have_ll, have_of, have_ml;
   int ll_log, of_log, ml_log;
   uint64_t rep0, rep1, rep2;
 };
+
+#ifdef RIO_ZPROF
+#define ZPROF_T(v) const uint64_t v = __builtin_readcyclecounter()
+#define ZPROF_ADD(i, t0) \
+  if (lane_id() == 0) atomicAdd(&zprof_ctl->zprof[i], (unsigned long long)(__builtin_readcyclecounter() - (t0)))
+__device__ Ctl *zprof_ctl;
+#else
+#define ZPROF_T(v)
+#define ZPROF_ADD(i, t0)
+#endif
+
+constexpr uint32_t kZSlow = 101;  // (internal) the fast path's scratch is too small: serial path
 
 // lane 0's value in every lane
 __device__ __forceinline__ int32_t zbcast(ZLds &L, int slot, int32_t v) {
@@ -368,38 +553,20 @@ __device__ __forceinline__ int32_t zbcast(ZLds &L, int slot, int32_t v) {
   return L.res[slot];
 }
 
-// Execute one sequence (the oracle's "execute"): the literal run from the
-// literal buffer, then the match copy from the frame's output, the whole
-// wave cooperating. Returns 0 or a ZErr.
-__device__ __forceinline__ uint32_t z_exec(ZFrame &z, uint64_t ll, uint64_t ml, uint64_t off, int64_t &lit_pos,
-                                           int64_t regen) {
-  const int l = lane_id();
-  if (lit_pos + (int64_t)ll > regen) return kZCorrupt;
-  if (z.olen + (int64_t)(ll + ml) > z.cap) return kZFull;
-  for (uint64_t k = l; k < ll; k += 64) z.out[z.olen + k] = z.lit[lit_pos + k];
-  z.olen += (int64_t)ll;
-  lit_pos += (int64_t)ll;
-  const int64_t produced = z.olen - z.frame_start;
-  if (off == 0 || (int64_t)off > produced) return kZCorrupt;
-  if (ml) {
-    zmem_sync();
-    const int64_t s0 = z.olen - (int64_t)off;
-    for (uint64_t k0 = 0; k0 < ml; k0 += 64) {
-      const uint64_t k = k0 + l;
-      // a match may overlap itself: byte k repeats byte k mod off
-      const uint64_t kk = off >= ml ? k : k % off;
-      uint8_t v = 0;
-      if (k < ml) v = z.out[s0 + kk];
-      if (k < ml) z.out[z.olen + k] = v;
-    }
-    z.olen += (int64_t)ml;
-    zmem_sync();
-  }
-  return 0;
+// src[start, start + min(n, kZDesc)) into L.desc, zero after; every lane
+__device__ __forceinline__ const uint8_t *z_stage(ZLds &L, const uint8_t *src, int64_t start, int64_t n) {
+  uint8_t *dsc = reinterpret_cast<uint8_t *>(L.desc);
+  zsync();
+  for (int k = lane_id(); k < kZDesc + 16; k += 64) dsc[k] = k < n && k < kZDesc ? src[start + k] : 0;
+  zsync();
+  return dsc;
 }
 
-// one compressed block (oracle decode_block): 0 or a ZErr
-__device__ uint32_t z_decode_block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n) {
+// Literals section of a compressed block (oracle decode_block, first part):
+// the block's literals into z.lit, pos advanced past the section. A
+// regenerated size above max_regen returns kZSlow before anything is written.
+__device__ uint32_t z_literals(ZFrame &z, ZLds &L, int64_t bstart, int64_t n, int64_t &pos, int64_t &regen_out,
+                               int64_t max_regen) {
   const int l = lane_id();
   const uint8_t *src = z.src;
   if (n < 1) return kZCorrupt;
@@ -448,13 +615,15 @@ __device__ uint32_t z_decode_block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n
     }
   }
   if (regen > kZBlockMax) return kZCorrupt;
-  int64_t pos = hsz;
+  pos = hsz;
   if (lt == 0) {
     if (pos + regen > n) return kZCorrupt;
+    if (regen > max_regen) return kZSlow;
     for (int64_t k = l; k < regen; k += 64) z.lit[k] = src[bstart + pos + k];
     pos += regen;
   } else if (lt == 1) {
     if (pos + 1 > n) return kZCorrupt;
+    if (regen > max_regen) return kZSlow;
     const uint8_t v = src[bstart + pos];
     for (int64_t k = l; k < regen; k += 64) z.lit[k] = v;
     pos += 1;
@@ -463,7 +632,8 @@ __device__ uint32_t z_decode_block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n
     int64_t hs = bstart + pos, hn = csize;
     if (lt == 2) {
       int mb = 0, k = 0;
-      if (l == 0) k = z_huf_read(L, &mb, src, hs, hn);
+      const uint8_t *dsc = z_stage(L, src, hs, hn);  // the tree description: < 129 bytes
+      if (l == 0) k = z_huf_read(L, &mb, dsc, 0, hn < kZDesc ? hn : kZDesc);
       k = zbcast(L, 0, k);
       mb = zbcast(L, 1, mb);
       if (k < 0) return kZCorrupt;
@@ -476,9 +646,8 @@ __device__ uint32_t z_decode_block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n
     }
     bool ok;
     if (streams == 1) {
-      int r = 0;
-      if (l == 0) r = z_huf_stream(L, z.max_bits, src, hs, hn, z.lit, regen) ? 1 : 0;
-      ok = zbcast(L, 2, r) != 0;
+      if (regen > max_regen) return kZSlow;
+      ok = z_huf_streams(L, z.max_bits, src, hs, hn, 1, z.lit, 0, regen);
     } else {
       if (hn < 6) return kZCorrupt;
       const int64_t s1 = src[hs] | (src[hs + 1] << 8), s2 = src[hs + 2] | (src[hs + 3] << 8),
@@ -487,22 +656,26 @@ __device__ uint32_t z_decode_block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n
       const int64_t s4 = hn - 6 - s1 - s2 - s3;
       const int64_t seg = (regen + 3) / 4;
       if (3 * seg > regen) return kZCorrupt;
+      if (regen > max_regen) return kZSlow;
       // the four streams at once, one lane each (the oracle stops at the first
       // bad stream; any failure is the same error)
-      int r = 1;
-      if (l < 4) {
-        const int64_t st = hs + 6 + (l > 0 ? s1 : 0) + (l > 1 ? s2 : 0) + (l > 2 ? s3 : 0);
-        const int64_t sn = l == 0 ? s1 : l == 1 ? s2 : l == 2 ? s3 : s4;
-        const int64_t cnt = l < 3 ? seg : regen - 3 * seg;
-        r = z_huf_stream(L, z.max_bits, src, st, sn, z.lit + l * seg, cnt) ? 1 : 0;
-      }
-      ok = __ballot(r == 0) == 0;
+      const int64_t st = hs + 6 + (l > 0 ? s1 : 0) + (l > 1 ? s2 : 0) + (l > 2 ? s3 : 0);
+      const int64_t sn = l == 0 ? s1 : l == 1 ? s2 : l == 2 ? s3 : s4;
+      const int64_t cnt = l < 3 ? seg : regen - 3 * seg;
+      ok = z_huf_streams(L, z.max_bits, src, st, sn, 4, z.lit, seg, cnt);
     }
     if (!ok) return kZCorrupt;
     pos += csize;
   }
-  zmem_sync();
-  // sequences section
+  regen_out = regen;
+  return 0;
+}
+
+// Sequences section header and its three FSE tables (lane 0 builds them into
+// L): nseq, pos advanced to the sequence bitstream.
+__device__ uint32_t z_seq_header(ZFrame &z, ZLds &L, int64_t bstart, int64_t n, int64_t &pos, int64_t &nseq_out) {
+  const int l = lane_id();
+  const uint8_t *src = z.src;
   if (pos >= n) return kZCorrupt;
   int64_t nseq;
   const uint32_t c0 = src[bstart + pos];
@@ -521,90 +694,404 @@ __device__ uint32_t z_decode_block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n
     nseq = src[bstart + pos + 1] + ((int64_t)src[bstart + pos + 2] << 8) + 0x7F00;
     pos += 3;
   }
-  int64_t lit_pos = 0;
-  if (nseq > 0) {
-    if (pos >= n) return kZCorrupt;
-    const int modes = src[bstart + pos++];
-    if (modes & 3) return kZCorrupt;
-    // tables: lane 0 builds them, every lane learns the bytes used / a failure
-    int u = 0, uo = 0, um = 0;
-    if (l == 0) {
-      u = z_seq_table(L.ll, L.next, L.norm, &z.have_ll, &z.ll_log, (modes >> 6) & 3, src, bstart + pos, n - pos,
-                      kLLDef, 6, 35, 9);
-      if (u >= 0)
-        uo = z_seq_table(L.of, L.next, L.norm, &z.have_of, &z.of_log, (modes >> 4) & 3, src, bstart + pos + u,
-                         n - pos - u, kOFDef, 5, 31, 8);
-      if (u >= 0 && uo >= 0)
-        um = z_seq_table(L.ml, L.next, L.norm, &z.have_ml, &z.ml_log, (modes >> 2) & 3, src, bstart + pos + u + uo,
-                         n - pos - u - uo, kMLDef, 6, 52, 9);
-    }
-    u = zbcast(L, 0, u);
-    uo = zbcast(L, 1, uo);
-    um = zbcast(L, 2, um);
-    z.have_ll = zbcast(L, 3, z.have_ll);
-    z.have_of = zbcast(L, 4, z.have_of);
-    z.have_ml = zbcast(L, 5, z.have_ml);
-    z.ll_log = zbcast(L, 6, z.ll_log);
-    z.of_log = zbcast(L, 7, z.of_log);
-    z.ml_log = zbcast(L, 8, z.ml_log);
-    if (u < 0 || uo < 0 || um < 0) return kZCorrupt;
-    pos += u + uo + um;
-    // the sequence bitstream, walked by every lane in step
-    ZBwd r;
-    if (!bwd_init(r, src, bstart + pos, n - pos)) return kZCorrupt;
-    uint32_t sll = r.read(z.ll_log), sof = r.read(z.of_log), sml = r.read(z.ml_log);
-    for (int64_t i = 0; i < nseq; i++) {
-      const uint32_t cll = L.ll[sll], cml = L.ml[sml], cof = L.of[sof];
-      const uint32_t llc = cll & 0xff, mlc = cml & 0xff, ofc = cof & 0xff;
-      if (llc > 35 || mlc > 52 || ofc > 31) return kZCorrupt;
-      const uint64_t ofv = (1ull << ofc) + r.read((int)ofc);
-      const uint64_t ml = kMLBase[mlc] + r.read(kMLBits[mlc]);
-      const uint64_t ll = kLLBase[llc] + r.read(kLLBits[llc]);
-      uint64_t off;
-      if (ofv > 3) {
-        off = ofv - 3;
-        z.rep2 = z.rep1;
-        z.rep1 = z.rep0;
-        z.rep0 = off;
-      } else {
-        const uint64_t idx = ofv + (ll == 0 ? 1 : 0);
-        if (idx == 1) {
-          off = z.rep0;
-        } else if (idx == 2) {
-          off = z.rep1;
-          z.rep1 = z.rep0;
-          z.rep0 = off;
-        } else if (idx == 3) {
-          off = z.rep2;
-          z.rep2 = z.rep1;
-          z.rep1 = z.rep0;
-          z.rep0 = off;
-        } else {
-          off = z.rep0 - 1;
-          if (off == 0) return kZCorrupt;
-          z.rep2 = z.rep1;
-          z.rep1 = z.rep0;
-          z.rep0 = off;
-        }
-      }
-      if (i + 1 < nseq) {
-        sll = (cll >> 16) + r.read((cll >> 8) & 0xff);
-        sml = (cml >> 16) + r.read((cml >> 8) & 0xff);
-        sof = (cof >> 16) + r.read((cof >> 8) & 0xff);
-      }
-      if (r.bit < 0) return kZCorrupt;
-      const uint32_t e = z_exec(z, ll, ml, off, lit_pos, regen);
-      if (e) return e;
-    }
-    if (r.bit != 0) return kZCorrupt;
+  nseq_out = nseq;
+  if (nseq == 0) return 0;
+  if (pos >= n) return kZCorrupt;
+  const int modes = src[bstart + pos++];
+  if (modes & 3) return kZCorrupt;
+  // tables: lane 0 builds them from the staged descriptions (three NCounts:
+  // < 300 bytes together), every lane learns the bytes used / a failure
+  int u = 0, uo = 0, um = 0;
+  const int64_t sn = n - pos < kZDesc ? n - pos : kZDesc;
+  const uint8_t *dsc = ((modes >> 2) & 0x3f) ? z_stage(L, src, bstart + pos, n - pos) : nullptr;
+  if (l == 0) {
+    u = z_seq_table(L.ll, L.next, L.norm, &z.have_ll, &z.ll_log, (modes >> 6) & 3, dsc, 0, sn, kLLDef, 6, 35, 9);
+    if (u >= 0)
+      uo = z_seq_table(L.of, L.next, L.norm, &z.have_of, &z.of_log, (modes >> 4) & 3, dsc, u, sn - u, kOFDef, 5, 31,
+                       8);
+    if (u >= 0 && uo >= 0)
+      um = z_seq_table(L.ml, L.next, L.norm, &z.have_ml, &z.ml_log, (modes >> 2) & 3, dsc, u + uo, sn - u - uo,
+                       kMLDef, 6, 52, 9);
   }
-  // remaining literals
-  if (z.olen + (regen - lit_pos) > z.cap) return kZFull;
-  for (int64_t k = l; k < regen - lit_pos; k += 64) z.out[z.olen + k] = z.lit[lit_pos + k];
-  z.olen += regen - lit_pos;
-  zmem_sync();
+  u = zbcast(L, 0, u);
+  uo = zbcast(L, 1, uo);
+  um = zbcast(L, 2, um);
+  z.have_ll = zbcast(L, 3, z.have_ll);
+  z.have_of = zbcast(L, 4, z.have_of);
+  z.have_ml = zbcast(L, 5, z.have_ml);
+  z.ll_log = zbcast(L, 6, z.ll_log);
+  z.of_log = zbcast(L, 7, z.of_log);
+  z.ml_log = zbcast(L, 8, z.ml_log);
+  if (u < 0 || uo < 0 || um < 0) return kZCorrupt;
+  pos += u + uo + um;
   return 0;
 }
+
+// FSE sequence decoder (wave-uniform state)
+struct ZSeqDec {
+  ZSeqBr r;
+  uint32_t sll, sof, sml;
+};
+__device__ __forceinline__ uint32_t z_seq_start(ZSeqDec &q, const ZFrame &z, ZLds &L, int64_t start, int64_t n) {
+  if (!q.r.init(z.src, start, n, L.sring)) return kZCorrupt;
+  q.sll = q.r.read(z.ll_log);
+  q.sof = q.r.read(z.of_log);
+  q.sml = q.r.read(z.ml_log);
+  return 0;
+}
+// the next sequence (oracle decode_block's loop body up to execute): ll, ml and
+// the resolved offset; `more`: another sequence follows (the states advance)
+__device__ __forceinline__ uint32_t z_seq_next(ZSeqDec &q, ZFrame &z, ZLds &L, bool more, uint64_t &ll,
+                                               uint64_t &ml, uint64_t &off) {
+  const uint32_t cll = uni(L.ll[q.sll]), cml = uni(L.ml[q.sml]), cof = uni(L.of[q.sof]);
+  const uint32_t llc = cll & 0xff, mlc = cml & 0xff, ofc = cof & 0xff;
+  if (llc > 35 || mlc > 52 || ofc > 31) return kZCorrupt;
+  const uint64_t ofv = (1ull << ofc) + q.r.read((int)ofc);
+  const uint32_t mlx = kZCodes.ml[mlc], llx = kZCodes.ll[llc];
+  ml = (mlx & 0xFFFFFFu) + q.r.read((int)(mlx >> 24));
+  ll = (llx & 0xFFFFFFu) + q.r.read((int)(llx >> 24));
+  if (ofv > 3) {
+    off = ofv - 3;
+    z.rep2 = z.rep1;
+    z.rep1 = z.rep0;
+    z.rep0 = off;
+  } else {
+    const uint64_t idx = ofv + (ll == 0 ? 1 : 0);
+    if (idx == 1) {
+      off = z.rep0;
+    } else if (idx == 2) {
+      off = z.rep1;
+      z.rep1 = z.rep0;
+      z.rep0 = off;
+    } else if (idx == 3) {
+      off = z.rep2;
+      z.rep2 = z.rep1;
+      z.rep1 = z.rep0;
+      z.rep0 = off;
+    } else {
+      off = z.rep0 - 1;
+      if (off == 0) return kZCorrupt;
+      z.rep2 = z.rep1;
+      z.rep1 = z.rep0;
+      z.rep0 = off;
+    }
+  }
+  if (more) {
+    q.sll = (cll >> 16) + q.r.read((cll >> 8) & 0xff);
+    q.sml = (cml >> 16) + q.r.read((cml >> 8) & 0xff);
+    q.sof = (cof >> 16) + q.r.read((cof >> 8) & 0xff);
+  }
+  if (q.r.overrun()) return kZCorrupt;
+  return 0;
+}
+
+// ---------------------------------------------------------------- serial path
+// Execute one sequence (the oracle's "execute"): the literal run from the
+// literal buffer, then the match copy from the frame's output, the whole
+// wave cooperating. Returns 0 or a ZErr.
+__device__ __forceinline__ uint32_t z_exec(ZFrame &z, uint64_t ll, uint64_t ml, uint64_t off, int64_t &lit_pos,
+                                           int64_t regen) {
+  const int l = lane_id();
+  if (lit_pos + (int64_t)ll > regen) return kZCorrupt;
+  if (z.olen + (int64_t)(ll + ml) > z.cap) return kZFull;
+  for (uint64_t k = l; k < ll; k += 64) z.out[z.olen + k] = z.lit[lit_pos + k];
+  z.olen += (int64_t)ll;
+  lit_pos += (int64_t)ll;
+  const int64_t produced = z.olen - z.frame_start;
+  if (off == 0 || (int64_t)off > produced) return kZCorrupt;
+  if (ml) {
+    zmem_sync();
+    const int64_t s0 = z.olen - (int64_t)off;
+    for (uint64_t k0 = 0; k0 < ml; k0 += 64) {
+      const uint64_t k = k0 + l;
+      // a match may overlap itself: byte k repeats byte k mod off
+      const uint64_t kk = off >= ml ? k : k % off;
+      uint8_t v = 0;
+      if (k < ml) v = z.out[s0 + kk];
+      if (k < ml) z.out[z.olen + k] = v;
+    }
+    z.olen += (int64_t)ml;
+    zmem_sync();
+  }
+  return 0;
+}
+
+// XXH64 (below)
+__device__ uint64_t z_xxh64(const uint8_t *p, uint64_t len);
+
+// The serial decoder's frame content: output written straight to the decode
+// region (k_zstd, the exact path for blocks the fast path declines).
+struct ZSerialSink {
+  __device__ uint32_t raw(ZFrame &z, int64_t at, int64_t size) {
+    if (z.olen + size > z.cap) return kZFull;
+    for (int64_t k = lane_id(); k < size; k += 64) z.out[z.olen + k] = z.src[at + k];
+    z.olen += size;
+    zmem_sync();
+    return 0;
+  }
+  __device__ uint32_t rle(ZFrame &z, uint8_t v, int64_t size) {
+    if (z.olen + size > z.cap) return kZFull;
+    for (int64_t k = lane_id(); k < size; k += 64) z.out[z.olen + k] = v;
+    z.olen += size;
+    zmem_sync();
+    return 0;
+  }
+  // one compressed block (oracle decode_block)
+  __device__ uint32_t block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n) {
+    const int l = lane_id();
+    int64_t pos = 0, regen = 0, nseq = 0;
+    uint32_t e = z_literals(z, L, bstart, n, pos, regen, kZBlockMax);
+    if (e) return e;
+    zmem_sync();
+    e = z_seq_header(z, L, bstart, n, pos, nseq);
+    if (e) return e;
+    int64_t lit_pos = 0;
+    if (nseq > 0) {
+      ZSeqDec q;
+      if ((e = z_seq_start(q, z, L, bstart + pos, n - pos))) return e;
+      for (int64_t i = 0; i < nseq; i++) {
+        uint64_t ll, ml, off;
+        if ((e = z_seq_next(q, z, L, i + 1 < nseq, ll, ml, off))) return e;
+        if ((e = z_exec(z, ll, ml, off, lit_pos, regen))) return e;
+      }
+      if (!q.r.exact()) return kZCorrupt;
+    }
+    // remaining literals
+    if (z.olen + (regen - lit_pos) > z.cap) return kZFull;
+    for (int64_t k = l; k < regen - lit_pos; k += 64) z.out[z.olen + k] = z.lit[lit_pos + k];
+    z.olen += regen - lit_pos;
+    zmem_sync();
+    return 0;
+  }
+  __device__ uint32_t frame_end(ZFrame &z, bool checksum, uint32_t want) {
+    if (!checksum) return 0;
+    const uint32_t got = (uint32_t)z_xxh64(z.out + z.frame_start, (uint64_t)(z.olen - z.frame_start));
+    return want != got ? kZChecksum : 0;
+  }
+};
+
+// ---------------------------------------------------------------- fast sequence decode
+// ll / ml cells extended with their code's base and extra-bit count, so that
+// one LDS load per table gives everything a sequence needs (every lane)
+__device__ void z_expand_tables(ZLds &L, const ZFrame &z) {
+  zsync();
+  const int nll = 1 << z.ll_log, nml = 1 << z.ml_log;
+  for (int u = lane_id(); u < nll; u += 64) {
+    const uint32_t c = L.ll[u], sym = (c & 0xff) < 35 ? (c & 0xff) : 35;
+    L.ll2[u] = c | ((uint64_t)kZCodes.ll[sym] << 32);
+  }
+  for (int u = lane_id(); u < nml; u += 64) {
+    const uint32_t c = L.ml[u], sym = (c & 0xff) < 52 ? (c & 0xff) : 52;
+    L.ml2[u] = c | ((uint64_t)kZCodes.ml[sym] << 32);
+  }
+  zsync();
+}
+
+// The sequences of one block, decoded 96 bits at a time: per sequence one
+// round of LDS loads (the three cells and the four stream dwords covering the
+// <= 89 bits it can read), then scalar shifts. Bits below the stream start are
+// never trusted: a sequence that reads them ends below `lo`, which is the
+// overrun error (every error here is "Corrupted block detected").
+template <class Emit>
+__device__ __forceinline__ uint32_t z_seq_fast(ZFrame &z, ZLds &L, Emit &k, int64_t start, int64_t n, int64_t nseq,
+                                               int64_t regen, int64_t &lit_pos) {
+  ZSeqBr r;
+  if (!r.init(z.src, start, n, L.sring)) return kZCorrupt;
+  // (the values are wave-uniform; left as vector values, the loop's bit
+  // arithmetic runs on the vector ALU beside the scalar control flow -- made
+  // scalar throughout it was slower: one scalar ALU per CU serves every wave)
+  uint32_t sll = r.read(z.ll_log), sof = r.read(z.of_log), sml = r.read(z.ml_log);
+  int32_t bit = r.bit;
+  const int32_t lo = r.lo;
+  int64_t olen = z.olen;
+  const int64_t fstart = z.frame_start;
+  uint64_t rep0 = z.rep0, rep1 = z.rep1, rep2 = z.rep2;
+  int64_t lp = lit_pos;
+  for (int64_t i = 0; i < nseq; i++) {
+    const int32_t b0 = bit - 96;
+    const int32_t q = b0 >> 5;
+    if ((q >> 6) < r.inst) {  // entering the next 256 B block of the stream
+      zsync();
+      L.sring[((r.inst - 1) & 1) * 64 + lane_id()] = r.pre;
+      zsync();
+      r.inst--;
+      r.pre = r.ld((r.inst - 1) * 64 + lane_id());
+    }
+    const uint64_t cll = L.ll2[sll], cml = L.ml2[sml];
+    const uint32_t cof = L.of[sof];
+    const uint32_t d0 = L.sring[q & 127], d1 = L.sring[(q + 1) & 127], d2 = L.sring[(q + 2) & 127],
+                   d3 = L.sring[(q + 3) & 127];
+    const uint32_t cll0 = uni((uint32_t)cll), cll1 = uni((uint32_t)(cll >> 32));
+    const uint32_t cml0 = uni((uint32_t)cml), cml1 = uni((uint32_t)(cml >> 32));
+    const uint32_t cf = uni(cof);
+    const uint32_t sh = (uint32_t)(b0 - 32 * q);
+    // 96 window bits [bit - 96, bit): w0 lowest
+    const uint32_t w0 = __builtin_amdgcn_alignbit(d1, d0, sh);
+    const uint32_t w1 = __builtin_amdgcn_alignbit(d2, d1, sh);
+    const uint32_t w2 = __builtin_amdgcn_alignbit(d3, d2, sh);
+    const uint64_t hi = ((uint64_t)w2 << 32) | w1, lo64 = ((uint64_t)w1 << 32) | w0;
+    int c = 0;
+    // the next nb bits down (nb <= 32): window bits [96 - c - nb, 96 - c)
+    auto take = [&](int nb) -> uint32_t {
+      if (nb == 0) return 0u;
+      c += nb;
+      const int o = 96 - c;
+      const uint64_t v = o >= 32 ? (hi >> (o - 32)) : (lo64 >> o);
+      return (uint32_t)v & (nb >= 32 ? ~0u : ((1u << nb) - 1u));
+    };
+    const uint32_t llc = cll0 & 0xff, mlc = cml0 & 0xff, ofc = cf & 0xff;
+    if (llc > 35 || mlc > 52 || ofc > 31) return kZCorrupt;
+    const uint64_t ofv = (1ull << ofc) + take((int)ofc);
+    const uint64_t ml = (cml1 & 0xFFFFFFu) + take((int)(cml1 >> 24));
+    const uint64_t ll = (cll1 & 0xFFFFFFu) + take((int)(cll1 >> 24));
+    uint64_t off;
+    if (ofv > 3) {
+      off = ofv - 3;
+      rep2 = rep1;
+      rep1 = rep0;
+      rep0 = off;
+    } else {
+      const uint64_t idx = ofv + (ll == 0 ? 1 : 0);
+      if (idx == 1) {
+        off = rep0;
+      } else if (idx == 2) {
+        off = rep1;
+        rep1 = rep0;
+        rep0 = off;
+      } else if (idx == 3) {
+        off = rep2;
+        rep2 = rep1;
+        rep1 = rep0;
+        rep0 = off;
+      } else {
+        off = rep0 - 1;
+        if (off == 0) return kZCorrupt;
+        rep2 = rep1;
+        rep1 = rep0;
+        rep0 = off;
+      }
+    }
+    if (i + 1 < nseq) {
+      sll = (cll0 >> 16) + take((int)((cll0 >> 8) & 0xff));
+      sml = (cml0 >> 16) + take((int)((cml0 >> 8) & 0xff));
+      sof = (cf >> 16) + take((int)((cf >> 8) & 0xff));
+    }
+    bit -= c;
+    if (bit < lo) return kZCorrupt;
+    // z_exec's checks, in its order (the region bound is the exec pass's)
+    if (lp + (int64_t)ll > regen) return kZCorrupt;
+    lp += (int64_t)ll;
+    olen += (int64_t)ll;
+    if (off == 0 || (int64_t)off > olen - fstart) return kZCorrupt;
+    olen += (int64_t)ml;
+    k.emit_seq(ll, ml, off);
+  }
+  z.olen = olen;
+  z.rep0 = rep0;
+  z.rep1 = rep1;
+  z.rep2 = rep2;
+  lit_pos = lp;
+  return bit == lo ? 0u : kZCorrupt;
+}
+
+// ---------------------------------------------------------------- fast path, entropy pass
+// Entries (u64, k_zstd_ent -> k_zstd_exec): literal count (bits 15:0), match
+// length (31:16), offset (63:32); literal runs and matches are split so that
+// each is at most kZPiece bytes (copying a long match in pieces with the same
+// offset is the same copy). Frame ends are marked: ll = 0xFFFF with ml = 0xFFFF
+// (checksum = offset field) or 0xFFFE (no checksum).
+constexpr uint32_t kZPiece = 2048;
+constexpr uint32_t kZMark = 0xFFFF;
+constexpr uint32_t kZMarkCk = 0xFFFF, kZMarkNoCk = 0xFFFE;
+
+struct ZEntrySink {
+  uint8_t *region;       // the block's scratch region (flattened input at its start)
+  int64_t lit_w;         // next literal byte (region offset)
+  int64_t ent_end;       // entries end here (entry e at ent_end - 8 (e + 1))
+  uint64_t ent, my;      // entries so far; this lane's pending entry (group of 64)
+  uint64_t ent_mark;     // entries up to the last frame-end marker
+  bool ck_done;          // a checksummed frame ended (its check is the exec pass's)
+
+  __device__ __forceinline__ bool room(int64_t nlit, int64_t nent) const {
+    return lit_w + nlit + 64 <= ent_end - 8 * (int64_t)(ent + nent);
+  }
+  // entries are gathered in lanes (lane e mod 64 holds entry e) and stored 64 at a time
+  __device__ __forceinline__ void emit(uint64_t e) {
+    const uint64_t slot = ent & 63;
+    if ((uint64_t)lane_id() == slot) my = e;
+    if (slot == 63) *reinterpret_cast<uint64_t *>(region + ent_end - 8 * (int64_t)(ent - 63 + lane_id() + 1)) = my;
+    ent++;
+  }
+  __device__ __forceinline__ void flush() {  // the partial last group
+    const uint64_t g0 = ent & ~63ull;
+    const int l = lane_id();
+    if ((uint64_t)l < ent - g0) *reinterpret_cast<uint64_t *>(region + ent_end - 8 * (int64_t)(g0 + l + 1)) = my;
+  }
+  // a run of ll literals then a match, split into pieces
+  __device__ __forceinline__ void emit_seq(uint64_t ll, uint64_t ml, uint64_t off) {
+    while (ll > kZPiece) {
+      emit(kZPiece);
+      ll -= kZPiece;
+    }
+    uint64_t m = ml < kZPiece ? ml : kZPiece;
+    emit(ll | (m << 16) | (off << 32));
+    ml -= m;
+    while (ml) {
+      m = ml < kZPiece ? ml : kZPiece;
+      emit((m << 16) | (off << 32));
+      ml -= m;
+    }
+  }
+  __device__ uint32_t raw(ZFrame &z, int64_t at, int64_t size) {
+    if (!room(size, size / kZPiece + 2)) return kZSlow;
+    for (int64_t k = lane_id(); k < size; k += 64) region[lit_w + k] = z.src[at + k];
+    lit_w += size;
+    z.olen += size;
+    emit_seq((uint64_t)size, 0, 0);
+    return 0;
+  }
+  __device__ uint32_t rle(ZFrame &z, uint8_t v, int64_t size) {
+    if (!room(size, size / kZPiece + 2)) return kZSlow;
+    for (int64_t k = lane_id(); k < size; k += 64) region[lit_w + k] = v;
+    lit_w += size;
+    z.olen += size;
+    emit_seq((uint64_t)size, 0, 0);
+    return 0;
+  }
+  __device__ uint32_t block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n) {
+    int64_t pos = 0, regen = 0, nseq = 0;
+    z.lit = region + lit_w;
+    // literals first: they need their room before the entries are known
+    const int64_t free_lit = ent_end - 8 * (int64_t)(ent + 2 * (kZBlockMax / kZPiece) + 4) - 64 - lit_w;
+    ZPROF_T(t0);
+    uint32_t e = z_literals(z, L, bstart, n, pos, regen, free_lit);
+    ZPROF_ADD(0, t0);
+    if (e) return e;
+    e = z_seq_header(z, L, bstart, n, pos, nseq);
+#ifdef RIO_ZPROF
+    if (lane_id() == 0) atomicAdd(&zprof_ctl->zprof[1], (unsigned long long)nseq);
+#endif
+    if (e) return e;
+    ZPROF_T(t2);
+    if (!room(regen, nseq + 2 * (kZBlockMax / kZPiece) + 4)) return kZSlow;
+    int64_t lit_pos = 0;
+    if (nseq > 0) {
+      z_expand_tables(L, z);
+      if ((e = z_seq_fast(z, L, *this, bstart + pos, n - pos, nseq, regen, lit_pos))) return e;
+    }
+    if (regen > lit_pos) emit_seq((uint64_t)(regen - lit_pos), 0, 0);
+    z.olen += regen - lit_pos;
+    lit_w += regen;
+    ZPROF_ADD(2, t2);
+    return 0;
+  }
+  __device__ uint32_t frame_end(ZFrame &z, bool checksum, uint32_t want) {
+    emit(checksum ? (kZMark | (kZMarkCk << 16) | ((uint64_t)want << 32)) : (kZMark | (kZMarkNoCk << 16)));
+    ent_mark = ent;
+    ck_done |= checksum;
+    return 0;
+  }
+};
 
 // ---------------------------------------------------------------- XXH64
 constexpr uint64_t kP1 = 0x9E3779B185EBCA87ull, kP2 = 0xC2B2AE3D27D4EB4Full, kP3 = 0x165667B19E3779F9ull,
@@ -670,8 +1157,8 @@ __device__ __forceinline__ uint32_t zrd24(const uint8_t *p, int64_t i) { return 
 __device__ __forceinline__ uint32_t zrd32(const uint8_t *p, int64_t i) { return zrd16(p, i) | (zrd16(p, i + 2) << 16); }
 
 // one frame at src[in, in + n) (oracle decode_frame): bytes consumed, or -(ZErr)
-__device__ int64_t z_decode_frame(ZFrame &z, ZLds &L, int64_t in, int64_t n) {
-  const int l = lane_id();
+template <class Sink>
+__device__ int64_t z_decode_frame(ZFrame &z, ZLds &L, Sink &k, int64_t in, int64_t n) {
   const uint8_t *src = z.src;
   if (n < 4) return -(int64_t)kZSrc;
   const uint32_t magic = zrd32(src, in);
@@ -726,37 +1213,32 @@ __device__ int64_t z_decode_frame(ZFrame &z, ZLds &L, int64_t in, int64_t n) {
     const uint64_t size = bh >> 3;
     if (type == 3) return -(int64_t)kZCorrupt;
     if (size > block_max) return -(int64_t)kZCorrupt;
+    uint32_t e;
     if (type == 0) {
       if (pos + (int64_t)size > n) return -(int64_t)kZSrc;
-      if (z.olen + (int64_t)size > z.cap) return -(int64_t)kZFull;
-      for (uint64_t k = l; k < size; k += 64) z.out[z.olen + k] = src[in + pos + k];
-      z.olen += (int64_t)size;
+      e = k.raw(z, in + pos, (int64_t)size);
       pos += (int64_t)size;
-      zmem_sync();
     } else if (type == 1) {
       if (pos + 1 > n) return -(int64_t)kZSrc;
-      if (z.olen + (int64_t)size > z.cap) return -(int64_t)kZFull;
-      const uint8_t v = src[in + pos];
-      for (uint64_t k = l; k < size; k += 64) z.out[z.olen + k] = v;
-      z.olen += (int64_t)size;
+      e = k.rle(z, src[in + pos], (int64_t)size);
       pos += 1;
-      zmem_sync();
     } else {
       if (pos + (int64_t)size > n) return -(int64_t)kZSrc;
-      const uint32_t e = z_decode_block(z, L, in + pos, (int64_t)size);
-      if (e) return -(int64_t)e;
+      e = k.block(z, L, in + pos, (int64_t)size);
       pos += (int64_t)size;
     }
+    if (e) return -(int64_t)e;
     if (last) break;
   }
   if (fcs >= 0 && z.olen - z.frame_start != fcs) return -(int64_t)kZCorrupt;
+  uint32_t want = 0;
   if (checksum) {
     if (pos + 4 > n) return -(int64_t)kZSrc;
-    const uint32_t want = zrd32(src, in + pos);
-    const uint32_t got = (uint32_t)z_xxh64(z.out + z.frame_start, (uint64_t)(z.olen - z.frame_start));
-    if (want != got) return -(int64_t)kZChecksum;
+    want = zrd32(src, in + pos);
     pos += 4;
   }
+  const uint32_t e = k.frame_end(z, checksum != 0, want);
+  if (e) return -(int64_t)e;
   return pos;
 }
 
@@ -842,6 +1324,335 @@ __device__ __forceinline__ uint32_t z_flat_dword(const uint8_t *span, const unsi
   return v;
 }
 
+enum ZsMode : uint32_t {
+  kZsSkip = 0,   // nothing to decode (not a transformed block, error already reported, capacity retry)
+  kZsExec = 1,   // entries ready for k_zstd_exec
+  kZsErrCk = 2,  // entropy error after checksummed frames: k_zstd_exec checks those first
+  kZsSlow = 3,   // scratch too small for the fast path: k_zstd (serial) decodes it
+};
+
+__device__ __forceinline__ void z_init(ZFrame &z, const uint8_t *src, uint8_t *out, int64_t cap, uint8_t *lit) {
+  z.src = src;
+  z.out = out;
+  z.cap = cap;
+  z.olen = 0;
+  z.frame_start = 0;
+  z.lit = lit;
+  z.max_bits = 0;
+  z.have_huf = z.have_ll = z.have_of = z.have_ml = 0;
+  z.ll_log = z.of_log = z.ml_log = 0;
+  z.rep0 = 1;
+  z.rep1 = 4;
+  z.rep2 = 8;
+}
+
+// flattenIov: block b's chunk payloads back to back at the start of its token
+// region (+8 zero bytes); false if the block is not decoded by the caller
+// (state and status written here)
+__device__ __forceinline__ void z_flatten(const uint8_t *span, const DevBufs &d, uint64_t c0, unsigned long long meta,
+                                          uint64_t n, uint32_t *flat) {
+  const int l = lane_id();
+  const uint64_t total = meta & kMetaTotalMask, pay0 = uni64(d.ck_pay[c0]);
+  const bool regular = (meta & kMetaRegular) != 0;
+  for (uint64_t p = 4 * (uint64_t)l; p < n + 8; p += 256)
+    flat[p >> 2] = z_flat_dword(span, d.ck_pay, c0, total, pay0, n, regular, p);
+  zmem_sync();
+}
+
+// ---------------------------------------------------------------- k_zstd_ent
+// Entropy pass, one wave per recordio block (grid-stride): frames and block
+// headers, Huffman literals (4 streams on 4 lanes) into the block's literal
+// area, the FSE sequence bitstream (wave-uniform, scalar) into entries. Every
+// check of the serial decoder except the decode region's bound, which is
+// known exactly here (the total output) and is the host's retry size.
+// Region of block b (its token region, 128 KiB per chunk): flattened input |
+// literals (growing up) ... entries (growing down from the end).
+__global__ void __launch_bounds__(64) k_zstd_ent(const uint8_t *__restrict__ span, DevBufs d,
+                                                 const unsigned long long *nblocks, uint64_t dec_cap) {
+  __shared__ ZLds L;
+  const int l = lane_id();
+  const uint64_t nb = uni64(*nblocks);
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    FlState *sp = &d.fl[b];
+    const uint64_t c0 = uni64(d.blk_c0[b]);
+    const unsigned long long meta = uni64(d.blk_meta[b]);
+    const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
+    // incomplete blocks, and magics that are never untransformed (the header
+    // block is idTransform, registry.go:31; others are errors): nothing decoded
+    if (!(meta & kMetaComplete) || (cls != kMagicPacked && cls != kMagicTrailer)) {
+      if (l == 0) {
+        sp->mode = kZsSkip;
+        d.blk_out_len[b] = 0;
+      }
+      continue;
+    }
+    const uint64_t off = uni64(d.blk_dec_off[b]), cap = uni64(d.blk_out_len[b]);
+    if (off + cap > dec_cap) {  // the regions need a larger buffer (host retries)
+      if (l == 0) {
+        sp->mode = kZsSkip;
+        atomicOr(&d.ctl->out_overflow, 0x40ull);
+        atomicMax(&d.ctl->dec_need, (unsigned long long)(off + cap));
+        d.blk_out_len[b] = 0;
+      }
+      continue;
+    }
+    const uint64_t n = uni64(d.blk_len[b]);
+    if (n == 0) {  // DataDog Decompress: ErrEmptySlice
+      if (l == 0) {
+        sp->mode = kZsSkip;
+        d.blk_status[b] = kBlkCodec;
+        d.blk_a[b] = kCodecZstdEmpty;
+        d.blk_b[b] = 0;
+        d.blk_out_len[b] = 0;
+      }
+      continue;
+    }
+#ifdef RIO_ZPROF
+    zprof_ctl = d.ctl;
+#endif
+    ZPROF_T(tb);
+    uint32_t *flat = d.tok + c0 * (uint64_t)kZTokPerChunk;
+    z_flatten(span, d, c0, meta, n, flat);
+    ZFrame z;
+    z_init(z, reinterpret_cast<const uint8_t *>(flat), nullptr, (int64_t)cap, nullptr);
+    ZEntrySink k;
+    k.region = reinterpret_cast<uint8_t *>(flat);
+    k.lit_w = (int64_t)((n + 16 + 15) & ~15ull);
+    k.ent_end = (int64_t)((meta & kMetaTotalMask) * (uint64_t)kZTokPerChunk * 4);
+    k.ent = 0;
+    k.my = 0;
+    k.ent_mark = 0;
+    k.ck_done = false;
+    const int64_t lit0 = k.lit_w;
+    uint32_t zerr = 0;
+    int64_t pos = 0;
+    while (pos < (int64_t)n) {
+      const int64_t r = z_decode_frame(z, L, k, pos, (int64_t)n - pos);
+      if (r < 0) {
+        zerr = (uint32_t)(-r);
+        break;
+      }
+      pos += r;
+    }
+    k.flush();
+    ZPROF_ADD(3, tb);
+    if (!zerr && z.olen >= (1ll << 31)) zerr = kZSlow;  // the exec pass counts in u32
+    if (l == 0) {
+      if (zerr == kZSlow) {
+        sp->mode = kZsSlow;
+        atomicAdd(&d.ctl->pad[1], 1ull);
+      } else if (zerr && !k.ck_done) {
+        sp->mode = kZsSkip;
+        d.blk_status[b] = kBlkCodec;
+        d.blk_a[b] = kCodecZstd;
+        d.blk_b[b] = zerr;
+        d.blk_out_len[b] = 0;
+      } else if (!zerr && z.olen > (int64_t)cap) {  // exact size: the host retries with it
+        sp->mode = kZsSkip;
+        d.blk_need[b] = (unsigned long long)z.olen;
+        atomicOr(&d.ctl->out_overflow, 8ull);
+        d.blk_status[b] = kBlkCodec;
+        d.blk_a[b] = kCodecFull;
+        d.blk_out_len[b] = 0;
+      } else {
+        sp->mode = zerr ? kZsErrCk : kZsExec;
+        sp->stored_left = zerr;
+        sp->ntok = (uint32_t)(zerr ? k.ent_mark : k.ent);
+        sp->olen = (unsigned long long)z.olen;
+        sp->bitpos = (unsigned long long)lit0;
+        sp->hdrpos = (unsigned long long)k.ent_end;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- k_zstd_exec
+// Execution pass, one wave per block: the entries in groups of 64, cut into
+// parts of at most kZPart output bytes (and at frame ends); per part the
+// literals are staged from the literal area into LDS, literal runs written,
+// then matches -- a parallel round for short ones whose source precedes the
+// part's first match, the rest in order, each by the whole wave -- into an LDS
+// ring holding the last kZHist bytes; completed 1 KiB units are flushed to the
+// decode region 16 B per lane. Sources further back than the ring are read
+// from the decode region (flushed, made visible by vmcnt(0) first).
+constexpr uint32_t kZRing = 20480;
+constexpr uint32_t kZPart = 2 * kZPiece;
+constexpr uint32_t kZHist = kZRing - kZPart;
+constexpr int kZExecWaves = 6;  // per CU (~25 KiB LDS each)
+
+__device__ __forceinline__ uint32_t zr_slot(uint32_t x) { return x - __umulhi(x >> 12, 0x33333334u) * kZRing; }
+__device__ __forceinline__ uint8_t zr_src(const uint8_t *ring, const uint8_t *out, uint32_t pos, uint32_t base) {
+  return pos + kZHist >= base ? ring[zr_slot(pos)] : out[pos];
+}
+__device__ __forceinline__ uint32_t zrl(uint32_t v, uint32_t lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+// k mod d for k < 2^20, d >= 1
+__device__ __forceinline__ uint32_t z_umod(uint32_t k, uint32_t dv) {
+  uint32_t q = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)dv));
+  int32_t r = (int32_t)(k - q * dv);
+  if (r < 0) r += (int32_t)dv;
+  if (r >= (int32_t)dv) r -= (int32_t)dv;
+  return (uint32_t)r;
+}
+// completed 1 KiB units of [flushed, olen) to HBM (a unit never wraps: 20 units)
+__device__ __forceinline__ void zr_flush(const uint8_t *ring, uint8_t *out, uint32_t &flushed, uint32_t olen) {
+  const int l = lane_id();
+  for (uint32_t u0 = flushed; u0 + 1024 <= olen; u0 += 1024) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(ring + zr_slot(u0) + 16 * l);
+    *reinterpret_cast<uint4 *>(out + u0 + 16 * l) = v;
+    flushed = u0 + 1024;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long long *nblocks) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kZRing];
+  __shared__ __attribute__((aligned(16))) uint32_t litbuf[kZPart / 4 + 8];
+  const int l = lane_id();
+  const uint64_t nb = uni64(*nblocks);
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    FlState *sp = &d.fl[b];
+    const uint32_t mode = uni(sp->mode);
+    if (mode != kZsExec && mode != kZsErrCk) continue;
+    const uint8_t *region = reinterpret_cast<const uint8_t *>(d.tok + uni64(d.blk_c0[b]) * (uint64_t)kZTokPerChunk);
+    const uint64_t lit0 = uni64(sp->bitpos), ent_end = uni64(sp->hdrpos);
+    const uint32_t ntok = uni(sp->ntok);
+    const uint64_t *ents = reinterpret_cast<const uint64_t *>(region + ent_end);  // entry e at ents[-1 - e]
+    const uint32_t *lit32 = reinterpret_cast<const uint32_t *>(region + lit0);    // 16-aligned
+    uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
+    uint32_t olen = 0, litpos = 0, flushed = 0, fstart = 0, zerr = 0;
+    wave_lds_sync();
+    for (uint32_t g0 = 0; g0 < ntok && !zerr; g0 += 64) {
+      const uint32_t n = ntok - g0 < 64 ? ntok - g0 : 64;
+      const uint64_t e = (uint32_t)l < n ? ents[-1 - (int64_t)(g0 + l)] : 0ull;
+      const uint32_t ll0 = (uint32_t)e & 0xffffu, ml0 = (uint32_t)(e >> 16) & 0xffffu, off = (uint32_t)(e >> 32);
+      const bool mark = ll0 == kZMark;
+      const uint32_t len = mark ? 0u : ll0 + ml0, lits = mark ? 0u : ll0;
+      const uint32_t incl = wave_incl_sum_dpp(len), lincl = wave_incl_sum_dpp(lits);
+      const uint32_t excl = incl - len, lexcl = lincl - lits;
+      const unsigned long long marks = __ballot(mark);
+      uint32_t s = 0;
+      while (s < n) {
+        const uint32_t bs = zrl(excl, s), ls = zrl(lexcl, s);
+        const unsigned long long over = __ballot((uint32_t)l >= s && (uint32_t)l < n && incl - bs > kZPart);
+        const unsigned long long mk = marks & (~0ull << s);
+        uint32_t e1 = n;
+        if (over) e1 = min(e1, (uint32_t)(__ffsll((long long)over) - 1));
+        if (mk) e1 = min(e1, (uint32_t)(__ffsll((long long)mk) - 1));
+        if (e1 > s) {
+          const uint32_t T = zrl(incl, e1 - 1) - bs, Ls = zrl(lincl, e1 - 1) - ls;
+          const bool mine = (uint32_t)l >= s && (uint32_t)l < e1;
+          const uint32_t base = olen;
+          const uint32_t p = excl - bs;  // part-relative output position
+          const uint32_t myll = mine ? ll0 : 0u, myml = mine ? ml0 : 0u;
+          if (Ls) {  // literals: stage the part's run of the literal area, then scatter
+            const uint32_t a0 = litpos & ~3u, nd = (litpos + Ls - a0 + 3) >> 2;
+            wave_lds_sync();
+            for (uint32_t j = l; j < nd; j += 64) litbuf[j] = lit32[(a0 >> 2) + j];
+            wave_lds_sync();
+            const uint8_t *lb = reinterpret_cast<const uint8_t *>(litbuf) + (litpos - a0);
+            const uint32_t lp = lexcl - ls;
+            if (myll && myll <= 32) {
+              const uint32_t q0 = base + p;
+              for (uint32_t k = 0; k < myll; k++) ring[zr_slot(q0 + k)] = lb[lp + k];
+            }
+            unsigned long long rem = __ballot(myll > 32);
+            while (rem) {
+              const uint32_t f = (uint32_t)(__ffsll((long long)rem) - 1);
+              rem &= rem - 1;
+              const uint32_t N = zrl(myll, f), P = base + zrl(p, f), LP = zrl(lp, f);
+              for (uint32_t k0 = 0; k0 < N; k0 += 64) {
+                const uint32_t k = k0 + (uint32_t)l;
+                if (k < N) ring[zr_slot(P + k)] = lb[LP + k];
+              }
+            }
+          }
+          wave_lds_sync();
+          const bool m = myml != 0;
+          const unsigned long long mm = __ballot(m);
+          if (mm) {
+            const uint32_t dst = base + p + myll, src = dst - off;
+            if (__ballot(m && src + kZHist < base)) zmem_sync();  // flushed sources: visible first
+            // one parallel round: short matches whose source ends before the
+            // part's first match, each by its own lane ...
+            const uint32_t R = zrl(dst, (uint32_t)(__ffsll((long long)mm) - 1));
+            const uint32_t src_end = src + (myml < off ? myml : off);
+            const bool ready = m && src_end <= R && myml <= 32;
+            if (ready) {
+              if (off >= 8 || myml <= off) {  // no byte of an 8-byte piece depends on another
+                for (uint32_t k = 0; k < myml; k += 8) {
+                  uint8_t v[8];
+#pragma unroll
+                  for (int jj = 0; jj < 8; jj++) v[jj] = k + jj < myml ? zr_src(ring, out, src + k + jj, base) : 0;
+#pragma unroll
+                  for (int jj = 0; jj < 8; jj++)
+                    if (k + jj < myml) ring[zr_slot(dst + k + jj)] = v[jj];
+                }
+              } else {  // overlapping run: byte by byte, each reads one written before it
+                for (uint32_t k = 0; k < myml; k++) ring[zr_slot(dst + k)] = ring[zr_slot(src + k)];
+              }
+            }
+            // ... then the rest in order, each by the whole wave (every byte it
+            // reads precedes it and is final by then)
+            unsigned long long rest = mm & ~__ballot(ready);
+            while (rest) {
+              const uint32_t f = (uint32_t)(__ffsll((long long)rest) - 1);
+              rest &= rest - 1;
+              wave_lds_sync();
+              const uint32_t P = zrl(dst, f), D = zrl(off, f), N = zrl(myml, f), S = P - D;
+              for (uint32_t k0 = 0; k0 < N; k0 += 64) {
+                const uint32_t k = k0 + (uint32_t)l;
+                const uint32_t kk = D >= N ? k : z_umod(k, D);
+                const uint8_t v = k < N ? zr_src(ring, out, S + kk, base) : 0;
+                if (k < N) ring[zr_slot(P + k)] = v;
+              }
+            }
+          }
+          olen += T;
+          litpos += Ls;
+          if ((olen & ~1023u) > flushed) {
+            wave_lds_sync();
+            zr_flush(ring, out, flushed, olen);
+          }
+        }
+        if (e1 < n && ((marks >> e1) & 1ull)) {  // frame end
+          if (zrl(ml0, e1) == kZMarkCk) {
+            wave_lds_sync();
+            zr_flush(ring, out, flushed, olen);
+            for (uint32_t k = flushed + l; k < olen; k += 64) out[k] = ring[zr_slot(k)];
+            zmem_sync();
+            const uint32_t got = (uint32_t)z_xxh64(out + fstart, olen - fstart);
+            if (got != zrl(off, e1)) {
+              zerr = kZChecksum;
+              break;
+            }
+          }
+          fstart = olen;
+          e1++;
+        }
+        s = e1;
+      }
+    }
+    wave_lds_sync();
+    zr_flush(ring, out, flushed, olen);
+    for (uint32_t k = flushed + l; k < olen; k += 64) out[k] = ring[zr_slot(k)];
+    if (l == 0) {
+      if (!zerr && mode == kZsExec) {
+        d.blk_out_len[b] = olen;
+      } else {
+        d.blk_status[b] = kBlkCodec;
+        d.blk_a[b] = kCodecZstd;
+        d.blk_b[b] = zerr ? zerr : sp->stored_left;
+        d.blk_out_len[b] = 0;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- k_zstd (serial path)
+// The exact serial decoder, for the blocks the fast path declined (kZsSlow):
+// one wave per block, sequences executed one at a time against the decode
+// region, literals in a per-wave buffer.
 __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, DevBufs d,
                                              const unsigned long long *nblocks, uint64_t dec_cap) {
   __shared__ ZLds L;
@@ -849,6 +1660,7 @@ __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, D
   const uint64_t nb = uni64(*nblocks);
   uint8_t *lit = d.zlit + (uint64_t)blockIdx.x * kZLitStride;
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    if (uni(d.fl[b].mode) != kZsSlow) continue;
     const uint64_t c0 = uni64(d.blk_c0[b]);
     const unsigned long long meta = uni64(d.blk_meta[b]);
     const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
@@ -873,29 +1685,14 @@ __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, D
     if (n == 0) {  // DataDog Decompress: ErrEmptySlice
       code = kCodecZstdEmpty;
     } else {
-      // flattenIov: the chunk payloads back to back, in this block's token region
-      const uint64_t total = meta & kMetaTotalMask, pay0 = uni64(d.ck_pay[c0]);
-      const bool regular = (meta & kMetaRegular) != 0;
-      uint32_t *flat = d.tok + c0 * (uint64_t)kTokPerChunk;
-      for (uint64_t p = 4 * (uint64_t)l; p < n + 8; p += 256)
-        flat[p >> 2] = z_flat_dword(span, d.ck_pay, c0, total, pay0, n, regular, p);
-      zmem_sync();
+      uint32_t *flat = d.tok + c0 * (uint64_t)kZTokPerChunk;
+      z_flatten(span, d, c0, meta, n, flat);
       ZFrame z;
-      z.src = reinterpret_cast<const uint8_t *>(flat);
-      z.out = d.dec + off;
-      z.cap = (int64_t)cap;
-      z.olen = 0;
-      z.frame_start = 0;
-      z.lit = lit;
-      z.max_bits = 0;
-      z.have_huf = z.have_ll = z.have_of = z.have_ml = 0;
-      z.ll_log = z.of_log = z.ml_log = 0;
-      z.rep0 = 1;
-      z.rep1 = 4;
-      z.rep2 = 8;
+      z_init(z, reinterpret_cast<const uint8_t *>(flat), d.dec + off, (int64_t)cap, lit);
+      ZSerialSink sink;
       int64_t pos = 0;
       while (pos < (int64_t)n) {
-        const int64_t k = z_decode_frame(z, L, pos, (int64_t)n - pos);
+        const int64_t k = z_decode_frame(z, L, sink, pos, (int64_t)n - pos);
         if (k < 0) {
           zerr = (uint32_t)(-k);
           break;
@@ -931,11 +1728,17 @@ __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, D
 uint64_t zstd_grid(int ncu) { return (uint64_t)ncu * kZWaves; }
 uint64_t zstd_lit_bytes(uint64_t grid) { return grid * kZLitStride; }
 
+// entropy pass -> serial path (declined blocks only) -> execution pass
 void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
                  uint64_t dec_cap, uint64_t grid, hipStream_t st) {
   uint64_t g = max_blocks < grid ? max_blocks : grid;
   if (g < 1) g = 1;
+  hipLaunchKernelGGL(k_zstd_ent, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
   hipLaunchKernelGGL(k_zstd, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
+  uint64_t g2 = grid / kZWaves * kZExecWaves;
+  if (g2 > max_blocks) g2 = max_blocks;
+  if (g2 < 1) g2 = 1;
+  hipLaunchKernelGGL(k_zstd_exec, dim3((unsigned)g2), dim3(64), 0, st, d, nblocks);
 }
 
 }  // namespace rio

@@ -226,9 +226,9 @@ static int ensure_dec(rio_ctx *c, uint64_t need) {
   return 0;
 }
 
-// flate token regions: kTokPerChunk u32 per chunk of the span
-static int ensure_tok(rio_ctx *c, uint64_t nchunks) {
-  const uint64_t need = nchunks * (uint64_t)kTokPerChunk;
+// flate token regions: kTokPerChunk u32 per chunk of the span (zstd: kZTokPerChunk)
+static int ensure_tok(rio_ctx *c, uint64_t nchunks, uint64_t per_chunk) {
+  const uint64_t need = nchunks * per_chunk;
   if (c->d.tok_cap >= need) return 0;
   if (dalloc(&c->d.tok, need)) return -1;
   c->d.tok_cap = need;
@@ -264,6 +264,9 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   // control words are min-reduced: reset to ~0 (out_overflow to 0)
   HIP_OK(hipMemsetAsync(d.ctl, 0xff, 4 * sizeof(unsigned long long), st));
   HIP_OK(hipMemsetAsync(&d.ctl->out_overflow, 0, 4 * sizeof(unsigned long long), st));  // + dec_need, pad
+#ifdef RIO_ZPROF
+  HIP_OK(hipMemsetAsync(d.ctl->zprof, 0, sizeof(d.ctl->zprof), st));
+#endif
   HIP_OK(hipMemsetAsync(&d.ctl->flstat_esc, 0, sizeof(unsigned long long), st));
   if (attempt == 0 && codec != RIO_CODEC_NONE && nchunks > 0)
     HIP_OK(hipMemsetAsync(d.blk_need, 0, nchunks * sizeof(unsigned long long), st));
@@ -279,7 +282,8 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     // decode regions: factor x the compressed bytes per block (+4 KiB each)
     if (ensure_dec(c, (uint64_t)c->dec_factor * nchunks * kChunk + nchunks * 4352ull)) return -1;
     // flate tokens / flattened zstd blocks
-    if ((codec == RIO_CODEC_FLATE || codec == RIO_CODEC_ZSTD) && ensure_tok(c, nchunks)) return -1;
+    if (codec == RIO_CODEC_FLATE && ensure_tok(c, nchunks, kTokPerChunk)) return -1;
+    if (codec == RIO_CODEC_ZSTD && ensure_tok(c, nchunks, kZTokPerChunk)) return -1;
     if (codec == RIO_CODEC_ZSTD && ensure_zlit(c)) return -1;
     launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
     launch_codec_decode(span, d, c->nblocks_dev, max_blocks, nchunks, codec, c->dec_cap, c->fl_rounds, c->ncu, st);
@@ -542,6 +546,10 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
   HIP_OK(hipSetDevice(ctx->device));
   HIP_OK(hipMemcpyAsync(ctx->h_ctl, ctx->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->st));
   HIP_OK(hipStreamSynchronize(ctx->st));
+  if (ctx->last_codec == RIO_CODEC_ZSTD && getenv("RIO_ZSTAT"))
+    fprintf(stderr, "rio: zstd blocks on the serial path: %llu; entropy-pass cycles lit %llu tables %llu seq %llu block %llu\n",
+            (unsigned long long)ctx->h_ctl->pad[1], ctx->h_ctl->zprof[0], ctx->h_ctl->zprof[1], ctx->h_ctl->zprof[2],
+            ctx->h_ctl->zprof[3]);
   float ms = 0;
   hipEventElapsedTime(&ms, ctx->ev[kEvStart], ctx->ev[kEvEnd]);
   if (collect(ctx, ctx->last_span, ctx->last_file_off, ctx->last_codec, ctx->last_mode, ctx->last_in_bytes, out,

@@ -62,7 +62,7 @@ struct Ctl {
   unsigned long long first_incomplete;   // min c0 of a block extending past the span
   unsigned long long out_overflow;       // nonzero if side/items exceeded capacity
   unsigned long long dec_need;           // decode regions' total size (when it exceeds dec_cap)
-  unsigned long long pad[2];             // (RIO_FLSTAT builds: flate pass counters)
+  unsigned long long pad[2];             // [0] (RIO_FLSTAT builds: flate pass counters); [1] zstd blocks on the serial path
   // filled by k_resolve
   unsigned long long stop_key;
   unsigned long long n_valid_blocks;
@@ -80,6 +80,7 @@ struct Ctl {
   unsigned long long consumed_chunks;
   unsigned long long mag_cur, mag_prev, mag_blk;  // little-endian magic bytes
   unsigned long long flstat_esc;                  // (RIO_FLSTAT builds: flate escapes)
+  unsigned long long zprof[4];                    // (RIO_ZPROF builds: zstd entropy-pass cycles per phase)
 };
 
 constexpr unsigned long long kNone = ~0ull;
@@ -122,6 +123,7 @@ struct FlState {
 };
 constexpr int kFlRounds = 6;          // Huffman/copy rounds launched per span
 constexpr int kTokPerChunk = kChunk;  // token region: 32,768 u32 per chunk of the block
+constexpr int kZTokPerChunk = 2 * kTokPerChunk;  // zstd scratch: input copy, literals, sequence entries
 
 // Device arrays of one context (capacities fixed at rio_open, grown on demand).
 struct DevBufs {

@@ -179,6 +179,17 @@ class Context:
         out._span_buf = buf  # item views point into it
         return out
 
+    def scan_host_ptr(self, host_ptr: int, nbytes: int, file_off: int = 0, is_file_end: bool = True,
+                      limit_off: int = U64_MAX, codec: int = RIO_CODEC_NONE) -> RioBatch:
+        """rio_scan_span over caller-owned host memory at host_ptr (pinned or
+        pageable); item views point into it, so it must outlive the batch."""
+        out = RioBatch()
+        rc = self.L.rio_scan_span(self.h, host_ptr, nbytes, file_off, int(is_file_end), limit_off, codec,
+                                  ctypes.byref(out))
+        if rc != 0:
+            raise RuntimeError("rio_scan_span: " + self.L.rio_last_error().decode())
+        return out
+
     def scan_device_async(self, dev_ptr: int, nbytes: int, file_off: int = 0, codec: int = RIO_CODEC_NONE):
         rc = self.L.rio_scan_device_async(self.h, dev_ptr, nbytes, file_off, codec)
         if rc != 0:

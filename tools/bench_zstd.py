@@ -40,13 +40,31 @@ def cpu_baseline_c4(data: bytes, nrec: int, budget_s: float = 8.0):
                       "the Go reference (DataDog/zstd = libzstd) cannot be built here" % (passes, len(data), nrec)}
 
 
-def run_c4(base_mib=128, replicas=80, steps=5, warmup=1, device=0, check=True, cpu_s=0.0):
+def load_or_make(base_mib, workers, path=None):
+    """The C4 base file; with `path`, cached there (a profiled run loads it: libzstd
+    cannot be called under rocprofv3, whose own zstd symbols interpose)."""
+    import c4_data
+    if path and os.path.exists(path):
+        with open(path + ".json") as f:
+            m = json.load(f)
+        with open(path, "rb") as f:
+            return f.read(), m["nblk"], m["nrec"], m["rec_bytes"]
+    data, nblk, nrec, rec_bytes = c4_data.make_file(base_mib << 20, workers=workers)
+    if path:
+        with open(path, "wb") as f:
+            f.write(data)
+        with open(path + ".json", "w") as f:
+            json.dump({"nblk": nblk, "nrec": nrec, "rec_bytes": rec_bytes}, f)
+    return data, nblk, nrec, rec_bytes
+
+
+def run_c4(base_mib=128, replicas=80, steps=5, warmup=1, device=0, check=True, cpu_s=0.0, workers=16, data_path=None):
     import bench_flate
     import c4_data
     from base_amd.recordio import gpu
 
     t0 = time.perf_counter()
-    data, nblk, nrec, rec_bytes = c4_data.make_file(base_mib << 20, workers=16)
+    data, nblk, nrec, rec_bytes = load_or_make(base_mib, workers, data_path)
     gen_s = time.perf_counter() - t0
     res = bench_flate.measure(data, nrec, rec_bytes, lambda: c4_data.all_records(nblk), gpu.RIO_CODEC_ZSTD,
                               "C4-like zstd level 5, records 64 B-64 KiB log-uniform, 1 MiB blocks",
@@ -63,8 +81,15 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-s", type=float, default=0.0)
+    ap.add_argument("--workers", type=int, default=16, help="generator processes (1: in-process)")
+    ap.add_argument("--data", default=None, help="cache the base file here (load it if present)")
+    ap.add_argument("--make-data", action="store_true", help="only write --data, no GPU")
     args = ap.parse_args()
-    print(json.dumps(run_c4(args.base_mib, args.replicas, args.steps, args.warmup, cpu_s=args.cpu_s)), flush=True)
+    if args.make_data:
+        load_or_make(args.base_mib, args.workers, args.data)
+        return
+    print(json.dumps(run_c4(args.base_mib, args.replicas, args.steps, args.warmup, cpu_s=args.cpu_s,
+                            workers=args.workers, data_path=args.data)), flush=True)
 
 
 if __name__ == "__main__":

@@ -62,11 +62,18 @@ def make_file(target_bytes: int, seed: int = SEED, workers: int = 8):
     nblk = max(1, target_bytes // BLOCK_BYTES)
     out = [F.chunk_block(F.MAGIC_HEADER, F.packed_block_payload([F.marshal_header([("transformer", "zstd")])]))]
     rec_bytes = nrec = 0
-    with ProcessPoolExecutor(max_workers=workers) as ex:
-        for blk, nb, ni in ex.map(_block, [(b, seed) for b in range(nblk)], chunksize=2):
-            out.append(blk)
-            rec_bytes += nb
-            nrec += ni
+    jobs = [(b, seed) for b in range(nblk)]
+    if workers <= 1:  # in-process (e.g. under a profiler that cannot follow a process pool)
+        results = map(_block, jobs)
+    else:
+        ex = ProcessPoolExecutor(max_workers=workers)
+        results = ex.map(_block, jobs, chunksize=2)
+    for blk, nb, ni in results:
+        out.append(blk)
+        rec_bytes += nb
+        nrec += ni
+    if workers > 1:
+        ex.shutdown()
     return b"".join(out), nblk, nrec, rec_bytes
 
 
