@@ -135,6 +135,29 @@ def c3_flate(args, local, world, dist):
     return r
 
 
+def c4_zstd(args, local, world, dist):
+    """BASELINE.json configs[3] beside the headline: ~10 GiB of records (sizes
+    log-uniform 64 B-64 KiB, 1 MiB blocks, zstd level 5) per GPU, device-resident,
+    one pass = chunk CRC + zstd entropy/execution passes + packed unpack
+    (tools/bench_zstd.py). Whole-job GiB/s of compressed input."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_zstd
+    cpu_s = 6.0 if (world == 1 and not args.no_cpu_baseline) else 0.0
+    r = bench_zstd.run_c4(replicas=args.zstd_replicas, steps=max(2, min(args.steps, 3)), warmup=1, device=local,
+                          check=True, cpu_s=cpu_s)
+    if dist is not None:
+        t = torch.tensor([r["ms_per_step"]], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+        r["value"] = round(r["config"]["span_bytes"] * world / (ms * 1e-3) / 2 ** 30, 2)
+        r["ms_per_step"] = round(ms, 3)
+    r["n_gpus"] = world
+    moved = (r["config"]["span_bytes"] + r["config"]["records_bytes"]) * world
+    r["hbm_frac"] = round(moved / (r["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,6 +167,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-flate", action="store_true", help="skip the C3 flate measurement (configs[2])")
     ap.add_argument("--flate-replicas", type=int, default=80)
+    ap.add_argument("--no-zstd", action="store_true", help="skip the C4 zstd measurement (configs[3])")
+    ap.add_argument("--zstd-replicas", type=int, default=80)
     args = ap.parse_args()
 
     import torch
@@ -245,6 +270,8 @@ def main():
     torch.cuda.empty_cache()
     if not args.no_flate:
         out["c3_flate"] = c3_flate(args, local, world, dist)
+    if not args.no_zstd:
+        out["c4_zstd"] = c4_zstd(args, local, world, dist)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data)
     if rank == 0:
