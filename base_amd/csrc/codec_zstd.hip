@@ -44,6 +44,8 @@ constexpr uint32_t kZMagic = 0xFD2FB528u;
 constexpr int kZBlockMax = 128 * 1024;
 constexpr uint64_t kZLitStride = kZBlockMax + 256;  // per-wave literal buffer
 constexpr int kZWaves = 12;                          // resident zstd waves per CU (LDS ~10 KiB each)
+constexpr int kZSeqWaves = 8;                        // k_zstd_seq waves per CU (64 jobs each)
+constexpr int kZFixWaves = 8;                        // k_zstd_fix waves per CU
 
 __constant__ uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,  12,   13,   14,   15,   16,   18,
                                      20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
@@ -94,7 +96,6 @@ struct ZLds {
   uint8_t w[256];
   int32_t res[12];  // lane 0's results, broadcast
   uint32_t sring[128];      // the sequence bitstream, two 256 B blocks (ZSeqBr)
-  uint64_t ll2[1 << 9], ml2[1 << 9];  // ll / ml cells | (code base | extra bits << 24) << 32 (fast path)
   uint8_t hout[4][256];     // Huffman streams' decoded literals, flushed 256 at a time
   // table descriptions (FSE NCount, Huffman tree) staged from HBM by the whole
   // wave: lane 0's serial bit walks over them then cost LDS, not HBM, latency
@@ -863,6 +864,10 @@ struct ZSerialSink {
     zmem_sync();
     return 0;
   }
+  __device__ void frame_begin(ZFrame &) {}
+  __device__ uint32_t frame_fcs(ZFrame &z, int64_t fcs) {
+    return (fcs >= 0 && z.olen - z.frame_start != fcs) ? kZCorrupt : 0u;
+  }
   __device__ uint32_t frame_end(ZFrame &z, bool checksum, uint32_t want) {
     if (!checksum) return 0;
     const uint32_t got = (uint32_t)z_xxh64(z.out + z.frame_start, (uint64_t)(z.olen - z.frame_start));
@@ -870,225 +875,146 @@ struct ZSerialSink {
   }
 };
 
-// ---------------------------------------------------------------- fast sequence decode
-// ll / ml cells extended with their code's base and extra-bit count, so that
-// one LDS load per table gives everything a sequence needs (every lane)
-__device__ void z_expand_tables(ZLds &L, const ZFrame &z) {
-  zsync();
-  const int nll = 1 << z.ll_log, nml = 1 << z.ml_log;
-  for (int u = lane_id(); u < nll; u += 64) {
-    const uint32_t c = L.ll[u], sym = (c & 0xff) < 35 ? (c & 0xff) : 35;
-    L.ll2[u] = c | ((uint64_t)kZCodes.ll[sym] << 32);
-  }
-  for (int u = lane_id(); u < nml; u += 64) {
-    const uint32_t c = L.ml[u], sym = (c & 0xff) < 52 ? (c & 0xff) : 52;
-    L.ml2[u] = c | ((uint64_t)kZCodes.ml[sym] << 32);
-  }
-  zsync();
-}
-
-// The sequences of one block, decoded 96 bits at a time: per sequence one
-// round of LDS loads (the three cells and the four stream dwords covering the
-// <= 89 bits it can read), then scalar shifts. Bits below the stream start are
-// never trusted: a sequence that reads them ends below `lo`, which is the
-// overrun error (every error here is "Corrupted block detected").
-template <class Emit>
-__device__ __forceinline__ uint32_t z_seq_fast(ZFrame &z, ZLds &L, Emit &k, int64_t start, int64_t n, int64_t nseq,
-                                               int64_t regen, int64_t &lit_pos) {
-  ZSeqBr r;
-  if (!r.init(z.src, start, n, L.sring)) return kZCorrupt;
-  // (the values are wave-uniform; left as vector values, the loop's bit
-  // arithmetic runs on the vector ALU beside the scalar control flow -- made
-  // scalar throughout it was slower: one scalar ALU per CU serves every wave)
-  uint32_t sll = r.read(z.ll_log), sof = r.read(z.of_log), sml = r.read(z.ml_log);
-  int32_t bit = r.bit;
-  const int32_t lo = r.lo;
-  int64_t olen = z.olen;
-  const int64_t fstart = z.frame_start;
-  uint64_t rep0 = z.rep0, rep1 = z.rep1, rep2 = z.rep2;
-  int64_t lp = lit_pos;
-  for (int64_t i = 0; i < nseq; i++) {
-    const int32_t b0 = bit - 96;
-    const int32_t q = b0 >> 5;
-    if ((q >> 6) < r.inst) {  // entering the next 256 B block of the stream
-      zsync();
-      L.sring[((r.inst - 1) & 1) * 64 + lane_id()] = r.pre;
-      zsync();
-      r.inst--;
-      r.pre = r.ld((r.inst - 1) * 64 + lane_id());
-    }
-    const uint64_t cll = L.ll2[sll], cml = L.ml2[sml];
-    const uint32_t cof = L.of[sof];
-    const uint32_t d0 = L.sring[q & 127], d1 = L.sring[(q + 1) & 127], d2 = L.sring[(q + 2) & 127],
-                   d3 = L.sring[(q + 3) & 127];
-    const uint32_t cll0 = uni((uint32_t)cll), cll1 = uni((uint32_t)(cll >> 32));
-    const uint32_t cml0 = uni((uint32_t)cml), cml1 = uni((uint32_t)(cml >> 32));
-    const uint32_t cf = uni(cof);
-    const uint32_t sh = (uint32_t)(b0 - 32 * q);
-    // 96 window bits [bit - 96, bit): w0 lowest
-    const uint32_t w0 = __builtin_amdgcn_alignbit(d1, d0, sh);
-    const uint32_t w1 = __builtin_amdgcn_alignbit(d2, d1, sh);
-    const uint32_t w2 = __builtin_amdgcn_alignbit(d3, d2, sh);
-    const uint64_t hi = ((uint64_t)w2 << 32) | w1, lo64 = ((uint64_t)w1 << 32) | w0;
-    int c = 0;
-    // the next nb bits down (nb <= 32): window bits [96 - c - nb, 96 - c)
-    auto take = [&](int nb) -> uint32_t {
-      if (nb == 0) return 0u;
-      c += nb;
-      const int o = 96 - c;
-      const uint64_t v = o >= 32 ? (hi >> (o - 32)) : (lo64 >> o);
-      return (uint32_t)v & (nb >= 32 ? ~0u : ((1u << nb) - 1u));
-    };
-    const uint32_t llc = cll0 & 0xff, mlc = cml0 & 0xff, ofc = cf & 0xff;
-    if (llc > 35 || mlc > 52 || ofc > 31) return kZCorrupt;
-    const uint64_t ofv = (1ull << ofc) + take((int)ofc);
-    const uint64_t ml = (cml1 & 0xFFFFFFu) + take((int)(cml1 >> 24));
-    const uint64_t ll = (cll1 & 0xFFFFFFu) + take((int)(cll1 >> 24));
-    uint64_t off;
-    if (ofv > 3) {
-      off = ofv - 3;
-      rep2 = rep1;
-      rep1 = rep0;
-      rep0 = off;
-    } else {
-      const uint64_t idx = ofv + (ll == 0 ? 1 : 0);
-      if (idx == 1) {
-        off = rep0;
-      } else if (idx == 2) {
-        off = rep1;
-        rep1 = rep0;
-        rep0 = off;
-      } else if (idx == 3) {
-        off = rep2;
-        rep2 = rep1;
-        rep1 = rep0;
-        rep0 = off;
-      } else {
-        off = rep0 - 1;
-        if (off == 0) return kZCorrupt;
-        rep2 = rep1;
-        rep1 = rep0;
-        rep0 = off;
-      }
-    }
-    if (i + 1 < nseq) {
-      sll = (cll0 >> 16) + take((int)((cll0 >> 8) & 0xff));
-      sml = (cml0 >> 16) + take((int)((cml0 >> 8) & 0xff));
-      sof = (cf >> 16) + take((int)((cf >> 8) & 0xff));
-    }
-    bit -= c;
-    if (bit < lo) return kZCorrupt;
-    // z_exec's checks, in its order (the region bound is the exec pass's)
-    if (lp + (int64_t)ll > regen) return kZCorrupt;
-    lp += (int64_t)ll;
-    olen += (int64_t)ll;
-    if (off == 0 || (int64_t)off > olen - fstart) return kZCorrupt;
-    olen += (int64_t)ml;
-    k.emit_seq(ll, ml, off);
-  }
-  z.olen = olen;
-  z.rep0 = rep0;
-  z.rep1 = rep1;
-  z.rep2 = rep2;
-  lit_pos = lp;
-  return bit == lo ? 0u : kZCorrupt;
-}
-
-// ---------------------------------------------------------------- fast path, entropy pass
-// Entries (u64, k_zstd_ent -> k_zstd_exec): literal count (bits 15:0), match
-// length (31:16), offset (63:32); literal runs and matches are split so that
-// each is at most kZPiece bytes (copying a long match in pieces with the same
-// offset is the same copy). Frame ends are marked: ll = 0xFFFF with ml = 0xFFFF
-// (checksum = offset field) or 0xFFFE (no checksum).
+// ---------------------------------------------------------------- fast path: jobs
+// The fast path turns every zstd block of a recordio block into a job
+// (k_zstd_ent: frame walk, literals, table descriptions), decodes every job's
+// sequence bitstream in its own lane (k_zstd_seq: one vector instruction
+// advances 64 jobs), then -- in file order, one wave per recordio block --
+// resolves repeat offsets, checks every sequence and writes the execution
+// entries (k_zstd_fix). A job's header, its three FSE tables (ll / ml cells
+// extended with their code's base and extra bits) and its raw sequences sit
+// in the second half of the block's scratch region; DevBufs::zjob lists the
+// headers.
+//
+// Execution entries (u64, k_zstd_fix -> k_zstd_exec): literal count (bits
+// 15:0), match length (31:16), offset (63:32); literal runs and matches are
+// split so that each is at most kZPiece bytes (copying a long match in pieces
+// with the same offset is the same copy). Frame ends are marked: ll = 0xFFFF
+// with ml = 0xFFFF (checksum = offset field) or 0xFFFE (no checksum).
 constexpr uint32_t kZPiece = 2048;
 constexpr uint32_t kZMark = 0xFFFF;
 constexpr uint32_t kZMarkCk = 0xFFFF, kZMarkNoCk = 0xFFFE;
 
-struct ZEntrySink {
-  uint8_t *region;       // the block's scratch region (flattened input at its start)
-  int64_t lit_w;         // next literal byte (region offset)
-  int64_t ent_end;       // entries end here (entry e at ent_end - 8 (e + 1))
-  uint64_t ent, my;      // entries so far; this lane's pending entry (group of 64)
-  uint64_t ent_mark;     // entries up to the last frame-end marker
-  bool ck_done;          // a checksummed frame ended (its check is the exec pass's)
+struct ZJob {
+  uint64_t seq_off;         // sequence bitstream (byte offset from d.tok)
+  uint32_t seq_len, nseq;
+  uint32_t regen, flags;    // the block's literals; kJ*
+  uint32_t checksum, logs;  // frame checksum (kJCk); ll_log | of_log << 8 | ml_log << 16
+  int64_t fcs;              // frame content size, at the frame's last job (-1: none)
+  uint64_t tab_off;         // ll cells (u64 x 2^ll_log), ml cells (u64), of cells (u32)
+  uint64_t raw_off;         // raw sequences (u64 x nseq): ll | ml << 17 | offset value << 35
+  uint64_t next;            // the block's next job header
+  uint32_t err, pad;        // k_zstd_seq: 0, kZCorrupt or kZSlow
+};
+constexpr int64_t kZJobHdr = (sizeof(ZJob) + 15) / 16 * 16;  // header bytes; 16-aligned tables follow
+constexpr uint32_t kJFirst = 1, kJLast = 2, kJCk = 4, kJLit = 8;
 
-  __device__ __forceinline__ bool room(int64_t nlit, int64_t nent) const {
-    return lit_w + nlit + 64 <= ent_end - 8 * (int64_t)(ent + nent);
-  }
-  // entries are gathered in lanes (lane e mod 64 holds entry e) and stored 64 at a time
-  __device__ __forceinline__ void emit(uint64_t e) {
-    const uint64_t slot = ent & 63;
-    if ((uint64_t)lane_id() == slot) my = e;
-    if (slot == 63) *reinterpret_cast<uint64_t *>(region + ent_end - 8 * (int64_t)(ent - 63 + lane_id() + 1)) = my;
-    ent++;
-  }
-  __device__ __forceinline__ void flush() {  // the partial last group
-    const uint64_t g0 = ent & ~63ull;
-    const int l = lane_id();
-    if ((uint64_t)l < ent - g0) *reinterpret_cast<uint64_t *>(region + ent_end - 8 * (int64_t)(g0 + l + 1)) = my;
-  }
-  // a run of ll literals then a match, split into pieces
-  __device__ __forceinline__ void emit_seq(uint64_t ll, uint64_t ml, uint64_t off) {
-    while (ll > kZPiece) {
-      emit(kZPiece);
-      ll -= kZPiece;
+// k_zstd_ent's frame content: literals into the literal area, every zstd
+// block a job (raw / RLE blocks are literal-only jobs)
+struct ZJobSink {
+  uint8_t *tok8;           // d.tok as bytes
+  uint64_t region;         // this block's scratch region (offset from d.tok)
+  int64_t lit_w, half;     // next literal byte; the first half's end (region offsets)
+  int64_t job_w, job_end;  // next job; region end
+  int64_t last;            // the last job's header (-1: none)
+  uint32_t njobs, pend_first;
+  unsigned long long *zjob;
+  uint64_t zjob_cap;
+  Ctl *ctl;
+
+  __device__ __forceinline__ ZJob *hdr(int64_t at) const { return reinterpret_cast<ZJob *>(tok8 + region + at); }
+  // a job with tabsz bytes of tables and nseq raw sequences: its region offset, or -1
+  __device__ int64_t new_job(int64_t tabsz, int64_t nseq, uint32_t regen, uint32_t flags) {
+    const int64_t tabr = (tabsz + 15) & ~15ll;
+    const int64_t need = kZJobHdr + tabr + 8 * nseq;
+    if (job_w + need > job_end) return -1;
+    unsigned long long idx = 0;
+    if (lane_id() == 0) idx = atomicAdd(&ctl->zjob_n, 1ull);
+    idx = uni64(idx);
+    if (idx >= zjob_cap) return -1;
+    const int64_t at = job_w;
+    job_w += need;
+    if (lane_id() == 0) {
+      zjob[idx] = region + (uint64_t)at;
+      ZJob *h = hdr(at);
+      h->seq_off = 0;
+      h->seq_len = 0;
+      h->nseq = (uint32_t)nseq;
+      h->regen = regen;
+      h->flags = flags | (pend_first ? kJFirst : 0u);
+      h->checksum = 0;
+      h->logs = 0;
+      h->fcs = -1;
+      h->tab_off = region + (uint64_t)(at + kZJobHdr);
+      h->raw_off = region + (uint64_t)(at + kZJobHdr + tabr);
+      h->next = 0;
+      h->err = 0;
+      h->pad = 0;
+      if (last >= 0) hdr(last)->next = region + (uint64_t)at;
     }
-    uint64_t m = ml < kZPiece ? ml : kZPiece;
-    emit(ll | (m << 16) | (off << 32));
-    ml -= m;
-    while (ml) {
-      m = ml < kZPiece ? ml : kZPiece;
-      emit((m << 16) | (off << 32));
-      ml -= m;
-    }
+    pend_first = 0;
+    last = at;
+    njobs++;
+    return at;
   }
-  __device__ uint32_t raw(ZFrame &z, int64_t at, int64_t size) {
-    if (!room(size, size / kZPiece + 2)) return kZSlow;
-    for (int64_t k = lane_id(); k < size; k += 64) region[lit_w + k] = z.src[at + k];
-    lit_w += size;
-    z.olen += size;
-    emit_seq((uint64_t)size, 0, 0);
+  __device__ void frame_begin(ZFrame &) { pend_first = 1; }
+  __device__ uint32_t frame_fcs(ZFrame &, int64_t fcs) {  // checked by k_zstd_fix (the output size is its)
+    if (lane_id() == 0) {
+      ZJob *h = hdr(last);
+      h->flags |= kJLast;
+      h->fcs = fcs;
+    }
     return 0;
   }
-  __device__ uint32_t rle(ZFrame &z, uint8_t v, int64_t size) {
-    if (!room(size, size / kZPiece + 2)) return kZSlow;
-    for (int64_t k = lane_id(); k < size; k += 64) region[lit_w + k] = v;
-    lit_w += size;
-    z.olen += size;
-    emit_seq((uint64_t)size, 0, 0);
+  __device__ uint32_t frame_end(ZFrame &, bool checksum, uint32_t want) {
+    if (checksum && lane_id() == 0) {
+      ZJob *h = hdr(last);
+      h->flags |= kJCk;
+      h->checksum = want;
+    }
     return 0;
   }
+  __device__ uint32_t lits(const uint8_t *from, uint8_t v, int64_t size) {  // raw (from) / RLE (v)
+    if (lit_w + size + 64 > half) return kZSlow;
+    if (new_job(0, 0, (uint32_t)size, kJLit) < 0) return kZSlow;
+    uint8_t *dst = tok8 + region + lit_w;
+    for (int64_t k = lane_id(); k < size; k += 64) dst[k] = from ? from[k] : v;
+    lit_w += size;
+    return 0;
+  }
+  __device__ uint32_t raw(ZFrame &z, int64_t at, int64_t size) { return lits(z.src + at, 0, size); }
+  __device__ uint32_t rle(ZFrame &, uint8_t v, int64_t size) { return lits(nullptr, v, size); }
   __device__ uint32_t block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n) {
     int64_t pos = 0, regen = 0, nseq = 0;
-    z.lit = region + lit_w;
-    // literals first: they need their room before the entries are known
-    const int64_t free_lit = ent_end - 8 * (int64_t)(ent + 2 * (kZBlockMax / kZPiece) + 4) - 64 - lit_w;
-    ZPROF_T(t0);
-    uint32_t e = z_literals(z, L, bstart, n, pos, regen, free_lit);
-    ZPROF_ADD(0, t0);
+    z.lit = tok8 + region + lit_w;
+    uint32_t e = z_literals(z, L, bstart, n, pos, regen, half - 64 - lit_w);
     if (e) return e;
     e = z_seq_header(z, L, bstart, n, pos, nseq);
-#ifdef RIO_ZPROF
-    if (lane_id() == 0) atomicAdd(&zprof_ctl->zprof[1], (unsigned long long)nseq);
-#endif
     if (e) return e;
-    ZPROF_T(t2);
-    if (!room(regen, nseq + 2 * (kZBlockMax / kZPiece) + 4)) return kZSlow;
-    int64_t lit_pos = 0;
-    if (nseq > 0) {
-      z_expand_tables(L, z);
-      if ((e = z_seq_fast(z, L, *this, bstart + pos, n - pos, nseq, regen, lit_pos))) return e;
+    const int nll = 1 << z.ll_log, nml = 1 << z.ml_log, nof = 1 << z.of_log;
+    const int64_t tabsz = nseq ? 8 * (int64_t)(nll + nml) + 4 * (int64_t)nof : 0;
+    const int64_t at = new_job(tabsz, nseq, (uint32_t)regen, 0);
+    if (at < 0) return kZSlow;
+    if (nseq) {
+      if (lane_id() == 0) {
+        ZJob *h = hdr(at);
+        h->seq_off = region + (uint64_t)(bstart + pos);
+        h->seq_len = (uint32_t)(n - pos);
+        h->logs = (uint32_t)z.ll_log | ((uint32_t)z.of_log << 8) | ((uint32_t)z.ml_log << 16);
+      }
+      uint64_t *tll = reinterpret_cast<uint64_t *>(tok8 + region + at + kZJobHdr), *tml = tll + nll;
+      uint32_t *tof = reinterpret_cast<uint32_t *>(tml + nml);
+      for (int u = lane_id(); u < nll; u += 64) {
+        const uint32_t c = L.ll[u], sym = (c & 0xff) < 35 ? (c & 0xff) : 35;
+        tll[u] = c | ((uint64_t)kZCodes.ll[sym] << 32);
+      }
+      for (int u = lane_id(); u < nml; u += 64) {
+        const uint32_t c = L.ml[u], sym = (c & 0xff) < 52 ? (c & 0xff) : 52;
+        tml[u] = c | ((uint64_t)kZCodes.ml[sym] << 32);
+      }
+      for (int u = lane_id(); u < nof; u += 64) tof[u] = L.of[u];
     }
-    if (regen > lit_pos) emit_seq((uint64_t)(regen - lit_pos), 0, 0);
-    z.olen += regen - lit_pos;
     lit_w += regen;
-    ZPROF_ADD(2, t2);
-    return 0;
-  }
-  __device__ uint32_t frame_end(ZFrame &z, bool checksum, uint32_t want) {
-    emit(checksum ? (kZMark | (kZMarkCk << 16) | ((uint64_t)want << 32)) : (kZMark | (kZMarkNoCk << 16)));
-    ent_mark = ent;
-    ck_done |= checksum;
     return 0;
   }
 };
@@ -1205,6 +1131,7 @@ __device__ int64_t z_decode_frame(ZFrame &z, ZLds &L, Sink &k, int64_t in, int64
   z.rep0 = 1;
   z.rep1 = 4;
   z.rep2 = 8;
+  k.frame_begin(z);
   for (;;) {
     if (pos + 3 > n) return -(int64_t)kZSrc;
     const uint32_t bh = zrd24(src, in + pos);
@@ -1230,7 +1157,7 @@ __device__ int64_t z_decode_frame(ZFrame &z, ZLds &L, Sink &k, int64_t in, int64
     if (e) return -(int64_t)e;
     if (last) break;
   }
-  if (fcs >= 0 && z.olen - z.frame_start != fcs) return -(int64_t)kZCorrupt;
+  if (const uint32_t ef = k.frame_fcs(z, fcs)) return -(int64_t)ef;
   uint32_t want = 0;
   if (checksum) {
     if (pos + 4 > n) return -(int64_t)kZSrc;
@@ -1329,6 +1256,7 @@ enum ZsMode : uint32_t {
   kZsExec = 1,   // entries ready for k_zstd_exec
   kZsErrCk = 2,  // entropy error after checksummed frames: k_zstd_exec checks those first
   kZsSlow = 3,   // scratch too small for the fast path: k_zstd (serial) decodes it
+  kZsJobs = 4,   // jobs made (k_zstd_ent): k_zstd_seq / k_zstd_fix finish them
 };
 
 __device__ __forceinline__ void z_init(ZFrame &z, const uint8_t *src, uint8_t *out, int64_t cap, uint8_t *lit) {
@@ -1360,13 +1288,12 @@ __device__ __forceinline__ void z_flatten(const uint8_t *span, const DevBufs &d,
 }
 
 // ---------------------------------------------------------------- k_zstd_ent
-// Entropy pass, one wave per recordio block (grid-stride): frames and block
-// headers, Huffman literals (4 streams on 4 lanes) into the block's literal
-// area, the FSE sequence bitstream (wave-uniform, scalar) into entries. Every
-// check of the serial decoder except the decode region's bound, which is
-// known exactly here (the total output) and is the host's retry size.
-// Region of block b (its token region, 128 KiB per chunk): flattened input |
-// literals (growing up) ... entries (growing down from the end).
+// Frame pass, one wave per recordio block (grid-stride): flattenIov, frames
+// and block headers, Huffman literals (4 streams on 4 lanes) into the block's
+// literal area, the sequence tables built from their descriptions; every zstd
+// block becomes a job (ZJob) for k_zstd_seq. Region of block b (512 KiB per
+// chunk): flattened input | literals (up) ... execution entries (down from
+// the middle) | jobs (from the middle up).
 __global__ void __launch_bounds__(64) k_zstd_ent(const uint8_t *__restrict__ span, DevBufs d,
                                                  const unsigned long long *nblocks, uint64_t dec_cap) {
   __shared__ ZLds L;
@@ -1415,14 +1342,20 @@ __global__ void __launch_bounds__(64) k_zstd_ent(const uint8_t *__restrict__ spa
     z_flatten(span, d, c0, meta, n, flat);
     ZFrame z;
     z_init(z, reinterpret_cast<const uint8_t *>(flat), nullptr, (int64_t)cap, nullptr);
-    ZEntrySink k;
-    k.region = reinterpret_cast<uint8_t *>(flat);
+    ZJobSink k;
+    const int64_t rbytes = (int64_t)((meta & kMetaTotalMask) * (uint64_t)kZTokPerChunk * 4);
+    k.tok8 = reinterpret_cast<uint8_t *>(d.tok);
+    k.region = c0 * (uint64_t)kZTokPerChunk * 4;
+    k.half = rbytes / 2;
     k.lit_w = (int64_t)((n + 16 + 15) & ~15ull);
-    k.ent_end = (int64_t)((meta & kMetaTotalMask) * (uint64_t)kZTokPerChunk * 4);
-    k.ent = 0;
-    k.my = 0;
-    k.ent_mark = 0;
-    k.ck_done = false;
+    k.job_w = k.half;
+    k.job_end = rbytes;
+    k.last = -1;
+    k.njobs = 0;
+    k.pend_first = 0;
+    k.zjob = d.zjob;
+    k.zjob_cap = d.zjob_cap;
+    k.ctl = d.ctl;
     const int64_t lit0 = k.lit_w;
     uint32_t zerr = 0;
     int64_t pos = 0;
@@ -1434,22 +1367,246 @@ __global__ void __launch_bounds__(64) k_zstd_ent(const uint8_t *__restrict__ spa
       }
       pos += r;
     }
-    k.flush();
     ZPROF_ADD(3, tb);
-    if (!zerr && z.olen >= (1ll << 31)) zerr = kZSlow;  // the exec pass counts in u32
     if (l == 0) {
       if (zerr == kZSlow) {
         sp->mode = kZsSlow;
         atomicAdd(&d.ctl->pad[1], 1ull);
-      } else if (zerr && !k.ck_done) {
+      } else {  // k_zstd_fix finishes it: the jobs, then this error (if any)
+        sp->mode = kZsJobs;
+        sp->final_ = zerr;
+        sp->ntok = k.njobs;
+        sp->olen = k.region + (uint64_t)k.half;  // the first job's header
+        sp->olen2 = (unsigned long long)k.lit_w;  // the literal area's end
+        sp->bitpos = (unsigned long long)lit0;
+        sp->hdrpos = (unsigned long long)k.half;  // execution entries end here
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- k_zstd_seq
+// Sequence pass: lane per job (grid-stride over DevBufs::zjob). The FSE cells
+// come from the job's tables in HBM (cache-resident while used), the bits
+// from a per-lane prefetching reader; each sequence becomes a raw entry (ll,
+// ml and the offset value before repeat-offset resolution, which needs the
+// previous block's last offsets and is k_zstd_fix's). The serial decoder's
+// checks that need only this stream (symbols in range, no overrun, exact end)
+// are made here; an offset code above 28 (windows beyond 256 MiB) sends the
+// recordio block to the serial path.
+__global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
+  uint8_t *tok8 = reinterpret_cast<uint8_t *>(d.tok);
+  const uint64_t nj0 = d.ctl->zjob_n, nj = nj0 < d.zjob_cap ? nj0 : d.zjob_cap;
+  for (uint64_t j = (uint64_t)blockIdx.x * 64 + lane_id(); j < nj; j += (uint64_t)gridDim.x * 64) {
+    ZJob *hp = reinterpret_cast<ZJob *>(tok8 + d.zjob[j]);
+    const uint32_t flags = hp->flags, nseq = hp->nseq;
+    if ((flags & kJLit) || nseq == 0) continue;
+    const uint64_t seq_off = hp->seq_off, tab_off = hp->tab_off, raw_off = hp->raw_off;
+    const uint32_t seq_len = hp->seq_len, logs = hp->logs;
+    uint32_t err = 0;
+    ZBr r;
+    if (!r.init(tok8, (int64_t)seq_off, (int64_t)seq_len)) {
+      err = kZCorrupt;
+    } else {
+      const int llg = logs & 0xff, ofg = (logs >> 8) & 0xff, mlg = (logs >> 16) & 0xff;
+      const uint64_t *tll = reinterpret_cast<const uint64_t *>(tok8 + tab_off), *tml = tll + (1 << llg);
+      const uint32_t *tof = reinterpret_cast<const uint32_t *>(tml + (1 << mlg));
+      uint64_t *raw = reinterpret_cast<uint64_t *>(tok8 + raw_off);
+      uint32_t sll = r.read(llg), sof = r.read(ofg), sml = r.read(mlg);
+      for (uint32_t i = 0; i < nseq; i++) {
+        const uint64_t cll = tll[sll], cml = tml[sml];
+        const uint32_t cof = tof[sof];
+        const uint32_t cl = (uint32_t)cll, cm = (uint32_t)cml;
+        const uint32_t llc = cl & 0xff, mlc = cm & 0xff, ofc = cof & 0xff;
+        if (llc > 35 || mlc > 52 || ofc > 31) {
+          err = kZCorrupt;
+          break;
+        }
+        if (ofc > 28) {
+          err = kZSlow;
+          break;
+        }
+        const uint32_t ofv = (1u << ofc) + r.read((int)ofc);
+        const uint32_t mlx = (uint32_t)(cml >> 32), llx = (uint32_t)(cll >> 32);
+        const uint32_t ml = (mlx & 0xFFFFFFu) + r.read((int)(mlx >> 24));
+        const uint32_t ll = (llx & 0xFFFFFFu) + r.read((int)(llx >> 24));
+        if (i + 1 < nseq) {
+          sll = (cl >> 16) + r.read((int)((cl >> 8) & 0xff));
+          sml = (cm >> 16) + r.read((int)((cm >> 8) & 0xff));
+          sof = (cof >> 16) + r.read((int)((cof >> 8) & 0xff));
+        }
+        if (r.overrun()) {
+          err = kZCorrupt;
+          break;
+        }
+        raw[i] = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
+      }
+      if (!err && !r.exact()) err = kZCorrupt;
+    }
+    hp->err = err;
+  }
+}
+
+// ---------------------------------------------------------------- k_zstd_fix
+// In file order, one wave per recordio block: every job's raw sequences 64 at
+// a time -- repeat offsets resolved in order (scalar), the serial decoder's
+// per-sequence checks made lane-parallel from prefix sums (literals left,
+// offset within the frame's output), execution entries written -- then the
+// frame checks (content size), then the frame walk's own error if it stopped
+// early. The result: entries for k_zstd_exec, an error, the exact size for
+// the host's retry, or the serial path.
+__device__ __forceinline__ uint32_t zrl(uint32_t v, uint32_t lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+__global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long long *nblocks) {
+  const int l = lane_id();
+  uint8_t *tok8 = reinterpret_cast<uint8_t *>(d.tok);
+  const uint64_t nb = uni64(*nblocks);
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    FlState *sp = &d.fl[b];
+    if (uni(sp->mode) != kZsJobs) continue;
+    const uint64_t region = uni64(d.blk_c0[b]) * (uint64_t)kZTokPerChunk * 4;
+    const int64_t half = (int64_t)uni64(sp->hdrpos), lit_end = (int64_t)uni64(sp->olen2);
+    uint8_t *ents = tok8 + region + half;  // entry e at ents - 8 (e + 1)
+    const int64_t cap = (int64_t)uni64(d.blk_out_len[b]);
+    const uint32_t njobs = uni(sp->ntok);
+    uint64_t jo = uni64(sp->olen);
+    uint32_t zerr = 0;
+    bool ck_done = false;
+    int64_t ent = 0, ent_mark = 0, olen = 0, fstart = 0;
+    uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
+    auto put = [&](uint64_t e) {
+      if (l == 0) *reinterpret_cast<uint64_t *>(ents - 8 * (ent + 1)) = e;
+      ent++;
+    };
+    auto pieces = [&](uint64_t ll, uint64_t ml, uint64_t off) {
+      while (ll > kZPiece) {
+        put(kZPiece);
+        ll -= kZPiece;
+      }
+      uint64_t m = ml < kZPiece ? ml : kZPiece;
+      put(ll | (m << 16) | (off << 32));
+      ml -= m;
+      while (ml) {
+        m = ml < kZPiece ? ml : kZPiece;
+        put((m << 16) | (off << 32));
+        ml -= m;
+      }
+    };
+    for (uint32_t j = 0; j < njobs && !zerr; j++) {
+      const ZJob *hp = reinterpret_cast<const ZJob *>(tok8 + jo);
+      const uint32_t flags = uni(hp->flags), regen = uni(hp->regen), nseq = uni(hp->nseq), jerr = uni(hp->err);
+      const uint64_t raw_off = uni64(hp->raw_off), next = uni64(hp->next);
+      const int64_t fcs = (int64_t)uni64((uint64_t)hp->fcs);
+      const uint32_t cks = uni(hp->checksum);
+      if (flags & kJFirst) {
+        fstart = olen;
+        rep0 = 1;
+        rep1 = 4;
+        rep2 = 8;
+      }
+      // entries grow down towards the literal area's end
+      if (lit_end + 64 > half - 8 * (ent + (int64_t)nseq + 2 * (kZBlockMax / kZPiece) + 4)) {
+        zerr = kZSlow;
+        break;
+      }
+      int64_t lp = 0;
+      if (!(flags & kJLit) && nseq) {
+        if (jerr) {
+          zerr = jerr;
+          break;
+        }
+        const uint64_t *raw = reinterpret_cast<const uint64_t *>(tok8 + raw_off);
+        for (uint32_t g0 = 0; g0 < nseq; g0 += 64) {
+          const uint32_t cnt = nseq - g0 < 64 ? nseq - g0 : 64;
+          const bool v = (uint32_t)l < cnt;
+          const uint64_t rv = v ? raw[g0 + l] : 0ull;
+          const uint32_t ll = (uint32_t)rv & 0x1FFFFu, ml = (uint32_t)(rv >> 17) & 0x3FFFFu;
+          const uint32_t ofv = (uint32_t)(rv >> 35);
+          // repeat offsets, in order
+          uint32_t off = 0;
+          for (uint32_t f = 0; f < cnt; f++) {
+            const uint32_t fo = zrl(ofv, f), fl = zrl(ll, f);
+            uint32_t o;
+            if (fo > 3) {
+              o = fo - 3;
+              rep2 = rep1;
+              rep1 = rep0;
+              rep0 = o;
+            } else {
+              const uint32_t idx = fo + (fl == 0 ? 1u : 0u);
+              if (idx == 1) {
+                o = rep0;
+              } else if (idx == 2) {
+                o = rep1;
+                rep1 = rep0;
+                rep0 = o;
+              } else if (idx == 3) {
+                o = rep2;
+                rep2 = rep1;
+                rep1 = rep0;
+                rep0 = o;
+              } else {  // o == 0 is the error below
+                o = rep0 - 1;
+                rep2 = rep1;
+                rep1 = rep0;
+                rep0 = o;
+              }
+            }
+            if ((uint32_t)l == f) off = o;
+          }
+          // z_exec's checks per sequence: literals left, offset within the frame's output
+          const uint32_t lin = wave_incl_sum_dpp(v ? ll : 0u), tin = wave_incl_sum_dpp(v ? ll + ml : 0u);
+          const int64_t my_lp = lp + (int64_t)(lin - ll);
+          const int64_t prod = olen - fstart + (int64_t)(tin - ml);  // output before its match
+          const bool bad = v && (my_lp + (int64_t)ll > (int64_t)regen || off == 0 || (int64_t)off > prod);
+          if (__ballot(bad)) {
+            zerr = kZCorrupt;
+            break;
+          }
+          if (__ballot(v && (ll > kZPiece || ml > kZPiece))) {
+            for (uint32_t f = 0; f < cnt; f++) pieces(zrl(ll, f), zrl(ml, f), zrl(off, f));
+          } else {
+            if (v)
+              *reinterpret_cast<uint64_t *>(ents - 8 * (ent + l + 1)) =
+                  (uint64_t)ll | ((uint64_t)ml << 16) | ((uint64_t)off << 32);
+            ent += cnt;
+          }
+          lp += zrl(lin, cnt - 1);
+          olen += zrl(tin, cnt - 1);
+        }
+        if (zerr) break;
+      }
+      if ((int64_t)regen > lp) pieces((uint64_t)((int64_t)regen - lp), 0, 0);  // the block's last literals
+      olen += (int64_t)regen - lp;
+      if (flags & kJLast) {
+        if (fcs >= 0 && olen - fstart != fcs) {
+          zerr = kZCorrupt;
+          break;
+        }
+        put((flags & kJCk) ? (kZMark | ((uint64_t)kZMarkCk << 16) | ((uint64_t)cks << 32))
+                           : (kZMark | ((uint64_t)kZMarkNoCk << 16)));
+        ent_mark = ent;
+        ck_done |= (flags & kJCk) != 0;
+      }
+      jo = next;
+    }
+    if (!zerr) zerr = uni(sp->final_);                // the frame walk stopped there
+    if (!zerr && olen >= (1ll << 31)) zerr = kZSlow;  // the execution pass counts in u32
+    if (l == 0) {
+      if (zerr == kZSlow) {
+        sp->mode = kZsSlow;
+        atomicAdd(&d.ctl->pad[1], 1ull);
+      } else if (zerr && !ck_done) {
         sp->mode = kZsSkip;
         d.blk_status[b] = kBlkCodec;
         d.blk_a[b] = kCodecZstd;
         d.blk_b[b] = zerr;
         d.blk_out_len[b] = 0;
-      } else if (!zerr && z.olen > (int64_t)cap) {  // exact size: the host retries with it
+      } else if (!zerr && olen > cap) {  // exact size: the host retries with it
         sp->mode = kZsSkip;
-        d.blk_need[b] = (unsigned long long)z.olen;
+        d.blk_need[b] = (unsigned long long)olen;
         atomicOr(&d.ctl->out_overflow, 8ull);
         d.blk_status[b] = kBlkCodec;
         d.blk_a[b] = kCodecFull;
@@ -1457,10 +1614,7 @@ __global__ void __launch_bounds__(64) k_zstd_ent(const uint8_t *__restrict__ spa
       } else {
         sp->mode = zerr ? kZsErrCk : kZsExec;
         sp->stored_left = zerr;
-        sp->ntok = (uint32_t)(zerr ? k.ent_mark : k.ent);
-        sp->olen = (unsigned long long)z.olen;
-        sp->bitpos = (unsigned long long)lit0;
-        sp->hdrpos = (unsigned long long)k.ent_end;
+        sp->ntok = (uint32_t)(zerr ? ent_mark : ent);
       }
     }
   }
@@ -1483,9 +1637,6 @@ constexpr int kZExecWaves = 6;  // per CU (~25 KiB LDS each)
 __device__ __forceinline__ uint32_t zr_slot(uint32_t x) { return x - __umulhi(x >> 12, 0x33333334u) * kZRing; }
 __device__ __forceinline__ uint8_t zr_src(const uint8_t *ring, const uint8_t *out, uint32_t pos, uint32_t base) {
   return pos + kZHist >= base ? ring[zr_slot(pos)] : out[pos];
-}
-__device__ __forceinline__ uint32_t zrl(uint32_t v, uint32_t lane) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
 // k mod d for k < 2^20, d >= 1
 __device__ __forceinline__ uint32_t z_umod(uint32_t k, uint32_t dv) {
@@ -1734,6 +1885,11 @@ void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long
   uint64_t g = max_blocks < grid ? max_blocks : grid;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(k_zstd_ent, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
+  hipLaunchKernelGGL(k_zstd_seq, dim3((unsigned)(grid / kZWaves * kZSeqWaves)), dim3(64), 0, st, d);
+  uint64_t g3 = grid / kZWaves * kZFixWaves;
+  if (g3 > max_blocks) g3 = max_blocks;
+  if (g3 < 1) g3 = 1;
+  hipLaunchKernelGGL(k_zstd_fix, dim3((unsigned)g3), dim3(64), 0, st, d, nblocks);
   hipLaunchKernelGGL(k_zstd, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
   uint64_t g2 = grid / kZWaves * kZExecWaves;
   if (g2 > max_blocks) g2 = max_blocks;

@@ -137,7 +137,7 @@ static void free_all(rio_ctx *c) {
   DevBufs &d = c->d;
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.item_off, d.item_len, d.side,
-                d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
+                d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span};
   for (void *p : ps)
     if (p) hipFree(p);
@@ -235,6 +235,15 @@ static int ensure_tok(rio_ctx *c, uint64_t nchunks, uint64_t per_chunk) {
   return 0;
 }
 
+// zstd job list: kZJobsPerChunk per chunk of the span
+static int ensure_zjob(rio_ctx *c, uint64_t nchunks) {
+  const uint64_t need = nchunks * (uint64_t)kZJobsPerChunk + 64;
+  if (c->d.zjob_cap >= need) return 0;
+  if (dalloc(&c->d.zjob, need)) return -1;
+  c->d.zjob_cap = need;
+  return 0;
+}
+
 // zstd literal buffers: one per decoder wave (allocated on first use)
 static int ensure_zlit(rio_ctx *c) {
   if (c->d.zlit) return 0;
@@ -284,7 +293,8 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     // flate tokens / flattened zstd blocks
     if (codec == RIO_CODEC_FLATE && ensure_tok(c, nchunks, kTokPerChunk)) return -1;
     if (codec == RIO_CODEC_ZSTD && ensure_tok(c, nchunks, kZTokPerChunk)) return -1;
-    if (codec == RIO_CODEC_ZSTD && ensure_zlit(c)) return -1;
+    if (codec == RIO_CODEC_ZSTD && (ensure_zlit(c) || ensure_zjob(c, nchunks))) return -1;
+    if (codec == RIO_CODEC_ZSTD) HIP_OK(hipMemsetAsync(&d.ctl->zjob_n, 0, sizeof(d.ctl->zjob_n), st));
     launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
     launch_codec_decode(span, d, c->nblocks_dev, max_blocks, nchunks, codec, c->dec_cap, c->fl_rounds, c->ncu, st);
     c->last_had_dec = true;

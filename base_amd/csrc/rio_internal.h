@@ -81,6 +81,7 @@ struct Ctl {
   unsigned long long mag_cur, mag_prev, mag_blk;  // little-endian magic bytes
   unsigned long long flstat_esc;                  // (RIO_FLSTAT builds: flate escapes)
   unsigned long long zprof[4];                    // (RIO_ZPROF builds: zstd entropy-pass cycles per phase)
+  unsigned long long zjob_n;                      // zstd jobs made (k_zstd_ent)
 };
 
 constexpr unsigned long long kNone = ~0ull;
@@ -123,7 +124,8 @@ struct FlState {
 };
 constexpr int kFlRounds = 6;          // Huffman/copy rounds launched per span
 constexpr int kTokPerChunk = kChunk;  // token region: 32,768 u32 per chunk of the block
-constexpr int kZTokPerChunk = 2 * kTokPerChunk;  // zstd scratch: input copy, literals, sequence entries
+constexpr int kZTokPerChunk = 4 * kTokPerChunk;  // zstd scratch: input copy, literals, entries | jobs
+constexpr int kZJobsPerChunk = 16;               // zstd job list capacity (a block past it takes the serial path)
 
 // Device arrays of one context (capacities fixed at rio_open, grown on demand).
 struct DevBufs {
@@ -161,6 +163,8 @@ struct DevBufs {
   uint64_t fl_grid;              // Huffman-pass workgroups (0: all resident; RIO_FL_GRID, tests)
   unsigned long long *fl_more;   // per round: blocks whose token region filled (kFlRounds)
   uint8_t *zlit;                 // zstd: one literal buffer per decoder wave (codec_zstd.hip)
+  unsigned long long *zjob;      // zstd: job header offsets (bytes from tok)
+  uint64_t zjob_cap;
   uint64_t zlit_waves;           // decoder waves zlit holds buffers for
   Ctl *ctl;
   // CRC tables (constant)
