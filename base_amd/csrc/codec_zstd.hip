@@ -21,6 +21,7 @@
 // the host's retry.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "device_common.h"
 #include "rio_internal.h"
@@ -44,7 +45,7 @@ constexpr uint32_t kZMagic = 0xFD2FB528u;
 constexpr int kZBlockMax = 128 * 1024;
 constexpr uint64_t kZLitStride = kZBlockMax + 256;  // per-wave literal buffer
 constexpr int kZWaves = 12;                          // resident zstd waves per CU (LDS ~10 KiB each)
-constexpr int kZSeqWaves = 8;                        // k_zstd_seq waves per CU (64 jobs each)
+constexpr int kZSeqWaves = 8;                        // k_zstd_seq waves per CU (64 jobs each; every job of a C4 span in flight)
 constexpr int kZFixWaves = 8;                        // k_zstd_fix waves per CU
 
 __constant__ uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,  12,   13,   14,   15,   16,   18,
@@ -881,8 +882,8 @@ struct ZSerialSink {
 // sequence bitstream in its own lane (k_zstd_seq: one vector instruction
 // advances 64 jobs), then -- in file order, one wave per recordio block --
 // resolves repeat offsets, checks every sequence and writes the execution
-// entries (k_zstd_fix). A job's header, its three FSE tables (ll / ml cells
-// extended with their code's base and extra bits) and its raw sequences sit
+// entries (k_zstd_fix). A job's header, its three FSE tables and its raw
+// sequences sit
 // in the second half of the block's scratch region; DevBufs::zjob lists the
 // headers.
 //
@@ -901,7 +902,7 @@ struct ZJob {
   uint32_t regen, flags;    // the block's literals; kJ*
   uint32_t checksum, logs;  // frame checksum (kJCk); ll_log | of_log << 8 | ml_log << 16
   int64_t fcs;              // frame content size, at the frame's last job (-1: none)
-  uint64_t tab_off;         // ll cells (u64 x 2^ll_log), ml cells (u64), of cells (u32)
+  uint64_t tab_off;         // ll, ml, of cells (u32 x 2^log each)
   uint64_t raw_off;         // raw sequences (u64 x nseq): ll | ml << 17 | offset value << 35
   uint64_t next;            // the block's next job header
   uint32_t err, pad;        // k_zstd_seq: 0, kZCorrupt or kZSlow
@@ -926,7 +927,7 @@ struct ZJobSink {
   // a job with tabsz bytes of tables and nseq raw sequences: its region offset, or -1
   __device__ int64_t new_job(int64_t tabsz, int64_t nseq, uint32_t regen, uint32_t flags) {
     const int64_t tabr = (tabsz + 15) & ~15ll;
-    const int64_t need = kZJobHdr + tabr + 8 * nseq;
+    const int64_t need = (kZJobHdr + tabr + 8 * nseq + 15) & ~15ll;  // raw entries are stored 16 B at a time
     if (job_w + need > job_end) return -1;
     unsigned long long idx = 0;
     if (lane_id() == 0) idx = atomicAdd(&ctl->zjob_n, 1ull);
@@ -992,7 +993,7 @@ struct ZJobSink {
     e = z_seq_header(z, L, bstart, n, pos, nseq);
     if (e) return e;
     const int nll = 1 << z.ll_log, nml = 1 << z.ml_log, nof = 1 << z.of_log;
-    const int64_t tabsz = nseq ? 8 * (int64_t)(nll + nml) + 4 * (int64_t)nof : 0;
+    const int64_t tabsz = nseq ? 4 * (int64_t)(nll + nml + nof) : 0;
     const int64_t at = new_job(tabsz, nseq, (uint32_t)regen, 0);
     if (at < 0) return kZSlow;
     if (nseq) {
@@ -1002,16 +1003,9 @@ struct ZJobSink {
         h->seq_len = (uint32_t)(n - pos);
         h->logs = (uint32_t)z.ll_log | ((uint32_t)z.of_log << 8) | ((uint32_t)z.ml_log << 16);
       }
-      uint64_t *tll = reinterpret_cast<uint64_t *>(tok8 + region + at + kZJobHdr), *tml = tll + nll;
-      uint32_t *tof = reinterpret_cast<uint32_t *>(tml + nml);
-      for (int u = lane_id(); u < nll; u += 64) {
-        const uint32_t c = L.ll[u], sym = (c & 0xff) < 35 ? (c & 0xff) : 35;
-        tll[u] = c | ((uint64_t)kZCodes.ll[sym] << 32);
-      }
-      for (int u = lane_id(); u < nml; u += 64) {
-        const uint32_t c = L.ml[u], sym = (c & 0xff) < 52 ? (c & 0xff) : 52;
-        tml[u] = c | ((uint64_t)kZCodes.ml[sym] << 32);
-      }
+      uint32_t *tll = reinterpret_cast<uint32_t *>(tok8 + region + at + kZJobHdr), *tml = tll + nll, *tof = tml + nml;
+      for (int u = lane_id(); u < nll; u += 64) tll[u] = L.ll[u];
+      for (int u = lane_id(); u < nml; u += 64) tml[u] = L.ml[u];
       for (int u = lane_id(); u < nof; u += 64) tof[u] = L.of[u];
     }
     lit_w += regen;
@@ -1386,18 +1380,35 @@ __global__ void __launch_bounds__(64) k_zstd_ent(const uint8_t *__restrict__ spa
 }
 
 // ---------------------------------------------------------------- k_zstd_seq
-// Sequence pass: lane per job (grid-stride over DevBufs::zjob). The FSE cells
-// come from the job's tables in HBM (cache-resident while used), the bits
-// from a per-lane prefetching reader; each sequence becomes a raw entry (ll,
-// ml and the offset value before repeat-offset resolution, which needs the
-// previous block's last offsets and is k_zstd_fix's). The serial decoder's
-// checks that need only this stream (symbols in range, no overrun, exact end)
-// are made here; an offset code above 28 (windows beyond 256 MiB) sends the
-// recordio block to the serial path.
+// Sequence pass: lane per job (grid-stride over DevBufs::zjob), every lane of
+// the wave decoding its own job's sequence bitstream (one vector instruction
+// advances 64 jobs); each sequence becomes a raw entry (ll, ml and the offset
+// value before repeat-offset resolution, which needs the previous block's last
+// offsets and is k_zstd_fix's). The FSE cells (u32, 5 KiB per job at most)
+// come from the job's tables in HBM: the grid is sized so that the tables of
+// the jobs in flight stay cache-resident. The code tables are in LDS and the
+// raw entries are staged in LDS and stored 16 at a time (a vector load or
+// store in the loop would be waited for behind the loads in flight: vmcnt
+// counts in order). The serial decoder's checks that need only this stream
+// (symbols in range, no overrun, exact end) are made here; an offset code
+// above 28 (windows beyond 256 MiB) sends the recordio block to the serial
+// path.
+__device__ __forceinline__ uint32_t zrl(uint32_t v, uint32_t lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+constexpr int kZStage = 16;  // raw entries per lane per store burst
 __global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
+  __shared__ ZCodes codes;
+  __shared__ __attribute__((aligned(16))) uint64_t stage[64][kZStage];
+  const int l = lane_id();
+  for (int u = l; u < 36; u += 64) codes.ll[u] = kZCodes.ll[u];
+  for (int u = l; u < 53; u += 64) codes.ml[u] = kZCodes.ml[u];
+  wave_lds_sync();
   uint8_t *tok8 = reinterpret_cast<uint8_t *>(d.tok);
+  uint64_t *st = stage[l];
   const uint64_t nj0 = d.ctl->zjob_n, nj = nj0 < d.zjob_cap ? nj0 : d.zjob_cap;
-  for (uint64_t j = (uint64_t)blockIdx.x * 64 + lane_id(); j < nj; j += (uint64_t)gridDim.x * 64) {
+  for (uint64_t j = (uint64_t)blockIdx.x * 64 + l; j < nj; j += (uint64_t)gridDim.x * 64) {
     ZJob *hp = reinterpret_cast<ZJob *>(tok8 + d.zjob[j]);
     const uint32_t flags = hp->flags, nseq = hp->nseq;
     if ((flags & kJLit) || nseq == 0) continue;
@@ -1409,14 +1420,13 @@ __global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
       err = kZCorrupt;
     } else {
       const int llg = logs & 0xff, ofg = (logs >> 8) & 0xff, mlg = (logs >> 16) & 0xff;
-      const uint64_t *tll = reinterpret_cast<const uint64_t *>(tok8 + tab_off), *tml = tll + (1 << llg);
-      const uint32_t *tof = reinterpret_cast<const uint32_t *>(tml + (1 << mlg));
-      uint64_t *raw = reinterpret_cast<uint64_t *>(tok8 + raw_off);
+      const uint32_t *tll = reinterpret_cast<const uint32_t *>(tok8 + tab_off), *tml = tll + (1 << llg);
+      const uint32_t *tof = tml + (1 << mlg);
+      uint4 *raw = reinterpret_cast<uint4 *>(tok8 + raw_off);
       uint32_t sll = r.read(llg), sof = r.read(ofg), sml = r.read(mlg);
-      for (uint32_t i = 0; i < nseq; i++) {
-        const uint64_t cll = tll[sll], cml = tml[sml];
-        const uint32_t cof = tof[sof];
-        const uint32_t cl = (uint32_t)cll, cm = (uint32_t)cml;
+      uint32_t i = 0;
+      for (; i < nseq; i++) {
+        const uint32_t cl = tll[sll], cm = tml[sml], cof = tof[sof];
         const uint32_t llc = cl & 0xff, mlc = cm & 0xff, ofc = cof & 0xff;
         if (llc > 35 || mlc > 52 || ofc > 31) {
           err = kZCorrupt;
@@ -1426,8 +1436,8 @@ __global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
           err = kZSlow;
           break;
         }
+        const uint32_t mlx = codes.ml[mlc], llx = codes.ll[llc];
         const uint32_t ofv = (1u << ofc) + r.read((int)ofc);
-        const uint32_t mlx = (uint32_t)(cml >> 32), llx = (uint32_t)(cll >> 32);
         const uint32_t ml = (mlx & 0xFFFFFFu) + r.read((int)(mlx >> 24));
         const uint32_t ll = (llx & 0xFFFFFFu) + r.read((int)(llx >> 24));
         if (i + 1 < nseq) {
@@ -1439,9 +1449,20 @@ __global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
           err = kZCorrupt;
           break;
         }
-        raw[i] = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
+        st[i & (kZStage - 1)] = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
+        if ((i & (kZStage - 1)) == kZStage - 1) {  // 16 entries (raw + 16 i is 16-aligned)
+          const uint4 *sv = reinterpret_cast<const uint4 *>(st);
+          uint4 *dv = raw + (i & ~(uint32_t)(kZStage - 1)) / 2;
+#pragma unroll
+          for (int k = 0; k < kZStage / 2; k++) dv[k] = sv[k];
+        }
       }
-      if (!err && !r.exact()) err = kZCorrupt;
+      if (!err) {  // the partial last burst
+        const uint32_t g = nseq & ~(uint32_t)(kZStage - 1);
+        uint64_t *dr = reinterpret_cast<uint64_t *>(raw);
+        for (uint32_t k = g; k < nseq; k++) dr[k] = st[k & (kZStage - 1)];
+        if (!r.exact()) err = kZCorrupt;
+      }
     }
     hp->err = err;
   }
@@ -1449,16 +1470,12 @@ __global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
 
 // ---------------------------------------------------------------- k_zstd_fix
 // In file order, one wave per recordio block: every job's raw sequences 64 at
-// a time -- repeat offsets resolved in order (scalar), the serial decoder's
+// a time -- repeat offsets resolved by a wave scan of history ops, the serial decoder's
 // per-sequence checks made lane-parallel from prefix sums (literals left,
 // offset within the frame's output), execution entries written -- then the
 // frame checks (content size), then the frame walk's own error if it stopped
 // early. The result: entries for k_zstd_exec, an error, the exact size for
 // the host's retry, or the serial path.
-__device__ __forceinline__ uint32_t zrl(uint32_t v, uint32_t lane) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
-}
-
 __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long long *nblocks) {
   const int l = lane_id();
   uint8_t *tok8 = reinterpret_cast<uint8_t *>(d.tok);
@@ -1524,37 +1541,60 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
           const uint64_t rv = v ? raw[g0 + l] : 0ull;
           const uint32_t ll = (uint32_t)rv & 0x1FFFFu, ml = (uint32_t)(rv >> 17) & 0x3FFFFu;
           const uint32_t ofv = (uint32_t)(rv >> 35);
-          // repeat offsets, in order
-          uint32_t off = 0;
-          for (uint32_t f = 0; f < cnt; f++) {
-            const uint32_t fo = zrl(ofv, f), fl = zrl(ll, f);
-            uint32_t o;
-            if (fo > 3) {
-              o = fo - 3;
-              rep2 = rep1;
-              rep1 = rep0;
-              rep0 = o;
-            } else {
-              const uint32_t idx = fo + (fl == 0 ? 1u : 0u);
-              if (idx == 1) {
-                o = rep0;
-              } else if (idx == 2) {
-                o = rep1;
-                rep1 = rep0;
-                rep0 = o;
-              } else if (idx == 3) {
-                o = rep2;
-                rep2 = rep1;
-                rep1 = rep0;
-                rep0 = o;
-              } else {  // o == 0 is the error below
-                o = rep0 - 1;
-                rep2 = rep1;
-                rep1 = rep0;
-                rep0 = o;
-              }
+          // Repeat offsets: a sequence maps the offset history (rep0, rep1, rep2)
+          // by an op "slot k <- slot src_k + c_k, or the constant c_k when
+          // src_k = 3" (RFC 8878 3.1.2.5); an inclusive scan of the composed ops
+          // gives each sequence the history after it, whose slot 0 is its offset.
+          uint32_t src, c0, c1 = 0, c2 = 0;
+          {
+            const uint32_t idx = ofv > 3 ? 0u : ofv + (ll == 0 ? 1u : 0u);
+            if (!v || idx == 1) {  // offset = rep0, history unchanged
+              src = 0u | (1u << 2) | (2u << 4);
+              c0 = 0;
+            } else if (idx == 0) {  // a new offset
+              src = 3u | (0u << 2) | (1u << 4);
+              c0 = ofv - 3;
+            } else if (idx == 2) {
+              src = 1u | (0u << 2) | (2u << 4);
+              c0 = 0;
+            } else if (idx == 3) {
+              src = 2u | (0u << 2) | (1u << 4);
+              c0 = 0;
+            } else {  // rep0 - 1 (0 is the error below)
+              src = 0u | (0u << 2) | (1u << 4);
+              c0 = ~0u;
             }
-            if ((uint32_t)l == f) off = o;
+          }
+#pragma unroll
+          for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t fs = (uint32_t)__shfl_up((int)src, dd), f0 = (uint32_t)__shfl_up((int)c0, dd),
+                           f1 = (uint32_t)__shfl_up((int)c1, dd), f2 = (uint32_t)__shfl_up((int)c2, dd);
+            if (l >= dd) {  // this lane's op after the earlier lanes' (g o f)
+              uint32_t ns = 0, nc[3];
+              const uint32_t cc[3] = {c0, c1, c2};
+#pragma unroll
+              for (int k = 0; k < 3; k++) {
+                const uint32_t gs = (src >> (2 * k)) & 3u;
+                const uint32_t fsel = gs == 0 ? f0 : (gs == 1 ? f1 : f2);
+                ns |= (gs == 3 ? 3u : (fs >> (2 * gs)) & 3u) << (2 * k);
+                nc[k] = gs == 3 ? cc[k] : fsel + cc[k];
+              }
+              src = ns;
+              c0 = nc[0];
+              c1 = nc[1];
+              c2 = nc[2];
+            }
+          }
+          auto apply = [&](uint32_t sk, uint32_t ck) {
+            return sk == 3 ? ck : (sk == 0 ? rep0 : (sk == 1 ? rep1 : rep2)) + ck;
+          };
+          const uint32_t off = apply(src & 3u, c0);
+          {  // the history after the group (lanes past cnt hold the identity)
+            const uint32_t ls = zrl(src, 63), l0 = zrl(c0, 63), l1 = zrl(c1, 63), l2 = zrl(c2, 63);
+            const uint32_t n0 = apply(ls & 3u, l0), n1 = apply((ls >> 2) & 3u, l1), n2 = apply((ls >> 4) & 3u, l2);
+            rep0 = n0;
+            rep1 = n1;
+            rep2 = n2;
           }
           // z_exec's checks per sequence: literals left, offset within the frame's output
           const uint32_t lin = wave_incl_sum_dpp(v ? ll : 0u), tin = wave_incl_sum_dpp(v ? ll + ml : 0u);
@@ -1885,7 +1925,8 @@ void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long
   uint64_t g = max_blocks < grid ? max_blocks : grid;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(k_zstd_ent, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
-  hipLaunchKernelGGL(k_zstd_seq, dim3((unsigned)(grid / kZWaves * kZSeqWaves)), dim3(64), 0, st, d);
+  static const int seq_wpc = getenv("RIO_ZSEQ_WPC") ? atoi(getenv("RIO_ZSEQ_WPC")) : kZSeqWaves;
+  hipLaunchKernelGGL(k_zstd_seq, dim3((unsigned)(grid / kZWaves * seq_wpc)), dim3(64), 0, st, d);
   uint64_t g3 = grid / kZWaves * kZFixWaves;
   if (g3 > max_blocks) g3 = max_blocks;
   if (g3 < 1) g3 = 1;
