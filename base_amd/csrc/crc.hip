@@ -28,7 +28,10 @@
 
 namespace rio {
 
-constexpr int kCrcWaves = 16;  // waves per workgroup (one workgroup per CU: 156 KiB LDS)
+#ifndef RIO_CRC_WAVES
+#define RIO_CRC_WAVES 16
+#endif
+constexpr int kCrcWaves = RIO_CRC_WAVES;  // waves per workgroup (one workgroup per CU: 156 KiB LDS at 32 copies)
 
 __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
   uint32_t p = 0;
@@ -57,8 +60,8 @@ __device__ __forceinline__ void fold_row(const char *__restrict__ tab, uint32_t 
   for (int k = 0; k < 4; k++) {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const uint32_t a = (((d[k] >> (8 * j)) & 0xffu) << 7) | lb;
-      t[k][j] = *reinterpret_cast<const uint32_t *>(tab + j * 32768 + a);
+      const uint32_t a = (((d[k] >> (8 * j)) & 0xffu) << kFoldShift) | lb;
+      t[k][j] = *reinterpret_cast<const uint32_t *>(tab + j * (256 * 4 * kFoldCopies) + a);
     }
   }
 #pragma unroll
@@ -132,7 +135,7 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
   }
   __syncthreads();
   const int l = lane_id();
-  const uint32_t lb = (uint32_t)(l & 31) << 2;
+  const uint32_t lb = (uint32_t)(l & (kFoldCopies - 1)) << 2;
   const char *tab = reinterpret_cast<const char *>(s_fold);
   const bool fold = !(ca.flags & 1);
   const uint64_t nwaves = (uint64_t)gridDim.x * kCrcWaves;

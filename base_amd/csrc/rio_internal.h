@@ -209,7 +209,11 @@ struct ResolveArgs {
 
 // ---- host helpers: GF(2) arithmetic of the reflected CRC-32 polynomial ----
 constexpr uint32_t kPoly = 0xEDB88320u;
-constexpr int kFoldCopies = 32;                  // bank-private replicas of each fold table
+#ifndef RIO_FOLD_COPIES
+#define RIO_FOLD_COPIES 32
+#endif
+constexpr int kFoldCopies = RIO_FOLD_COPIES;     // bank-private replicas of each fold table
+constexpr int kFoldShift = kFoldCopies == 32 ? 7 : (kFoldCopies == 16 ? 6 : 5);  // log2(4 * copies)
 constexpr int kFoldWords = 4 * 256 * kFoldCopies;  // 128 KiB
 constexpr int kMulTables = 7;                    // x^-32, then x^-(128*2^l), l = 0..5
 uint32_t gf_mul(uint32_t a, uint32_t b);         // a*b mod P (reflected; 1 = 0x80000000)
