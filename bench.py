@@ -81,6 +81,54 @@ def pmc_traffic(kernel: str, replicas: int):
     return int(e.get("fetch_bytes", 0) + e.get("write_bytes", 0))
 
 
+def _shard_worker(args):
+    """One core of the all-cores CPU baseline: NewShardScanner(start=i, limit=i+1,
+    nshard=n) over the file, repeated for `budget_s` (v2_test.go:483-509 shape)."""
+    data_path, i, n, budget_s = args
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    with open(data_path, "rb") as f:
+        data = f.read()
+    t0 = time.perf_counter()
+    items = passes = 0
+    while True:
+        k, _ = O.scan_count(data, i, i + 1, n)
+        assert k >= 0
+        items += k
+        passes += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    return passes, items, time.perf_counter() - t0
+
+
+def cpu_baseline_all_cores(data: bytes, budget_s: float = 8.0):
+    """The C oracle on every host core this process may use (at most 16, the GPU
+    box's CPU share): one shard per core, each core rescanning its shard."""
+    import tempfile
+    from concurrent.futures import ProcessPoolExecutor
+    from oracle import oracle as O
+    O.build()
+    try:
+        ncores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        ncores = os.cpu_count() or 1
+    ncores = max(1, min(ncores, 16))
+    with tempfile.NamedTemporaryFile(suffix=".rio", delete=False) as f:
+        f.write(data)
+        path = f.name
+    try:
+        with ProcessPoolExecutor(max_workers=ncores) as ex:
+            res = list(ex.map(_shard_worker, [(path, i, ncores, budget_s) for i in range(ncores)]))
+    finally:
+        os.unlink(path)
+    # each core covers 1/ncores of the file per pass
+    gib = sum(p * len(data) / ncores for p, _, _ in res) / 2 ** 30
+    wall = max(t for _, _, t in res)
+    return {"value": round(gib / wall, 3), "unit": "GiB/s", "cores": ncores, "kind": "port",
+            "sample": "C2 1x file split into %d shards (NewShardScanner shape), C oracle, one process per "
+                      "core, %.0f s" % (ncores, budget_s)}
+
+
 def cpu_baseline(data: bytes, budget_s: float = 10.0):
     """The C oracle (restatement of recordio.NewScanner's loop) on one host core."""
     from oracle import oracle as O
@@ -274,6 +322,7 @@ def main():
         out["c4_zstd"] = c4_zstd(args, local, world, dist)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(data)
+        out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(data)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
