@@ -16,7 +16,13 @@
 namespace rio {
 
 constexpr uint32_t kNoBlockId = 0xffffffffu;
-constexpr int kBatch = 4;  // blocks per wave iteration: their loads are issued together
+#ifndef RIO_PARSE_BATCH
+#define RIO_PARSE_BATCH 4
+#endif
+#ifndef RIO_PARSE_GRID
+#define RIO_PARSE_GRID 2048
+#endif
+constexpr int kBatch = RIO_PARSE_BATCH;  // blocks per wave iteration: their loads are issued together
 
 __device__ __forceinline__ Payload desc_payload(const uint8_t *span, const DevBufs &d, uint64_t c0,
                                                 unsigned long long meta, unsigned long long len) {
@@ -453,7 +459,7 @@ static inline unsigned grid_of(uint64_t n, unsigned per, unsigned cap) {
 }
 
 void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_parse, dim3(grid_of(max_blocks, 4 * kBatch, 2048)), dim3(256), 0, st, d, a);
+  hipLaunchKernelGGL(k_parse, dim3(grid_of(max_blocks, 4 * kBatch, RIO_PARSE_GRID)), dim3(256), 0, st, d, a);
 }
 
 void launch_parse_slow(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {

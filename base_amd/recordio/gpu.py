@@ -21,7 +21,7 @@ from .format import Uint
 from .writer import ItemLocation
 
 _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_ROOT, "lib", "librio_gpu.so")
+LIB_PATH = os.environ.get("RIO_GPU_LIB") or os.path.join(_ROOT, "lib", "librio_gpu.so")  # (override: experiments)
 
 RIO_CODEC_NONE, RIO_CODEC_FLATE, RIO_CODEC_ZSTD = 0, 1, 2
 RIO_STOP_MORE, RIO_STOP_EOF, RIO_STOP_ERROR = 0, 1, 2
