@@ -69,6 +69,43 @@ void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned l
   hipLaunchKernelGGL(k_codec_unsupported, dim3(grid_blocks(max_blocks)), dim3(256), 0, st, d, nblocks_dev);
 }
 
+// ---------------------------------------------------------------- host results
+// The valid blocks' decoded bytes gathered back to back (16-aligned) and their
+// item views rebased, so that a host result (rio_scan_span) copies only record
+// bytes back over PCIe, not the decode regions with their slack.
+__global__ void k_compact_len(DevBufs d, const unsigned long long *nblocks_dev, unsigned long long *padded) {
+  const uint64_t nb = *nblocks_dev, nv = d.ctl->n_valid_blocks;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x)
+    padded[b] = b < nv ? (d.blk_out_len[b] + 15) & ~15ull : 0ull;
+}
+
+__global__ void __launch_bounds__(256) k_compact(DevBufs d, const unsigned long long *nblocks_dev) {
+  const uint64_t nv = d.ctl->n_valid_blocks;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const int l = __lane_id();
+  if (wave == 0 && l == 0) d.ctl->rec_bytes = d.blk_coff[nv];
+  for (uint64_t b = wave; b < nv; b += nwaves) {
+    const uint64_t off = d.blk_dec_off[b], co = d.blk_coff[b], n = d.blk_out_len[b];
+    const uint4 *src = reinterpret_cast<const uint4 *>(d.dec + off);  // regions are 256-aligned
+    uint4 *dst = reinterpret_cast<uint4 *>(d.cmp + co);
+    for (uint64_t k = l; k < (n + 15) / 16; k += 64) dst[k] = src[k];
+    for (uint64_t i = d.blk_item_base[b] + l; i < d.blk_item_base[b + 1]; i += 64) {
+      const unsigned long long v = d.item_off[i];
+      if (v & kItemInRecords) d.item_off[i] = kItemInRecords | ((v & ~kItemInRecords) - off + co);
+    }
+  }
+}
+
+void launch_compact(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_compact_len, dim3(grid_blocks(max_blocks)), dim3(256), 0, st, d, nblocks_dev,
+                     d.blk_coff + max_blocks + 1);
+  launch_block_scan(d.blk_coff + max_blocks + 1, d.blk_coff, d.scan_tmp, nblocks_dev, max_blocks, st);
+  unsigned g = (unsigned)((max_blocks + 3) / 4);
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(k_compact, dim3(g < 1 ? 1 : g), dim3(256), 0, st, d, nblocks_dev);
+}
+
 // libzstd's error names (ZSTD_getErrorName) for codec_zstd.hip's ZErr codes
 static const char *const kZstdErrNames[] = {
     "",

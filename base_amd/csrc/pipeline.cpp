@@ -40,6 +40,7 @@ void launch_resolve(const DevBufs &d, const ResolveArgs &a, hipStream_t st);
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
                 hipStream_t st);
 // codec.hip
+void launch_compact(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
                           uint32_t factor, hipStream_t st);
 void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks_dev,
@@ -79,6 +80,7 @@ struct rio_ctx {
   hipEvent_t ev[kNumEv] = {};
   hipEvent_t evA = nullptr, evB = nullptr;  // stream hand-offs (no timing)
   bool last_had_dec = false;
+  bool last_cmp = false;  // the last host result's records are the compacted blocks (d.cmp)
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
   uint64_t side_cap = 0, item_cap = 0, dec_cap = 0;
   uint32_t dec_factor = 8;  // first-attempt decode-region bound: compressed bytes x this
@@ -125,7 +127,7 @@ static int alloc_bufs(rio_ctx *c) {
   if (dalloc(&d.blk_c0, nb) || dalloc(&d.blk_meta, nb) || dalloc(&d.blk_len, nb) || dalloc(&d.blk_nitems, nb) ||
       dalloc(&d.blk_hdr, nb) || dalloc(&d.blk_item_base, nb + 1) || dalloc(&d.blk_status, nb) ||
       dalloc(&d.blk_a, nb) || dalloc(&d.blk_b, nb) || dalloc(&d.blk_out_len, nb) || dalloc(&d.blk_dec_off, nb + 1) ||
-      dalloc(&d.blk_need, nb) || dalloc(&d.fl, nb))
+      dalloc(&d.blk_need, nb) || dalloc(&d.fl, nb) || dalloc(&d.blk_coff, 2 * (nb + 1)))
     return -1;
   if (dalloc(&d.scan_tmp, (n + 2047) / 2048 + 16) || dalloc(&d.strad, n)) return -1;
   if (dalloc(&d.item_off, c->item_cap) || dalloc(&d.item_len, c->item_cap) || dalloc(&d.side, c->side_cap))
@@ -136,7 +138,7 @@ static int alloc_bufs(rio_ctx *c) {
 static void free_all(rio_ctx *c) {
   DevBufs &d = c->d;
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
-                d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.item_off, d.item_len, d.side,
+                d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.cmp, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span};
   for (void *p : ps)
@@ -346,7 +348,7 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
   out->stop = (int32_t)k.stop_kind;
   out->span = span;
   if (k.stop_kind == 2) rio_fill_error(k, file_off, mode, &out->err);
-  const uint8_t *d_records = (codec == RIO_CODEC_NONE) ? c->d.side : c->d.dec;
+  const uint8_t *d_records = (codec == RIO_CODEC_NONE) ? c->d.side : (c->last_cmp ? c->d.cmp : c->d.dec);
   const uint64_t nb = k.n_valid_blocks;
   if (!to_host) {
     out->records = d_records;
@@ -477,6 +479,20 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
   if (getenv("RIO_DEBUG")) debug_dump(c);
   float ms = 0;
   hipEventElapsedTime(&ms, c->ev[kEvStart], c->ev[kEvEnd]);
+  // host results of a compressed codec: only the decoded record bytes cross PCIe
+  c->last_cmp = false;
+  if (to_host && codec != RIO_CODEC_NONE && c->h_ctl->out_overflow == 0 && c->h_ctl->n_valid_blocks > 0 &&
+      c->h_ctl->rec_bytes > 0) {
+    if (c->d.cmp_cap < c->h_ctl->rec_bytes + 64) {
+      if (dalloc(&c->d.cmp, c->h_ctl->rec_bytes + 64)) return -1;
+      c->d.cmp_cap = c->h_ctl->rec_bytes + 64;
+    }
+    launch_compact(c->d, c->nblocks_dev, nchunks ? nchunks : 1, c->st);
+    HIP_OK(hipMemcpyAsync(&c->h_ctl->rec_bytes, &c->d.ctl->rec_bytes, sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, c->st));
+    HIP_OK(hipStreamSynchronize(c->st));
+    c->last_cmp = true;
+  }
   if (collect(c, report_span, file_off, codec, mode, nbytes, out, to_host)) return -1;
   out->kernel_ms = ms;
   if (c->h_ctl->out_overflow) {  // still short after the retries: report that, not what it garbled

@@ -148,6 +148,7 @@ struct DevBufs {
   unsigned long long *blk_out_len;    // decoded length (compressed codecs)
   unsigned long long *blk_dec_off;    // offset of the block's decoded bytes in dec (n + 1)
   unsigned long long *blk_need;       // decoded size found by the exact pass after a region overflow
+  unsigned long long *blk_coff;       // host results: compact offsets of the decoded blocks (n + 1), then a scratch (n + 1)
   // outputs: item views into the span or the records buffer (side / dec)
   unsigned long long *item_off, *item_len;
   uint8_t *side;        // straddling items (none codec)
@@ -155,6 +156,8 @@ struct DevBufs {
   // scratch
   unsigned long long *scan_tmp;  // tile partials
   uint8_t *dec;                  // decoded blocks (compressed codecs)
+  uint8_t *cmp;                  // host results: the valid blocks' decoded bytes back to back
+  uint64_t cmp_cap;
   uint64_t dec_cap;              // bytes at dec
   FlState *fl;                   // per block (flate)
   uint32_t *tok;                 // flate tokens: block b's region starts at blk_c0[b] * kTokPerChunk
