@@ -141,17 +141,3 @@ void codec_error_text(uint64_t code, uint64_t off, uint64_t file_off, rio_error 
 }
 
 }  // namespace rio
-
-int rio_decode_block_codec(rio_ctx *ctx, const uint8_t *const *payloads, const uint32_t *lens, int n,
-                           int32_t codec, uint8_t *scratch, uint64_t cap, uint64_t *out_len, rio_error *err) {
-  (void)ctx;
-  (void)payloads;
-  (void)lens;
-  (void)n;
-  (void)codec;
-  (void)scratch;
-  (void)cap;
-  *out_len = 0;
-  if (err) rio_set_error(err, RIO_ERR_ARG, 0, "codec not supported by this build");
-  return RIO_ERR_ARG;
-}

@@ -2,8 +2,9 @@
 // (include/rio_gpu.h). One rio_ctx = one device, two HIP streams, buffers sized
 // at rio_open and grown only when a span needs more.
 //
-// Launch order per span (one stream; RIO_TWO_STREAMS=1 puts the parse path on
-// a second stream beside k_crc, which only pays when k_crc leaves CU room):
+// Launch order per span (one stream; an ablation build with -DRIO_TWO_STREAMS=1
+// puts the parse path on a second stream beside k_crc, which only pays when
+// k_crc leaves CU room):
 //   memsets, k_chunk_meta, chunk scans, [codec decode],
 //   block scan (item slots), k_parse, straddler scan, k_strad   (parse path)
 //   k_crc (streams every chunk byte), k_resolve
@@ -72,10 +73,35 @@ static void set_last_error(const char *fmt, ...) {
 
 enum { kEvStart, kEvScans, kEvDec, kEvCrc0, kEvCrc1, kEvParse0, kEvParse1, kEvEnd, kNumEv };
 
+// Pinned host copies of one span's results (records, item views, block table).
+// Each owner -- the ctx for rio_scan_span, every rio_scanner for its batches,
+// a scanner's trailer read -- has its own, so results of one never alias
+// another's (the reference's scanners share no state).
+struct rio_results {
+  uint8_t *records = nullptr;
+  uint64_t records_cap = 0;
+  unsigned long long *items = nullptr;  // off | len
+  uint64_t items_cap = 0;
+  unsigned long long *blk = nullptr;  // first_item (n+1) | file_off (n)
+  uint64_t blk_cap = 0;
+  void release() {
+    if (records) hipHostFree(records);
+    if (items) hipHostFree(items);
+    if (blk) hipHostFree(blk);
+    *this = rio_results();
+  }
+};
+
+rio_results *rio_results_new() { return new rio_results(); }
+void rio_results_free(rio_results *r) {
+  if (!r) return;
+  r->release();
+  delete r;
+}
+
 struct rio_ctx {
   int device = 0;
   int ncu = 256;
-  int kernel_flags = 0;  // RIO_KERNEL_FLAGS (measurement only): 1 no CRC fold, 2 no parse path, 4 no CRC
   hipStream_t st = nullptr, st2 = nullptr;
   hipEvent_t ev[kNumEv] = {};
   hipEvent_t evA = nullptr, evB = nullptr;  // stream hand-offs (no timing)
@@ -88,14 +114,10 @@ struct rio_ctx {
   DevBufs d{};
   unsigned long long *nblocks_dev = nullptr;
   uint8_t *d_span = nullptr;  // staging for host spans (lazy)
-  // pinned host results (lazy, grown on demand)
-  Ctl *h_ctl = nullptr;
-  uint8_t *h_records = nullptr;
-  uint64_t h_records_cap = 0;
-  unsigned long long *h_items = nullptr;  // off | len
-  uint64_t h_items_cap = 0;
-  unsigned long long *h_blk = nullptr;  // first_item (n+1) | file_off (n)
-  uint64_t h_blk_cap = 0;
+  Ctl *h_ctl = nullptr;  // pinned copy of the control block
+  rio_results res;       // host results of rio_scan_span (scanners bring their own)
+  uint8_t *h_stage = nullptr;  // pinned staging of rio_decode_block's chunk stream
+  uint64_t h_stage_cap = 0;
   // last async call
   uint64_t last_nchunks = 0, last_file_off = 0, last_in_bytes = 0;
   int32_t last_codec = 0, last_mode = 0;
@@ -144,9 +166,8 @@ static void free_all(rio_ctx *c) {
   for (void *p : ps)
     if (p) hipFree(p);
   if (c->h_ctl) hipHostFree(c->h_ctl);
-  if (c->h_records) hipHostFree(c->h_records);
-  if (c->h_items) hipHostFree(c->h_items);
-  if (c->h_blk) hipHostFree(c->h_blk);
+  c->res.release();
+  if (c->h_stage) hipHostFree(c->h_stage);
   for (hipEvent_t e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->evA) hipEventDestroy(c->evA);
@@ -161,7 +182,6 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, c->device));
   c->ncu = prop.multiProcessorCount;
-  if (const char *f = getenv("RIO_KERNEL_FLAGS")) c->kernel_flags = atoi(f);
   // test hook: a small flate token region per block and round forces the
   // yield / resume path across rounds (and the host retry with more rounds)
   if (const char *f = getenv("RIO_FL_TOKCAP")) c->d.tok_limit = strtoull(f, nullptr, 10);
@@ -176,8 +196,7 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   c->item_cap = (cfg && cfg->max_items) ? cfg->max_items : span / 64 + 1024;
   c->dec_cap = 0;
   HIP_OK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-  const char *two = getenv("RIO_TWO_STREAMS");
-  if (two && atoi(two)) HIP_OK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
+  if (RIO_TWO_STREAMS) HIP_OK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
   else c->st2 = c->st;
   for (hipEvent_t &e : c->ev) HIP_OK(hipEventCreate(&e));
   HIP_OK(hipEventCreateWithFlags(&c->evA, hipEventDisableTiming));
@@ -271,6 +290,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   DevBufs &d = c->d;
   hipStream_t st = c->st, st2 = c->st2;
   c->last_nchunks = nchunks;
+  c->last_cmp = false;  // records are d.dec / d.side until a host result compacts them
   HIP_OK(hipEventRecord(c->ev[kEvStart], st));
   // control words are min-reduced: reset to ~0 (out_overflow to 0)
   HIP_OK(hipMemsetAsync(d.ctl, 0xff, 4 * sizeof(unsigned long long), st));
@@ -306,7 +326,9 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   // parse path on st2, beside the CRC stream on st
   HIP_OK(hipStreamWaitEvent(st2, c->evA, 0));
   HIP_OK(hipEventRecord(c->ev[kEvParse0], st2));
-  const bool run_parse = !(c->kernel_flags & 2), run_crc = !(c->kernel_flags & 4);
+  // the shipped library always runs every stage; RIO_ABLATE (a -D of ablation
+  // builds, tools/ablate.py) drops stages for measurement only
+  const bool run_parse = !(RIO_ABLATE & 2) && mode != kModeRaw, run_crc = !(RIO_ABLATE & 4) && mode != kModeRaw;
   if (nchunks > 0 && run_parse) {
     ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap, sparse, 0};
     if (codec != RIO_CODEC_NONE) launch_dec_nitems(d, c->nblocks_dev, max_blocks, st2);
@@ -325,19 +347,21 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   HIP_OK(hipEventRecord(c->evB, st2));
   HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
   if (nchunks > 0 && run_crc) {
-    CrcArgs ca{c->kernel_flags, 0};
+    CrcArgs ca{RIO_ABLATE, 0};
     launch_crc(span, nchunks, d, ca, c->ncu, st);
   }
   HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
   HIP_OK(hipStreamWaitEvent(st, c->evB, 0));
-  ResolveArgs ra{span, nchunks, is_file_end, tail_partial, mode, codec, c->nblocks_dev, limit_chunk, sparse, 0};
-  launch_resolve(d, ra, st);
+  if (mode != kModeRaw) {
+    ResolveArgs ra{span, nchunks, is_file_end, tail_partial, mode, codec, c->nblocks_dev, limit_chunk, sparse, 0};
+    launch_resolve(d, ra, st);
+  }
   HIP_OK(hipEventRecord(c->ev[kEvEnd], st));
   return 0;
 }
 
 static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t codec, int32_t mode,
-                   uint64_t in_bytes, rio_batch *out, bool to_host) {
+                   uint64_t in_bytes, rio_batch *out, rio_results *res) {
   const Ctl &k = *c->h_ctl;
   memset(out, 0, sizeof(*out));
   out->in_bytes = in_bytes;
@@ -350,7 +374,7 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
   if (k.stop_kind == 2) rio_fill_error(k, file_off, mode, &out->err);
   const uint8_t *d_records = (codec == RIO_CODEC_NONE) ? c->d.side : (c->last_cmp ? c->d.cmp : c->d.dec);
   const uint64_t nb = k.n_valid_blocks;
-  if (!to_host) {
+  if (!res) {  // device results
     out->records = d_records;
     out->item_off = reinterpret_cast<const uint64_t *>(c->d.item_off);
     out->item_len = reinterpret_cast<const uint64_t *>(c->d.item_len);
@@ -359,27 +383,28 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
     return 0;
   }
   // host copies of the valid prefix: item views, block table, straddlers / decoded bytes
-  if (c->h_records_cap < k.rec_bytes + 16) {
-    if (c->h_records) hipHostFree(c->h_records);
-    c->h_records = nullptr;
-    c->h_records_cap = k.rec_bytes + k.rec_bytes / 4 + 4096;
-    HIP_OK(hipHostMalloc((void **)&c->h_records, c->h_records_cap, hipHostMallocDefault));
+  rio_results &r = *res;
+  if (r.records_cap < k.rec_bytes + 16) {
+    if (r.records) hipHostFree(r.records);
+    r.records = nullptr;
+    r.records_cap = k.rec_bytes + k.rec_bytes / 4 + 4096;
+    HIP_OK(hipHostMalloc((void **)&r.records, r.records_cap, hipHostMallocDefault));
   }
-  if (c->h_items_cap < k.n_items + 1) {
-    if (c->h_items) hipHostFree(c->h_items);
-    c->h_items = nullptr;
-    c->h_items_cap = k.n_items + k.n_items / 4 + 1024;
-    HIP_OK(hipHostMalloc((void **)&c->h_items, c->h_items_cap * 16, hipHostMallocDefault));
+  if (r.items_cap < k.n_items + 1) {
+    if (r.items) hipHostFree(r.items);
+    r.items = nullptr;
+    r.items_cap = k.n_items + k.n_items / 4 + 1024;
+    HIP_OK(hipHostMalloc((void **)&r.items, r.items_cap * 16, hipHostMallocDefault));
   }
-  if (c->h_blk_cap < 2 * (nb + 1)) {
-    if (c->h_blk) hipHostFree(c->h_blk);
-    c->h_blk = nullptr;
-    c->h_blk_cap = 2 * (nb + 1) + 2048;
-    HIP_OK(hipHostMalloc((void **)&c->h_blk, c->h_blk_cap * 8, hipHostMallocDefault));
+  if (r.blk_cap < 2 * (nb + 1)) {
+    if (r.blk) hipHostFree(r.blk);
+    r.blk = nullptr;
+    r.blk_cap = 2 * (nb + 1) + 2048;
+    HIP_OK(hipHostMalloc((void **)&r.blk, r.blk_cap * 8, hipHostMallocDefault));
   }
-  unsigned long long *h_off = c->h_items, *h_len = c->h_items + c->h_items_cap;
-  unsigned long long *first = c->h_blk, *foff = c->h_blk + nb + 1;
-  if (k.rec_bytes) HIP_OK(hipMemcpyAsync(c->h_records, d_records, k.rec_bytes, hipMemcpyDeviceToHost, c->st));
+  unsigned long long *h_off = r.items, *h_len = r.items + r.items_cap;
+  unsigned long long *first = r.blk, *foff = r.blk + nb + 1;
+  if (k.rec_bytes) HIP_OK(hipMemcpyAsync(r.records, d_records, k.rec_bytes, hipMemcpyDeviceToHost, c->st));
   if (k.n_items) {
     HIP_OK(hipMemcpyAsync(h_off, c->d.item_off, k.n_items * 8, hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipMemcpyAsync(h_len, c->d.item_len, k.n_items * 8, hipMemcpyDeviceToHost, c->st));
@@ -388,7 +413,7 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
   if (nb) HIP_OK(hipMemcpyAsync(foff, c->d.blk_c0, nb * 8, hipMemcpyDeviceToHost, c->st));
   HIP_OK(hipStreamSynchronize(c->st));
   for (uint64_t b = 0; b < nb; b++) foff[b] = file_off + foff[b] * kChunk;
-  out->records = c->h_records;
+  out->records = r.records;
   out->item_off = reinterpret_cast<const uint64_t *>(h_off);
   out->item_len = reinterpret_cast<const uint64_t *>(h_len);
   out->block_first_item = reinterpret_cast<const uint64_t *>(first);
@@ -452,7 +477,8 @@ static void debug_dump(rio_ctx *c) {
 
 static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span, uint64_t nbytes,
                     uint64_t file_off, int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode,
-                    bool to_host, rio_batch *out) {
+                    rio_results *res, rio_batch *out) {
+  const bool to_host = res != nullptr;
   HIP_OK(hipSetDevice(c->device));
   const uint64_t nchunks = nbytes / kChunk;
   const int tail_partial = (nbytes % kChunk) != 0;
@@ -493,7 +519,7 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
     HIP_OK(hipStreamSynchronize(c->st));
     c->last_cmp = true;
   }
-  if (collect(c, report_span, file_off, codec, mode, nbytes, out, to_host)) return -1;
+  if (collect(c, report_span, file_off, codec, mode, nbytes, out, res)) return -1;
   out->kernel_ms = ms;
   if (c->h_ctl->out_overflow) {  // still short after the retries: report that, not what it garbled
     memset(&out->err, 0, sizeof(out->err));
@@ -508,7 +534,7 @@ extern "C" int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbyt
   if (!ctx || !out) return -1;
   memset(out, 0, sizeof(*out));
   return run_span(ctx, (const uint8_t *)dev_span, (const uint8_t *)dev_span, nbytes, file_off, is_file_end,
-                  limit_off, codec, kModeBody, false, out);
+                  limit_off, codec, kModeBody, nullptr, out);
 }
 
 static int stage_span(rio_ctx *c, const uint8_t *span, uint64_t nbytes) {
@@ -518,7 +544,7 @@ static int stage_span(rio_ctx *c, const uint8_t *span, uint64_t nbytes) {
 }
 
 int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
-                       uint64_t limit_off, int32_t codec, int32_t mode, rio_batch *out) {
+                       uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res, rio_batch *out) {
   if (!ctx || !out) return -1;
   memset(out, 0, sizeof(*out));
   if (nbytes > ctx->max_span + kChunk) {
@@ -532,7 +558,8 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
   hipEventCreate(&t1);
   hipEventRecord(t0, ctx->st);
   if (stage_span(ctx, span, nbytes)) return -1;
-  const int rc = run_span(ctx, ctx->d_span, span, nbytes, file_off, is_file_end, limit_off, codec, mode, true, out);
+  const int rc = run_span(ctx, ctx->d_span, span, nbytes, file_off, is_file_end, limit_off, codec, mode,
+                          res ? res : &ctx->res, out);
   hipEventRecord(t1, ctx->st);
   hipEventSynchronize(t1);
   float ms = 0;
@@ -545,7 +572,7 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
 
 extern "C" int rio_scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
                              int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_batch *out) {
-  return rio_scan_span_mode(ctx, span, nbytes, file_off, is_file_end, limit_off, codec, kModeBody, out);
+  return rio_scan_span_mode(ctx, span, nbytes, file_off, is_file_end, limit_off, codec, kModeBody, nullptr, out);
 }
 
 extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, uint64_t file_off,
@@ -579,7 +606,7 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
   float ms = 0;
   hipEventElapsedTime(&ms, ctx->ev[kEvStart], ctx->ev[kEvEnd]);
   if (collect(ctx, ctx->last_span, ctx->last_file_off, ctx->last_codec, ctx->last_mode, ctx->last_in_bytes, out,
-              false))
+              nullptr))
     return -1;
   out->kernel_ms = ms;
   if (ctx->h_ctl->out_overflow) {
@@ -603,15 +630,104 @@ extern "C" int rio_stage_times(rio_ctx *ctx, float *ms, int n) {
 }
 
 // TransformFunc analogue (recordio.go:12).
+//
+// none: idTransform, the concatenation of the payloads (registry.go:31-39).
+// flate / zstd (recordioflate.go:54-65, recordiozstd.go:67-78): the payload
+// views are laid out as one block of whole chunks in pinned staging -- the
+// chunk stream the codec kernels read, whose logical payload view is
+// recordioiov's gather over the slices (recordioiov.go:14-58) -- copied to the
+// device and run through the chunk scans and the codec stage alone (kModeRaw:
+// no CRC, no packed parse). The decoded block, varint header included, comes
+// back into scratch.
+static const uint8_t kPackedMagic[8] = {0x2e, 0x76, 0x47, 0xeb, 0x34, 0x07, 0x3c, 0x2e};  // magic.go:21
+
+static int decode_raw(rio_ctx *c, const uint8_t *const *payloads, const uint32_t *lens, int n, int32_t codec,
+                      uint8_t *scratch, uint64_t cap, uint64_t *out_len, rio_error *err) {
+  uint64_t total = 0;
+  for (int i = 0; i < n; i++) total += lens[i];
+  const uint64_t nch = total ? (total + kMaxPayload - 1) / kMaxPayload : 1;
+  const uint64_t nbytes = nch * kChunk;
+  if (nch > c->max_chunks) {
+    rio_set_error(err, RIO_ERR_CAPACITY, 0, "block of %" PRIu64 " bytes exceeds ctx capacity", total);
+    return RIO_ERR_CAPACITY;
+  }
+  if (c->h_stage_cap < nbytes) {
+    if (c->h_stage) hipHostFree(c->h_stage);
+    c->h_stage = nullptr;
+    c->h_stage_cap = 0;
+    HIP_OK(hipHostMalloc((void **)&c->h_stage, nbytes, hipHostMallocDefault));
+    c->h_stage_cap = nbytes;
+  }
+  int pi = 0;
+  uint32_t po = 0;  // position in payloads[pi]
+  for (uint64_t k = 0; k < nch; k++) {
+    uint8_t *ck = c->h_stage + k * kChunk;
+    const uint64_t left = total - k * (uint64_t)kMaxPayload;
+    const uint32_t sz = (uint32_t)(left < (uint64_t)kMaxPayload ? left : (uint64_t)kMaxPayload);
+    const uint32_t hdr[5] = {0u, 0u, sz, (uint32_t)nch, (uint32_t)k};  // crc flag size total index (chunk.go:31-53)
+    memcpy(ck, kPackedMagic, 8);
+    memcpy(ck + 8, hdr, sizeof(hdr));
+    uint32_t o = 0;
+    while (o < sz) {
+      while (pi < n && po >= lens[pi]) {
+        pi++;
+        po = 0;
+      }
+      const uint32_t m = (lens[pi] - po) < (sz - o) ? (lens[pi] - po) : (sz - o);
+      memcpy(ck + kChunkHdr + o, payloads[pi] + po, m);
+      o += m;
+      po += m;
+    }
+    memset(ck + kChunkHdr + sz, 0, kChunk - kChunkHdr - sz);
+  }
+  if (!c->d_span) HIP_OK(hipMalloc((void **)&c->d_span, c->max_span + kChunk));
+  HIP_OK(hipMemcpyAsync(c->d_span, c->h_stage, nbytes, hipMemcpyHostToDevice, c->st));
+  for (int attempt = 0; attempt < 4; attempt++) {
+    if (enqueue(c, c->d_span, nch, UINT64_MAX, 1, 0, codec, kModeRaw, false, attempt)) return -1;
+    HIP_OK(hipMemcpyAsync(c->h_ctl, c->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->st));
+    HIP_OK(hipStreamSynchronize(c->st));
+    const unsigned long long ov = c->h_ctl->out_overflow;
+    if (ov == 0) break;
+    if ((ov & 0x40) && ensure_dec(c, c->h_ctl->dec_need)) return -1;
+    if ((ov & 0x1000) && c->fl_rounds < 64) c->fl_rounds = c->fl_rounds * 2 > 64 ? 64 : c->fl_rounds * 2;
+  }
+  if (c->h_ctl->out_overflow) {
+    rio_set_error(err, RIO_ERR_CAPACITY, 0, "output capacity exceeded");
+    return RIO_ERR_CAPACITY;
+  }
+  unsigned long long st = 0, ea = 0, eb = 0, olen = 0, doff = 0;
+  HIP_OK(hipMemcpy(&st, c->d.blk_status, 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&ea, c->d.blk_a, 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&eb, c->d.blk_b, 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&olen, c->d.blk_out_len, 8, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&doff, c->d.blk_dec_off, 8, hipMemcpyDeviceToHost));
+  if (st == kBlkCodec) {
+    codec_error_text(ea, eb, 0, err);
+    *out_len = 0;
+    return err->code;
+  }
+  *out_len = olen;
+  if (olen > cap) {
+    rio_set_error(err, RIO_ERR_CAPACITY, 0, "scratch too small: need %" PRIu64, (uint64_t)olen);
+    return RIO_ERR_CAPACITY;
+  }
+  if (olen) HIP_OK(hipMemcpy(scratch, c->d.dec + doff, olen, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 extern "C" int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, const uint32_t *lens, int n,
                                 int32_t codec, uint8_t *scratch, uint64_t cap, uint64_t *out_len, rio_error *err) {
-  if (!ctx || (n > 0 && (!payloads || !lens)) || !out_len) return -1;
+  if (!ctx || n < 0 || (n > 0 && (!payloads || !lens)) || !out_len) return -1;
+  rio_error scratch_err;
+  if (!err) err = &scratch_err;
+  memset(err, 0, sizeof(*err));
+  *out_len = 0;
   uint64_t total = 0;
   for (int i = 0; i < n; i++) total += lens[i];
   if (codec == RIO_CODEC_NONE) {  // idTransform: concatenation (registry.go:31-39)
     *out_len = total;
     if (total > cap) {
-      if (err) rio_set_error(err, RIO_ERR_CAPACITY, 0, "scratch too small: need %" PRIu64, total);
+      rio_set_error(err, RIO_ERR_CAPACITY, 0, "scratch too small: need %" PRIu64, total);
       return RIO_ERR_CAPACITY;
     }
     uint64_t o = 0;
@@ -621,5 +737,10 @@ extern "C" int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, co
     }
     return 0;
   }
-  return rio_decode_block_codec(ctx, payloads, lens, n, codec, scratch, cap, out_len, err);
+  if (codec != RIO_CODEC_FLATE && codec != RIO_CODEC_ZSTD) {
+    rio_set_error(err, RIO_ERR_ARG, 0, "unknown codec %d", codec);
+    return RIO_ERR_ARG;
+  }
+  if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+  return decode_raw(ctx, payloads, lens, n, codec, scratch, cap, out_len, err);
 }

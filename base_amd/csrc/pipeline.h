@@ -5,14 +5,19 @@
 
 #include "rio_gpu.h"
 
+// Pinned host result buffers (pipeline.cpp); one per owner of a result.
+struct rio_results;
+rio_results *rio_results_new();
+void rio_results_free(rio_results *r);
+
 // decode one span already in host memory; mode: 0 body, 1 header block, 2 trailer
-// block, 3 the last chunk alone (size + CRC only)
+// block, 3 the last chunk alone (size + CRC only). Results land in *res (the
+// ctx's own when null) and stay valid until the next call with the same res.
 int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
-                       int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode, rio_batch *out);
+                       int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res,
+                       rio_batch *out);
 uint64_t rio_ctx_max_span(rio_ctx *c);
 extern "C" void rio_set_error(rio_error *e, int32_t code, uint64_t file_off, const char *fmt, ...);
-int rio_decode_block_codec(rio_ctx *ctx, const uint8_t *const *payloads, const uint32_t *lens, int n,
-                           int32_t codec, uint8_t *scratch, uint64_t cap, uint64_t *out_len, rio_error *err);
 
 namespace rio {
 struct DevBufs;

@@ -52,7 +52,18 @@ enum CodecErr : uint32_t {
   kCodecPending = 255,    // (internal) left to k_inflate_exact
 };
 
-enum Mode : int32_t { kModeBody = 0, kModeHeader = 1, kModeTrailer = 2, kModeLastChunk = 3 };
+// kModeRaw: rio_decode_block (TransformFunc analogue): chunk headers, scans and
+// the codec only -- no CRC, no packed parse, no resolve.
+enum Mode : int32_t { kModeBody = 0, kModeHeader = 1, kModeTrailer = 2, kModeLastChunk = 3, kModeRaw = 4 };
+
+// Ablation builds only (tools/ablate.py compiles with -DRIO_ABLATE=n): 1 no CRC
+// fold, 2 no parse path, 4 no CRC. The shipped library is built with 0.
+#ifndef RIO_ABLATE
+#define RIO_ABLATE 0
+#endif
+#ifndef RIO_TWO_STREAMS
+#define RIO_TWO_STREAMS 0
+#endif
 
 // Control block written by the kernels, read back by the host (one copy).
 struct Ctl {
@@ -194,7 +205,7 @@ struct ParseArgs {
   int32_t pad;
 };
 struct CrcArgs {
-  int32_t flags;  // measurement-only ablations (RIO_KERNEL_FLAGS): 1 no CRC fold
+  int32_t flags;  // RIO_ABLATE of ablation builds (1 no CRC fold); 0 in the shipped library
   int32_t pad;
 };
 struct ResolveArgs {

@@ -149,9 +149,11 @@ struct rio_scanner {
   int32_t codec = RIO_CODEC_NONE;
   // ChunkScanner position
   uint64_t off = 0, limit = UINT64_MAX;
-  // current batch
-  uint8_t *span = nullptr;  // pinned host staging
+  // current batch: the span (pinned host staging; none-codec items are views
+  // into it) and the result buffers, both owned by this scanner
+  uint8_t *span = nullptr;
   uint64_t span_cap = 0;
+  rio_results *res = nullptr;
   rio_batch batch{};
   bool have_batch = false;
   bool done = false;  // no further batches (EOF or error)
@@ -194,23 +196,26 @@ struct rio_scanner {
     *st = (got == n) ? 0 : (got == 0 ? 1 : 2);
     return got;
   }
-  int ensure_span(uint64_t n) {
-    if (span_cap >= n) return 0;
-    if (span) hipHostFree(span);
-    span = nullptr;
-    if (hipHostMalloc((void **)&span, n, hipHostMallocDefault) != hipSuccess) return -1;
-    span_cap = n;
+  static int ensure_buf(uint8_t **buf, uint64_t *cap, uint64_t n) {
+    if (*cap >= n) return 0;
+    if (*buf) hipHostFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    if (hipHostMalloc((void **)buf, n, hipHostMallocDefault) != hipSuccess) return -1;
+    *cap = n;
     return 0;
   }
-  // read [at, at+n) and decode it on the GPU
-  int decode(uint64_t at, uint64_t n, int32_t cdc, int32_t mode, uint64_t lim, rio_batch *out) {
-    if (ensure_span(n ? n : 1)) {
+  // read [at, at+n) into *buf and decode it on the GPU into *rs
+  int decode_into(uint8_t **buf, uint64_t *cap, rio_results *rs, uint64_t at, uint64_t n, int32_t cdc, int32_t mode,
+                  uint64_t lim, rio_batch *out) {
+    if (ensure_buf(buf, cap, n ? n : 1)) {
+      memset(out, 0, sizeof(*out));
       rio_set_error(&out->err, RIO_ERR_HIP, at, "pinned allocation failed");
       out->stop = RIO_STOP_ERROR;
       return 0;
     }
     int st;
-    uint64_t got = read_full(span, n, at, &st);
+    uint64_t got = read_full(*buf, n, at, &st);
     if (st == 3) {
       memset(out, 0, sizeof(*out));
       rio_set_error(&out->err, RIO_ERR_IO, at, "read error at offset %" PRIu64, at + got);
@@ -218,7 +223,10 @@ struct rio_scanner {
       return 0;
     }
     const int is_end = (at + got >= file_size);
-    return rio_scan_span_mode(ctx, span, got, at, is_end, lim, cdc, mode, out);
+    return rio_scan_span_mode(ctx, *buf, got, at, is_end, lim, cdc, mode, rs, out);
+  }
+  int decode(uint64_t at, uint64_t n, int32_t cdc, int32_t mode, uint64_t lim, rio_batch *out) {
+    return decode_into(&span, &span_cap, res, at, n, cdc, mode, lim, out);
   }
 };
 
@@ -399,15 +407,15 @@ int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec,
     size_t len = sp ? (size_t)(sp - v) : strlen(v);
     if (len == 5 && strncmp(v, "flate", 5) == 0) c = RIO_CODEC_FLATE;
     else if (len == 4 && strncmp(v, "zstd", 4) == 0) c = RIO_CODEC_ZSTD;
-    else {
-      rio_set_error(err, RIO_ERR_TRANSFORMER, 0, "Transformer %s not found", v);
-      return RIO_ERR_TRANSFORMER;
+    else {  // not decoded here: the reference registry may hold it (registry.go:166)
+      rio_set_error(err, RIO_ERR_FALLBACK, 0, "Transformer %s not found", v);
+      return RIO_ERR_FALLBACK;
     }
     found++;
   }
-  if (found > 1) {
-    rio_set_error(err, RIO_ERR_ARG, 0, "transformer chains are not decoded on the GPU");
-    return RIO_ERR_ARG;
+  if (found > 1) {  // a chain, untransformed in reverse order (registry.go:121-146)
+    rio_set_error(err, RIO_ERR_FALLBACK, 0, "transformer chain of %d: decode with recordio.NewScanner", found);
+    return RIO_ERR_FALLBACK;
   }
   *codec = c;
   return 0;
@@ -416,6 +424,7 @@ int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec,
 rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int limit, int nshard) {
   rio_scanner *s = new rio_scanner();
   s->ctx = ctx;
+  s->res = rio_results_new();
   s->r = *r;
   s->file_size = r->size < 0 ? 0 : (uint64_t)r->size;
   // NewShardScanner (scannerv2.go:211-235)
@@ -456,6 +465,10 @@ int rio_scanner_scan(rio_scanner *s) {
   for (;;) {
     if (s->have_batch && s->item < s->batch.n_items) {
       const rio_batch &b = s->batch;
+      // a sticky error set meanwhile (Trailer, Seek) ends the scan at the end of
+      // the current block: the reference only re-checks it in scanNextBlock
+      // (scannerv2.go:363-368, 390-395)
+      if (s->err_set && s->item >= b.block_first_item[s->blk + 1]) return 0;
       while (s->item >= b.block_first_item[s->blk + 1]) s->blk++;
       const uint64_t first = b.block_first_item[s->blk];
       s->cur = batch_item(b, s->item, &s->cur_len);
@@ -512,7 +525,10 @@ int rio_scanner_header_kv(rio_scanner *s, int i, const char **key, int32_t *type
   return 1;
 }
 
-// Trailer (scannerv2.go:316-342) + ReadLastBlock (chunk.go:380-407)
+// Trailer (scannerv2.go:316-342) + ReadLastBlock (chunk.go:380-407). The
+// trailer is read into its own staging and result buffers, so the current
+// batch -- and the scan position -- are untouched, like the reference's
+// deferred Seek(curOff) (scannerv2.go:320-321).
 int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len) {
   if (!s || s->error_scanner || !has_trailer(s)) return 0;
   if (s->err_set) return 0;
@@ -520,10 +536,21 @@ int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len) {
     s->set_errf(RIO_ERR_TRAILER, 0, "bytes.Reader.Seek: negative position");
     return 0;
   }
+  uint8_t *tspan = nullptr;
+  uint64_t tcap = 0;
+  rio_results *tres = rio_results_new();
+  struct Cleanup {
+    uint8_t *&p;
+    rio_results *r;
+    ~Cleanup() {
+      if (p) hipHostFree(p);
+      rio_results_free(r);
+    }
+  } cleanup{tspan, tres};
   const uint64_t last = s->file_size - kCk;
   rio_batch b;
   // the last chunk alone: its size/CRC first (readChunk), then its magic
-  if (s->decode(last, kCk, RIO_CODEC_NONE, 3, UINT64_MAX, &b) != 0) {
+  if (s->decode_into(&tspan, &tcap, tres, last, kCk, RIO_CODEC_NONE, 3, UINT64_MAX, &b) != 0) {
     s->set_errf(RIO_ERR_HIP, last, "%s", rio_last_error());
     return 0;
   }
@@ -556,7 +583,7 @@ int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len) {
       return 0;
     }
   }
-  if (s->decode(start, s->file_size - start, s->codec, 2, UINT64_MAX, &b) != 0) {
+  if (s->decode_into(&tspan, &tcap, tres, start, s->file_size - start, s->codec, 2, UINT64_MAX, &b) != 0) {
     s->set_errf(RIO_ERR_HIP, start, "%s", rio_last_error());
     return 0;
   }
@@ -575,24 +602,18 @@ int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len) {
   uint64_t tlen = 0;
   const uint8_t *t0 = batch_item(b, 0, &tlen);
   s->trailer.assign(t0, t0 + tlen);
-  // The ctx buffers are shared with the scan batches: resume the scan at the
-  // block of the next undelivered item (the deferred Seek(curOff) of Trailer).
-  if (s->have_batch && s->item < s->batch.n_items) {
-    uint64_t bk = s->blk;
-    while (s->item >= s->batch.block_first_item[bk + 1]) bk++;
-    s->off = s->batch.block_file_off[bk];
-    s->skip = s->item - s->batch.block_first_item[bk];
-    s->done = false;
-    s->pending_set = false;
-  }
-  s->have_batch = false;
   *data = s->trailer.data();
   *len = s->trailer.size();
   return 1;
 }
 
 void rio_scanner_seek(rio_scanner *s, uint64_t block, int64_t item) {
-  if (!s || s->error_scanner || s->err_set) return;
+  if (!s || s->error_scanner) return;
+  if (s->err_set) {  // scanNextBlock clears rawItems, then fails on the sticky error
+    s->have_batch = false;
+    s->cur = nullptr;
+    return;
+  }
   // Seek (scannerv2.go:348-361): restart at the block, skip `item` items
   s->have_batch = false;
   s->pending_set = false;
@@ -622,6 +643,7 @@ int rio_scanner_finish(rio_scanner *s, rio_error *err) {
   if (!s) return 0;
   int rc = rio_scanner_err(s, err);
   if (s->span) hipHostFree(s->span);
+  rio_results_free(s->res);
   delete s;
   return rc;
 }

@@ -25,6 +25,9 @@ LIB_PATH = os.environ.get("RIO_GPU_LIB") or os.path.join(_ROOT, "lib", "librio_g
 
 RIO_CODEC_NONE, RIO_CODEC_FLATE, RIO_CODEC_ZSTD = 0, 1, 2
 RIO_STOP_MORE, RIO_STOP_EOF, RIO_STOP_ERROR = 0, 1, 2
+RIO_ERR_CAPACITY = 98
+RIO_ERR_LEGACY = 20    # v1 file: the reference scanner decodes it (scannerv2.go:228-233)
+RIO_ERR_FALLBACK = 23  # transformer chain / name other than flate, zstd (registry.go:113-148)
 U64_MAX = (1 << 64) - 1
 ITEM_IN_RECORDS = 1 << 63  # RIO_ITEM_IN_RECORDS
 
@@ -207,6 +210,32 @@ class Context:
         n = self.L.rio_stage_times(self.h, ms, 5)
         return [float(ms[i]) for i in range(n)]
 
+    def decode_block(self, payloads, codec: int, cap: int = -1) -> bytes:
+        """rio_decode_block, the TransformFunc analogue (recordio.go:12): the
+        untransformed block of one block's chunk payloads. Raises RecordioError
+        with the codec's error (or RIO_ERR_CAPACITY when cap is too small)."""
+        n = len(payloads)
+        bufs = [(ctypes.c_char * max(len(p), 1)).from_buffer_copy(bytes(p) or b"\0") for p in payloads]
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(b) for b in bufs])
+        lens = (ctypes.c_uint32 * max(n, 1))(*[len(p) for p in payloads])
+        if cap < 0:
+            cap = max(64 << 10, 16 * sum(len(p) for p in payloads))
+        for _ in range(2):
+            scratch = ctypes.create_string_buffer(max(cap, 1))
+            olen = ctypes.c_uint64()
+            err = RioError()
+            rc = self.L.rio_decode_block(self.h, ptrs, lens, n, codec, scratch, cap, ctypes.byref(olen),
+                                         ctypes.byref(err))
+            if rc < 0:
+                raise RuntimeError("rio_decode_block: " + self.L.rio_last_error().decode())
+            if rc == RIO_ERR_CAPACITY and olen.value > cap:
+                cap = olen.value  # like scratch[:cap] too small in the reference: grow once
+                continue
+            if rc != 0:
+                raise _err(err)
+            return scratch.raw[:olen.value]
+        raise _err(err)
+
     def scan_device(self, dev_ptr: int, nbytes: int, file_off: int = 0, is_file_end: bool = True,
                     codec: int = RIO_CODEC_NONE) -> RioBatch:
         out = RioBatch()
@@ -319,7 +348,14 @@ class _FileReader:
 
 
 class Scanner:
-    """Mirror of the recordio.Scanner interface (scannerv2.go:120-161)."""
+    """Mirror of the recordio.Scanner interface (scannerv2.go:120-161).
+
+    Every scanner owns its staging and result buffers (the C scanner does), so
+    scanners sharing one Context never see each other's records. A file this
+    library does not decode -- v1 (RIO_ERR_LEGACY) or a transformer chain /
+    other registered transformer (RIO_ERR_FALLBACK) -- reports that code from
+    Err(); the Go shim hands such files to recordio.NewShardScanner
+    (INTEGRATION.md)."""
 
     def __init__(self, src, opts: ScannerOpts = None, start: int = 0, limit: int = 1, nshard: int = 1,
                  ctx: Optional[Context] = None):
@@ -356,6 +392,8 @@ class Scanner:
         return out
 
     def Scan(self) -> bool:
+        if self._err is not None:  # errors.Once: the first error is sticky (scannerv2.go:242)
+            return False
         if not self.L.rio_scanner_scan(self.h):
             return False
         p = ctypes.c_void_p()

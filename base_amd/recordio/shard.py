@@ -57,18 +57,22 @@ def ordered_prefix(n_items: int, n_bytes: int, group=None):
 
 
 def scan_rank(data, rank: int, world: int, k: int = 1,
-              scan: Callable = None, group=None):
+              scan: Callable = None, group=None, device: int = None):
     """Decode this rank's shard of one file and place it in file order.
 
     scan(data, start, limit, nshard) -> list of record bytes; by default the GPU
-    scanner (gpu.NewShardScanner on this rank's device). Returns (records,
+    scanner (gpu.NewShardScanner) on `device` -- this rank's LOCAL_RANK unless
+    given (several ranks may share one device, e.g. tests). Returns (records,
     item_offset, total_items)."""
     start, limit, nshard = rank_shard(rank, world, k)
     if scan is None:
+        import os
         from base_amd.recordio import gpu
+        dev = int(os.environ.get("LOCAL_RANK", "0")) if device is None else device
+        ctx = gpu.default_context(dev)
 
         def scan(d, s, l, n):
-            sc = gpu.NewShardScanner(d, gpu.ScannerOpts(), s, l, n)
+            sc = gpu.NewShardScanner(d, gpu.ScannerOpts(), s, l, n, ctx=ctx)
             out = []
             while sc.Scan():
                 out.append(sc.Get())

@@ -51,18 +51,25 @@ def c2_records() -> np.ndarray:
     return splitmix64(SEED, N_RECORDS * RECORD_SIZE // 8).view(np.uint8).reshape(N_RECORDS, RECORD_SIZE)
 
 
-def make_c2_file():
-    """C2 file bytes (header chunk + 3,953 two-chunk blocks) and the record count."""
+def make_c2_file(max_items: int = MAX_ITEMS):
+    """C2 file bytes (header chunk + 3,953 two-chunk blocks) and the record count.
+    max_items=16384 (the writer default, writerv2.go:28-29) gives the C1 file:
+    62 blocks of 130 chunks."""
     from base_amd.recordio import format as F
     recs = c2_records()
     out = [F.chunk_block(F.MAGIC_HEADER, F.packed_block_payload([F.marshal_header([])]))]
     # every block: uvarint(n) + n x uvarint(256) + n x 256 bytes (writerv2.go:388-441)
-    for b0 in range(0, N_RECORDS, MAX_ITEMS):
-        blk = recs[b0:b0 + MAX_ITEMS]
+    for b0 in range(0, N_RECORDS, max_items):
+        blk = recs[b0:b0 + max_items]
         hdr = F.put_uvarint(len(blk)) + F.put_uvarint(RECORD_SIZE) * len(blk)
         out.append(F.chunk_block(F.MAGIC_PACKED, hdr + blk.tobytes()))
     data = b"".join(out)
     return data, N_RECORDS
+
+
+def make_c1_file():
+    """C1 (configs[0]): the same records at the default MaxItems = 16384."""
+    return make_c2_file(16384)
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "r01_c2_pmc.json")

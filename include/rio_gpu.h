@@ -69,6 +69,10 @@ enum rio_err_code {
     RIO_ERR_LEGACY = 20,        /* v1 file: decode with the reference scanner  scannerv2.go:228 */
     RIO_ERR_IO = 21,            /* reader callback failed                      */
     RIO_ERR_LOCATION = 22,      /* "Invalid location %+v, block has only %d items" scannerv2.go:358 */
+    RIO_ERR_FALLBACK = 23,      /* transformers this library does not decode: a chain of several, or a
+                                   name other than flate/zstd (registry.go:113-148). Decode the file with
+                                   recordio.NewShardScanner; msg is the reference's text for the case the
+                                   name is not registered there either ("Transformer %s not found") */
     RIO_ERR_CAPACITY = 98,      /* span or output exceeds the ctx capacity      */
     RIO_ERR_HIP = 99,           /* HIP runtime failure                          */
 };
@@ -85,8 +89,8 @@ typedef struct rio_config {
     int32_t device;             /* HIP device ordinal */
     int32_t flags;              /* reserved, 0 */
     uint64_t max_span_bytes;    /* largest span per call (multiple of 32768); 0 = 256 MiB */
-    uint64_t max_out_bytes;     /* decoded-bytes capacity per call; 0 = 4 x max_span_bytes */
-    uint64_t max_items;         /* item-offset capacity per call; 0 = max_span_bytes / 16 */
+    uint64_t max_out_bytes;     /* straddler-bytes capacity per call (grown on demand); 0 = span/8 + 1 MiB */
+    uint64_t max_items;         /* item-view capacity per call (grown on demand); 0 = span/64 + 1024 */
 } rio_config;
 
 typedef struct rio_ctx rio_ctx;
@@ -142,8 +146,9 @@ void *rio_stream(rio_ctx *ctx);
 
 /* Transformer registry lookup (registry.go:113-148 + recordioflate/zstd Init):
  * resolves the header's "transformer" values to a codec. Returns 0 and sets
- * *codec, or RIO_ERR_TRANSFORMER ("Transformer %s not found") / RIO_ERR_ARG
- * (chains of several transformers are not decoded on the GPU). */
+ * *codec, or RIO_ERR_FALLBACK for a chain of several transformers or a name
+ * other than flate / zstd: the caller decodes such a file with the reference
+ * scanner, whose registry may hold user transformers (registry.go:166). */
 int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec, rio_error *err);
 
 /* ---- batch layer ----
@@ -172,8 +177,12 @@ int rio_sync(rio_ctx *ctx, rio_batch *out);
 int rio_stage_times(rio_ctx *ctx, float *ms, int n);
 
 /* TransformFunc analogue (recordio.go:12): untransform one block given its
- * chunk payload views; writes into scratch if it fits (returns the length in
- * *out_len), else returns RIO_ERR_CAPACITY with the needed size in *out_len. */
+ * chunk payload views (in order, any lengths; their concatenation is the
+ * transformed block). none concatenates on the host; flate / zstd decode on the
+ * GPU (recordioflate.go:54-65, recordiozstd.go:67-78). Writes into scratch if
+ * it fits and returns 0 with the length in *out_len; RIO_ERR_CAPACITY with the
+ * needed size in *out_len when it does not fit; the codec's error (code and
+ * the reference's text in *err) for a corrupt stream; < 0 on a runtime failure. */
 int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, const uint32_t *lens, int n,
                      int32_t codec, uint8_t *scratch, uint64_t cap, uint64_t *out_len,
                      rio_error *err);

@@ -42,12 +42,14 @@ def test_codec_registry_lookup(gpu_lib):
     assert look(["flate"])[:2] == (0, 1)
     assert look(["flate 5"])[:2] == (0, 1)
     assert look(["zstd -1"])[:2] == (0, 2)
+    # not decoded here -> RIO_ERR_FALLBACK (23): the shim's recordio.NewShardScanner
+    # decodes it, or reports the reference's own "not found" text
     rc, _, msg = look(["nonexistent 3"])
-    assert rc == 18 and msg == "Transformer nonexistent 3 not found"
+    assert rc == 23 and msg == "Transformer nonexistent 3 not found"
     rc, _, msg = look(["flatex"])
-    assert msg == "Transformer flatex not found"
-    rc, _, _ = look(["flate", "zstd"])
-    assert rc == 19
+    assert rc == 23 and msg == "Transformer flatex not found"
+    rc, _, _ = look(["flate", "zstd"])  # a chain: reverse-order untransform (registry.go:121-146)
+    assert rc == 23
 
 
 def test_struct_layouts_match_header(tmp_path):

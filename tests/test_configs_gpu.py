@@ -1,0 +1,216 @@
+"""BASELINE.json configs at full size on the GPU (pytest -m gpu), plus the
+reference's randomized sharding tests restated (recordio/v2_test.go:458-591).
+
+- C1 (configs[0]): 1M x 256 B at the writer's default MaxItems = 16384
+  (130-chunk blocks, 32 KiB varint headers: the general parser's path), every
+  record byte-exact against the generator and against the oracle's scan;
+- C4 (configs[3]): the zstd workload's base file (tools/c4_data.py: record sizes
+  log-uniform 64 B-64 KiB, >= 1 MiB blocks, level 5), records by SHA-256 and
+  lengths against the generator, a few blocks against the oracle;
+- TestRandomLargeWrites (v2_test.go:574-591): 100k records, 10 shards, and
+  nshard = 1e9 with stride 1e8: the shards concatenate to the input and the
+  largest holds 8,000 < n < 12,000 records -- bounds from the reference test;
+- TestV2Random-shaped cases (v2_test.go:544-572): up to 2,000 shards, none and
+  zstd, Seek to every record's ItemLocation.
+
+The reference generates its records with Go's math/rand; these use Python's
+random with the same shapes (lengths rnd.Intn(datasize)+1 of 'A'+Intn(64)
+characters, flush probability, trailer "Trailer"), so the bounds, not the exact
+byte streams, are the reference's.
+"""
+import ctypes
+import hashlib
+import io
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, oracle_has_zstd
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def _views_to_array(b, span, nrec, rec_len):
+    """Materialise a host batch of fixed-size records (rio_scan_span views)."""
+    off = np.ctypeslib.as_array(b.item_off, shape=(b.n_items,)).copy()
+    ln = np.ctypeslib.as_array(b.item_len, shape=(b.n_items,))
+    assert np.all(ln == rec_len)
+    side = np.frombuffer(ctypes.string_at(b.records, b.records_len), dtype=np.uint8) if b.records_len else None
+    in_rec = (off >> np.uint64(63)).astype(bool)
+    off = (off & np.uint64((1 << 63) - 1)).astype(np.int64)
+    ar = np.arange(rec_len, dtype=np.int64)
+    out = np.empty((nrec, rec_len), dtype=np.uint8)
+    for lo in range(0, nrec, 100000):
+        hi = min(nrec, lo + 100000)
+        idx = off[lo:hi, None] + ar
+        m = in_rec[lo:hi]
+        blk = np.empty((hi - lo, rec_len), dtype=np.uint8)
+        blk[~m] = span[idx[~m]]
+        if m.any():
+            blk[m] = side[idx[m]]
+        out[lo:hi] = blk
+    return out
+
+
+def test_full_size_c1(oracle):
+    """configs[0] at full size: 1,000,000 x 256 B, MaxItems 16384 -> 62 blocks of
+    130 chunks (last block 576 items in 5 chunks), SURVEY.md §8(a)."""
+    import bench
+    from base_amd.recordio import gpu
+    data, nrec = bench.make_c1_file()
+    assert len(data) == 260046848
+    ctx = gpu.Context(0, max_span_bytes=len(data) + 32768)
+    b = ctx.scan_span(data[32768:], file_off=32768, is_file_end=True)
+    assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
+    assert b.n_items == nrec and b.n_blocks == 62
+    first = np.ctypeslib.as_array(b.block_first_item, shape=(b.n_blocks + 1,)).astype(np.int64)
+    assert np.all(np.diff(first)[:-1] == 16384) and first[-1] - first[-2] == 576
+    span = np.frombuffer(data, dtype=np.uint8)[32768:]
+    got = _views_to_array(b, span, nrec, 256)
+    recs = bench.c2_records()
+    assert np.array_equal(got, recs)
+    ctx.close()
+    # the oracle reads the same file to the same records (and through the scanner API)
+    ref = oracle.scan(data)
+    assert ref.err == "" and len(ref.items) == nrec
+    assert b"".join(ref.items) == recs.tobytes()
+    sc = gpu.NewScanner(data, ctx=gpu.Context(0, max_span_bytes=64 << 20))
+    h = hashlib.sha256()
+    n = 0
+    while True:
+        got = sc.ScanBatch(1 << 16)
+        if not got:
+            break
+        for r in got:
+            h.update(r)
+        n += len(got)
+    assert sc.Finish() is None and n == nrec
+    assert h.hexdigest() == hashlib.sha256(recs.tobytes()).hexdigest()
+
+
+def test_c4_base_file(oracle):
+    """configs[3]'s base file through the device path and the scanner API."""
+    from base_amd.recordio import gpu
+    from base_amd.recordio.codecs import have_zstd
+    if not have_zstd() or not oracle_has_zstd(oracle):
+        pytest.skip("libzstd not present to write the fixture")
+    import c4_data
+    import torch
+    data, nblk, nrec, rec_bytes = c4_data.make_file(24 << 20)
+    want = c4_data.all_records(nblk)
+    assert len(want) == nrec and sum(map(len, want)) == rec_bytes
+    body = data[32768:]
+    dev = torch.frombuffer(bytearray(body), dtype=torch.uint8).to("cuda:0")
+    ctx = gpu.Context(0, max_span_bytes=len(body) + 32768)
+    b = ctx.scan_device(dev.data_ptr(), len(body), file_off=32768, is_file_end=True, codec=gpu.RIO_CODEC_ZSTD)
+    assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
+    got = gpu.device_batch_items(b, body)
+    assert [len(x) for x in got] == [len(x) for x in want]
+    assert hashlib.sha256(b"".join(got)).digest() == hashlib.sha256(b"".join(want)).digest()
+    ctx.close()
+    # a few blocks against the oracle, file-shaped (header + block)
+    hdr = data[:32768]
+    pos, blocks = 32768, []
+    while pos < len(data):
+        total = int.from_bytes(data[pos + 20:pos + 24], "little")
+        blocks.append(data[pos:pos + total * 32768])
+        pos += total * 32768
+    assert len(blocks) == nblk
+    for k in (0, nblk // 2, nblk - 1):
+        ref = oracle.scan(hdr + blocks[k])
+        assert ref.err == ""
+        sc = gpu.NewScanner(hdr + blocks[k])
+        items = []
+        while sc.Scan():
+            items.append(sc.Get())
+        assert sc.Finish() is None and items == ref.items
+
+
+def random_string(n, rnd):
+    return bytes(65 + rnd.randrange(64) for _ in range(n))
+
+
+def generate_random_recordio(rnd, flush_p, n_records, datasize, transformers=()):
+    """generateRandomRecordio (v2_test.go:458-481): KeyTrailer header, random
+    flushes, trailer "Trailer", the ItemLocation index of every record."""
+    from base_amd.recordio.writer import Writer, WriterOpts
+    buf = io.BytesIO()
+    index = {}
+    w = Writer(buf, WriterOpts(Transformers=list(transformers),
+                               Index=lambda loc, v: index.__setitem__(bytes(v), loc)))
+    w.AddHeader("trailer", True)
+    items = []
+    for _ in range(n_records):
+        d = random_string(rnd.randrange(datasize) + 1, rnd)
+        w.Append(d)
+        items.append(d)
+        if rnd.random() < flush_p:
+            w.Flush()
+    w.SetTrailer(b"Trailer")
+    w.Finish()
+    return buf.getvalue(), items, index
+
+
+def do_sharded_reads(data, stride, nshard, items, ctx):
+    """doShardedReads (v2_test.go:483-509): shards [s, s+stride) of nshard, each
+    with Trailer() == "Trailer"; returns the largest shard's record count."""
+    from base_amd.recordio import gpu
+    expected = list(items)
+    pos = 0
+    max_shard = 0
+    for shard in range(0, nshard, stride):
+        limit = min(shard + stride, nshard)
+        sc = gpu.NewShardScanner(data, gpu.ScannerOpts(), shard, limit, nshard, ctx=ctx)
+        assert sc.Trailer() == b"Trailer", (shard, nshard, sc.Err())
+        n = 0
+        while sc.Scan():
+            assert sc.Get() == expected[pos], (pos, shard, nshard)
+            pos += 1
+            n += 1
+        assert sc.Finish() is None
+        max_shard = max(max_shard, n)
+    assert pos == len(expected)
+    return max_shard
+
+
+def test_random_large_writes(gpu_ctx):
+    """TestRandomLargeWrites (v2_test.go:574-591)."""
+    rnd = random.Random(0)
+    data, items, _ = generate_random_recordio(rnd, 0.01, 100000, 1024)
+    m = do_sharded_reads(data, 1, 10, items, gpu_ctx)
+    assert 8000 < m < 12000, m
+    n = 1000000000  # a large absolute shard count: rounding of the float64 shard math
+    m = do_sharded_reads(data, n // 10, n, items, gpu_ctx)
+    assert 8000 < m < 12000, m
+
+
+@pytest.mark.parametrize("codec", ["", "zstd"])
+@pytest.mark.parametrize("flush_p,nshard,maxrecords,datasize", [
+    (0.001, 2000, 2000, 10 << 10),  # blocks big enough that shards straddle them
+    (0.1, 1000, 2000, 30),
+    (1.0, 3, 2000, 30),
+    (0.0, 2, 2000, 30),
+    (0.001, 2000, 1, 30),           # many shards, a single record
+    (0.001, 2000, 0, 30),           # an empty file
+])
+def test_v2_random(gpu_ctx, oracle, codec, flush_p, nshard, maxrecords, datasize):
+    """doRandomTest (v2_test.go:511-542) as TestV2Random runs it (544-572)."""
+    from base_amd.recordio import gpu
+    from base_amd.recordio.writer import ItemLocation
+    if codec == "zstd" and not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    rnd = random.Random(0)
+    n = rnd.randrange(maxrecords) + 1 if maxrecords > 0 else 0
+    data, items, index = generate_random_recordio(rnd, flush_p, n, datasize, [codec] if codec else [])
+    do_sharded_reads(data, 1, nshard, items, gpu_ctx)
+    sc = gpu.NewScanner(data, ctx=gpu_ctx)
+    for v in items[:300]:
+        loc = index[v]
+        sc.Seek(ItemLocation(loc.Block, loc.Item))
+        assert sc.Err() is None
+        assert sc.Scan() and sc.Get() == v
+    sc.Finish()

@@ -20,36 +20,41 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, data, k, q):
+def _worker(rank, world, port, data, k, q, on_gpu=False):
     import sys
     sys.path.insert(0, ROOT)
+    if on_gpu:
+        import torch  # noqa: F401  (one HIP runtime for torch and librio_gpu.so)
     import torch.distributed as dist
     from base_amd.recordio import shard
-    from oracle import oracle as O
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        def scan(d, s, l, n):
-            r = O.scan(d, s, l, n)
-            assert r.err == "", r.err
-            return r.items
-        recs, off, total = shard.scan_rank(data, rank, world, k, scan=scan)
+        if on_gpu:  # the default path: gpu.NewShardScanner on this rank's device (both on 0 here)
+            recs, off, total = shard.scan_rank(data, rank, world, k, device=0)
+        else:
+            from oracle import oracle as O
+
+            def scan(d, s, l, n):
+                r = O.scan(d, s, l, n)
+                assert r.err == "", r.err
+                return r.items
+            recs, off, total = shard.scan_rank(data, rank, world, k, scan=scan)
         q.put((rank, off, total, recs))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k", [1, 3])
-def test_two_ranks_reassemble_file_order(oracle, k):
+def _run_two_ranks(k, codec="", on_gpu=False):
     import torch.multiprocessing as mp
     from base_amd.recordio.writer import write_file, WriterOpts
     rng = random.Random(5 + k)
     recs = [bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 400))) for _ in range(3000)]
-    data = write_file(recs, WriterOpts(MaxItems=29))
+    data = write_file(recs, WriterOpts(MaxItems=29, Transformers=[codec] if codec else []))
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, data, k, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data, k, q, on_gpu)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(world)]
@@ -64,6 +69,19 @@ def test_two_ranks_reassemble_file_order(oracle, k):
     assert out == recs
     # the ranks' shards are disjoint and non-empty at this size
     assert all(len(g[3]) > 0 for g in got)
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_two_ranks_reassemble_file_order(oracle, k):
+    _run_two_ranks(k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,codec", [(1, ""), (3, "flate")])
+def test_two_ranks_gpu_scanner(gpu_lib, k, codec):
+    """shard.scan_rank's default path -- the GPU scanner -- on two gloo ranks
+    sharing device 0 (the 8-GPU bench gives each rank its own)."""
+    _run_two_ranks(k, codec, on_gpu=True)
 
 
 def test_rank_shard_and_file_assignment():

@@ -170,3 +170,25 @@ def test_writer_round_trips_through_oracle(oracle):
         data = write_file(recs, WriterOpts(Transformers=tr, MaxItems=rng.randrange(1, 60)), trailer=b"T")
         r = oracle.scan(data)
         assert r.err == "" and r.items == recs and r.trailer == b"T"
+
+
+def test_random_large_writes_bounds(oracle):
+    """TestRandomLargeWrites (recordio/v2_test.go:574-591) against the oracle:
+    100k records (lengths 1..1024, flush probability 0.01) in 10 shards, then
+    nshard = 1e9 with stride 1e8; the shards concatenate to the input and the
+    largest holds 8,000 < n < 12,000 records. The bounds are the reference's --
+    this pins the oracle's LimitShard (float64) math independently of itself."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_configs_gpu import generate_random_recordio
+    rnd = random.Random(0)
+    data, items, _ = generate_random_recordio(rnd, 0.01, 100000, 1024)
+    for nshard, stride in ((10, 1), (1000000000, 100000000)):
+        got, biggest = [], 0
+        for s in range(0, nshard, stride):
+            r = oracle.scan(data, s, min(s + stride, nshard), nshard)
+            assert r.err == "" and r.trailer == b"Trailer"
+            got += r.items
+            biggest = max(biggest, len(r.items))
+        assert got == items
+        assert 8000 < biggest < 12000, (nshard, biggest)

@@ -22,7 +22,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 
 step smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 480 python -m pytest tests -x -q -m gpu ${PYTEST_ARGS}
+step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:---maxfail=8}
 if [ -n "$ABLATE" ]; then
   step ablate 300 python tools/ablate.py
 fi
