@@ -18,9 +18,9 @@ Prints ONE JSON line (rank 0).
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
-import platform
 import sys
 import time
 
@@ -88,81 +88,26 @@ def pmc_traffic(kernel: str, replicas: int):
     return int(e.get("fetch_bytes", 0) + e.get("write_bytes", 0))
 
 
-def _shard_worker(args):
-    """One core of the all-cores CPU baseline: NewShardScanner(start=i, limit=i+1,
-    nshard=n) over the file, repeated for `budget_s` (v2_test.go:483-509 shape)."""
-    data_path, i, n, budget_s = args
-    sys.path.insert(0, ROOT)
-    from oracle import oracle as O
-    with open(data_path, "rb") as f:
-        data = f.read()
-    t0 = time.perf_counter()
-    items = passes = 0
-    while True:
-        k, _ = O.scan_count(data, i, i + 1, n)
-        assert k >= 0
-        items += k
-        passes += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    return passes, items, time.perf_counter() - t0
+REHEARSE = os.environ.get("RIO_BENCH_REHEARSE") == "1"  # N ranks on one GPU over gloo (rehearsal only)
 
 
-def cpu_baseline_all_cores(data: bytes, budget_s: float = 8.0):
-    """The C oracle on every host core this process may use (at most 16, the GPU
-    box's CPU share): one shard per core, each core rescanning its shard."""
-    import tempfile
-    from concurrent.futures import ProcessPoolExecutor
-    from oracle import oracle as O
-    O.build()
-    try:
-        ncores = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        ncores = os.cpu_count() or 1
-    ncores = max(1, min(ncores, 16))
-    with tempfile.NamedTemporaryFile(suffix=".rio", delete=False) as f:
-        f.write(data)
-        path = f.name
-    try:
-        with ProcessPoolExecutor(max_workers=ncores) as ex:
-            res = list(ex.map(_shard_worker, [(path, i, ncores, budget_s) for i in range(ncores)]))
-    finally:
-        os.unlink(path)
-    # each core covers 1/ncores of the file per pass
-    gib = sum(p * len(data) / ncores for p, _, _ in res) / 2 ** 30
-    wall = max(t for _, _, t in res)
-    return {"value": round(gib / wall, 3), "unit": "GiB/s", "cores": ncores, "kind": "port",
-            "sample": "C2 1x file split into %d shards (NewShardScanner shape), C oracle, one process per "
-                      "core, %.0f s" % (ncores, budget_s)}
+def coll_dev(local):
+    """Device of the collectives' tensors: the rank's GPU under RCCL, the CPU under gloo."""
+    return "cpu" if REHEARSE else f"cuda:{local}"
 
 
-def cpu_baseline(data: bytes, budget_s: float = 10.0):
-    """The C oracle (restatement of recordio.NewScanner's loop) on one host core."""
-    from oracle import oracle as O
-    O.build()
-    t0 = time.perf_counter()
-    passes = 0
-    nbytes = 0
-    while True:
-        n, _ = O.scan_count(data)
-        assert n == N_RECORDS
-        passes += 1
-        nbytes += len(data)
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    cpu = platform.processor() or ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": round(nbytes / dt / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{passes} x C2 1x file ({len(data)} B, {N_RECORDS} records), C oracle "
-                      f"(oracle/scanner.c) single thread on {cpu}; the Go reference cannot be built here"}
+def cpu_baselines(args):
+    """cpu_baseline legs (rank 0, N=1 only; tools/cpu_base.py): the C2 file (the
+    headline's workload) and the C1 file (configs[0], the reference's own
+    CPU-runnable case: default MaxItems), one core and all cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import cpu_base
+    d2, n2 = make_c2_file()
+    one, allc = cpu_base.baselines(d2, 0, n2, "C2 1x file", args.cpu_s)
+    d1, n1 = make_c1_file()
+    c1_one, c1_all = cpu_base.baselines(d1, 0, n1, "C1 file", args.cpu_s)
+    return one, allc, {"config": "C1 (configs[0]): 1e6 x 256 B, MaxItems=16384", "cpu_baseline": c1_one,
+                       "cpu_baseline_all_cores": c1_all}
 
 
 def c3_flate(args, local, world, dist):
@@ -173,11 +118,11 @@ def c3_flate(args, local, world, dist):
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_flate
-    cpu_s = 8.0 if (world == 1 and not args.no_cpu_baseline) else 0.0
+    cpu_s = args.cpu_s if (world == 1 and not args.no_cpu_baseline) else 0.0
     r = bench_flate.run_c3(replicas=args.flate_replicas, steps=max(2, min(args.steps, 5)), warmup=1,
                            device=local, check=True, cpu_s=cpu_s)
     if dist is not None:
-        t = torch.tensor([r["ms_per_step"]], device=f"cuda:{local}", dtype=torch.float64)
+        t = torch.tensor([r["ms_per_step"]], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item())
         r["value"] = round(r["config"]["span_bytes"] * world / (ms * 1e-3) / 2 ** 30, 2)
@@ -198,11 +143,11 @@ def c4_zstd(args, local, world, dist):
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_zstd
-    cpu_s = 6.0 if (world == 1 and not args.no_cpu_baseline) else 0.0
+    cpu_s = args.cpu_s if (world == 1 and not args.no_cpu_baseline) else 0.0
     r = bench_zstd.run_c4(replicas=args.zstd_replicas, steps=max(2, min(args.steps, 3)), warmup=1, device=local,
                           check=True, cpu_s=cpu_s)
     if dist is not None:
-        t = torch.tensor([r["ms_per_step"]], device=f"cuda:{local}", dtype=torch.float64)
+        t = torch.tensor([r["ms_per_step"]], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item())
         r["value"] = round(r["config"]["span_bytes"] * world / (ms * 1e-3) / 2 ** 30, 2)
@@ -213,6 +158,130 @@ def c4_zstd(args, local, world, dist):
     return r
 
 
+def c5_flate(args, local, rank, world, dist):
+    """BASELINE.json configs[4]: 1024 trailer-indexed flate files (64 MiB of C3
+    records each, tools/c5_data.py) over the ranks -- files assigned by
+    size-balanced greedy assignment (shard.assign_files), every rank's files
+    device-resident, decoded as batches of whole file bodies back to back (block
+    ranges from each file's trailer index). Strong scaling: the 1024 files are
+    fixed as N grows; value = all files' bytes / max time over ranks. No record
+    byte crosses xGMI; the one collective is the ordered-output prefix (RCCL)."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import c5_data
+    from base_amd.recordio import gpu, shard
+    cache = os.path.join(args.c5_cache, "rio_c5_%d" % (c5_data.FILE_RECORD_BYTES >> 20))
+    os.makedirs(cache, exist_ok=True)
+    t0 = time.perf_counter()
+    for k in range(c5_data.N_BASE):  # bases generated in parallel across ranks, cached on the host
+        path = os.path.join(cache, "base%d.rio" % k)
+        if k % world == rank and not os.path.exists(path):
+            data, nrec, rec_bytes, offsets = c5_data.make_base(k, workers=16 if world == 1 else 4)
+            with open(path + ".tmp", "wb") as f:
+                f.write(data)
+            with open(path + ".json", "w") as f:
+                json.dump({"nrec": nrec, "rec_bytes": rec_bytes}, f)
+            os.replace(path + ".tmp", path)
+    if dist is not None:
+        dist.barrier()
+    bases, metas = [], []
+    for k in range(c5_data.N_BASE):
+        path = os.path.join(cache, "base%d.rio" % k)
+        with open(path, "rb") as f:
+            bases.append(f.read())
+        with open(path + ".json") as f:
+            metas.append(json.load(f))
+    gen_s = time.perf_counter() - t0
+    # each file's block index (its trailer item; parsed on the host at open time)
+    spans = []
+    for k, data in enumerate(bases):
+        sc = gpu.NewScanner(data, ctx=gpu.default_context(local))
+        offs = c5_data.parse_index(sc.Trailer())
+        assert sc.Finish() is None and len(offs) == -(-metas[k]["nrec"] // c5_data.PER_BLOCK)
+        spans.append((offs[0], shard.trailer_offset(data)))
+    sizes = [len(bases[f % c5_data.N_BASE]) for f in range(c5_data.N_FILES)]
+    mine = shard.assign_files(sizes, world)[rank]
+    body_len = [spans[k][1] - spans[k][0] for k in range(c5_data.N_BASE)]
+    # batches of whole file bodies, <= args.c5_batch_gib each
+    cap = int(args.c5_batch_gib * 2 ** 30)
+    batches, cur, cur_b = [], [], 0
+    for f in mine:
+        n = body_len[f % c5_data.N_BASE]
+        if cur and cur_b + n > cap:
+            batches.append(cur)
+            cur, cur_b = [], 0
+        cur.append(f)
+        cur_b += n
+    if cur:
+        batches.append(cur)
+    total = sum(body_len[f % c5_data.N_BASE] for f in mine)
+    dev = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{local}")
+    dbase = [torch.frombuffer(bytearray(bases[k][spans[k][0]:spans[k][1]]), dtype=torch.uint8).to(dev.device)
+             for k in range(c5_data.N_BASE)]
+    layout, pos = [], 0
+    for bt in batches:
+        lo = pos
+        for f in bt:
+            n = body_len[f % c5_data.N_BASE]
+            dev[pos:pos + n].copy_(dbase[f % c5_data.N_BASE])
+            pos += n
+        layout.append((lo, pos - lo, sum(metas[f % c5_data.N_BASE]["nrec"] for f in bt)))
+    del dbase
+    torch.cuda.synchronize()
+    biggest = max((n for _, n, _ in layout), default=0)
+    max_items = max((k for _, _, k in layout), default=0)
+    ctx = gpu.Context(local, max_span_bytes=max(biggest, 32768), max_items=max_items + 1024)
+    parity = None
+    if mine:  # the first file of this rank's first batch against the generator
+        f0 = batches[0][0] % c5_data.N_BASE
+        b = ctx.scan_device(dev.data_ptr(), body_len[f0], file_off=spans[f0][0], is_file_end=True,
+                            codec=gpu.RIO_CODEC_FLATE)
+        items = gpu.device_batch_items(b, bases[f0][spans[f0][0]:spans[f0][1]])
+        want = c5_data.base_records(f0)
+        parity = (b.err.code == 0 and len(items) == len(want)
+                  and hashlib.sha256(b"".join(items)).digest() == hashlib.sha256(b"".join(want)).digest())
+
+    def step():
+        n = 0
+        for lo, nbytes, nrec in layout:
+            ctx.scan_device_async(dev.data_ptr() + lo, nbytes, spans[0][0], gpu.RIO_CODEC_FLATE)
+            r = ctx.sync()
+            assert r.err.code == 0 and r.n_items == nrec, (r.err.msg, r.n_items, nrec)
+            n += r.n_items
+        return n
+
+    steps = max(1, min(args.steps, 3))
+    step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        n_items = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = (time.perf_counter() - t0) / steps
+    all_bytes = sum(sizes)
+    ok = bool(parity) if mine else True
+    if dist is not None:
+        t = torch.tensor([dt, 0.0 if ok else 1.0], device=coll_dev(local), dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, ok = float(t[0].item()), t[1].item() == 0.0
+        # the ordered-output prefix: where this rank's records land in the file-set order
+        shard.ordered_prefix(n_items, sum(metas[f % c5_data.N_BASE]["rec_bytes"] for f in mine))
+    ctx.close()
+    del dev
+    torch.cuda.empty_cache()
+    return {"metric": "recordio scan GiB/s device-resident (compressed in), C5 1024 trailer-indexed flate files",
+            "value": round(all_bytes / dt / 2 ** 30, 2), "unit": "GiB/s", "n_gpus": world,
+            "scaling": "strong", "ms_per_step": round(dt * 1e3, 3), "steps": steps, "parity": ok,
+            "config": {"files": c5_data.N_FILES, "file_record_bytes": c5_data.FILE_RECORD_BYTES,
+                       "records_per_block": c5_data.PER_BLOCK, "distinct_base_files": c5_data.N_BASE,
+                       "files_bytes_total": all_bytes, "files_this_rank": len(mine),
+                       "batches_this_rank": len(batches), "gen_s": round(gen_s, 1)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,17 +290,38 @@ def main():
     ap.add_argument("--replicas", type=int, default=REPLICAS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-flate", action="store_true", help="skip the C3 flate measurement (configs[2])")
-    ap.add_argument("--flate-replicas", type=int, default=80)
+    ap.add_argument("--flate-replicas", type=int, default=0, help="0: enough for 10 GiB of records")
     ap.add_argument("--no-zstd", action="store_true", help="skip the C4 zstd measurement (configs[3])")
-    ap.add_argument("--zstd-replicas", type=int, default=80)
+    ap.add_argument("--zstd-replicas", type=int, default=0, help="0: enough for 10 GiB of records")
+    ap.add_argument("--cpu-s", type=float, default=4.0, help="seconds per CPU-baseline measurement")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 many-file measurement (configs[4])")
+    ap.add_argument("--c5-batch-gib", type=float, default=4.0, help="file bodies per decode batch")
+    ap.add_argument("--c5-cache", default="/tmp", help="host directory caching the C5 base files")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start torchrun as a child before anything touches
+        # the GPU here, and exit with its status (never exec over this process)
+        import socket
+        import subprocess
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 and REHEARSE:  # every rank on GPU 0, collectives over gloo
+        import torch.distributed as dist
+        local = 0
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    elif world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -287,7 +377,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        t = torch.tensor([dt], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt / args.steps * 1e3
@@ -327,9 +417,10 @@ def main():
         out["c3_flate"] = c3_flate(args, local, world, dist)
     if not args.no_zstd:
         out["c4_zstd"] = c4_zstd(args, local, world, dist)
+    if not args.no_c5:
+        out["c5_flate"] = c5_flate(args, local, rank, world, dist)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(data)
-        out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(data)
+        out["cpu_baseline"], out["cpu_baseline_all_cores"], out["c1_cpu"] = cpu_baselines(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -20,7 +20,7 @@ _lib = None
 
 def build(force: bool = False) -> str:
     """Compile the oracle with its committed Makefile (gcc)."""
-    if force or not os.path.exists(_LIB_PATH):
+    if force or not os.path.exists(_LIB_PATH) or not os.path.exists(os.path.join(_HERE, "_build", "libcpuscan.so")):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH
 
@@ -187,6 +187,28 @@ def shard_range(file_size: int, off: int, start: int, limit: int, nshard: int):
     a, b = ctypes.c_int64(), ctypes.c_int64()
     L.orc_shard_range(file_size, off, start, limit, nshard, ctypes.byref(a), ctypes.byref(b))
     return a.value, b.value
+
+
+_CPU_PATH = os.path.join(_HERE, "_build", "libcpuscan.so")
+_cpu = None
+
+
+def cpu_scan(data: bytes, codec: int, nthreads: int = 1):
+    """CPU baseline (oracle/cpu_scan.c): the scan loop with zlib crc32 / zlib
+    inflate / libzstd, thread i scanning NewShardScanner(i, i+1, nthreads).
+    Returns (records, record bytes); records = -1 on any error."""
+    global _cpu
+    if _cpu is None:
+        if not os.path.exists(_CPU_PATH):
+            build(force=True)
+        L = ctypes.CDLL(_CPU_PATH)
+        L.cpu_scan.restype = ctypes.c_int64
+        L.cpu_scan.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                               ctypes.POINTER(ctypes.c_int64)]
+        _cpu = L
+    b = ctypes.c_int64()
+    n = _cpu.cpu_scan(data, len(data), codec, nthreads, ctypes.byref(b))
+    return n, b.value
 
 
 def scan_count(data: bytes, start: int = 0, limit: int = 1, nshard: int = 1):

@@ -95,3 +95,92 @@ def test_rank_shard_and_file_assignment():
     assert sorted(i for r in a for i in r) == list(range(len(sizes)))
     loads = [sum(sizes[i] for i in r) for r in a]
     assert sorted(loads, reverse=True) == [64, 45, 41]  # largest first onto the least-loaded rank
+
+
+def _split_worker(rank, world, port, data, q, on_gpu=False):
+    """scan_file_split on one rank: trailer index broadcast from rank 0, this
+    rank's block range decoded (GPU batch, or the oracle on CPU)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    if on_gpu:
+        import torch  # noqa: F401
+    import torch.distributed as dist
+    import c5_data
+    from base_amd.recordio import shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        hdr_end = int.from_bytes(data[20:24], "little") * 32768
+        if on_gpu:
+            from base_amd.recordio import gpu
+            ctx = gpu.Context(0, max_span_bytes=len(data))
+
+            def scan_range(lo, hi):
+                b = ctx.scan_span(data[lo:hi], file_off=lo, is_file_end=True, codec=gpu.RIO_CODEC_FLATE)
+                assert b.err.code == 0, b.err.msg
+                return gpu.batch_items(b)
+            read_trailer = None
+        else:
+            from oracle import oracle as O
+
+            def scan_range(lo, hi):
+                r = O.scan(data[:hdr_end] + data[lo:hi], read_trailer=False)
+                assert r.err == "", r.err
+                return r.items
+
+            def read_trailer(d):
+                return O.scan(d).trailer
+        recs, off, total = shard.scan_file_split(data, rank, world, c5_data.parse_index, scan_range,
+                                                 read_trailer=read_trailer)
+        q.put((rank, off, total, recs))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_split(world, on_gpu=False):
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import c5_data
+    data, nrec, _, offsets = c5_data.make_base(0, record_bytes=4 << 20, workers=4)
+    want = c5_data.base_records(0, record_bytes=4 << 20)
+    assert len(want) == nrec and len(offsets) == (nrec + 1023) // 1024
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, data, q, on_gpu)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out = [None] * nrec
+    for rank, off, total, part in got:
+        assert total == nrec and len(part) > 0
+        out[off:off + len(part)] = part
+    assert out == want
+
+
+def test_index_split_two_ranks(oracle):
+    """configs[4]'s single-file case: a trailer-indexed flate file split by its
+    block index over two gloo ranks (index broadcast, ordered prefix)."""
+    _run_split(2)
+
+
+def test_split_blocks_ranges():
+    from base_amd.recordio import shard
+    offs = [32768 * k for k in (1, 2, 5, 6, 7, 20)]
+    end = 32768 * 25
+    for world in (1, 2, 3, 7):
+        rs = [shard.split_blocks(offs, end, r, world) for r in range(world)]
+        assert rs[0][0] == offs[0] and rs[-1][1] == end
+        for (a, b), (c, d) in zip(rs, rs[1:]):
+            assert b == c  # contiguous, on block boundaries
+        assert all(lo in offs + [end] for lo, _ in rs)
+    assert shard.split_blocks([], end, 0, 2) == (end, end)
+
+
+@pytest.mark.gpu
+def test_index_split_two_ranks_gpu(gpu_lib):
+    _run_split(2, on_gpu=True)

@@ -22,26 +22,6 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def cpu_baseline_c3(data: bytes, nrec: int, budget_s: float = 8.0):
-    """The C oracle (oracle/scanner.c + oracle/inflate.c: recordio.NewScanner's loop
-    with Go-semantics inflate) on one host core over the C3 base file."""
-    sys.path.insert(0, ROOT)
-    from oracle import oracle as O
-    O.build()
-    t0 = time.perf_counter()
-    passes = 0
-    while True:
-        n, _ = O.scan_count(data)
-        assert n == nrec, (n, nrec)
-        passes += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(passes * len(data) / dt / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": "%d x C3 base file (%d B compressed, %d records), C oracle single thread; "
-                      "the Go reference cannot be built here" % (passes, len(data), nrec)}
-
-
 def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, warmup, device=0, check=True):
     """One compressed workload on cuda:`device`: the base file `data` copied to
     HBM, its body replicated `replicas` times; one step = the scan pipeline over
@@ -111,8 +91,18 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
         "parity": parity}
 
 
-def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0):
-    """The C3 workload on cuda:`device`; returns the measurement dict (no print)."""
+TARGET_RECORD_BYTES = 10 << 30  # configs[2]: 10 GiB of uncompressed records
+
+
+def replicas_for(rec_bytes: int) -> int:
+    """Replicas of the base file that reach >= 10 GiB of records."""
+    return -(-TARGET_RECORD_BYTES // rec_bytes)
+
+
+def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0):
+    """The C3 workload on cuda:`device` (replicas=0: enough for 10 GiB of records);
+    returns the measurement dict (no print). cpu_s > 0 adds the one-core and
+    all-core CPU baselines (zlib inflate) on the base file."""
     import c3_data
     from base_amd.recordio import gpu
 
@@ -126,22 +116,29 @@ def run_c3(base_mib=128, replicas=80, steps=5, warmup=1, per_block=1024, device=
             w.extend(c3_data.records(first, min(per_block, nrec - first)))
         return w
 
+    if replicas <= 0:
+        replicas = replicas_for(rec_bytes)
     res = measure(data, nrec, rec_bytes, want, gpu.RIO_CODEC_FLATE,
                   "C3-like flate FASTQ, %d records/block" % per_block, replicas, steps, warmup, device, check)
     res["config"]["gen_s"] = round(gen_s, 1)
-    res["cpu_baseline"] = cpu_baseline_c3(data, nrec, cpu_s) if cpu_s > 0 else None
+    if cpu_s > 0:
+        import cpu_base
+        res["cpu_baseline"], res["cpu_baseline_all_cores"] = cpu_base.baselines(
+            data, 1, nrec, "C3 base file", cpu_s)
     return dict({"metric": "recordio scan GiB/s device-resident (compressed in), flate"}, **res)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--base-mib", type=int, default=128)
-    ap.add_argument("--replicas", type=int, default=80)
+    ap.add_argument("--replicas", type=int, default=0, help="0: enough for 10 GiB of records")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--per-block", type=int, default=1024)
+    ap.add_argument("--cpu-s", type=float, default=0.0)
     args = ap.parse_args()
-    print(json.dumps(run_c3(args.base_mib, args.replicas, args.steps, args.warmup, args.per_block)), flush=True)
+    print(json.dumps(run_c3(args.base_mib, args.replicas, args.steps, args.warmup, args.per_block,
+                            cpu_s=args.cpu_s)), flush=True)
 
 
 if __name__ == "__main__":

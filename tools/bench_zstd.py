@@ -21,25 +21,6 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def cpu_baseline_c4(data: bytes, nrec: int, budget_s: float = 8.0):
-    """The C oracle (oracle/scanner.c + oracle/zstd_dec.c: recordio.NewScanner's
-    loop with an RFC 8878 restatement of ZSTD_decompress) on one host core."""
-    from oracle import oracle as O
-    O.build()
-    t0 = time.perf_counter()
-    passes = 0
-    while True:
-        n, _ = O.scan_count(data)
-        assert n == nrec, (n, nrec)
-        passes += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(passes * len(data) / dt / 2 ** 30, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": "%d x C4 base file (%d B compressed, %d records), C oracle single thread; "
-                      "the Go reference (DataDog/zstd = libzstd) cannot be built here" % (passes, len(data), nrec)}
-
-
 def load_or_make(base_mib, workers, path=None):
     """The C4 base file; with `path`, cached there (a profiled run loads it: libzstd
     cannot be called under rocprofv3, whose own zstd symbols interpose)."""
@@ -58,7 +39,9 @@ def load_or_make(base_mib, workers, path=None):
     return data, nblk, nrec, rec_bytes
 
 
-def run_c4(base_mib=128, replicas=80, steps=5, warmup=1, device=0, check=True, cpu_s=0.0, workers=16, data_path=None):
+def run_c4(base_mib=128, replicas=0, steps=5, warmup=1, device=0, check=True, cpu_s=0.0, workers=16, data_path=None):
+    """The C4 workload (replicas=0: enough for 10 GiB of records); cpu_s > 0 adds
+    the one-core and all-core CPU baselines (libzstd) on the base file."""
     import bench_flate
     import c4_data
     from base_amd.recordio import gpu
@@ -66,18 +49,23 @@ def run_c4(base_mib=128, replicas=80, steps=5, warmup=1, device=0, check=True, c
     t0 = time.perf_counter()
     data, nblk, nrec, rec_bytes = load_or_make(base_mib, workers, data_path)
     gen_s = time.perf_counter() - t0
+    if replicas <= 0:
+        replicas = bench_flate.replicas_for(rec_bytes)
     res = bench_flate.measure(data, nrec, rec_bytes, lambda: c4_data.all_records(nblk), gpu.RIO_CODEC_ZSTD,
                               "C4-like zstd level 5, records 64 B-64 KiB log-uniform, 1 MiB blocks",
                               replicas, steps, warmup, device, check)
     res["config"]["gen_s"] = round(gen_s, 1)
-    res["cpu_baseline"] = cpu_baseline_c4(data, nrec, cpu_s) if cpu_s > 0 else None
+    if cpu_s > 0:
+        import cpu_base
+        res["cpu_baseline"], res["cpu_baseline_all_cores"] = cpu_base.baselines(
+            data, 2, nrec, "C4 base file", cpu_s)
     return dict({"metric": "recordio scan GiB/s device-resident (compressed in), zstd"}, **res)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--base-mib", type=int, default=128)
-    ap.add_argument("--replicas", type=int, default=80)
+    ap.add_argument("--replicas", type=int, default=0, help="0: enough for 10 GiB of records")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-s", type=float, default=0.0)
