@@ -11,7 +11,8 @@ from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "base_amd", "csrc")
-OUT_DIR = os.path.join(ROOT, "base_amd", "lib")
+# RIO_BUILD_DIR: build an experiment variant elsewhere (load it with RIO_GPU_LIB)
+OUT_DIR = os.environ.get("RIO_BUILD_DIR") or os.path.join(ROOT, "base_amd", "lib")
 LIB = os.path.join(OUT_DIR, "librio_gpu.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RIO_OFFLOAD_ARCH", "gfx950")

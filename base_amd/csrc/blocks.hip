@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include "device_common.h"
+#include "parse_block.h"
 #include "rio_internal.h"
 
 namespace rio {
@@ -23,21 +24,6 @@ constexpr uint32_t kNoBlockId = 0xffffffffu;
 #define RIO_PARSE_GRID 2048
 #endif
 constexpr int kBatch = RIO_PARSE_BATCH;  // blocks per wave iteration: their loads are issued together
-
-__device__ __forceinline__ Payload desc_payload(const uint8_t *span, const DevBufs &d, uint64_t c0,
-                                                unsigned long long meta, unsigned long long len) {
-  Payload pl;
-  pl.span = span;
-  pl.ck_size = d.ck_size;
-  pl.ck_pay = d.ck_pay;
-  pl.c0 = c0;
-  pl.total = meta & kMetaTotalMask;
-  pl.pay0 = d.ck_pay[c0];
-  pl.len = len;
-  pl.regular = (meta & kMetaRegular) != 0;
-  pl.contig = nullptr;
-  return pl;
-}
 
 // Wave per block, kBatch blocks per iteration: block magic handling
 // (scanNextBlock, scannerv2.go:374-387), the header of parseChunksToItems
@@ -107,68 +93,8 @@ __global__ void __launch_bounds__(256) k_parse(DevBufs d, ParseArgs a) {
     for (int j = 0; j < kBatch; j++) {
       const uint64_t b = b0 + j;
       if (b >= nb) break;
-      const uint64_t c0 = c0s[j];
-      const unsigned long long meta = metas[j];
-      const uint64_t total = meta & kMetaTotalMask;
-      const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
-      unsigned long long status = kBlkOk, ea = 0, eb = 0, hdr = 0;
-      unsigned long long event = kNone;
-      if (c0 >= a.limit_chunk && a.mode == kModeBody) {
-        status = kBlkLimit;
-        event = 2 * c0;
-      } else if (!(meta & kMetaComplete)) {
-        status = kBlkIncomplete;
-        if (l == 0) atomicMin(&d.ctl->first_incomplete, (unsigned long long)c0);
-      } else {
-        const uint64_t end = c0 + total - 1;
-        bool parse = false;
-        if (a.mode == kModeBody) {
-          if (cls == kMagicPacked) parse = true;
-          else if (cls == kMagicTrailer) status = kBlkTrailer;
-          else status = kBlkBadMagic;
-        } else if (a.mode == kModeHeader) {
-          parse = (cls == kMagicHeader);
-          if (!parse) status = kBlkBadMagic;
-        } else {
-          parse = (cls == kMagicTrailer);
-          if (!parse) status = kBlkBadMagic;
-        }
-        if (parse && a.codec != RIO_CODEC_NONE && d.blk_status[b] == kBlkCodec) {
-          parse = false;
-          status = kBlkCodec;
-          ea = d.blk_a[b];
-          eb = d.blk_b[b];
-        }
-        if (parse) {
-          Payload pl = (a.codec != RIO_CODEC_NONE) ? make_contig_payload(d.dec + d.blk_dec_off[b], lens[j])
-                                                   : desc_payload(a.span, d, c0, meta, lens[j]);
-          ParseOut po;
-          po.item_off = d.item_off;
-          po.item_len = d.item_len;
-          po.item_base = bases[j];
-          po.item_cap = a.item_cap;
-          po.view_base = (a.codec != RIO_CODEC_NONE) ? (kItemInRecords | d.blk_dec_off[b]) : 0;
-          po.strad = d.strad;
-          po.ssz = d.ck_ssz;
-          po.c0 = c0;
-          po.overflow = &d.ctl->out_overflow;
-          HdrResult r{};
-          if (fast_header(pl, win[j], r, po, lwin, ltpos, a.sparse ? d.side : nullptr)) {
-            status = r.status;
-            hdr = r.hdr_len;
-          } else {
-            status = kBlkSlow;  // k_parse_slow finishes the block (and its event)
-          }
-        }
-        if (status != kBlkOk && status != kBlkSlow && a.mode == kModeBody) event = 2 * end + 1;
-      }
-      if (l == 0) {
-        d.blk_status[b] = status;
-        d.blk_a[b] = ea;
-        d.blk_b[b] = eb;
-        d.blk_hdr[b] = hdr;
-        if (event != kNone) atomicMin(&d.ctl->first_block_event, event);
-      }
+      const unsigned long long pay0 = (a.codec == RIO_CODEC_NONE) ? d.ck_pay[c0s[j]] : 0;
+      parse_block(d, a, b, c0s[j], metas[j], lens[j], bases[j], pay0, win[j], lwin, ltpos);
     }
   }
 }
@@ -192,7 +118,7 @@ __global__ void __launch_bounds__(256) k_parse_slow(DevBufs d, ParseArgs a) {
       const uint64_t total = meta & kMetaTotalMask;
       const unsigned long long len = (a.codec == RIO_CODEC_NONE) ? d.blk_len[b] : d.blk_out_len[b];
       const Payload pl = (a.codec != RIO_CODEC_NONE) ? make_contig_payload(d.dec + d.blk_dec_off[b], len)
-                                                     : desc_payload(a.span, d, c0, meta, len);
+                                                     : desc_payload(a.span, d, c0, meta, len, d.ck_pay[c0]);
       ParseOut po;
       po.item_off = d.item_off;
       po.item_len = d.item_len;

@@ -20,10 +20,21 @@
 // Loads are software-pipelined in 4 KiB stages through 4 register buffers:
 // while one stage is folded the next three are in flight (16 waves per CU keep
 // 192 KiB outstanding).
+//
+// Fused parse (ablation builds with -DRIO_FUSED_PARSE=1; none codec, k_crc<true>): the wave that checksums a block's
+// first chunk also parses the block (parse_block.h: magic handling, the
+// varint header, one view per item, straddler copies). The header window --
+// payload bytes 0..1023 = chunk bytes 28..1051 -- is taken from the rows the
+// wave already holds (row 0 and the first 32 bytes of row 1, staged in LDS),
+// and the block descriptor comes through scalar loads, so the parse issues no
+// vector load that would wait behind the next chunk's prefetched rows; it runs
+// while those rows are in flight. One pass over the span replaces the CRC
+// pass + the separate parse pass.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "device_common.h"
+#include "parse_block.h"
 #include "rio_internal.h"
 
 namespace rio {
@@ -118,15 +129,30 @@ __device__ __forceinline__ void load_stage(uint4 (&u)[kRows], const uint8_t *ck,
   }
 }
 
-// sizes / fix tables are separate restrict-const arguments so that their
-// wave-uniform reads compile to scalar loads (a vector load of the next
-// chunk's size would make the wave drain its prefetched rows)
+// sizes / fix tables (and the fused parse's descriptors) are separate
+// restrict-const arguments so that their wave-uniform reads compile to scalar
+// loads (a vector load of the next chunk's size would make the wave drain its
+// prefetched rows)
+struct CrcParseIn {
+  const uint32_t *__restrict__ ck_index;
+  const uint32_t *__restrict__ ck_block;
+  const unsigned long long *__restrict__ blk_meta;
+  const unsigned long long *__restrict__ blk_len;
+  const unsigned long long *__restrict__ blk_item_base;
+  const unsigned long long *__restrict__ ck_pay;
+};
+constexpr int kStageBytes = 1088;  // payload window staging: row 0 + 32 B of row 1 (then reused as the window)
+
+template <bool kParse>
 __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restrict__ span, uint64_t nchunks,
                                                        const uint32_t *__restrict__ ck_size,
                                                        const uint32_t *__restrict__ fix_a,
-                                                       const uint32_t *__restrict__ fix_b, DevBufs d, CrcArgs ca) {
+                                                       const uint32_t *__restrict__ fix_b, DevBufs d, CrcArgs ca,
+                                                       CrcParseIn pin, ParseArgs pa) {
   __shared__ __attribute__((aligned(16))) uint32_t s_fold[kFoldWords];
   __shared__ __attribute__((aligned(16))) uint32_t s_mul[kMulTables * 1024];
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[kParse ? kCrcWaves : 1][kParse ? kStageBytes : 16];
+  __shared__ uint16_t s_tpos[kParse ? kCrcWaves : 1][kParse ? 1024 : 1];
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(d.crc_fold);
     uint4 *dst = reinterpret_cast<uint4 *>(s_fold);
@@ -143,6 +169,8 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
   uint64_t c = (uint64_t)blockIdx.x * kCrcWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (c >= nchunks) return;
   uint4 buf[kBufs][kRows];
+  uint8_t *stage = kParse ? s_stage[threadIdx.x >> 6] : nullptr;
+  uint16_t *tpos = kParse ? s_tpos[threadIdx.x >> 6] : nullptr;
   uint32_t size = ck_size[c];
 #pragma unroll
   for (int q = 0; q < kBufs - 1; q++) load_stage(buf[q], span + c * kChunk, q, l);
@@ -154,6 +182,8 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
     const uint32_t sz = size > (uint32_t)kMaxPayload ? (uint32_t)kMaxPayload : size;
     const int end = kChunkHdr + (int)sz;
     const bool full = (sz == (uint32_t)kMaxPayload);
+    // a block starts here: this wave parses it after the checksum (scalar load)
+    const bool starts = kParse && pin.ck_index[c] == 0;
     uint32_t s[4] = {0, 0, 0, 0};
     uint32_t stored = 0;
     const uint32_t fa = fix_a[sz], fb = fix_b[sz];
@@ -162,6 +192,10 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
       const int nq = q + kBufs - 1;  // stage to prefetch (this chunk or the next)
       if (nq < kStages) load_stage(buf[nq % kBufs], ck, nq, l);
       else if (more) load_stage(buf[nq % kBufs], span + cn * kChunk, nq - kStages, l);
+      if (kParse && q == 0 && starts) {  // rows 0..1 raw, before the fold masks them
+        *reinterpret_cast<uint4 *>(stage + 16 * l) = buf[0][0];
+        if (l < 2) *reinterpret_cast<uint4 *>(stage + 1024 + 16 * l) = buf[0][1];
+      }
       fold_stage(buf[q % kBufs], s, tab, lb, l, q, end, fold, stored);
     }
     // lane: V_t = s0 + s1 x^-32 + s2 x^-64 + s3 x^-96
@@ -182,6 +216,22 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
       d.ck_crc[c] = crc;
       if (crc != stored && fold) atomicMin(&d.ctl->first_crc_err, (unsigned long long)c);
     }
+    if (kParse && starts) {
+      const uint32_t b = pin.ck_block[c];
+      const unsigned long long meta = pin.blk_meta[b], len = pin.blk_len[b];
+      const unsigned long long base = pin.blk_item_base[b], pay0 = pin.ck_pay[c];
+      // the header window: payload bytes 16l .. 16l+15 (0x80: past the first chunk's payload)
+      uint32_t win[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
+      const uint64_t size0 = len < (uint64_t)kMaxPayload ? len : (uint64_t)kMaxPayload;
+      if ((meta & kMetaComplete) && 16ull * l + 16 <= size0) {
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(stage + kChunkHdr + 16 * l);
+        win[0] = q[0];
+        win[1] = q[1];
+        win[2] = q[2];
+        win[3] = q[3];
+      }
+      parse_block(d, pa, b, c, meta, len, base, pay0, win, stage, tpos);
+    }
     if (!more) break;
     c = cn;
     size = size_n;
@@ -189,13 +239,20 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
 }
 
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
-                hipStream_t st) {
+                hipStream_t st, const ParseArgs *fused) {
   uint64_t g = (nchunks + kCrcWaves - 1) / kCrcWaves;
   const uint64_t cap = (uint64_t)(ncu > 0 ? ncu : 256);
   if (g > cap) g = cap;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(k_crc, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size, d.crc_fix_a,
-                     d.crc_fix_b, d, ca);
+  const CrcParseIn pin{d.ck_index, d.ck_block, d.blk_meta, d.blk_len, d.blk_item_base, d.ck_pay};
+#if RIO_FUSED_PARSE
+  if (fused)
+    hipLaunchKernelGGL(k_crc<true>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
+                       d.crc_fix_a, d.crc_fix_b, d, ca, pin, *fused);
+  else
+#endif
+    hipLaunchKernelGGL(k_crc<false>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
+                       d.crc_fix_a, d.crc_fix_b, d, ca, pin, ParseArgs{});
 }
 
 }  // namespace rio

@@ -3,11 +3,11 @@
 // at rio_open and grown only when a span needs more.
 //
 // Launch order per span (one stream; an ablation build with -DRIO_TWO_STREAMS=1
-// puts the parse path on a second stream beside k_crc, which only pays when
-// k_crc leaves CU room):
-//   memsets, k_chunk_meta, chunk scans, [codec decode],
-//   block scan (item slots), k_parse, straddler scan, k_strad   (parse path)
-//   k_crc (streams every chunk byte), k_resolve
+// puts the parse path on a second stream):
+//   none:       memsets, k_chunk_meta, chunk scans, block scan (item slots),
+//               k_parse, k_parse_slow, [straddler scan], k_strad, k_crc, k_resolve
+//   flate/zstd: memsets, k_chunk_meta, chunk scans, codec decode, item counts,
+//               block scan, k_parse, k_parse_slow, k_crc, k_resolve
 #include <hip/hip_runtime.h>
 #include <inttypes.h>
 #include <stdarg.h>
@@ -39,7 +39,7 @@ void launch_strad(const uint8_t *span, const DevBufs &d, uint64_t nslots, uint64
 void launch_resolve(const DevBufs &d, const ResolveArgs &a, hipStream_t st);
 // crc.hip
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
-                hipStream_t st);
+                hipStream_t st, const ParseArgs *fused);
 // codec.hip
 void launch_compact(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
@@ -323,17 +323,27 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   }
   HIP_OK(hipEventRecord(c->ev[kEvDec], st));
   HIP_OK(hipEventRecord(c->evA, st));
-  // parse path on st2, beside the CRC stream on st
+  // parse path on st2 (the ctx's one stream unless an ablation build splits it)
   HIP_OK(hipStreamWaitEvent(st2, c->evA, 0));
   HIP_OK(hipEventRecord(c->ev[kEvParse0], st2));
   // the shipped library always runs every stage; RIO_ABLATE (a -D of ablation
   // builds, tools/ablate.py) drops stages for measurement only
   const bool run_parse = !(RIO_ABLATE & 2) && mode != kModeRaw, run_crc = !(RIO_ABLATE & 4) && mode != kModeRaw;
+  // ablation builds (-DRIO_FUSED_PARSE=1): none codec in one pass -- the wave
+  // that checksums a block's first chunk parses the block
+  const bool fused = RIO_FUSED_PARSE && codec == RIO_CODEC_NONE && run_parse && run_crc && nchunks > 0;
+  const CrcArgs ca{RIO_ABLATE, 0};
   if (nchunks > 0 && run_parse) {
     ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap, sparse, 0};
     if (codec != RIO_CODEC_NONE) launch_dec_nitems(d, c->nblocks_dev, max_blocks, st2);
     launch_block_scan(d.blk_nitems, d.blk_item_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
-    launch_parse(d, pa, max_blocks, st2);
+    if (fused) {
+      HIP_OK(hipEventRecord(c->ev[kEvCrc0], st2));
+      launch_crc(span, nchunks, d, ca, c->ncu, st2, &pa);
+      HIP_OK(hipEventRecord(c->ev[kEvCrc1], st2));
+    } else {
+      launch_parse(d, pa, max_blocks, st2);
+    }
     launch_parse_slow(d, pa, max_blocks, st2);
     if (codec == RIO_CODEC_NONE) {
       if (!sparse) launch_chunk_scan(d.ck_ssz, d.ck_sbase, d.scan_tmp, nchunks, st2);
@@ -345,12 +355,11 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   }
   HIP_OK(hipEventRecord(c->ev[kEvParse1], st2));
   HIP_OK(hipEventRecord(c->evB, st2));
-  HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
-  if (nchunks > 0 && run_crc) {
-    CrcArgs ca{RIO_ABLATE, 0};
-    launch_crc(span, nchunks, d, ca, c->ncu, st);
+  if (!fused) {
+    HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
+    if (nchunks > 0 && run_crc) launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr);
+    HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
   }
-  HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
   HIP_OK(hipStreamWaitEvent(st, c->evB, 0));
   if (mode != kModeRaw) {
     ResolveArgs ra{span, nchunks, is_file_end, tail_partial, mode, codec, c->nblocks_dev, limit_chunk, sparse, 0};
