@@ -116,6 +116,7 @@ static const char *const kZstdErrNames[] = {
     "Dictionary mismatch",
     "Frame requires too much memory for decoding",
     "Unsupported frame parameter",
+    "Dictionary is corrupted",
 };
 
 void codec_error_text(uint64_t code, uint64_t off, uint64_t file_off, rio_error *e) {

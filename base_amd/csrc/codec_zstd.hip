@@ -1071,6 +1071,10 @@ __device__ uint64_t z_xxh64(const uint8_t *p, uint64_t len) {
   return h;
 }
 
+}  // namespace rio
+#include "zstd_exact.h"
+namespace rio {
+
 // ---------------------------------------------------------------- frame
 __device__ __forceinline__ uint32_t zrd16(const uint8_t *p, int64_t i) { return p[i] | ((uint32_t)p[i + 1] << 8); }
 __device__ __forceinline__ uint32_t zrd24(const uint8_t *p, int64_t i) { return zrd16(p, i) | ((uint32_t)p[i + 2] << 16); }
@@ -1635,16 +1639,10 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
     if (!zerr) zerr = uni(sp->final_);                // the frame walk stopped there
     if (!zerr && olen >= (1ll << 31)) zerr = kZSlow;  // the execution pass counts in u32
     if (l == 0) {
-      if (zerr == kZSlow) {
+      if (zerr) {  // declined or corrupt: the exact decoder decides (libzstd's semantics)
         sp->mode = kZsSlow;
         atomicAdd(&d.ctl->pad[1], 1ull);
-      } else if (zerr && !ck_done) {
-        sp->mode = kZsSkip;
-        d.blk_status[b] = kBlkCodec;
-        d.blk_a[b] = kCodecZstd;
-        d.blk_b[b] = zerr;
-        d.blk_out_len[b] = 0;
-      } else if (!zerr && olen > cap) {  // exact size: the host retries with it
+      } else if (olen > cap) {  // exact size: the host retries with it
         sp->mode = kZsSkip;
         d.blk_need[b] = (unsigned long long)olen;
         atomicOr(&d.ctl->out_overflow, 8ull);
@@ -1652,9 +1650,9 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
         d.blk_a[b] = kCodecFull;
         d.blk_out_len[b] = 0;
       } else {
-        sp->mode = zerr ? kZsErrCk : kZsExec;
-        sp->stored_left = zerr;
-        sp->ntok = (uint32_t)(zerr ? ent_mark : ent);
+        sp->mode = kZsExec;
+        sp->stored_left = 0;
+        sp->ntok = (uint32_t)ent;
       }
     }
   }
@@ -1830,23 +1828,21 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
     if (l == 0) {
       if (!zerr && mode == kZsExec) {
         d.blk_out_len[b] = olen;
-      } else {
-        d.blk_status[b] = kBlkCodec;
-        d.blk_a[b] = kCodecZstd;
-        d.blk_b[b] = zerr ? zerr : sp->stored_left;
-        d.blk_out_len[b] = 0;
+      } else {  // a checksum mismatch: the exact decoder re-decodes the block and names the error
+        sp->mode = kZsSlow;
+        atomicAdd(&d.ctl->pad[1], 1ull);
       }
     }
   }
 }
 
 // ---------------------------------------------------------------- k_zstd (serial path)
-// The exact serial decoder, for the blocks the fast path declined (kZsSlow):
-// one wave per block, sequences executed one at a time against the decode
-// region, literals in a per-wave buffer.
+// The exact decoder (zstd_exact.h: libzstd's semantics, lane 0 of a wave per
+// block) for every block the fast passes declined or found corrupt: its result
+// -- bytes, or the error and its name -- is the block's. Runs after
+// k_zstd_exec, which hands checksum failures here too.
 __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, DevBufs d,
                                              const unsigned long long *nblocks, uint64_t dec_cap) {
-  __shared__ ZLds L;
   const int l = lane_id();
   const uint64_t nb = uni64(*nblocks);
   uint8_t *lit = d.zlit + (uint64_t)blockIdx.x * kZLitStride;
@@ -1878,21 +1874,22 @@ __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, D
     } else {
       uint32_t *flat = d.tok + c0 * (uint64_t)kZTokPerChunk;
       z_flatten(span, d, c0, meta, n, flat);
-      ZFrame z;
-      z_init(z, reinterpret_cast<const uint8_t *>(flat), d.dec + off, (int64_t)cap, lit);
-      ZSerialSink sink;
-      int64_t pos = 0;
-      while (pos < (int64_t)n) {
-        const int64_t k = z_decode_frame(z, L, sink, pos, (int64_t)n - pos);
-        if (k < 0) {
-          zerr = (uint32_t)(-k);
-          break;
-        }
-        pos += k;
+      if (l == 0) {
+        // decoder state after the flattened input in the block's region (512 KiB per chunk)
+        uint8_t *region = reinterpret_cast<uint8_t *>(flat);
+        zx::Ctx z;
+        z.s = reinterpret_cast<zx::State *>(region + ((n + 64 + 255) & ~255ull));
+        z.in = region;
+        z.out = d.dec + off;
+        z.cap = (int64_t)cap;
+        z.lit = lit;
+        zerr = zx::decompress(z, (int64_t)n);
+        olen = z.olen;
       }
-      olen = z.olen;
-      if (zerr == kZFull) {  // size the retry from the declared content size
-        int64_t need = z_size_bound(z.src, (int64_t)n);
+      zerr = (uint32_t)__builtin_amdgcn_readfirstlane(zerr);
+      olen = (int64_t)readlane_u64((unsigned long long)olen, 0);
+      if (zerr == zx::kFull) {  // size the retry from the declared content size
+        int64_t need = z_size_bound(reinterpret_cast<const uint8_t *>(flat), (int64_t)n);
         if (need <= (int64_t)cap) need = 4 * (int64_t)cap + 4096;
         if (l == 0) {
           d.blk_need[b] = (unsigned long long)need;
@@ -1919,7 +1916,8 @@ __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, D
 uint64_t zstd_grid(int ncu) { return (uint64_t)ncu * kZWaves; }
 uint64_t zstd_lit_bytes(uint64_t grid) { return grid * kZLitStride; }
 
-// entropy pass -> serial path (declined blocks only) -> execution pass
+// entropy pass -> sequence pass -> fix-up pass -> execution pass -> exact serial
+// decoder (blocks declined or found corrupt on the way)
 void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
                  uint64_t dec_cap, uint64_t grid, hipStream_t st) {
   uint64_t g = max_blocks < grid ? max_blocks : grid;
@@ -1931,11 +1929,11 @@ void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long
   if (g3 > max_blocks) g3 = max_blocks;
   if (g3 < 1) g3 = 1;
   hipLaunchKernelGGL(k_zstd_fix, dim3((unsigned)g3), dim3(64), 0, st, d, nblocks);
-  hipLaunchKernelGGL(k_zstd, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
   uint64_t g2 = grid / kZWaves * kZExecWaves;
   if (g2 > max_blocks) g2 = max_blocks;
   if (g2 < 1) g2 = 1;
   hipLaunchKernelGGL(k_zstd_exec, dim3((unsigned)g2), dim3(64), 0, st, d, nblocks);
+  hipLaunchKernelGGL(k_zstd, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
 }
 
 }  // namespace rio
