@@ -691,18 +691,23 @@ __device__ Seq decode_seq(Ctx &z, Bit &b, uint32_t &sll, uint32_t &sml, uint32_t
   sof = ofi.next + (uint32_t)bit_read(b, ofi.nbits);
   return q;
 }
-// 0 ok, 1 corruption, 2 output full
-__device__ int exec_seq(Ctx &z, const Seq &q, uint64_t &lit_pos, uint64_t lit_size) {
-  if (q.ll > lit_size - lit_pos) return 1;
-  if (q.ll + q.ml < q.ll || z.olen + (int64_t)(q.ll + q.ml) > z.cap) return 2;
+// ZSTD_execSequence with a buffer that grows as needed (DataDog retries
+// dstSize_tooSmall with larger buffers): false = corruption. Output past `cap`
+// is not written (full: the host retries with more room) but still counted,
+// so that the checks of later sequences see the unlimited buffer's positions.
+__device__ bool exec_seq(Ctx &z, const Seq &q, uint64_t &lit_pos, uint64_t lit_size, bool &full) {
+  if (q.ll > lit_size - lit_pos) return false;
   const int64_t produced = z.olen + (int64_t)q.ll - z.frame_start;
-  if (q.off > (uint64_t)produced) return 1;
-  for (uint64_t k = 0; k < q.ll; k++) z.out[z.olen + (int64_t)k] = z.lit[lit_pos + k];
-  z.olen += (int64_t)q.ll;
+  if (q.off > (uint64_t)produced) return false;
+  if (q.ll + q.ml < q.ll || z.olen + (int64_t)(q.ll + q.ml) > z.cap) full = true;
+  if (!full) {
+    for (uint64_t k = 0; k < q.ll; k++) z.out[z.olen + (int64_t)k] = z.lit[lit_pos + k];
+    const int64_t m = z.olen + (int64_t)q.ll;
+    for (uint64_t k = 0; k < q.ml; k++) z.out[m + (int64_t)k] = z.out[m - (int64_t)q.off + (int64_t)k];
+  }
+  z.olen += (int64_t)(q.ll + q.ml);
   lit_pos += q.ll;
-  for (uint64_t k = 0; k < q.ml; k++) z.out[z.olen + (int64_t)k] = z.out[z.olen - (int64_t)q.off + (int64_t)k];
-  z.olen += (int64_t)q.ml;
-  return 0;
+  return true;
 }
 
 // ZSTD_decompressBlock_internal: kOk, an error, or kFull
@@ -818,14 +823,19 @@ __device__ uint32_t decode_block(Ctx &z, const uint8_t *src, uint64_t n) {
     bit_reload(b);
     uint32_t sml = (uint32_t)bit_read(b, z.ml->log);
     bit_reload(b);
-    if (!long_dec) {
+    bool full = false;
+    if (!long_dec) {  // every sequence decoded and executed; errors reported after the loop
       bool err = false;
       for (int i = 0; i < nseq; i++) {
         const Seq q = decode_seq(z, b, sll, sml, sof, rep);
-        const int r = exec_seq(z, q, lit_pos, lit_size);
+        const int64_t olen0 = z.olen;
+        const uint64_t lp0 = lit_pos;
+        if (!exec_seq(z, q, lit_pos, lit_size, full)) {  // op and the literals do not advance
+          err = true;
+          z.olen = olen0;
+          lit_pos = lp0;
+        }
         bit_reload(b);
-        if (r == 2) return kFull;
-        if (r) err = true;
       }
       if (err || bit_reload(b) < kCompleted) return kCorrupt;
     } else {
@@ -836,18 +846,14 @@ __device__ uint32_t decode_block(Ctx &z, const uint8_t *src, uint64_t n) {
       if (i < adv) return kCorrupt;
       for (; (bit_reload(b) <= kCompleted) && i < nseq; i++) {
         const Seq q = decode_seq(z, b, sll, sml, sof, rep);
-        const int r = exec_seq(z, qs[(i - 4) & 3], lit_pos, lit_size);
-        if (r == 2) return kFull;
-        if (r) return kCorrupt;
+        if (!exec_seq(z, qs[(i - 4) & 3], lit_pos, lit_size, full)) return kCorrupt;
         qs[i & 3] = q;
       }
       if (i < nseq) return kCorrupt;
-      for (i -= adv; i < nseq; i++) {
-        const int r = exec_seq(z, qs[i & 3], lit_pos, lit_size);
-        if (r == 2) return kFull;
-        if (r) return kCorrupt;
-      }
+      for (i -= adv; i < nseq; i++)
+        if (!exec_seq(z, qs[i & 3], lit_pos, lit_size, full)) return kCorrupt;
     }
+    if (full) return kFull;
     for (int k = 0; k < 3; k++) z.rep[k] = (uint32_t)rep[k];
   }
   if (z.olen + (int64_t)(lit_size - lit_pos) > z.cap) return kFull;

@@ -809,20 +809,23 @@ static seq_t decode_seq(zctx *z, bitd_t *b, uint32_t *sll, uint32_t *sml, uint32
     return s;
 }
 
-/* ZSTD_execSequence: 0 ok, -1 corruption, -2 output full */
-static int exec_seq(zctx *z, const seq_t *s, size_t *lit_pos, size_t lit_size) {
+/* ZSTD_execSequence with a buffer that grows as needed (DataDog retries
+ * dstSize_tooSmall with larger buffers): 0 ok, -1 corruption. Output past
+ * `cap` is not written (*full is set: the caller retries with more room) but
+ * still counted, so that the checks of later sequences see the unlimited
+ * buffer's positions. */
+static int exec_seq(zctx *z, const seq_t *s, size_t *lit_pos, size_t lit_size, int *full) {
     if (s->ll > lit_size - *lit_pos) return -1;
-    if (z->olen + (int64_t)(s->ll + s->ml) > z->cap || s->ll + s->ml < s->ll) {
-        z->full = 1;
-        return -2;
-    }
     const int64_t produced = z->olen + (int64_t)s->ll - z->frame_start;
     if (s->off > (uint64_t)produced) return -1;
-    memcpy(z->out + z->olen, g_lit + *lit_pos, s->ll);
-    z->olen += (int64_t)s->ll;
+    if (s->ll + s->ml < s->ll || z->olen + (int64_t)(s->ll + s->ml) > z->cap) *full = 1;
+    if (!*full) {
+        memcpy(z->out + z->olen, g_lit + *lit_pos, s->ll);
+        for (uint64_t k = 0; k < s->ml; k++)
+            z->out[z->olen + (int64_t)s->ll + (int64_t)k] = z->out[z->olen + (int64_t)s->ll - (int64_t)s->off + (int64_t)k];
+    }
+    z->olen += (int64_t)(s->ll + s->ml);
     *lit_pos += s->ll;
-    for (uint64_t k = 0; k < s->ml; k++) z->out[z->olen + (int64_t)k] = z->out[z->olen - (int64_t)s->off + (int64_t)k];
-    z->olen += (int64_t)s->ml;
     return 0;
 }
 
@@ -959,14 +962,19 @@ static int decode_block(zctx *z, const uint8_t *src, size_t n) {
         bitd_reload(&b);
         uint32_t sml = (uint32_t)bitd_read(&b, z->ml->log);
         bitd_reload(&b);
-        if (!long_dec) {
+        int full = 0;
+        if (!long_dec) { /* every sequence decoded and executed; errors reported after the loop */
             int err = 0;
             for (int i = 0; i < nseq; i++) {
                 const seq_t s = decode_seq(z, &b, &sll, &sml, &sof, rep);
-                const int r = exec_seq(z, &s, &lit_pos, lit_size);
+                const int64_t olen0 = z->olen;
+                const size_t lp0 = lit_pos;
+                if (exec_seq(z, &s, &lit_pos, lit_size, &full)) { /* op and the literals do not advance */
+                    err = 1;
+                    z->olen = olen0;
+                    lit_pos = lp0;
+                }
                 bitd_reload(&b);
-                if (r == -2) return 0;
-                if (r) err = 1;
             }
             if (err) CORRUPT;
             if (bitd_reload(&b) < BIT_COMPLETED) CORRUPT;
@@ -978,17 +986,16 @@ static int decode_block(zctx *z, const uint8_t *src, size_t n) {
             if (i < adv) CORRUPT;
             for (; (bitd_reload(&b) <= BIT_COMPLETED) && i < nseq; i++) {
                 const seq_t s = decode_seq(z, &b, &sll, &sml, &sof, rep);
-                const int r = exec_seq(z, &q[(i - 4) & 3], &lit_pos, lit_size);
-                if (r == -2) return 0;
-                if (r) CORRUPT;
+                if (exec_seq(z, &q[(i - 4) & 3], &lit_pos, lit_size, &full)) CORRUPT;
                 q[i & 3] = s;
             }
             if (i < nseq) CORRUPT;
-            for (i -= adv; i < nseq; i++) {
-                const int r = exec_seq(z, &q[i & 3], &lit_pos, lit_size);
-                if (r == -2) return 0;
-                if (r) CORRUPT;
-            }
+            for (i -= adv; i < nseq; i++)
+                if (exec_seq(z, &q[i & 3], &lit_pos, lit_size, &full)) CORRUPT;
+        }
+        if (full) {
+            z->full = 1;
+            return 0;
         }
         for (int k = 0; k < 3; k++) z->rep[k] = (uint32_t)rep[k];
     }
