@@ -487,6 +487,10 @@ enum : int { kTokDone = 0, kTokYield = -1 };
 #endif
 constexpr int kTokLitRoot = RIO_LIT_ROOT;  // literal/length root table bits
 constexpr int kTokDistRoot = 8;
+#ifndef RIO_FLATE_SYNC
+#define RIO_FLATE_SYNC 1
+#endif
+constexpr bool kFlateSync = RIO_FLATE_SYNC != 0;  // k_flate_sync first (ablation builds: -DRIO_FLATE_SYNC=0)
 
 // RFC 1951 §3.2.5 length / distance bases and extra bits
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -952,6 +956,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           const uint64_t c0 = uni64(d.blk_c0[sb]);
           const unsigned long long meta = uni64(d.blk_meta[sb]);
           uint32_t stm;
+          if (round == 0 && kFlateSync && uni(sp->mode) != kFlHeader) continue;  // k_flate_sync handled it
           if (round == 0) {
             const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
             // incomplete blocks, and magics that are never untransformed (the header
@@ -1298,6 +1303,309 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
   }
 }
 
+// ================================================================ k_flate_sync
+// Huffman pass with the whole wave on ONE recordio block (used first; blocks it
+// declines go to k_flate_tok). Within a DEFLATE block the compressed bits are
+// cut into 64 segments of kSyncSeg bits, one per lane, and every lane decodes
+// its segment from a guessed start -- the segment's first bit, which is almost
+// never a symbol boundary. Huffman codes self-synchronise: a decode from a wrong
+// start falls into step with the true symbol sequence within a few symbols, so
+// the position where a lane leaves its segment (the first symbol boundary at or
+// after the segment end) is, after a few symbols, the true one. Each lane then
+// restarts from its predecessor's exit; when no start changes any more every
+// lane is on the true chain (lane 0 starts at a known boundary, and lane i's
+// start is lane i-1's exit). A prefix sum of the lanes' token / byte counts
+// places each lane's tokens, and a last pass writes them (same token format as
+// k_flate_tok, so k_flate_lz is unchanged). The first lane that decodes the
+// end-of-block symbol ends the DEFLATE block; lanes after it were decoding the
+// next block's bits and are discarded.
+//
+// Parallelism is 64 segments of one stream per wave (k_flate_tok: 8 streams per
+// wave, each replicated on 8 lanes), with one table set per wave in LDS, so a
+// few large recordio blocks (the writer's default MaxItems = 16384: ~5 MB
+// blocks) fill the GPU as well as many small ones. Anything unusual -- no
+// convergence within kSyncIters rounds, a token region too small, the stream's
+// size beyond this kernel's 32-bit positions -- declines the block to
+// k_flate_tok; corrupt or oversized streams go to k_inflate_exact as there.
+constexpr uint32_t kSyncSeg = 1024;                       // bits per lane per round
+constexpr uint32_t kSyncBits = 64 * kSyncSeg;             // bits per round
+constexpr uint32_t kSyncWinDw = kSyncBits / 32 + 32;      // staged dwords (+ run-out margin)
+constexpr int kSyncIters = 8;
+constexpr int kSyncWaves = 8;                             // per CU (launch sizing)
+
+struct SyncLds {
+  StreamLds T;  // the DEFLATE block's tables (ring / tbuf unused)
+  WaveLds W;
+  uint32_t win[kSyncWinDw];
+};
+
+// 32 bits of the staged window at relative bit r
+__device__ __forceinline__ uint32_t sync_bits(const uint32_t *win, uint32_t r) {
+  const uint32_t d = r >> 5;
+  return __builtin_amdgcn_alignbit(win[d + 1], win[d], r & 31);
+}
+
+enum : uint32_t { kSyEob = 1, kSyBad = 2, kSyHist = 4, kSyFull = 8 };
+
+// Decode tokens from relative bit r while r < end (or to the end-of-block
+// symbol). Counting mode skips an undecodable code by one bit (a lane off the
+// true chain); writing mode stops there. Returns the exit position.
+template <bool kWrite>
+__device__ __forceinline__ uint32_t sync_decode(const StreamLds &T, const uint32_t *win, uint32_t r, uint32_t end,
+                                                uint32_t lim, uint32_t &ntok, uint32_t &nout, uint32_t &flags,
+                                                uint32_t *tk, uint32_t olen0, uint32_t cap) {
+  while (r < end && r < lim) {
+    const uint32_t w = sync_bits(win, r);
+    uint32_t e = T.lit[w & ((1u << kTokLitRoot) - 1)];
+    if ((e & 15) == 0 && (e & kEnLenBit)) e = slow_walk<kTokLitRoot>(T.lfco, T.lent, w);
+    const uint32_t L = e & 15, E = (e >> 5) & 7;
+    if (L == 0) {
+      flags |= kSyBad;
+      if (kWrite) break;
+      r += 1;
+      continue;
+    }
+    if (!(e & kEnLenBit)) {
+      if (kWrite) {
+        if (olen0 + nout >= cap) {
+          flags |= kSyFull;
+          break;
+        }
+        tk[ntok] = (e >> 8) | (1u << 24);
+      }
+      r += L;
+      ntok++;
+      nout++;
+      continue;
+    }
+    if (E == kEobExtra) {
+      r += L;
+      flags |= kSyEob;
+      break;
+    }
+    const uint32_t len = (e >> 8) + 3 + __builtin_amdgcn_ubfe(w, L, E);
+    const uint32_t r1 = r + L + E;
+    const uint32_t w2 = sync_bits(win, r1);
+    uint32_t dd = T.dst[w2 & ((1u << kTokDistRoot) - 1)];
+    if ((dd & 15) == 0 && (dd & kEnLenBit)) dd = slow_walk<kTokDistRoot>(T.dfco, T.dent, w2);
+    const uint32_t L2 = dd & 15, E2 = (dd >> 7) & 15;
+    if (L2 == 0) {
+      flags |= kSyBad;
+      if (kWrite) break;
+      r = r1;
+      continue;
+    }
+    const uint32_t dist = (((dd >> 5) & 3) << E2) + 1 + __builtin_amdgcn_ubfe(w2, L2, E2);
+    if (kWrite) {
+      const uint32_t at = olen0 + nout, hist = at < 32768u ? at : 32768u;
+      if (dist > hist) {
+        flags |= kSyHist;
+        break;
+      }
+      if (len > cap - at) {
+        flags |= kSyFull;
+        break;
+      }
+      tk[ntok] = 0x80000000u | ((len - 3) << 16) | (dist - 1);
+    }
+    r = r1 + L2 + E2;
+    ntok++;
+    nout += len;
+  }
+  return r;
+}
+
+__global__ void __launch_bounds__(64) k_flate_sync(const uint8_t *__restrict__ span, DevBufs d,
+                                                   const unsigned long long *nblocks, uint64_t nchunks,
+                                                   uint64_t dec_cap) {
+  __shared__ SyncLds S;
+  StreamLds &T = S.T;
+  const int l = lane_id();
+  const uint64_t nb = uni64(*nblocks);
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    FlState *sp = &d.fl[b];
+    const uint64_t c0 = uni64(d.blk_c0[b]);
+    const unsigned long long meta = uni64(d.blk_meta[b]);
+    const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
+    // incomplete blocks, and magics that are never untransformed (the header
+    // block is idTransform, registry.go:31; others are errors): nothing decoded
+    bool skip = !(meta & kMetaComplete) || (cls != kMagicPacked && cls != kMagicTrailer);
+    const uint64_t doff = uni64(d.blk_dec_off[b]), cp = uni64(d.blk_out_len[b]);
+    if (!skip && doff + cp > dec_cap) {  // the regions need a larger buffer (host retries)
+      skip = true;
+      if (l == 0) {
+        atomicOr(&d.ctl->out_overflow, 0x40ull);
+        atomicMax(&d.ctl->dec_need, (unsigned long long)(doff + cp));
+      }
+    }
+    if (skip) {
+      if (l == 0) {
+        sp->mode = kFlSkip;
+        sp->round = 0;
+        d.blk_out_len[b] = 0;
+      }
+      continue;
+    }
+    const uint64_t n = uni64(d.blk_len[b]);
+    const uint64_t total = meta & kMetaTotalMask;
+    uint64_t tcap64 = total * (uint64_t)kTokPerChunk;
+    if (d.tok_limit && d.tok_limit < tcap64) tcap64 = d.tok_limit < 64 ? 64 : d.tok_limit;
+    const CompIn in = make_in(span, d, nchunks, c0, total, n, (meta & kMetaRegular) != 0);
+    // outside this kernel's 32-bit bit positions: k_flate_tok
+    bool decline = n >= (1ull << 28) || c0 >= (1ull << 32);
+    const uint32_t cap = cp > 0xfffff000ull ? 0xfffff000u : (uint32_t)cp;
+    const uint32_t tcap = tcap64 > 0xffffff00ull ? 0xffffff00u : (uint32_t)tcap64;
+    uint32_t *tok = d.tok + c0 * (uint64_t)kTokPerChunk;
+    uint64_t bit = 0;
+    uint32_t olen = 0, ntok = 0, res = 0;  // res: 0 ok, else a CodecErr for k_inflate_exact
+    bool fin = false, fixed = false;
+    while (!decline && !res && !fin) {
+      // ---- DEFLATE block header (wave-uniform)
+      TokDec t;
+      t.in = in;
+      t.T = &T;
+      t.W = &S.W;
+      t.seek(bit);
+      if (t.nb < 32) t.refill();
+      fin = t.take(1) != 0;
+      const uint32_t type = t.take(2);
+      if (type == 0) {  // stored: its bytes become literal tokens, 3 per token
+        t.take(t.nb & 7);
+        if (t.nb < 32) t.refill();
+        const uint32_t len = t.take(16), nlen = t.take(16);
+        const uint64_t at = t.bitpos() / 8;
+        if ((uint16_t)nlen != (uint16_t)~len) {
+          res = kCodecCorrupt;
+        } else if (at + len > n) {
+          res = kCodecEof;
+        } else if (len > cap - olen) {
+          res = kCodecFull;
+        } else {
+          const uint32_t nt = (len + 2) / 3;
+          if ((uint64_t)ntok + nt > tcap) {
+            decline = true;
+            break;
+          }
+          for (uint32_t k = (uint32_t)l; k < nt; k += 64) {
+            const uint32_t c = (len - 3 * k) < 3 ? len - 3 * k : 3u;
+            uint32_t v = 0;
+            for (uint32_t q = 0; q < c; q++) v |= in.byte(at + 3 * k + q) << (8 * q);
+            tok[ntok + k] = v | (c << 24);
+          }
+          ntok += nt;
+          olen += len;
+          bit = 8 * (at + len);
+        }
+        continue;
+      }
+      if (type == 1) {
+        if (!fixed) fixed_tables(T, S.W);
+        fixed = true;
+      } else if (type == 2) {
+        if (read_dynamic(t)) res = kCodecCorrupt;
+        fixed = false;
+      } else {
+        res = kCodecCorrupt;
+      }
+      if (!res && t.overrun()) res = kCodecEof;
+      if (res) break;
+      bit = t.bitpos();
+      // ---- the block body, kSyncBits per round
+      for (;;) {
+        if (bit > 8 * n + 64) {  // ran past the input without an end-of-block
+          res = kCodecEof;
+          break;
+        }
+        const uint64_t w0 = bit >> 5;  // staged window: dwords [w0, w0 + kSyncWinDw)
+        wave_lds_sync();
+        for (uint32_t k = (uint32_t)l; k < kSyncWinDw; k += 64) S.win[k] = fetch_dword(in, 4 * (w0 + k));
+        wave_lds_sync();
+        const uint32_t r0 = (uint32_t)(bit - 32 * w0), lim = 32 * (kSyncWinDw - 2);
+        const uint32_t seg_end = r0 + kSyncSeg * (uint32_t)(l + 1);
+        uint32_t st = r0 + kSyncSeg * (uint32_t)l, ex = 0, nt = 0, no = 0, fl = 0;
+        bool need = true, conv = false;
+        for (int it = 0; it < kSyncIters; it++) {
+          if (need) {
+            nt = no = fl = 0;
+            ex = sync_decode<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, 0, 0);
+          }
+          // the true chain ends at the first lane reaching end-of-block
+          const unsigned long long eobm = __ballot((fl & kSyEob) != 0);
+          const int ke = eobm ? __ffsll((long long)eobm) - 1 : 63;
+          uint32_t prev = __shfl_up(ex, 1, 64);
+          const uint32_t nst = l == 0 ? r0 : prev;
+          need = l <= ke && nst != st;  // lanes after the end keep their start until the end moves
+          if (need) st = nst;
+          if (!__ballot(need)) {
+            conv = true;
+            break;
+          }
+        }
+        if (!conv) {
+          decline = true;
+          break;
+        }
+        const unsigned long long eobm = __ballot((fl & kSyEob) != 0);
+        const int ke = eobm ? __ffsll((long long)eobm) - 1 : 63;
+        const bool live = l <= ke;
+        if (__ballot(live && (fl & kSyBad))) {  // an undecodable code on the true chain
+          res = kCodecCorrupt;
+          break;
+        }
+        const uint32_t tn = live ? nt : 0u, on = live ? no : 0u;
+        const uint32_t ti = wave_incl_sum_dpp(tn), oi = wave_incl_sum_dpp(on);
+        const uint32_t ttot = (uint32_t)__builtin_amdgcn_readlane(ti, 63);
+        const uint32_t otot = (uint32_t)__builtin_amdgcn_readlane(oi, 63);
+        if ((uint64_t)ntok + ttot > tcap) {
+          decline = true;
+          break;
+        }
+        uint32_t f2 = 0;
+        if (live) {
+          uint32_t wt = 0, wo = 0;
+          sync_decode<true>(T, S.win, st, seg_end, lim, wt, wo, f2, tok + ntok + (ti - tn), olen + (oi - on), cap);
+        }
+        const uint32_t fall = (uint32_t)__reduce_or_sync(~0ull, f2);
+        if (fall & kSyHist) {
+          res = kCodecCorrupt;
+          break;
+        }
+        if (fall & kSyFull) {
+          res = kCodecFull;
+          break;
+        }
+        ntok += ttot;
+        olen += otot;
+        const uint32_t exk = (uint32_t)__builtin_amdgcn_readlane(ex, ke);
+        bit = 32 * w0 + exk;
+        if (eobm) break;  // the DEFLATE block ended
+      }
+    }
+    if (!decline && !res && bit > 8 * n) res = kCodecEof;  // the final block ran past the input
+    if (l == 0) {
+      sp->round = 0;
+      sp->olen2 = 0;
+      if (decline) {
+        sp->mode = kFlHeader;  // k_flate_tok decodes it from the start
+      } else if (res) {        // k_inflate_exact classifies it (Go's lazy byte pulls) or sizes it
+        sp->bitpos = bit;
+        sp->olen = olen;
+        sp->pad = res;
+        sp->ntok = 0;
+        sp->mode = kFlError;
+        d.blk_status[b] = kBlkCodec;
+        d.blk_a[b] = kCodecPending;
+        d.blk_b[b] = res;
+        d.blk_out_len[b] = 0;
+      } else {
+        sp->mode = kFlDone;
+        sp->ntok = ntok;
+        sp->olen = olen;
+      }
+    }
+  }
+}
+
 // k mod d for k < 2^20, d >= 1 (float reciprocal, one correction step)
 __device__ __forceinline__ uint32_t umod_small(uint32_t k, uint32_t d) {
   uint32_t q = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)d));
@@ -1520,6 +1828,13 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
   const uint64_t r2 = (uint64_t)ncu * 4;  // 36 KiB windows: 4 per CU
   if (g2 > r2) g2 = r2;
   if (g2 < 1) g2 = 1;
+  if (kFlateSync) {  // the wave-per-block Huffman pass first; k_flate_tok takes what it declines
+    uint64_t gs = max_blocks;
+    const uint64_t rs = (uint64_t)ncu * kSyncWaves;
+    if (gs > rs) gs = rs;
+    if (gs < 1) gs = 1;
+    hipLaunchKernelGGL(k_flate_sync, dim3((unsigned)gs), dim3(64), 0, st, span, d, nblocks, nchunks, dec_cap);
+  }
   for (int r = 0; r < rounds; r++) {
     hipLaunchKernelGGL(k_flate_tok, dim3((unsigned)g1), dim3(64), 0, st, span, d, nblocks, nchunks,
                        dec_cap, r, (int)(r == rounds - 1));
