@@ -102,17 +102,25 @@ __global__ void __launch_bounds__(256) k_parse(DevBufs d, ParseArgs a) {
 // The blocks k_parse left to the general parser (headers past the first 1 KiB,
 // irregular chunk layouts, and every malformed header: parse_header computes
 // the reference's error values).
+// Teams of kSlowTeam waves share a group of 64 blocks, member m taking the
+// group's slow blocks m, m + kSlowTeam, ...: a run of slow blocks (every block
+// of a file written with a large MaxItems) spreads over the team.
+constexpr uint32_t kSlowTeam = 16;
+
 __global__ void __launch_bounds__(256) k_parse_slow(DevBufs d, ParseArgs a) {
   const uint64_t nb = *a.nblocks;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const uint64_t team = wave / kSlowTeam, nteams = nwaves / kSlowTeam;
+  const uint32_t member = (uint32_t)(wave % kSlowTeam);
   const int l = lane_id();
-  for (uint64_t g = wave * 64; g < nb; g += nwaves * 64) {
+  for (uint64_t g = team * 64; g < nb; g += nteams * 64) {
     const bool slow = (g + l < nb) && d.blk_status[g + l] == kBlkSlow;
     unsigned long long sm = __ballot(slow);
-    while (sm) {
+    for (uint32_t rank = 0; sm; rank++) {
       const uint64_t b = g + __ffsll((long long)sm) - 1;
       sm &= sm - 1;
+      if (rank % kSlowTeam != member) continue;
       const uint64_t c0 = d.blk_c0[b];
       const unsigned long long meta = d.blk_meta[b];
       const uint64_t total = meta & kMetaTotalMask;
@@ -389,7 +397,10 @@ void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hip
 }
 
 void launch_parse_slow(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_parse_slow, dim3(grid_of(max_blocks, 256, 1024)), dim3(256), 0, st, d, a);
+  // whole teams: 4 waves per workgroup, kSlowTeam waves per team
+  unsigned g = grid_of(max_blocks, 16, 2048);
+  g = (g + kSlowTeam / 4 - 1) / (kSlowTeam / 4) * (kSlowTeam / 4);
+  hipLaunchKernelGGL(k_parse_slow, dim3(g), dim3(256), 0, st, d, a);
 }
 
 void launch_dec_nitems(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st) {

@@ -491,6 +491,10 @@ constexpr int kTokDistRoot = 8;
 #define RIO_FLATE_SYNC 1
 #endif
 constexpr bool kFlateSync = RIO_FLATE_SYNC != 0;  // k_flate_sync first (ablation builds: -DRIO_FLATE_SYNC=0)
+#ifndef RIO_FLATE_LZ2
+#define RIO_FLATE_LZ2 1
+#endif
+constexpr bool kFlateLz2 = RIO_FLATE_LZ2 != 0;  // HBM-history copy pass (ablation builds: -DRIO_FLATE_LZ2=0)
 
 // RFC 1951 §3.2.5 length / distance bases and extra bits
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -1331,18 +1335,22 @@ constexpr uint32_t kSyncSeg = 1024;                       // bits per lane per r
 constexpr uint32_t kSyncBits = 64 * kSyncSeg;             // bits per round
 constexpr uint32_t kSyncWinDw = kSyncBits / 32 + 32;      // staged dwords (+ run-out margin)
 constexpr int kSyncIters = 8;
-constexpr int kSyncWaves = 8;                             // per CU (launch sizing)
+constexpr int kSyncWaves = 12;                            // per CU (launch sizing)
 
 struct SyncLds {
   StreamLds T;  // the DEFLATE block's tables (ring / tbuf unused)
   WaveLds W;
-  uint32_t win[kSyncWinDw];
+  uint32_t win[kSyncWinDw + kSyncWinDw / 32 + 1];  // skewed: see sync_at
 };
 
 // 32 bits of the staged window at relative bit r
+// Window dword d lives at d + d/32: the lanes' segments start 32 dwords
+// apart, which unskewed would put all 32 lanes of a ds_read_b32 group on one
+// LDS bank (a 32-way conflict); skewed, segment i starts on bank i.
+__device__ __forceinline__ uint32_t sync_at(uint32_t d) { return d + (d >> 5); }
 __device__ __forceinline__ uint32_t sync_bits(const uint32_t *win, uint32_t r) {
   const uint32_t d = r >> 5;
-  return __builtin_amdgcn_alignbit(win[d + 1], win[d], r & 31);
+  return __builtin_amdgcn_alignbit(win[sync_at(d + 1)], win[sync_at(d)], r & 31);
 }
 
 enum : uint32_t { kSyEob = 1, kSyBad = 2, kSyHist = 4, kSyFull = 8 };
@@ -1518,7 +1526,7 @@ __global__ void __launch_bounds__(64) k_flate_sync(const uint8_t *__restrict__ s
         }
         const uint64_t w0 = bit >> 5;  // staged window: dwords [w0, w0 + kSyncWinDw)
         wave_lds_sync();
-        for (uint32_t k = (uint32_t)l; k < kSyncWinDw; k += 64) S.win[k] = fetch_dword(in, 4 * (w0 + k));
+        for (uint32_t k = (uint32_t)l; k < kSyncWinDw; k += 64) S.win[sync_at(k)] = fetch_dword(in, 4 * (w0 + k));
         wave_lds_sync();
         const uint32_t r0 = (uint32_t)(bit - 32 * w0), lim = 32 * (kSyncWinDw - 2);
         const uint32_t seg_end = r0 + kSyncSeg * (uint32_t)(l + 1);
@@ -1771,6 +1779,252 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
   }
 }
 
+// ================================================================ k_flate_lz2
+// Copy pass with the 32 KiB history in HBM: the block's own output region,
+// which the wave has already written. LDS holds only a 4 KiB ring per wave
+// (the batch being built plus the 2,544 bytes before it), so ~28 waves fit a
+// CU where k_flate_lz's 36 KiB windows fit 4: the copy pass is latency-bound,
+// and occupancy is what hides the latency.
+//
+// A batch is up to 256 tokens (4 per lane, token order k-major) whose output
+// fits kL2Span bytes. Its bytes are produced in the ring:
+//  - literals, and matches whose source lies wholly before the batch, at once:
+//    sources within kL2Near bytes from the ring, older ones from HBM, the
+//    four token slots' source dwords loaded together (one memory latency per
+//    16 bytes of the longest copy, not one per token);
+//  - matches whose source reaches into the batch, in rounds: a round copies
+//    every such match whose source ends at or before R, the start of the first
+//    match still pending (every byte before R is final), and the first pending
+//    match itself (a source overlapping its own output -- dist < len, a run --
+//    is copied by the whole wave with period dist).
+// Then the batch's complete 16 B units go to HBM (coalesced and aligned:
+// decode regions are 256-aligned).
+//
+// HBM sources are more than kL2Near >= kL2Span + 16 + 258 bytes back, so they
+// were flushed two batches ago or earlier; the wave has since waited for the
+// token loads it issued after those stores (the tokens of this batch), and a
+// gfx9 wave's vector memory operations complete in issue order, so the stores
+// are done. Sources are read with agent-scope loads (from L2, never a stale L1
+// line).
+constexpr uint32_t kL2Ring = 4096, kL2Mask = kL2Ring - 1;
+constexpr uint32_t kL2Span = 1536;                   // output bytes per batch at most
+constexpr uint32_t kL2Near = kL2Ring - kL2Span - 16;  // bytes before the batch kept in the ring (the
+                                                       // batch's zeroing may round up one dword)
+constexpr int kL2Waves = 16;                          // per CU (launch sizing)
+static_assert(kL2Near >= kL2Span + 16 + 258, "HBM sources must be flushed two batches back");
+
+__device__ __forceinline__ uint32_t tok_len(uint32_t t) {
+  return (t >> 31) ? ((t >> 16) & 0xffu) + 3 : (t >> 24) & 3u;
+}
+
+__device__ __forceinline__ uint32_t pick4(const uint32_t (&a)[4], int k) {
+  return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3];
+}
+
+// Four copies at once (one per token slot; n[k] == 0: none): n[k] bytes from
+// position s[k] to t[k] (t - s >= n: no overlap), sources in HBM where bit k of
+// glob is set, else in the ring. The batch's ring bytes are zeroed first and
+// every byte belongs to one token, so a token ORs its bytes into the
+// destination dwords (an LDS atomic, in any order) -- no byte stores, no races
+// with the neighbours sharing its end dwords. Source dwords are read aligned
+// and funnel-shifted; each step issues every slot's loads before using any.
+__device__ __forceinline__ void l2_copy4(uint8_t *ring, const uint32_t *gw, const uint32_t (&s)[4], uint32_t B0,
+                                         const uint32_t (&p)[4], const uint32_t (&n)[4], uint32_t glob) {
+  uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
+  const uint8_t *g = reinterpret_cast<const uint8_t *>(gw);
+  // per slot (recomputed where used, to keep registers for occupancy): the
+  // destination t = B0 + p, its dwords [t/4, (t+n+3)/4), and the source dword
+  // under the first one, floor((s - t%4) / 4) (~0 for -1)
+  for (uint32_t D = 0;; D += 4) {
+    bool any = false;
+    uint32_t w[4][5];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t t = B0 + p[k];
+      const bool act = n[k] != 0 && (t >> 2) + D < (t + n[k] + 3) >> 2;
+      any |= act;
+      const uint32_t q = (s[k] >> 2) - ((s[k] & 3) < (t & 3) ? 1u : 0u) + D;
+#pragma unroll
+      for (int i = 0; i < 5; i++) w[k][i] = 0;
+      if (act && ((glob >> k) & 1)) {
+        // dword -1 (a source at position < 3) only feeds bytes before the
+        // destination, which are masked off: any dword will do (dword 0)
+        w[k][0] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(g + (q == 0xffffffffu ? 0u : q << 2)),
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint8_t *g1 = g + ((q + 1) << 2);
+#pragma unroll
+        for (int i = 1; i < 5; i++)
+          w[k][i] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(g1 + 4 * (i - 1)), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+      } else if (act) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) w[k][i] = rw[(q + i) & (kL2Mask >> 2)];
+      }
+    }
+    if (!__builtin_amdgcn_ballot_w64(any)) break;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t t = B0 + p[k], d0 = t >> 2, d1 = n[k] ? (t + n[k] + 3) >> 2 : d0;
+      const uint32_t sh = 8 * ((s[k] - t) & 3);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t Dj = d0 + D + j;
+        if (Dj < d1) {
+          const uint32_t v = __builtin_amdgcn_alignbit(w[k][j + 1], w[k][j], sh);
+          const uint32_t x0 = 4 * Dj;
+          const uint32_t lo = t > x0 ? t - x0 : 0u;                         // 0..3
+          const uint32_t hi = t + n[k] < x0 + 4 ? t + n[k] - x0 : 4u;      // 1..4
+          const uint32_t m = (0xffffffffu << (8 * lo)) & (0xffffffffu >> (8 * (4 - hi)));
+          atomicOr(&rw[Dj & (kL2Mask >> 2)], v & m);
+        }
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) k_flate_lz2(DevBufs d, const unsigned long long *nblocks, int round) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kL2Ring];
+  const int l = lane_id();
+  if (round > 0 && uni64(d.fl_more[round - 1]) == 0) return;
+  const uint64_t nb = uni64(*nblocks);
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    FlState *sp = &d.fl[b];
+    const uint32_t mode = uni(sp->mode);
+    if (uni(sp->round) != (uint32_t)round || mode == kFlError || mode == kFlSkip) continue;
+    uint32_t olen = (uint32_t)uni64(sp->olen2);
+    const uint32_t ntok = uni(sp->ntok);
+    uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
+    const uint32_t *gw = reinterpret_cast<const uint32_t *>(out);
+    const uint32_t *tk = d.tok + uni64(d.blk_c0[b]) * (uint64_t)kTokPerChunk;
+    wave_lds_sync();
+    if (olen > 0) {  // resumed: the history this block has already written, into the ring
+      const uint32_t h0 = (olen > kL2Near ? olen - kL2Near : 0u) & ~15u;
+      for (uint32_t x = h0 + 16 * (uint32_t)l; x < olen; x += 1024)
+        *reinterpret_cast<uint4 *>(ring + (x & kL2Mask)) = *reinterpret_cast<const uint4 *>(out + x);
+    }
+    uint32_t pre[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) pre[k] = (64u * k + (uint32_t)l < ntok) ? tk[64 * k + l] : 0u;
+    uint32_t cur = 0;
+    while (cur < ntok) {
+      uint32_t t[4], len[4], p[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) t[k] = pre[k];
+      // output positions (relative to the batch) and the tokens this batch takes
+      uint32_t carry = 0, take = 0, emax = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const bool valid = cur + 64u * k + (uint32_t)l < ntok;
+        len[k] = valid ? tok_len(t[k]) : 0u;
+        const uint32_t incl = wave_incl_sum_dpp(len[k]) + carry;
+        p[k] = incl - len[k];
+        const bool ok = valid && incl <= kL2Span;  // a prefix of the tokens (positions only grow)
+        take += (uint32_t)__popcll(__ballot(ok));
+        if (ok) emax = incl;
+        else len[k] = 0;
+        carry = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+      }
+      const uint32_t total = (uint32_t)__reduce_max_sync(~0ull, emax);
+      const uint32_t B0 = olen;
+      {  // zero the batch's ring bytes (their dwords; the history bytes of the first one stay)
+        uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
+        const uint32_t z0 = (B0 + 3) >> 2, z1 = (B0 + total + 3) >> 2;
+        for (uint32_t z = z0 + (uint32_t)l; z < z1; z += 64) rw[z & (kL2Mask >> 2)] = 0u;
+        if ((B0 & 3) && l == 0) atomicAnd(&rw[(B0 >> 2) & (kL2Mask >> 2)], (1u << (8 * (B0 & 3))) - 1);
+        wave_lds_sync();
+      }
+      const uint32_t near = B0 > kL2Near ? B0 - kL2Near : 0u;  // positions >= near: in the ring
+      // literals now; matches sourced before the batch now; the others pending
+      bool pend[4];
+      uint32_t cs[4], cn[4], glob = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        pend[k] = false;
+        cn[k] = 0;
+        const uint32_t n = len[k];
+        const uint32_t x = B0 + p[k];
+        cs[k] = x - ((t[k] & 0xffffu) + 1);
+        if (n == 0) continue;
+        if (!(t[k] >> 31)) {  // 1-3 literal bytes
+          uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
+          const uint32_t v = t[k] & 0xffffffu, o = 8 * (x & 3);
+          atomicOr(&rw[(x >> 2) & (kL2Mask >> 2)], v << o);
+          if ((x & 3) + n > 4) atomicOr(&rw[((x >> 2) + 1) & (kL2Mask >> 2)], v >> (32 - o));
+        } else if (cs[k] < near) {
+          cn[k] = n;
+          glob |= 1u << k;
+        } else if (cs[k] + n <= B0) {
+          cn[k] = n;
+        } else {
+          pend[k] = true;
+        }
+      }
+      // the next batch's tokens (issued before this batch's stores: see above)
+      const uint32_t nx = cur + take;
+#pragma unroll
+      for (int k = 0; k < 4; k++) pre[k] = (nx + 64u * k + (uint32_t)l < ntok) ? tk[nx + 64 * k + l] : 0u;
+      // the copies above, then the matches sourced inside the batch, in rounds
+      bool run = false;
+      uint32_t R = 0, Df = 0, Nf = 0;
+      for (;;) {
+        l2_copy4(ring, gw, cs, B0, p, cn, glob);
+        if (run) {  // byte k of the run = byte (k mod dist) of the dist bytes before it (final)
+          const uint32_t xs = B0 + R - Df, xd = B0 + R;
+          for (uint32_t k0 = 0; k0 < Nf; k0 += 64) {
+            const uint32_t k = k0 + (uint32_t)l;
+            if (k < Nf) {
+              const uint32_t v = ring[(xs + umod_small(k, Df)) & kL2Mask];
+              atomicOr(reinterpret_cast<uint32_t *>(ring) + (((xd + k) >> 2) & (kL2Mask >> 2)), v << (8 * ((xd + k) & 3)));
+            }
+          }
+        }
+        wave_lds_sync();
+        int kf = -1, lf = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const unsigned long long m = __ballot(pend[k]);
+          if (kf < 0 && m) {
+            kf = k;
+            lf = __ffsll((long long)m) - 1;
+          }
+        }
+        if (kf < 0) break;
+        // R: the first pending match; every byte before it is final
+        R = (uint32_t)__builtin_amdgcn_readlane(pick4(p, kf), lf);
+        Df = ((uint32_t)__builtin_amdgcn_readlane(pick4(t, kf), lf) & 0xffffu) + 1;
+        Nf = (uint32_t)__builtin_amdgcn_readlane(pick4(len, kf), lf);
+        run = Df < Nf;  // it overlaps its own output: the whole wave copies it
+        glob = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          cn[k] = 0;
+          if (!pend[k]) continue;
+          const bool first = k == kf && l == lf;
+          if (first || cs[k] + len[k] <= B0 + R) {  // source ends at or before R
+            if (!first || !run) cn[k] = len[k];
+            pend[k] = false;
+          }
+        }
+      }
+      // complete 16 B units of the batch to HBM
+      const uint32_t e = B0 + total;
+      for (uint32_t x = (B0 & ~15u) + 16 * (uint32_t)l; x + 16 <= e; x += 1024)
+        *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
+      olen = e;
+      cur += take;
+    }
+    // the last partial unit (the decode region is 256-aligned and sized in 256 B steps)
+    if ((olen & 15) && l == 0) {
+      const uint32_t x = olen & ~15u;
+      *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
+    }
+    if (l == 0) {
+      sp->olen2 = olen;
+      if (mode == kFlDone) d.blk_out_len[b] = olen;
+    }
+  }
+}
+
 // The blocks the fast path failed on: the exact restatement gives the
 // reference's error (and CorruptInputError offset). One wave per failing block, lane 0.
 __global__ void __launch_bounds__(64) k_inflate_exact(const uint8_t *__restrict__ span, DevBufs d,
@@ -1828,6 +2082,9 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
   const uint64_t r2 = (uint64_t)ncu * 4;  // 36 KiB windows: 4 per CU
   if (g2 > r2) g2 = r2;
   if (g2 < 1) g2 = 1;
+  uint64_t g3 = max_blocks;
+  if (g3 > (uint64_t)ncu * kL2Waves) g3 = (uint64_t)ncu * kL2Waves;
+  if (g3 < 1) g3 = 1;
   if (kFlateSync) {  // the wave-per-block Huffman pass first; k_flate_tok takes what it declines
     uint64_t gs = max_blocks;
     const uint64_t rs = (uint64_t)ncu * kSyncWaves;
@@ -1838,7 +2095,10 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
   for (int r = 0; r < rounds; r++) {
     hipLaunchKernelGGL(k_flate_tok, dim3((unsigned)g1), dim3(64), 0, st, span, d, nblocks, nchunks,
                        dec_cap, r, (int)(r == rounds - 1));
-    hipLaunchKernelGGL(k_flate_lz, dim3((unsigned)g2), dim3(64), 0, st, d, nblocks, r);
+    if (kFlateLz2)
+      hipLaunchKernelGGL(k_flate_lz2, dim3((unsigned)g3), dim3(64), 0, st, d, nblocks, r);
+    else
+      hipLaunchKernelGGL(k_flate_lz, dim3((unsigned)g2), dim3(64), 0, st, d, nblocks, r);
   }
   uint64_t ge = (max_blocks + 63) / 64;
   if (ge > 1024) ge = 1024;
