@@ -47,6 +47,10 @@ constexpr uint64_t kZLitStride = kZBlockMax + 256;  // per-wave literal buffer
 constexpr int kZWaves = 12;                          // resident zstd waves per CU (LDS ~10 KiB each)
 constexpr int kZSeqWaves = 8;                        // k_zstd_seq waves per CU (64 jobs each; every job of a C4 span in flight)
 constexpr int kZFixWaves = 8;                        // k_zstd_fix waves per CU
+#ifndef RIO_ZSTD_SEQ2
+#define RIO_ZSTD_SEQ2 1
+#endif
+constexpr bool kZstdSeq2 = RIO_ZSTD_SEQ2 != 0;  // LDS-table sequence pass (ablation builds: -DRIO_ZSTD_SEQ2=0)
 
 __constant__ uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,  12,   13,   14,   15,   16,   18,
                                      20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
@@ -341,9 +345,9 @@ __device__ int z_huf_read(ZLds &L, int *max_bits_out, const uint8_t *src, int64_
 // U: the state is wave-uniform (every lane walks the same stream): a dword is
 // made scalar only when it enters the window, never at its load (that would
 // wait for the load right there).
-template <bool U>
+template <bool U, int PF = 4>
 struct ZBrT {
-  static constexpr int kPf = 4;
+  static constexpr int kPf = PF;
   const uint32_t *w;
   int32_t bit, lo, q;
   uint32_t c0, c1, pf[kPf];
@@ -1472,6 +1476,302 @@ __global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
   }
 }
 
+// ---------------------------------------------------------------- k_zstd_seq2
+// Sequence pass with the FSE tables in LDS: four waves per CU, each decoding
+// kZs2Jobs jobs at a time (a lane per job, lanes kZs2Jobs..63 idle), each job's
+// three tables in its own LDS slot as u16 cells. 60 jobs per CU is far fewer
+// than k_zstd_seq keeps in flight, but a cell load is an LDS access (~100
+// cycles) instead of an HBM/MALL miss: with every job of a span in flight
+// (82k for C4) the tables (up to 5 KiB each) outgrow every cache, and each
+// sequence waited on a DRAM access. A cell here is the symbol (6 bits) and
+// FSE's nextState (10 bits); nbBits = log - highbit(nextState) and the new
+// state's base = (nextState << nbBits) - 2^log are recomputed per use. A job's
+// tables are loaded by the whole wave (u32 cells from k_zstd_ent); the lanes
+// then decode independently, and a lane whose job ends takes the next one.
+// Backward bitstream reader for the sequence pass. Stream dword D_i (i = 0, 1,
+// ... from the end) = w[qtop - i]. A 64-bit container holds the bits below the
+// read position (`avail` of them); a reload (when avail <= 32) shifts in
+// D_cons from the lane's 32-dword LDS ring, which k_zstd_seq2 refills group by
+// group. The sequence loop reloads before the offset, before the match /
+// literal extras and before the state updates, which bounds every read
+// (offset <= 28 bits, extras <= 16 + 16, states <= 9 + 9 + 8), so a sequence
+// takes at most 3 dwords.
+constexpr int kZs2Ring = 32;
+struct ZBr64 {
+  const uint32_t *w;
+  uint64_t win;
+  int32_t avail, qtop, lo;
+  int32_t cons, nf;  // D_cons is the next dword into the container; the ring holds [cons, nf)
+  __device__ __forceinline__ uint32_t ld(int32_t i) const { return i >= 0 ? w[i] : 0u; }
+  __device__ __forceinline__ uint32_t D(int32_t i) const { return ld(qtop - i); }
+  // D_i without the zero fill past the stream's start (a clamped address, no
+  // select on the loaded value): those bits are only read by an overrun,
+  // which is an error whatever they hold
+  __device__ __forceinline__ uint32_t Dc(int32_t i) const { return w[max(qtop - i, 0)]; }
+  // ring: this lane's kZs2Ring dwords (D_i at i mod kZs2Ring)
+  __device__ __forceinline__ void reload(const uint32_t (&ring)[kZs2Ring]) {
+    if (avail <= 32) {
+      // in the ring once retired from the registers (else a direct load: rare)
+      // the ring always holds it: >= 24 dwords at the start of every group of
+      // 8 sequences. No global load on this path (its wait would drain every
+      // load in flight).
+      const uint32_t v = ring[cons & (kZs2Ring - 1)];
+      win = (win << 32) | v;
+      cons++;
+      avail += 32;
+    }
+  }
+  __device__ __forceinline__ uint32_t read(int nb) {  // nb <= 31
+    avail -= nb;
+    return (uint32_t)(win >> avail) & ((1u << nb) - 1u);
+  }
+  // bit position above the stream's dword base: the container's low bit is D_(cons-1)'s
+  __device__ __forceinline__ int32_t pos() const { return 32 * (qtop - cons + 1) + avail; }
+  __device__ __forceinline__ bool overrun() const { return pos() < lo; }
+  __device__ __forceinline__ bool exact() const { return pos() == lo; }
+};
+
+// An empty asm that reads and rewrites x: the wait for x's load lands here.
+template <class T>
+__device__ __forceinline__ void zs2_settle(T &x) {
+  asm volatile("" : "+v"(x));
+}
+
+constexpr int kZs2Jobs = 15;
+constexpr int kZs2Cells = 512 + 512 + 256;  // ll (log <= 9), ml (<= 9), of (<= 8)
+
+__device__ __forceinline__ uint16_t zs2_cell(uint32_t c, int log) {
+  const uint32_t sym = c & 0xffu, nb = (c >> 8) & 0xffu, base = c >> 16;
+  const uint32_t ns = (base + (1u << log)) >> nb;  // FSE's nextState: base = (ns << nb) - 2^log
+  return (uint16_t)(sym | (ns << 6));
+}
+// cell -> symbol; state <- base + bits (read by the caller)
+__device__ __forceinline__ uint32_t zs2_nb(uint32_t e, int log) { return (uint32_t)(log - highbit(e >> 6)); }
+__device__ __forceinline__ uint32_t zs2_base(uint32_t e, uint32_t nb, int log) {
+  return ((e >> 6) << nb) - (1u << log);
+}
+
+__global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
+  __shared__ uint16_t tabs[4][kZs2Jobs][kZs2Cells];
+  __shared__ uint32_t rings[4][kZs2Jobs][kZs2Ring];
+  __shared__ ZCodes codes;
+  const int l = lane_id(), wv = (int)(threadIdx.x >> 6);
+  for (int u = (int)threadIdx.x; u < 36; u += 256) codes.ll[u] = kZCodes.ll[u];
+  for (int u = (int)threadIdx.x; u < 53; u += 256) codes.ml[u] = kZCodes.ml[u];
+  __syncthreads();
+  uint8_t *tok8 = reinterpret_cast<uint8_t *>(d.tok);
+  const uint64_t nj0 = d.ctl->zjob_n, nj = nj0 < d.zjob_cap ? nj0 : d.zjob_cap;
+  const bool slot = l < kZs2Jobs;
+  const int ls = slot ? l : 0;  // (indices into the __shared__ arrays, not pointers: a
+                                // selected pointer becomes a flat access that waits on vmcnt)
+  const uint64_t stride = (uint64_t)gridDim.x * 4 * kZs2Jobs;
+  uint64_t j = ((uint64_t)blockIdx.x * 4 + (uint64_t)wv) * kZs2Jobs + (uint64_t)l;
+  bool active = false, exhausted = !slot;
+  ZJob *hp = nullptr;
+  uint32_t nseq = 0, i = 0, err = 0, sll = 0, sml = 0, sof = 0;
+  int llg = 0, mlg = 0, ofg = 0;
+  uint64_t *raw = nullptr;
+  ZBr64 r;
+  for (;;) {
+    // lanes without a job take their next one (literal-only and empty jobs need no pass)
+    bool starting = false;
+    uint64_t tab_off = 0;
+    if (!active && !exhausted) {
+      for (;;) {
+        if (j >= nj) {
+          exhausted = true;
+          break;
+        }
+        hp = reinterpret_cast<ZJob *>(tok8 + d.zjob[j]);
+        j += stride;
+        const uint32_t flags = hp->flags;
+        nseq = hp->nseq;
+        if ((flags & kJLit) || nseq == 0) continue;
+        const uint32_t logs = hp->logs;
+        llg = logs & 0xff;
+        ofg = (logs >> 8) & 0xff;
+        mlg = (logs >> 16) & 0xff;
+        if (llg > 9 || mlg > 9 || ofg > 8) {  // beyond the format's accuracy logs: not from ent
+          hp->err = kZSlow;
+          continue;
+        }
+        tab_off = hp->tab_off;
+        raw = reinterpret_cast<uint64_t *>(tok8 + hp->raw_off);
+        starting = true;
+        // the job's values become plain registers here: the hot loop's first
+        // use of a value loaded on this rare path would otherwise wait for
+        // every load in flight (the loop's vmcnt bookkeeping is conservative)
+        zs2_settle(nseq);
+        zs2_settle(llg);
+        zs2_settle(mlg);
+        zs2_settle(ofg);
+        break;
+      }
+    }
+    // the starting lanes' tables into their slots, each by the whole wave
+    unsigned long long sm = __ballot(starting);
+    while (sm) {
+      const int s = __ffsll((long long)sm) - 1;
+      sm &= sm - 1;
+      const uint64_t to = readlane_u64(tab_off, s);
+      const int lg = __builtin_amdgcn_readlane(llg, s), mg = __builtin_amdgcn_readlane(mlg, s);
+      const int og = __builtin_amdgcn_readlane(ofg, s);
+      const uint32_t nll = 1u << lg, nml = 1u << mg, nof = 1u << og, n = nll + nml + nof;
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(tok8 + to);
+      uint16_t *dst = tabs[wv][s];
+      for (uint32_t k0 = 0; k0 < n; k0 += 512) {
+        uint32_t c[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const uint32_t k = k0 + 64 * q + (uint32_t)l;
+          c[q] = k < n ? src[k] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const uint32_t k = k0 + 64 * q + (uint32_t)l;
+          if (k < nll) dst[k] = zs2_cell(c[q], lg);
+          else if (k < nll + nml) dst[512 + (k - nll)] = zs2_cell(c[q], mg);
+          else if (k < n) dst[1024 + (k - nll - nml)] = zs2_cell(c[q], og);
+        }
+      }
+    }
+    if (starting) {  // the bitstream: container, ring, registers
+      i = 0;
+      err = 0;
+      const int64_t start = (int64_t)hp->seq_off, n = (int64_t)hp->seq_len;
+      const uint32_t last = n > 0 ? tok8[start + n - 1] : 0u;
+      if (last == 0) {  // empty stream or no end marker in its last byte
+        err = kZCorrupt;
+      } else {
+        r.w = reinterpret_cast<const uint32_t *>(tok8 + (start & ~3ll));
+        r.lo = 8 * (int32_t)(start & 3);
+        const int32_t P = r.lo + 8 * (int32_t)n - (8 - highbit(last));  // first bit not yet read
+        r.qtop = (P - 1) >> 5;
+        r.win = ((uint64_t)r.D(0) << 32) | r.D(1);
+        r.avail = P - 32 * (r.qtop - 1);
+        r.cons = 2;
+        // D_2 .. D_(kZs2Ring + 1) into the ring
+#pragma unroll
+        for (int t = 2; t < 2 + kZs2Ring; t++) rings[wv][ls][t & (kZs2Ring - 1)] = r.D(t);
+        r.nf = 2 + kZs2Ring;
+        sll = r.read(llg);
+        sof = r.read(ofg);
+        sml = r.read(mlg);
+        r.reload(rings[wv][ls]);
+      }
+      active = err == 0;
+      if (!active) hp->err = err;
+      zs2_settle(r.win);
+      zs2_settle(r.avail);
+      zs2_settle(r.qtop);
+      zs2_settle(r.lo);
+      zs2_settle(sll);
+      zs2_settle(sml);
+      zs2_settle(sof);
+    }
+    // top up rings below 24 dwords (a lane that outran its feed; rare: waits)
+    if (active && r.nf - r.cons < 24) {
+      const int32_t nn = r.cons + kZs2Ring;
+      for (int32_t t = r.nf; t < nn; t++) rings[wv][ls][t & (kZs2Ring - 1)] = r.D(t);
+      r.nf = nn;
+    }
+    wave_lds_sync();
+    if (!__ballot(active) && !__ballot(!exhausted)) break;
+    // Groups of 8 unrolled steps, a sequence each, until a lane needs a job
+    // or a top-up. A group starts by loading up to 8 dwords to refill the
+    // ring (the ring holds >= 24: enough for 8 sequences of <= 3 dwords) and
+    // keeps its 8 raw entries in registers; at its end the loads go into the
+    // ring and the entries out. So the group's body issues no vector memory
+    // operation whose wait would queue behind others (vmcnt counts in order),
+    // and nothing in flight crosses the loop's back edge.
+    uint64_t E0 = 0, E1 = 0, E2 = 0, E3 = 0, E4 = 0, E5 = 0, E6 = 0, E7 = 0;
+    uint32_t pi0 = 0, pne = 0;  // the previous group's entries (stored by the next group)
+    do {
+      // the previous group's entries out first: registers of a store in
+      // flight are rewritten only once it has read them, and issued before
+      // this group's loads that wait does not include them
+      if (pne > 0) raw[pi0 + 0] = E0;
+      if (pne > 1) raw[pi0 + 1] = E1;
+      if (pne > 2) raw[pi0 + 2] = E2;
+      if (pne > 3) raw[pi0 + 3] = E3;
+      if (pne > 4) raw[pi0 + 4] = E4;
+      if (pne > 5) raw[pi0 + 5] = E5;
+      if (pne > 6) raw[pi0 + 6] = E6;
+      if (pne > 7) raw[pi0 + 7] = E7;
+      const int32_t c = active ? min(8, kZs2Ring - (r.nf - r.cons)) : 0;
+      // (no initial values: writing a register whose previous load may be in
+      // flight waits for it; each L_t is read only under the condition that loads it)
+      uint32_t L0, L1, L2, L3, L4, L5, L6, L7;
+      if (c > 0) L0 = r.Dc(r.nf);
+      if (c > 1) L1 = r.Dc(r.nf + 1);
+      if (c > 2) L2 = r.Dc(r.nf + 2);
+      if (c > 3) L3 = r.Dc(r.nf + 3);
+      if (c > 4) L4 = r.Dc(r.nf + 4);
+      if (c > 5) L5 = r.Dc(r.nf + 5);
+      if (c > 6) L6 = r.Dc(r.nf + 6);
+      if (c > 7) L7 = r.Dc(r.nf + 7);
+      const uint32_t i0 = i;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if (active) {
+          const uint32_t cl = tabs[wv][ls][sll], cm = tabs[wv][ls][512 + sml], cof = tabs[wv][ls][1024 + sof];
+          const uint32_t llc = cl & 63u, mlc = cm & 63u, ofc = cof & 63u;
+          if (llc > 35 || mlc > 52 || ofc > 31) {
+            err = kZCorrupt;
+          } else if (ofc > 28) {
+            err = kZSlow;
+          } else {
+            const uint32_t mlx = codes.ml[mlc], llx = codes.ll[llc];
+            const uint32_t ofv = (1u << ofc) + r.read((int)ofc);
+            r.reload(rings[wv][ls]);
+            const uint32_t ml = (mlx & 0xFFFFFFu) + r.read((int)(mlx >> 24));
+            const uint32_t ll = (llx & 0xFFFFFFu) + r.read((int)(llx >> 24));
+            r.reload(rings[wv][ls]);
+            if (i + 1 < nseq) {
+              const uint32_t nl = zs2_nb(cl, llg), nm = zs2_nb(cm, mlg), no = zs2_nb(cof, ofg);
+              sll = zs2_base(cl, nl, llg) + r.read((int)nl);
+              sml = zs2_base(cm, nm, mlg) + r.read((int)nm);
+              sof = zs2_base(cof, no, ofg) + r.read((int)no);
+              r.reload(rings[wv][ls]);
+            }
+            if (r.overrun()) {
+              err = kZCorrupt;
+            } else {
+              uint64_t &Ek = k == 0 ? E0 : k == 1 ? E1 : k == 2 ? E2 : k == 3 ? E3 : k == 4 ? E4 : k == 5 ? E5 : k == 6 ? E6 : E7;
+              Ek = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
+              i++;
+              if (i == nseq && !r.exact()) err = kZCorrupt;
+            }
+          }
+          if (err || i == nseq) active = false;
+        }
+      }
+      // the group's loads into the ring, its entries out (entries i0 .. i - 1)
+      const uint32_t ne = i - i0;
+      if (c > 0) rings[wv][ls][(r.nf + 0) & (kZs2Ring - 1)] = L0;
+      if (c > 1) rings[wv][ls][(r.nf + 1) & (kZs2Ring - 1)] = L1;
+      if (c > 2) rings[wv][ls][(r.nf + 2) & (kZs2Ring - 1)] = L2;
+      if (c > 3) rings[wv][ls][(r.nf + 3) & (kZs2Ring - 1)] = L3;
+      if (c > 4) rings[wv][ls][(r.nf + 4) & (kZs2Ring - 1)] = L4;
+      if (c > 5) rings[wv][ls][(r.nf + 5) & (kZs2Ring - 1)] = L5;
+      if (c > 6) rings[wv][ls][(r.nf + 6) & (kZs2Ring - 1)] = L6;
+      if (c > 7) rings[wv][ls][(r.nf + 7) & (kZs2Ring - 1)] = L7;
+      if (c > 0) r.nf += c;
+      pi0 = i0;
+      pne = ne;
+      if (hp && !active && (err || (i == nseq && ne > 0))) hp->err = err;  // the job ended in this group
+    } while (!__ballot((slot && !active && !exhausted) || (active && r.nf - r.cons < 24)));
+    if (pne > 0) raw[pi0 + 0] = E0;
+    if (pne > 1) raw[pi0 + 1] = E1;
+    if (pne > 2) raw[pi0 + 2] = E2;
+    if (pne > 3) raw[pi0 + 3] = E3;
+    if (pne > 4) raw[pi0 + 4] = E4;
+    if (pne > 5) raw[pi0 + 5] = E5;
+    if (pne > 6) raw[pi0 + 6] = E6;
+    if (pne > 7) raw[pi0 + 7] = E7;
+  }
+}
+
 // ---------------------------------------------------------------- k_zstd_fix
 // In file order, one wave per recordio block: every job's raw sequences 64 at
 // a time -- repeat offsets resolved by a wave scan of history ops, the serial decoder's
@@ -1923,8 +2223,10 @@ void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long
   uint64_t g = max_blocks < grid ? max_blocks : grid;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(k_zstd_ent, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
-  static const int seq_wpc = getenv("RIO_ZSEQ_WPC") ? atoi(getenv("RIO_ZSEQ_WPC")) : kZSeqWaves;
-  hipLaunchKernelGGL(k_zstd_seq, dim3((unsigned)(grid / kZWaves * seq_wpc)), dim3(64), 0, st, d);
+  if (kZstdSeq2)  // one 4-wave workgroup per CU (its LDS is the CU's)
+    hipLaunchKernelGGL(k_zstd_seq2, dim3((unsigned)(grid / kZWaves)), dim3(256), 0, st, d);
+  else
+    hipLaunchKernelGGL(k_zstd_seq, dim3((unsigned)(grid / kZWaves * kZSeqWaves)), dim3(64), 0, st, d);
   uint64_t g3 = grid / kZWaves * kZFixWaves;
   if (g3 > max_blocks) g3 = max_blocks;
   if (g3 < 1) g3 = 1;
