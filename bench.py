@@ -72,17 +72,18 @@ def make_c1_file():
     return make_c2_file(16384)
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_c2_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_c2_pmc.json")
 
 
 def pmc_traffic(kernel: str, replicas: int):
-    """HBM bytes per launch of `kernel` from the committed PMC pass (tools/pmc.sh:
+    """HBM bytes per launch of `kernel` from the committed PMC pass (tools/profile_r02.sh:
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over this same bench command, FETCH_SIZE
     doubled per MI355X_MICROARCH.md). Only valid for the default replica count."""
     if replicas != REPLICAS or not os.path.exists(PMC_FILE):
         return None
     with open(PMC_FILE) as f:
-        e = json.load(f).get("rio::" + kernel)
+        pm = json.load(f)
+    e = pm.get("rio::" + kernel) or pm.get("rio::%s<false>" % kernel)  # k_crc is a template
     if not e:
         return None
     return int(e.get("fetch_bytes", 0) + e.get("write_bytes", 0))

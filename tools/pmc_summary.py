@@ -1,4 +1,4 @@
-"""Average per-dispatch PMC bytes per kernel from rocprofv3 counter_collection CSVs.
+"""Average per-dispatch PMC values per kernel from rocprofv3 counter_collection CSVs.
 
 FETCH_SIZE / WRITE_SIZE are in KB (1024 B). On gfx950 FETCH_SIZE reports half
 the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM section):
@@ -37,6 +37,9 @@ def main(dirs):
         if "WRITE_SIZE" in ctrs:
             v = ctrs["WRITE_SIZE"]
             e["write_bytes"] = sum(v) / len(v) * 1024
+        for c, v in ctrs.items():  # other counters: mean per dispatch
+            if c not in ("FETCH_SIZE", "WRITE_SIZE"):
+                e[c] = sum(v) / len(v)
         out[k] = e
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
