@@ -19,6 +19,7 @@
 
 #include "device_common.h"
 #include "rio_internal.h"
+#include "lz_ring.h"
 
 namespace rio {
 
@@ -1806,82 +1807,6 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
 // gfx9 wave's vector memory operations complete in issue order, so the stores
 // are done. Sources are read with agent-scope loads (from L2, never a stale L1
 // line).
-constexpr uint32_t kL2Ring = 4096, kL2Mask = kL2Ring - 1;
-constexpr uint32_t kL2Span = 1536;                   // output bytes per batch at most
-constexpr uint32_t kL2Near = kL2Ring - kL2Span - 16;  // bytes before the batch kept in the ring (the
-                                                       // batch's zeroing may round up one dword)
-constexpr int kL2Waves = 16;                          // per CU (launch sizing)
-static_assert(kL2Near >= kL2Span + 16 + 258, "HBM sources must be flushed two batches back");
-
-__device__ __forceinline__ uint32_t tok_len(uint32_t t) {
-  return (t >> 31) ? ((t >> 16) & 0xffu) + 3 : (t >> 24) & 3u;
-}
-
-__device__ __forceinline__ uint32_t pick4(const uint32_t (&a)[4], int k) {
-  return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3];
-}
-
-// Four copies at once (one per token slot; n[k] == 0: none): n[k] bytes from
-// position s[k] to t[k] (t - s >= n: no overlap), sources in HBM where bit k of
-// glob is set, else in the ring. The batch's ring bytes are zeroed first and
-// every byte belongs to one token, so a token ORs its bytes into the
-// destination dwords (an LDS atomic, in any order) -- no byte stores, no races
-// with the neighbours sharing its end dwords. Source dwords are read aligned
-// and funnel-shifted; each step issues every slot's loads before using any.
-__device__ __forceinline__ void l2_copy4(uint8_t *ring, const uint32_t *gw, const uint32_t (&s)[4], uint32_t B0,
-                                         const uint32_t (&p)[4], const uint32_t (&n)[4], uint32_t glob) {
-  uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
-  const uint8_t *g = reinterpret_cast<const uint8_t *>(gw);
-  // per slot (recomputed where used, to keep registers for occupancy): the
-  // destination t = B0 + p, its dwords [t/4, (t+n+3)/4), and the source dword
-  // under the first one, floor((s - t%4) / 4) (~0 for -1)
-  for (uint32_t D = 0;; D += 4) {
-    bool any = false;
-    uint32_t w[4][5];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t t = B0 + p[k];
-      const bool act = n[k] != 0 && (t >> 2) + D < (t + n[k] + 3) >> 2;
-      any |= act;
-      const uint32_t q = (s[k] >> 2) - ((s[k] & 3) < (t & 3) ? 1u : 0u) + D;
-#pragma unroll
-      for (int i = 0; i < 5; i++) w[k][i] = 0;
-      if (act && ((glob >> k) & 1)) {
-        // dword -1 (a source at position < 3) only feeds bytes before the
-        // destination, which are masked off: any dword will do (dword 0)
-        w[k][0] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(g + (q == 0xffffffffu ? 0u : q << 2)),
-                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint8_t *g1 = g + ((q + 1) << 2);
-#pragma unroll
-        for (int i = 1; i < 5; i++)
-          w[k][i] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(g1 + 4 * (i - 1)), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-      } else if (act) {
-#pragma unroll
-        for (int i = 0; i < 5; i++) w[k][i] = rw[(q + i) & (kL2Mask >> 2)];
-      }
-    }
-    if (!__builtin_amdgcn_ballot_w64(any)) break;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t t = B0 + p[k], d0 = t >> 2, d1 = n[k] ? (t + n[k] + 3) >> 2 : d0;
-      const uint32_t sh = 8 * ((s[k] - t) & 3);
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t Dj = d0 + D + j;
-        if (Dj < d1) {
-          const uint32_t v = __builtin_amdgcn_alignbit(w[k][j + 1], w[k][j], sh);
-          const uint32_t x0 = 4 * Dj;
-          const uint32_t lo = t > x0 ? t - x0 : 0u;                         // 0..3
-          const uint32_t hi = t + n[k] < x0 + 4 ? t + n[k] - x0 : 4u;      // 1..4
-          const uint32_t m = (0xffffffffu << (8 * lo)) & (0xffffffffu >> (8 * (4 - hi)));
-          atomicOr(&rw[Dj & (kL2Mask >> 2)], v & m);
-        }
-      }
-    }
-  }
-}
-
 __global__ void __launch_bounds__(64) k_flate_lz2(DevBufs d, const unsigned long long *nblocks, int round) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[kL2Ring];
   const int l = lane_id();

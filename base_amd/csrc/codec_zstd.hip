@@ -25,6 +25,14 @@
 
 #include "device_common.h"
 #include "rio_internal.h"
+#include "lz_ring.h"
+
+// k_zstd_exec2 (the flate copy pass's ring machinery) measured slower than
+// k_zstd_exec on C4: 65.6 against 58.6 ms (134 VGPRs: 3 waves/SIMD; every
+// literal run a global read). Built with -DRIO_ZSTD_EXEC2=1.
+#ifndef RIO_ZSTD_EXEC2
+#define RIO_ZSTD_EXEC2 0
+#endif
 
 namespace rio {
 
@@ -896,7 +904,7 @@ struct ZSerialSink {
 // split so that each is at most kZPiece bytes (copying a long match in pieces
 // with the same offset is the same copy). Frame ends are marked: ll = 0xFFFF
 // with ml = 0xFFFF (checksum = offset field) or 0xFFFE (no checksum).
-constexpr uint32_t kZPiece = 2048;
+constexpr uint32_t kZPiece = RIO_ZSTD_EXEC2 ? 512 : 2048;  // exec2: within its batch span and far-source margin
 constexpr uint32_t kZMark = 0xFFFF;
 constexpr uint32_t kZMarkCk = 0xFFFF, kZMarkNoCk = 0xFFFE;
 
@@ -1958,7 +1966,7 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
   }
 }
 
-// ---------------------------------------------------------------- k_zstd_exec
+// ---------------------------------------------------------------- k_zstd_exec (previous)
 // Execution pass, one wave per block: the entries in groups of 64, cut into
 // parts of at most kZPart output bytes (and at frame ends); per part the
 // literals are staged from the literal area into LDS, literal runs written,
@@ -2213,6 +2221,221 @@ __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, D
   }
 }
 
+#if RIO_ZSTD_EXEC2
+// ---------------------------------------------------------------- k_zstd_exec2
+// Execution pass on the copy-pass machinery of k_flate_lz2 (lz_ring.h): one
+// wave per block, a 4 KiB LDS ring, history older than the ring read back
+// from the decode region (agent-scope loads), literals read from the block's
+// literal area the same way. A batch is up to 128 entries (2 per lane), each
+// two copies -- its literal run, then its match -- whose output fits kL2Span;
+// a frame-end mark ends a batch (checksummed frames are hashed from HBM once
+// their bytes are flushed). Entries are at most kZPiece + kZPiece bytes
+// (k_zstd_fix splits longer runs and matches).
+static_assert(kL2Near >= kL2Span + 16 + kZPiece, "zstd copies from HBM must be flushed two batches back");
+static_assert(2 * kZPiece <= kL2Span, "an entry must fit a batch");
+
+__global__ void __launch_bounds__(64) k_zstd_exec2(DevBufs d, const unsigned long long *nblocks) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kL2Ring];
+  const int l = lane_id();
+  const uint64_t nb = uni64(*nblocks);
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    FlState *sp = &d.fl[b];
+    const uint32_t mode = uni(sp->mode);
+    if (mode != kZsExec && mode != kZsErrCk) continue;
+    const uint8_t *region = reinterpret_cast<const uint8_t *>(d.tok + uni64(d.blk_c0[b]) * (uint64_t)kZTokPerChunk);
+    const uint64_t lit0 = uni64(sp->bitpos), ent_end = uni64(sp->hdrpos);
+    const uint32_t ntok = uni(sp->ntok);
+    const uint64_t *ents = reinterpret_cast<const uint64_t *>(region + ent_end);  // entry e at ents[-1 - e]
+    const uint32_t *gl = reinterpret_cast<const uint32_t *>(region + lit0);       // 16-aligned
+    uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
+    const uint32_t *gw = reinterpret_cast<const uint32_t *>(out);
+    uint32_t olen = 0, litpos = 0, fstart = 0, zerr = 0;
+    wave_lds_sync();
+    uint64_t pre[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) pre[k] = (64u * k + (uint32_t)l < ntok) ? ents[-1 - (int64_t)(64 * k + l)] : 0ull;
+    uint32_t cur = 0;
+    while (cur < ntok && !zerr) {
+      uint64_t e[2];
+#pragma unroll
+      for (int k = 0; k < 2; k++) e[k] = pre[k];
+      // a frame end first in line: flush, check the frame's checksum
+      const uint64_t e0 = readlane_u64(e[0], 0);
+      if ((e0 & 0xffffu) == kZMark) {
+        if (((e0 >> 16) & 0xffffu) == kZMarkCk) {
+          if (olen & 15) {
+            if (l == 0) {
+              const uint32_t x = olen & ~15u;
+              *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
+            }
+          }
+          zmem_sync();
+          const uint32_t got = (uint32_t)z_xxh64(out + fstart, olen - fstart);
+          if (got != (uint32_t)(e0 >> 32)) {
+            zerr = kZChecksum;
+            break;
+          }
+        }
+        fstart = olen;
+        cur++;
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+          pre[k] = (cur + 64u * k + (uint32_t)l < ntok) ? ents[-1 - (int64_t)(cur + 64 * k + l)] : 0ull;
+        continue;
+      }
+      // this batch: entries up to the first mark, output within kL2Span
+      uint32_t fm = 128;
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const bool valid = cur + 64u * k + (uint32_t)l < ntok;
+        const unsigned long long m = __ballot(valid && (e[k] & 0xffffu) == kZMark);
+        if (fm == 128 && m) fm = 64 * k + (__ffsll((long long)m) - 1);
+      }
+      uint32_t ll[2], ml[2], p[2], lp[2];
+      uint32_t carry = 0, lcarry = 0, take = 0, emax = 0, lmax = 0;
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const uint32_t idx = 64 * k + (uint32_t)l;
+        const bool valid = cur + idx < ntok && idx < fm;
+        ll[k] = valid ? (uint32_t)e[k] & 0xffffu : 0u;
+        ml[k] = valid ? (uint32_t)(e[k] >> 16) & 0xffffu : 0u;
+        const uint32_t len = ll[k] + ml[k];
+        const uint32_t incl = wave_incl_sum_dpp(len) + carry;
+        const uint32_t lincl = wave_incl_sum_dpp(ll[k]) + lcarry;
+        p[k] = incl - len;
+        lp[k] = lincl - ll[k];
+        const bool ok = valid && incl <= kL2Span;  // a prefix of the entries
+        take += (uint32_t)__popcll(__ballot(ok));
+        if (ok) {
+          emax = incl;
+          lmax = lincl;
+        } else {
+          ll[k] = ml[k] = 0;
+        }
+        carry = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+        lcarry = (uint32_t)__builtin_amdgcn_readlane(lincl, 63);
+      }
+      const uint32_t total = (uint32_t)__reduce_max_sync(~0ull, emax);
+      const uint32_t ltotal = (uint32_t)__reduce_max_sync(~0ull, lmax);
+      const uint32_t B0 = olen;
+      {  // zero the batch's ring bytes (their dwords; the history bytes of the first one stay)
+        uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
+        const uint32_t z0 = (B0 + 3) >> 2, z1 = (B0 + total + 3) >> 2;
+        for (uint32_t z = z0 + (uint32_t)l; z < z1; z += 64) rw[z & (kL2Mask >> 2)] = 0u;
+        if ((B0 & 3) && l == 0) atomicAnd(&rw[(B0 >> 2) & (kL2Mask >> 2)], (1u << (8 * (B0 & 3))) - 1);
+        wave_lds_sync();
+      }
+      const uint32_t near = B0 > kL2Near ? B0 - kL2Near : 0u;  // positions >= near: in the ring
+      // slots 2k (entry k's literals, from the literal area) and 2k + 1 (its
+      // match): literals and matches sourced before the batch now, the others pending
+      uint32_t cs[4], cn[4], cp[4], dist[4], clen[4], glob = 0, litm = 0;
+      bool pend[4];
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const int a = 2 * k, m = 2 * k + 1;
+        cp[a] = p[k];
+        clen[a] = ll[k];
+        cs[a] = litpos + lp[k];
+        cn[a] = ll[k];
+        dist[a] = 0;
+        pend[a] = false;
+        if (ll[k]) {
+          glob |= 1u << a;
+          litm |= 1u << a;
+        }
+        cp[m] = p[k] + ll[k];
+        clen[m] = ml[k];
+        dist[m] = (uint32_t)(e[k] >> 32);
+        const uint32_t x = B0 + cp[m];
+        cs[m] = x - dist[m];
+        cn[m] = 0;
+        pend[m] = false;
+        if (ml[k]) {
+          if (cs[m] < near) {
+            cn[m] = ml[k];
+            glob |= 1u << m;
+          } else if (cs[m] + ml[k] <= B0) {
+            cn[m] = ml[k];
+          } else {
+            pend[m] = true;
+          }
+        }
+      }
+      // the next batch's entries (issued before this batch's stores: see k_flate_lz2)
+      const uint32_t nx = cur + take;
+#pragma unroll
+      for (int k = 0; k < 2; k++)
+        pre[k] = (nx + 64u * k + (uint32_t)l < ntok) ? ents[-1 - (int64_t)(nx + 64 * k + l)] : 0ull;
+      // the copies above, then the matches sourced inside the batch, in rounds
+      bool run = false;
+      uint32_t R = 0, Df = 0, Nf = 0;
+      for (;;) {
+        l2_copy4(ring, gw, cs, B0, cp, cn, glob, gl, litm);
+        if (run) {  // byte k of the run = byte (k mod dist) of the dist bytes before it (final)
+          const uint32_t xs = B0 + R - Df, xd = B0 + R;
+          for (uint32_t k0 = 0; k0 < Nf; k0 += 64) {
+            const uint32_t k = k0 + (uint32_t)l;
+            if (k < Nf) {
+              const uint32_t v = ring[(xs + z_umod(k, Df)) & kL2Mask];
+              atomicOr(reinterpret_cast<uint32_t *>(ring) + (((xd + k) >> 2) & (kL2Mask >> 2)), v << (8 * ((xd + k) & 3)));
+            }
+          }
+        }
+        wave_lds_sync();
+        int kf = -1, lf = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const unsigned long long mm = __ballot(pend[k]);
+          if (kf < 0 && mm) {
+            kf = k;
+            lf = __ffsll((long long)mm) - 1;
+          }
+        }
+        if (kf < 0) break;
+        // R: the first pending match; every byte before it is final
+        R = (uint32_t)__builtin_amdgcn_readlane(pick4(cp, kf), lf);
+        Df = (uint32_t)__builtin_amdgcn_readlane(pick4(dist, kf), lf);
+        Nf = (uint32_t)__builtin_amdgcn_readlane(pick4(clen, kf), lf);
+        run = Df < Nf;  // it overlaps its own output: the whole wave copies it
+        glob = 0;
+        litm = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          cn[k] = 0;
+          if (!pend[k]) continue;
+          const bool first = k == kf && l == lf;
+          if (first || cs[k] + clen[k] <= B0 + R) {  // source ends at or before R
+            if (!first || !run) cn[k] = clen[k];
+            pend[k] = false;
+          }
+        }
+      }
+      // complete 16 B units of the batch to HBM
+      const uint32_t end = B0 + total;
+      for (uint32_t x = (B0 & ~15u) + 16 * (uint32_t)l; x + 16 <= end; x += 1024)
+        *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
+      olen = end;
+      litpos += ltotal;
+      cur += take;
+    }
+    // the last partial unit (the decode region is 256-aligned and sized in 256 B steps)
+    if ((olen & 15) && l == 0) {
+      const uint32_t x = olen & ~15u;
+      *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
+    }
+    if (l == 0) {
+      if (!zerr && mode == kZsExec) {
+        d.blk_out_len[b] = olen;
+      } else {  // a checksum mismatch: the exact decoder re-decodes the block and names the error
+        sp->mode = kZsSlow;
+        atomicAdd(&d.ctl->pad[1], 1ull);
+      }
+    }
+  }
+}
+
+#endif  // RIO_ZSTD_EXEC2
+
 uint64_t zstd_grid(int ncu) { return (uint64_t)ncu * kZWaves; }
 uint64_t zstd_lit_bytes(uint64_t grid) { return grid * kZLitStride; }
 
@@ -2234,7 +2457,14 @@ void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long
   uint64_t g2 = grid / kZWaves * kZExecWaves;
   if (g2 > max_blocks) g2 = max_blocks;
   if (g2 < 1) g2 = 1;
+#if RIO_ZSTD_EXEC2
+  uint64_t g4 = (uint64_t)(grid / kZWaves) * kL2Waves;
+  if (g4 > max_blocks) g4 = max_blocks;
+  if (g4 < 1) g4 = 1;
+  hipLaunchKernelGGL(k_zstd_exec2, dim3((unsigned)g4), dim3(64), 0, st, d, nblocks);
+#else
   hipLaunchKernelGGL(k_zstd_exec, dim3((unsigned)g2), dim3(64), 0, st, d, nblocks);
+#endif
   hipLaunchKernelGGL(k_zstd, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
 }
 
