@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "pipeline.h"
@@ -164,6 +165,13 @@ struct rio_scanner {
   uint64_t cur_block = 0;
   int64_t cur_item = 0;
   std::vector<uint8_t> trailer;
+  int shard_start = 0, shard_limit = 1, shard_n = 1;
+  // rio_scanner_gather: staging, results and the gathered items' bytes
+  uint8_t *gspan = nullptr;
+  uint64_t gspan_cap = 0;
+  rio_results *gres = nullptr;
+  std::vector<uint8_t> gbytes;
+  std::vector<uint64_t> goff;
 
   void set_err(const rio_error &e) {
     if (!err_set) {
@@ -425,6 +433,9 @@ rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int l
   rio_scanner *s = new rio_scanner();
   s->ctx = ctx;
   s->res = rio_results_new();
+  s->shard_start = start;
+  s->shard_limit = limit;
+  s->shard_n = nshard;
   s->r = *r;
   s->file_size = r->size < 0 ? 0 : (uint64_t)r->size;
   // NewShardScanner (scannerv2.go:211-235)
@@ -639,10 +650,148 @@ int rio_scanner_version(rio_scanner *s) {
   return 2;
 }
 
+// Gather: the items at n ItemLocations, as n Seek + Scan +
+// Get calls would return them (scannerv2.go:348-361, 390-403), with the
+// distinct blocks read and decoded as one batch: each block's chunks (its
+// first chunk header gives their count, chunk.go:31-53) are staged back to
+// back and run through the pipeline at once. A location whose block did not
+// decode cleanly in the batch, or whose item index is out of range, is
+// resolved exactly as Seek + Scan on a scanner of the same file and shard
+// (its error is the one Seek / Scan would set). The scan position is
+// untouched. Views stay valid until the next gather on this scanner.
+int64_t rio_scanner_gather(rio_scanner *s, const uint64_t *blocks, const int64_t *items, int64_t n,
+                           const uint8_t **data, uint64_t *lens, rio_error *err) {
+  rio_error err_local;
+  if (!err) err = &err_local;
+  memset(err, 0, sizeof(*err));
+  if (!s || n < 0 || (n > 0 && (!blocks || !items || !data || !lens))) return -1;
+  if (s->error_scanner || s->err_set) {  // a scanner that failed to open: its error
+    *err = s->err;
+    return 0;
+  }
+  if (!s->gres) s->gres = rio_results_new();
+  s->gbytes.clear();
+  s->goff.assign((size_t)n, UINT64_MAX);
+  std::vector<uint64_t> uniq(blocks, blocks + n);
+  std::sort(uniq.begin(), uniq.end());
+  uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+  // per distinct block: its extent, then (after decoding) its items
+  struct Blk {
+    uint64_t off = 0, bytes = 0, span_at = 0;
+    bool ok = false;
+    std::vector<uint64_t> item_pos;  // offsets into gbytes, and lengths
+    std::vector<uint64_t> item_len;
+  };
+  std::vector<Blk> bl(uniq.size());
+  for (size_t i = 0; i < uniq.size(); i++) {
+    bl[i].off = uniq[i];
+    uint8_t hdr[RIO_CHUNK_HEADER_SIZE];
+    int st;
+    if (uniq[i] % kCk != 0 || uniq[i] >= s->file_size) continue;  // the exact path reports it
+    s->read_full(hdr, sizeof(hdr), uniq[i], &st);
+    if (st != 0) continue;
+    uint32_t total, index;
+    memcpy(&total, hdr + 20, 4);
+    memcpy(&index, hdr + 24, 4);
+    if (index != 0 || total == 0) continue;
+    const uint64_t bytes = (uint64_t)total * kCk;
+    if (uniq[i] + bytes > s->file_size || bytes > rio_ctx_max_span(s->ctx)) continue;
+    bl[i].bytes = bytes;
+  }
+  // batches of blocks up to the ctx's span capacity
+  const uint64_t maxspan = rio_ctx_max_span(s->ctx);
+  size_t i0 = 0;
+  while (i0 < bl.size()) {
+    uint64_t used = 0;
+    size_t i1 = i0;
+    while (i1 < bl.size() && (bl[i1].bytes == 0 || used + bl[i1].bytes <= maxspan)) used += bl[i1++].bytes;
+    if (used) {
+      if (rio_scanner::ensure_buf(&s->gspan, &s->gspan_cap, used)) {
+        rio_set_error(err, RIO_ERR_HIP, 0, "pinned allocation failed");
+        return 0;
+      }
+      uint64_t at = 0;
+      bool io_ok = true;
+      for (size_t k = i0; k < i1 && io_ok; k++) {
+        if (!bl[k].bytes) continue;
+        int st;
+        s->read_full(s->gspan + at, bl[k].bytes, bl[k].off, &st);
+        if (st != 0) bl[k].bytes = 0;  // short read: the exact path reports it
+        bl[k].span_at = at;
+        at += bl[k].bytes;
+      }
+      rio_batch b;
+      if (at && rio_scan_span_mode(s->ctx, s->gspan, at, 0, 1, UINT64_MAX, s->codec, 0, s->gres, &b) != 0) {
+        rio_set_error(err, RIO_ERR_HIP, 0, "%s", rio_last_error());
+        return 0;
+      }
+      if (at) {
+        // blocks decoded before the batch's first error (if any) are good
+        size_t k = i0;
+        for (uint64_t j = 0; j < b.n_blocks; j++) {
+          const uint64_t so = b.block_file_off[j];
+          while (k < i1 && (bl[k].bytes == 0 || bl[k].span_at < so)) k++;
+          if (k >= i1 || bl[k].span_at != so) break;  // a block the batch split: not trusted
+          Blk &B = bl[k];
+          const uint64_t f = b.block_first_item[j], e = b.block_first_item[j + 1];
+          for (uint64_t it = f; it < e; it++) {
+            uint64_t len = 0;
+            const uint8_t *p = batch_item(b, it, &len);
+            B.item_pos.push_back(s->gbytes.size());
+            B.item_len.push_back(len);
+            s->gbytes.insert(s->gbytes.end(), p, p + len);
+          }
+          B.ok = true;  // (the batch's blocks end before its first error)
+        }
+      }
+    }
+    i0 = i1 > i0 ? i1 : i0 + 1;
+  }
+  // the locations, in order
+  for (int64_t i = 0; i < n; i++) {
+    const size_t k = (size_t)(std::lower_bound(uniq.begin(), uniq.end(), blocks[i]) - uniq.begin());
+    const Blk &B = bl[k];
+    if (B.ok && items[i] >= 0 && (uint64_t)items[i] < B.item_pos.size()) {
+      s->goff[(size_t)i] = B.item_pos[(size_t)items[i]];
+      lens[i] = B.item_len[(size_t)items[i]];
+      continue;
+    }
+    // exact: Seek + Scan + Get on a scanner of the same file and shard
+    rio_scanner *t = rio_scanner_new(s->ctx, &s->r, s->shard_start, s->shard_limit, s->shard_n);
+    rio_error te{};
+    bool got = false;
+    if (!rio_scanner_err(t, &te)) {
+      rio_scanner_seek(t, blocks[i], items[i]);
+      if (!rio_scanner_err(t, &te) && rio_scanner_scan(t)) {
+        const uint8_t *p = nullptr;
+        uint64_t len = 0;
+        rio_scanner_get(t, &p, &len);
+        s->goff[(size_t)i] = s->gbytes.size();
+        lens[i] = len;
+        s->gbytes.insert(s->gbytes.end(), p, p + len);
+        got = true;
+      } else if (!rio_scanner_err(t, &te)) {  // Scan found nothing (EOF / a trailer): no item
+        rio_set_error(&te, RIO_ERR_LOCATION, blocks[i], "no item at {Block:%" PRIu64 " Item:%" PRId64 "}",
+                      blocks[i], items[i]);
+      }
+    }
+    rio_scanner_finish(t, nullptr);
+    if (!got) {
+      *err = te;
+      for (int64_t q = 0; q < i; q++) data[q] = s->gbytes.data() + s->goff[(size_t)q];
+      return i;
+    }
+  }
+  for (int64_t q = 0; q < n; q++) data[q] = s->gbytes.data() + s->goff[(size_t)q];
+  return n;
+}
+
 int rio_scanner_finish(rio_scanner *s, rio_error *err) {
   if (!s) return 0;
   int rc = rio_scanner_err(s, err);
   if (s->span) hipHostFree(s->span);
+  if (s->gspan) hipHostFree(s->gspan);
+  rio_results_free(s->gres);
   rio_results_free(s->res);
   delete s;
   return rc;

@@ -68,7 +68,7 @@ EXPORTS = [
     "rio_scan_span", "rio_scan_device", "rio_scan_device_async", "rio_sync", "rio_stage_times", "rio_decode_block",
     "rio_scanner_new", "rio_scanner_scan", "rio_scanner_get", "rio_scanner_next_batch", "rio_scanner_err",
     "rio_scanner_header_len", "rio_scanner_header_kv", "rio_scanner_trailer", "rio_scanner_seek",
-    "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish",
+    "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish", "rio_scanner_gather",
 ]
 
 _lib = None
@@ -132,6 +132,9 @@ def load(path: str = LIB_PATH):
         L.rio_scanner_version.argtypes = [P]
         L.rio_scanner_finish.restype = ctypes.c_int
         L.rio_scanner_finish.argtypes = [P, ctypes.POINTER(RioError)]
+        L.rio_scanner_gather.restype = I64
+        L.rio_scanner_gather.argtypes = [P, ctypes.POINTER(U64), ctypes.POINTER(I64), I64,
+                                         ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(U64), ctypes.POINTER(RioError)]
         _lib = L
         return L
 
@@ -433,6 +436,28 @@ class Scanner:
 
     def Seek(self, loc: ItemLocation):
         self.L.rio_scanner_seek(self.h, loc.Block, loc.Item)
+
+    def Gather(self, locs: List[ItemLocation]) -> List[bytes]:
+        """rio_scanner_gather: the raw items at locs (as Seek + Scan + Get each),
+        their blocks decoded as one batch. Raises RecordioError (with .index,
+        the first failing location, and .items, those before it) on the error
+        Seek / Scan would set there. The scan position is untouched."""
+        n = len(locs)
+        blocks = (ctypes.c_uint64 * max(n, 1))(*[int(x.Block) for x in locs])
+        items = (ctypes.c_int64 * max(n, 1))(*[int(x.Item) for x in locs])
+        ptrs = (ctypes.c_void_p * max(n, 1))()
+        lens = (ctypes.c_uint64 * max(n, 1))()
+        e = RioError()
+        k = self.L.rio_scanner_gather(self.h, blocks, items, n, ptrs, lens, ctypes.byref(e))
+        if k < 0:
+            raise ValueError("rio_scanner_gather: bad arguments")
+        got = [ctypes.string_at(ptrs[i], lens[i]) if lens[i] else b"" for i in range(k)]
+        if k < n:
+            err = _err(e)
+            err.index = k
+            err.items = got
+            raise err
+        return got
 
     def Trailer(self) -> Optional[bytes]:
         p = ctypes.c_void_p()

@@ -217,6 +217,15 @@ int rio_scanner_header_kv(rio_scanner *s, int i, const char **key, int32_t *type
 int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len);
 /* Seek (scannerv2.go:348-361) to ItemLocation{block, item} */
 void rio_scanner_seek(rio_scanner *s, uint64_t block, int64_t item);
+/* Gather (random access): the items at n ItemLocations
+ * {blocks[i], items[i]}, as Seek + Scan + Get would return them
+ * (scannerv2.go:348-361, 390-403), the distinct blocks decoded as one batch.
+ * Returns n, or the index of the first location that fails (err filled with
+ * the error Seek / Scan sets there; views before it are valid), or -1 on bad
+ * arguments. The scan position is untouched; views stay valid until the next
+ * gather on this scanner. */
+int64_t rio_scanner_gather(rio_scanner *s, const uint64_t *blocks, const int64_t *items, int64_t n,
+                           const uint8_t **data, uint64_t *lens, rio_error *err);
 /* ItemLocation of the current record */
 void rio_scanner_location(rio_scanner *s, uint64_t *block, int64_t *item);
 /* Version (scannerv2.go:308): 2 */
