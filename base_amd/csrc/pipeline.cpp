@@ -15,7 +15,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "pipeline.h"
@@ -118,6 +120,12 @@ struct rio_ctx {
   rio_results res;       // host results of rio_scan_span (scanners bring their own)
   uint8_t *h_stage = nullptr;  // pinned staging of rio_decode_block's chunk stream
   uint64_t h_stage_cap = 0;
+  // pools of pinned host buffers and result sets that finished scanners hand
+  // back (a scanner per file would otherwise pin and unpin hundreds of MB
+  // per file: SURVEY.md §8(f) 2, cf. file/internal/s3bufpool)
+  std::mutex pool_mu;
+  std::vector<std::pair<uint8_t *, uint64_t>> buf_pool;
+  std::vector<rio_results *> res_pool;
   // last async call
   uint64_t last_nchunks = 0, last_file_off = 0, last_in_bytes = 0;
   int32_t last_codec = 0, last_mode = 0;
@@ -228,11 +236,71 @@ rio_ctx *rio_open(const rio_config *cfg) {
   return c;
 }
 
+constexpr size_t kPoolMax = 8;  // pooled pinned buffers (and result sets) per ctx
+
+int rio_ctx_take_buf(rio_ctx *c, uint64_t need, uint8_t **p, uint64_t *cap) {
+  {
+    std::lock_guard<std::mutex> g(c->pool_mu);
+    size_t best = c->buf_pool.size();
+    for (size_t i = 0; i < c->buf_pool.size(); i++)  // the smallest that fits
+      if (c->buf_pool[i].second >= need && (best == c->buf_pool.size() || c->buf_pool[i].second < c->buf_pool[best].second))
+        best = i;
+    if (best < c->buf_pool.size()) {
+      *p = c->buf_pool[best].first;
+      *cap = c->buf_pool[best].second;
+      c->buf_pool.erase(c->buf_pool.begin() + (long)best);
+      return 0;
+    }
+  }
+  *p = nullptr;
+  *cap = 0;
+  if (hipHostMalloc((void **)p, need, hipHostMallocDefault) != hipSuccess) {
+    *p = nullptr;
+    return -1;
+  }
+  *cap = need;
+  return 0;
+}
+
+void rio_ctx_give_buf(rio_ctx *c, uint8_t *p, uint64_t cap) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> g(c->pool_mu);
+    if (c->buf_pool.size() < kPoolMax) {
+      c->buf_pool.emplace_back(p, cap);
+      return;
+    }
+  }
+  hipHostFree(p);
+}
+
+rio_results *rio_ctx_take_results(rio_ctx *c) {
+  std::lock_guard<std::mutex> g(c->pool_mu);
+  if (c->res_pool.empty()) return rio_results_new();
+  rio_results *r = c->res_pool.back();
+  c->res_pool.pop_back();
+  return r;
+}
+
+void rio_ctx_give_results(rio_ctx *c, rio_results *r) {
+  if (!r) return;
+  {
+    std::lock_guard<std::mutex> g(c->pool_mu);
+    if (c->res_pool.size() < kPoolMax) {
+      c->res_pool.push_back(r);
+      return;
+    }
+  }
+  rio_results_free(r);
+}
+
 void rio_close(rio_ctx *ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->st);
   if (ctx->st2 != ctx->st) hipStreamSynchronize(ctx->st2);
+  for (auto &b : ctx->buf_pool) hipHostFree(b.first);
+  for (rio_results *r : ctx->res_pool) rio_results_free(r);
   free_all(ctx);
   delete ctx;
 }

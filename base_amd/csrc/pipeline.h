@@ -17,6 +17,11 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
                        int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res,
                        rio_batch *out);
 uint64_t rio_ctx_max_span(rio_ctx *c);
+// the ctx's pools of pinned buffers and result sets (scanners borrow and return them)
+int rio_ctx_take_buf(rio_ctx *c, uint64_t need, uint8_t **p, uint64_t *cap);
+void rio_ctx_give_buf(rio_ctx *c, uint8_t *p, uint64_t cap);
+rio_results *rio_ctx_take_results(rio_ctx *c);
+void rio_ctx_give_results(rio_ctx *c, rio_results *r);
 extern "C" void rio_set_error(rio_error *e, int32_t code, uint64_t file_off, const char *fmt, ...);
 
 namespace rio {

@@ -12,6 +12,7 @@
 
 #include <string>
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "pipeline.h"
@@ -166,6 +167,41 @@ struct rio_scanner {
   int64_t cur_item = 0;
   std::vector<uint8_t> trailer;
   int shard_start = 0, shard_limit = 1, shard_n = 1;
+  // Read-ahead: while the caller consumes a batch, a
+  // thread reads the file bytes after its span into the other pinned buffer
+  // (kRaRoom bytes of room in front of them); the next span is the previous
+  // span's unconsumed tail (a partial block, copied into that room) followed
+  // by those bytes. Only file reads run on the thread, never the ctx.
+  static constexpr uint64_t kRaRoom = 8ull << 20;
+  uint8_t *ra_buf = nullptr;
+  uint64_t ra_cap = 0;
+  std::thread ra_th;
+  bool ra_running = false, ra_valid = false;
+  uint64_t ra_at = 0, ra_len = 0, ra_got = 0;  // prefetched file bytes [ra_at, ra_at + ra_got)
+  int ra_st = 0;
+  const uint8_t *span_data = nullptr;  // the current batch's span bytes (views point into them)
+  uint64_t span_at = 0, span_n = 0;    // its file offset and length
+  void ra_join() {
+    if (ra_running) {
+      ra_th.join();
+      ra_running = false;
+    }
+  }
+  void ra_drop() {
+    ra_join();
+    ra_valid = false;
+  }
+  void ra_start(uint64_t at, uint64_t len) {  // read [at, at + len) into ra_buf + kRaRoom
+    ra_drop();
+    if (len == 0 || ensure_buf(&ra_buf, &ra_cap, kRaRoom + rio_ctx_max_span(ctx))) return;
+    ra_at = at;
+    ra_len = len;
+    ra_got = 0;
+    ra_st = 0;
+    ra_valid = true;
+    ra_running = true;
+    ra_th = std::thread([this] { ra_got = read_full(ra_buf + kRaRoom, ra_len, ra_at, &ra_st); });
+  }
   // rio_scanner_gather: staging, results and the gathered items' bytes
   uint8_t *gspan = nullptr;
   uint64_t gspan_cap = 0;
@@ -190,7 +226,7 @@ struct rio_scanner {
     err_set = true;
   }
   // io.ReadFull at off: returns bytes read; *st 0 ok, 1 EOF, 2 unexpected EOF, 3 io error
-  uint64_t read_full(uint8_t *buf, uint64_t n, uint64_t at, int *st) {
+  uint64_t read_serial(uint8_t *buf, uint64_t n, uint64_t at, int *st) const {
     uint64_t got = 0;
     while (got < n) {
       int64_t k = r.read_at(r.user, buf + got, n - got, at + got);
@@ -204,14 +240,51 @@ struct rio_scanner {
     *st = (got == n) ? 0 : (got == 0 ? 1 : 2);
     return got;
   }
-  static int ensure_buf(uint8_t **buf, uint64_t *cap, uint64_t n) {
+  // Large reads run as parallel range reads of kPiece bytes (the reader is an
+  // io.ReaderAt: concurrent ReadAt calls are allowed), like the reference's
+  // S3 reader's parallel chunk reads (file/s3file/file_chunk_read.go:72-102).
+  static constexpr uint64_t kPiece = 16ull << 20;
+  static constexpr int kReaders = 8;
+  uint64_t read_full(uint8_t *buf, uint64_t n, uint64_t at, int *st) const {
+    if (n < 2 * kPiece) return read_serial(buf, n, at, st);
+    const uint64_t np = (n + kPiece - 1) / kPiece;
+    std::vector<uint64_t> got(np, 0);
+    std::vector<int> pst(np, 0);
+    std::vector<std::thread> th;
+    const int nt = (int)(np < (uint64_t)kReaders ? np : (uint64_t)kReaders);
+    for (int t = 0; t < nt; t++)
+      th.emplace_back([&, t] {
+        for (uint64_t i = (uint64_t)t; i < np; i += (uint64_t)nt) {
+          const uint64_t o = i * kPiece, len = n - o < kPiece ? n - o : kPiece;
+          got[i] = read_serial(buf + o, len, at + o, &pst[i]);
+        }
+      });
+    for (auto &x : th) x.join();
+    uint64_t total = 0;  // the bytes read contiguously from `at`, and why they stop
+    for (uint64_t i = 0; i < np; i++) {
+      total += got[i];
+      if (pst[i] == 3) {
+        *st = 3;
+        return total;
+      }
+      const uint64_t len = n - i * kPiece < kPiece ? n - i * kPiece : kPiece;
+      if (got[i] < len) break;
+    }
+    *st = (total == n) ? 0 : (total == 0 ? 1 : 2);
+    return total;
+  }
+  // pinned staging of at least n bytes, from (and back to) the ctx's pool
+  int ensure_buf(uint8_t **buf, uint64_t *cap, uint64_t n) {
     if (*cap >= n) return 0;
-    if (*buf) hipHostFree(*buf);
+    rio_ctx_give_buf(ctx, *buf, *cap);
     *buf = nullptr;
     *cap = 0;
-    if (hipHostMalloc((void **)buf, n, hipHostMallocDefault) != hipSuccess) return -1;
-    *cap = n;
-    return 0;
+    return rio_ctx_take_buf(ctx, n, buf, cap);
+  }
+  void give_buf(uint8_t **buf, uint64_t *cap) {
+    if (*buf) rio_ctx_give_buf(ctx, *buf, *cap);
+    *buf = nullptr;
+    *cap = 0;
   }
   // read [at, at+n) into *buf and decode it on the GPU into *rs
   int decode_into(uint8_t **buf, uint64_t *cap, rio_results *rs, uint64_t at, uint64_t n, int32_t cdc, int32_t mode,
@@ -234,7 +307,35 @@ struct rio_scanner {
     return rio_scan_span_mode(ctx, *buf, got, at, is_end, lim, cdc, mode, rs, out);
   }
   int decode(uint64_t at, uint64_t n, int32_t cdc, int32_t mode, uint64_t lim, rio_batch *out) {
+    ra_drop();
+    span_data = nullptr;
     return decode_into(&span, &span_cap, res, at, n, cdc, mode, lim, out);
+  }
+  // the body's next span [at, at + n): from the read-ahead when it holds it
+  int decode_body(uint64_t at, uint64_t n, rio_batch *out) {
+    ra_join();
+    const uint64_t pend = span_at + span_n;  // where the previous span ended
+    if (ra_valid && span_data && ra_at == pend && at >= span_at && at <= pend && pend - at <= kRaRoom &&
+        ra_st == 0 && at + n <= pend + ra_got) {
+      const uint64_t t = pend - at;  // the previous span's unconsumed tail
+      uint8_t *base = ra_buf + kRaRoom - t;
+      if (t) memcpy(base, span_data + (at - span_at), t);
+      ra_valid = false;
+      std::swap(span, ra_buf);  // the batch's views will point into this buffer
+      std::swap(span_cap, ra_cap);
+      const int is_end = (at + n >= file_size);
+      const int rc = rio_scan_span_mode(ctx, base, n, at, is_end, limit, codec, 0, res, out);
+      span_data = base;
+      span_at = at;
+      span_n = n;
+      return rc;
+    }
+    ra_valid = false;
+    const int rc = decode_into(&span, &span_cap, res, at, n, codec, 0, limit, out);
+    span_data = span;
+    span_at = at;
+    span_n = n;
+    return rc;
   }
 };
 
@@ -249,9 +350,18 @@ bool has_trailer(const rio_scanner *s) {  // header.go:242-254
 }
 
 void read_header(rio_scanner *s) {
-  // readSpecialBlock(MagicHeader, idTransform) (scannerv2.go:260-306)
+  // readSpecialBlock(MagicHeader, idTransform) (scannerv2.go:260-306): the
+  // header block's chunks (its first chunk's `total`), not a whole span
   const uint64_t maxspan = rio_ctx_max_span(s->ctx);
   uint64_t n = s->file_size < maxspan ? s->file_size : maxspan;
+  {
+    uint8_t hdr[RIO_CHUNK_HEADER_SIZE];
+    int st;
+    s->read_serial(hdr, sizeof(hdr), 0, &st);
+    uint32_t total;
+    memcpy(&total, hdr + 20, 4);
+    if (st == 0 && total > 0 && (uint64_t)total * kCk < n) n = (uint64_t)total * kCk;
+  }
   rio_batch b;
   if (s->decode(0, n, RIO_CODEC_NONE, 1, UINT64_MAX, &b) != 0) {
     s->set_errf(RIO_ERR_HIP, 0, "%s", rio_last_error());
@@ -366,7 +476,7 @@ bool next_batch(rio_scanner *s) {
     uint64_t n = s->file_size - s->off;
     if (n > maxspan) n = maxspan;
     rio_batch &b = s->batch;
-    if (s->decode(s->off, n, s->codec, 0, s->limit, &b) != 0) {
+    if (s->decode_body(s->off, n, &b) != 0) {
       s->set_errf(RIO_ERR_HIP, s->off, "%s", rio_last_error());
       return false;
     }
@@ -391,6 +501,12 @@ bool next_batch(rio_scanner *s) {
         return false;
       }
       s->off += b.consumed;
+      // the bytes after this span, read while the batch is consumed
+      const uint64_t end = s->span_at + s->span_n;
+      if (end < s->file_size && s->off < s->limit) {
+        const uint64_t left = s->file_size - end;
+        s->ra_start(end, left < maxspan ? left : maxspan);
+      }
     }
     if (b.n_items > 0) return true;
     if (s->pending_set) {
@@ -404,6 +520,22 @@ bool next_batch(rio_scanner *s) {
 }  // namespace
 
 extern "C" {
+
+static int64_t memory_read_at(void *user, uint8_t *buf, uint64_t n, uint64_t off) {
+  const rio_memory *m = static_cast<const rio_memory *>(user);
+  if (off >= m->size) return 0;
+  const uint64_t k = n < m->size - off ? n : m->size - off;
+  memcpy(buf, m->data + off, k);
+  return (int64_t)k;
+}
+
+rio_reader rio_memory_reader(const rio_memory *m) {
+  rio_reader r;
+  r.user = const_cast<rio_memory *>(m);
+  r.read_at = memory_read_at;
+  r.size = m ? (int64_t)m->size : 0;
+  return r;
+}
 
 int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec, rio_error *err) {
   // registry.getTransformers (registry.go:51-73): split on the first space
@@ -432,7 +564,7 @@ int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec,
 rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int limit, int nshard) {
   rio_scanner *s = new rio_scanner();
   s->ctx = ctx;
-  s->res = rio_results_new();
+  s->res = ctx ? rio_ctx_take_results(ctx) : rio_results_new();
   s->shard_start = start;
   s->shard_limit = limit;
   s->shard_n = nshard;
@@ -549,15 +681,17 @@ int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len) {
   }
   uint8_t *tspan = nullptr;
   uint64_t tcap = 0;
-  rio_results *tres = rio_results_new();
+  rio_results *tres = rio_ctx_take_results(s->ctx);
   struct Cleanup {
+    rio_scanner *s;
     uint8_t *&p;
+    uint64_t &cap;
     rio_results *r;
     ~Cleanup() {
-      if (p) hipHostFree(p);
-      rio_results_free(r);
+      s->give_buf(&p, &cap);
+      rio_ctx_give_results(s->ctx, r);
     }
-  } cleanup{tspan, tres};
+  } cleanup{s, tspan, tcap, tres};
   const uint64_t last = s->file_size - kCk;
   rio_batch b;
   // the last chunk alone: its size/CRC first (readChunk), then its magic
@@ -626,6 +760,7 @@ void rio_scanner_seek(rio_scanner *s, uint64_t block, int64_t item) {
     return;
   }
   // Seek (scannerv2.go:348-361): restart at the block, skip `item` items
+  s->ra_drop();
   s->have_batch = false;
   s->pending_set = false;
   s->done = false;
@@ -669,7 +804,7 @@ int64_t rio_scanner_gather(rio_scanner *s, const uint64_t *blocks, const int64_t
     *err = s->err;
     return 0;
   }
-  if (!s->gres) s->gres = rio_results_new();
+  if (!s->gres) s->gres = rio_ctx_take_results(s->ctx);
   s->gbytes.clear();
   s->goff.assign((size_t)n, UINT64_MAX);
   std::vector<uint64_t> uniq(blocks, blocks + n);
@@ -706,7 +841,7 @@ int64_t rio_scanner_gather(rio_scanner *s, const uint64_t *blocks, const int64_t
     size_t i1 = i0;
     while (i1 < bl.size() && (bl[i1].bytes == 0 || used + bl[i1].bytes <= maxspan)) used += bl[i1++].bytes;
     if (used) {
-      if (rio_scanner::ensure_buf(&s->gspan, &s->gspan_cap, used)) {
+      if (s->ensure_buf(&s->gspan, &s->gspan_cap, used)) {
         rio_set_error(err, RIO_ERR_HIP, 0, "pinned allocation failed");
         return 0;
       }
@@ -789,10 +924,16 @@ int64_t rio_scanner_gather(rio_scanner *s, const uint64_t *blocks, const int64_t
 int rio_scanner_finish(rio_scanner *s, rio_error *err) {
   if (!s) return 0;
   int rc = rio_scanner_err(s, err);
-  if (s->span) hipHostFree(s->span);
-  if (s->gspan) hipHostFree(s->gspan);
-  rio_results_free(s->gres);
-  rio_results_free(s->res);
+  s->ra_drop();
+  if (s->ctx) {  // buffers and result sets back to the ctx's pools
+    s->give_buf(&s->span, &s->span_cap);
+    s->give_buf(&s->ra_buf, &s->ra_cap);
+    s->give_buf(&s->gspan, &s->gspan_cap);
+    rio_ctx_give_results(s->ctx, s->gres);
+    rio_ctx_give_results(s->ctx, s->res);
+  } else {
+    rio_results_free(s->res);
+  }
   delete s;
   return rc;
 }

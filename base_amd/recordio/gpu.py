@@ -62,6 +62,10 @@ class RioReader(ctypes.Structure):
     _fields_ = [("user", ctypes.c_void_p), ("read_at", READ_AT), ("size", ctypes.c_int64)]
 
 
+class RioMemory(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("size", ctypes.c_uint64)]
+
+
 # every symbol include/rio_gpu.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "rio_open", "rio_close", "rio_last_error", "rio_abi_version", "rio_stream", "rio_codec_for_transformers",
@@ -69,6 +73,7 @@ EXPORTS = [
     "rio_scanner_new", "rio_scanner_scan", "rio_scanner_get", "rio_scanner_next_batch", "rio_scanner_err",
     "rio_scanner_header_len", "rio_scanner_header_kv", "rio_scanner_trailer", "rio_scanner_seek",
     "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish", "rio_scanner_gather",
+    "rio_memory_reader",
 ]
 
 _lib = None
@@ -132,6 +137,8 @@ def load(path: str = LIB_PATH):
         L.rio_scanner_version.argtypes = [P]
         L.rio_scanner_finish.restype = ctypes.c_int
         L.rio_scanner_finish.argtypes = [P, ctypes.POINTER(RioError)]
+        L.rio_memory_reader.restype = RioReader
+        L.rio_memory_reader.argtypes = [ctypes.POINTER(RioMemory)]
         L.rio_scanner_gather.restype = I64
         L.rio_scanner_gather.argtypes = [P, ctypes.POINTER(U64), ctypes.POINTER(I64), I64,
                                          ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(U64), ctypes.POINTER(RioError)]
@@ -333,16 +340,42 @@ class _BytesReader:
         self.cb = READ_AT(read_at)
 
 
+class MemorySource:
+    """A file held in host memory, read by the library's own reader
+    (rio_memory_reader): no Python callback on the read path. `buf` is any
+    object with the buffer protocol (bytes, bytearray, numpy array, pinned
+    torch tensor via .numpy()); it is kept alive here."""
+
+    def __init__(self, buf):
+        import numpy as np
+        self._arr = np.frombuffer(buf, dtype=np.uint8)
+        self.size = int(self._arr.size)
+        self.mem = RioMemory(self._arr.ctypes.data if self.size else None, self.size)
+
+
 class _FileReader:
+    """io.ReaderAt over a file object: os.pread when it has a descriptor,
+    else seek + read under a lock (the scanner's read-ahead thread and the
+    caller's thread -- Trailer, Gather -- may read at once)."""
+
     def __init__(self, f):
         self.f = f
         f.seek(0, os.SEEK_END)
         self.size = f.tell()
+        self._lock = threading.Lock()
+        try:
+            self._fd = f.fileno()
+        except (AttributeError, OSError, ValueError):
+            self._fd = None
 
         def read_at(user, buf, n, off):
             try:
-                self.f.seek(off)
-                b = self.f.read(n)
+                if self._fd is not None:
+                    b = os.pread(self._fd, n, off)
+                else:
+                    with self._lock:
+                        self.f.seek(off)
+                        b = self.f.read(n)
             except Exception:
                 return -1
             ctypes.memmove(buf, b, len(b))
@@ -366,8 +399,12 @@ class Scanner:
         self.L = self.ctx.L
         self.opts = opts or ScannerOpts()
         self.unmarshal = self.opts.Unmarshal or (lambda b: b)
-        self._rd = _BytesReader(src) if isinstance(src, (bytes, bytearray, memoryview)) else _FileReader(src)
-        self._rr = RioReader(None, self._rd.cb, self._rd.size)
+        if isinstance(src, MemorySource):  # rio_memory_reader: reads are a memcpy in C (any thread)
+            self._rd = src
+            self._rr = self.L.rio_memory_reader(ctypes.byref(src.mem))
+        else:
+            self._rd = _BytesReader(src) if isinstance(src, (bytes, bytearray, memoryview)) else _FileReader(src)
+            self._rr = RioReader(None, self._rd.cb, self._rd.size)
         self.h = self.L.rio_scanner_new(self.ctx.h, ctypes.byref(self._rr), start, limit, nshard)
         self._item = None
         self._err = None

@@ -195,6 +195,14 @@ typedef struct rio_reader {
     int64_t size; /* file size in bytes */
 } rio_reader;
 
+/* A reader over a file already in host memory (the caller keeps *m alive
+ * while scanners use the reader): read_at is a memcpy, safe from any thread. */
+typedef struct rio_memory {
+    const uint8_t *data;
+    uint64_t size;
+} rio_memory;
+rio_reader rio_memory_reader(const rio_memory *m);
+
 typedef struct rio_scanner rio_scanner;
 
 /* NewScanner / NewShardScanner (scannerv2.go:200-235). The reader is used

@@ -83,3 +83,34 @@ def test_gather_many_batches(oracle):
     assert sc.Gather([ItemLocation(*ref.locations[i]) for i in idx]) == [recs[i] for i in idx]
     sc.Finish()
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transformers", CODECS)
+def test_memory_reader_and_readahead(oracle, transformers):
+    """rio_memory_reader (no Python on the read path) with spans much smaller
+    than the file, so every span after the first comes from the read-ahead
+    thread (previous span's tail + prefetched bytes); scanners in 4 threads,
+    each with its own ctx. Items equal the oracle's."""
+    import threading
+    from base_amd.recordio import gpu
+    _skip(transformers, oracle)
+    recs, data = _file(transformers, 41 + len(transformers), n=2500, max_items=23)
+    ref = oracle.scan(data)
+    out = [None] * 4
+
+    def work(w):
+        ctx = gpu.Context(max_span_bytes=(5 + w) * 32768)
+        sc = gpu.NewScanner(gpu.MemorySource(data), ctx=ctx)
+        items = []
+        while sc.Scan():
+            items.append(sc.Get())
+        out[w] = (items, sc.Finish())
+        ctx.close()
+    th = [threading.Thread(target=work, args=(w,)) for w in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for items, err in out:
+        assert err is None and items == ref.items
