@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--threads", default="1,4,8,16")
     ap.add_argument("--files", type=int, default=16)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--files-per-batch", type=int, default=8)
+    ap.add_argument("--ctx-threads", default="1,2")
     args = ap.parse_args()
     import torch  # noqa: F401  (one HIP runtime: torch's)
     import bench
@@ -102,6 +104,52 @@ def main():
         for c in ctxs:
             c.close()
     out["c3_many_files"] = {"files": len(files), "file_bytes": sum(f.size for f in files), **c3}
+    # the same files as batches of whole file bodies (each body: the blocks
+    # between the header and the trailer, from the file's trailer index), one
+    # rio_scan_span (H2D, decode, D2H) per batch, two ctx threads alternating
+    from base_amd.recordio import shard
+    import numpy as np
+    import torch
+    bodies = []
+    for f in files:
+        raw = f._arr.tobytes()
+        sc = gpu.NewScanner(f, ctx=gpu.default_context(0))
+        lo = c5_data.parse_index(sc.Trailer())[0]
+        assert sc.Finish() is None
+        bodies.append(raw[lo:shard.trailer_offset(raw)])
+    per = max(1, args.files_per_batch)
+    batches = [bodies[i:i + per] for i in range(0, len(bodies), per)]
+    pinned = [torch.frombuffer(bytearray(b"".join(bt)), dtype=torch.uint8).pin_memory() for bt in batches]
+    span = max(p.numel() for p in pinned)
+    nrec_b = [None] * len(batches)
+    c3b = {}
+    for T in [int(x) for x in args.ctx_threads.split(",")]:
+        ctxs = [gpu.Context(0, max_span_bytes=span + (1 << 20), max_items=4 << 20) for _ in range(T)]
+        for c in ctxs:
+            for i, p_ in enumerate(pinned):  # warm (buffers sized); record counts
+                bt = c.scan_host_ptr(p_.data_ptr(), p_.numel(), 0, True, codec=gpu.RIO_CODEC_FLATE)
+                assert bt.err.code == 0, bt.err.msg
+                nrec_b[i] = bt.n_items
+
+        def work(w):
+            for i in range(w, len(pinned), T):
+                bt = ctxs[w].scan_host_ptr(pinned[i].data_ptr(), pinned[i].numel(), 0, True, codec=gpu.RIO_CODEC_FLATE)
+                assert bt.err.code == 0 and bt.n_items == nrec_b[i]
+        ts = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            th = [threading.Thread(target=work, args=(w,)) for w in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            ts.append(time.perf_counter() - t0)
+        t = sorted(ts)[len(ts) // 2]
+        c3b["ctx_threads_%d" % T] = {"GiBs": round(sum(f.size for f in files) / t / 2 ** 30, 2),
+                                     "wall_ms": round(t * 1e3, 1), "records": sum(nrec_b)}
+        for c in ctxs:
+            c.close()
+    out["c3_batched_bodies"] = {"files": len(files), "files_per_batch": per, **c3b}
     print(json.dumps(out), flush=True)
 
 
