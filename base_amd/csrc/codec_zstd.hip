@@ -1978,7 +1978,10 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
 constexpr uint32_t kZRing = 20480;
 constexpr uint32_t kZPart = 2 * kZPiece;
 constexpr uint32_t kZHist = kZRing - kZPart;
-constexpr int kZExecWaves = 6;  // per CU (~25 KiB LDS each)
+#ifndef RIO_ZEXEC_WAVES
+#define RIO_ZEXEC_WAVES 6
+#endif
+constexpr int kZExecWaves = RIO_ZEXEC_WAVES;  // per CU (~25 KiB LDS each)
 
 __device__ __forceinline__ uint32_t zr_slot(uint32_t x) { return x - __umulhi(x >> 12, 0x33333334u) * kZRing; }
 __device__ __forceinline__ uint8_t zr_src(const uint8_t *ring, const uint8_t *out, uint32_t pos, uint32_t base) {
