@@ -1975,7 +1975,11 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
 // ring holding the last kZHist bytes; completed 1 KiB units are flushed to the
 // decode region 16 B per lane. Sources further back than the ring are read
 // from the decode region (flushed, made visible by vmcnt(0) first).
-constexpr uint32_t kZRing = 20480;
+#ifndef RIO_ZRING_K
+#define RIO_ZRING_K 5
+#endif
+constexpr uint32_t kZRingK = RIO_ZRING_K;  // ring = kZRingK x 4 KiB
+constexpr uint32_t kZRing = kZRingK * 4096;
 constexpr uint32_t kZPart = 2 * kZPiece;
 constexpr uint32_t kZHist = kZRing - kZPart;
 #ifndef RIO_ZEXEC_WAVES
@@ -1983,7 +1987,10 @@ constexpr uint32_t kZHist = kZRing - kZPart;
 #endif
 constexpr int kZExecWaves = RIO_ZEXEC_WAVES;  // per CU (~25 KiB LDS each)
 
-__device__ __forceinline__ uint32_t zr_slot(uint32_t x) { return x - __umulhi(x >> 12, 0x33333334u) * kZRing; }
+// x mod kZRing: (x >> 12) / kZRingK by a multiply-high, exact below 2^20
+__device__ __forceinline__ uint32_t zr_slot(uint32_t x) {
+  return x - __umulhi(x >> 12, 0xFFFFFFFFu / kZRingK + 1u) * kZRing;
+}
 __device__ __forceinline__ uint8_t zr_src(const uint8_t *ring, const uint8_t *out, uint32_t pos, uint32_t base) {
   return pos + kZHist >= base ? ring[zr_slot(pos)] : out[pos];
 }
@@ -1995,7 +2002,7 @@ __device__ __forceinline__ uint32_t z_umod(uint32_t k, uint32_t dv) {
   if (r >= (int32_t)dv) r -= (int32_t)dv;
   return (uint32_t)r;
 }
-// completed 1 KiB units of [flushed, olen) to HBM (a unit never wraps: 20 units)
+// completed 1 KiB units of [flushed, olen) to HBM (a unit never wraps: the ring is whole KiB)
 __device__ __forceinline__ void zr_flush(const uint8_t *ring, uint8_t *out, uint32_t &flushed, uint32_t olen) {
   const int l = lane_id();
   for (uint32_t u0 = flushed; u0 + 1024 <= olen; u0 += 1024) {
