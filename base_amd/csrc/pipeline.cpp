@@ -20,6 +20,7 @@
 #include <utility>
 #include <vector>
 
+#include "legacy.h"
 #include "pipeline.h"
 #include "rio_internal.h"
 
@@ -119,6 +120,14 @@ struct rio_ctx {
   Ctl *h_ctl = nullptr;  // pinned copy of the control block
   rio_results res;       // host results of rio_scan_span (scanners bring their own)
   uint8_t *h_stage = nullptr;  // pinned staging of rio_decode_block's chunk stream
+  // v1 (legacy) spans: device staging of the packed records, jobs, views
+  uint8_t *d_v1 = nullptr;
+  uint64_t d_v1_cap = 0;
+  V1Job *d_v1_jobs = nullptr;
+  V1Res *d_v1_res = nullptr;
+  uint64_t d_v1_jobs_cap = 0;
+  unsigned long long *d_v1_off = nullptr, *d_v1_len = nullptr;
+  uint64_t d_v1_items_cap = 0;
   uint64_t h_stage_cap = 0;
   // pools of pinned host buffers and result sets that finished scanners hand
   // back (a scanner per file would otherwise pin and unpin hundreds of MB
@@ -170,7 +179,7 @@ static void free_all(rio_ctx *c) {
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.cmp, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
-                c->nblocks_dev, c->d_span};
+                c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len};
   for (void *p : ps)
     if (p) hipFree(p);
   if (c->h_ctl) hipHostFree(c->h_ctl);
@@ -820,4 +829,273 @@ extern "C" int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, co
   }
   if (hipSetDevice(ctx->device) != hipSuccess) return -1;
   return decode_raw(ctx, payloads, lens, n, codec, scratch, cap, out_len, err);
+}
+
+// ------------------------------------------------------------ v1 (legacy) spans
+// A span of v1 records (recordio/deprecated/recordio.go:80-86: [magic 8][size
+// u64][crc32 of size u32][payload]) decoded as legacyScannerAdapter reads them
+// (recordio/legacyscanner.go:84-117). The record chain is serial -- each
+// record starts where the previous one ends -- so the host walks the 20-byte
+// headers (InternalScan, recordio.go:258-300: header CRC, size limit, truncation,
+// magic) and checks each packed record's item count; every packed record's
+// sizes, header CRC and item views run on the GPU at once (legacy.hip). An
+// unpacked record is one item, the record itself.
+namespace {
+
+const uint8_t kV1MagicUnpacked[8] = {0xfc, 0xae, 0x95, 0x31, 0xf0, 0xd9, 0xbd, 0x20};
+const uint8_t kV1MagicPacked[8] = {0x2e, 0x76, 0x47, 0xeb, 0x34, 0x07, 0x3c, 0x2e};
+constexpr uint64_t kV1MaxRecord = 1ull << 29;  // internal.MaxReadRecordSize, magic.go:33
+
+uint64_t v1_uvarint(const uint8_t *p, uint64_t n, int64_t *cnt) {  // binary.Uvarint, Go 1.13
+  uint64_t x = 0;
+  unsigned s = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint8_t b = p[i];
+    if (b < 0x80) {
+      if (i > 9 || (i == 9 && b > 1)) {
+        *cnt = -(int64_t)(i + 1);
+        return 0;
+      }
+      *cnt = (int64_t)i + 1;
+      return x | ((uint64_t)b << s);
+    }
+    if (s < 64) x |= (uint64_t)(b & 0x7f) << s;
+    s += 7;
+  }
+  *cnt = 0;
+  return 0;
+}
+
+int dgrow(uint8_t **p, uint64_t *cap, uint64_t n) {
+  if (*cap >= n) return 0;
+  const uint64_t c = n + n / 4 + 64;
+  if (dalloc(p, c)) return -1;
+  *cap = c;
+  return 0;
+}
+
+int host_results(rio_results &r, uint64_t n_items, uint64_t nb) {
+  if (r.items_cap < n_items + 1) {
+    if (r.items) hipHostFree(r.items);
+    r.items = nullptr;
+    r.items_cap = n_items + n_items / 4 + 1024;
+    HIP_OK(hipHostMalloc((void **)&r.items, r.items_cap * 16, hipHostMallocDefault));
+  }
+  if (r.blk_cap < 2 * (nb + 1)) {
+    if (r.blk) hipHostFree(r.blk);
+    r.blk = nullptr;
+    r.blk_cap = 2 * (nb + 1) + 2048;
+    HIP_OK(hipHostMalloc((void **)&r.blk, r.blk_cap * 8, hipHostMallocDefault));
+  }
+  return 0;
+}
+
+}  // namespace
+
+int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
+                          rio_results *res, rio_batch *out) {
+  if (!c || !out) return -1;
+  memset(out, 0, sizeof(*out));
+  HIP_OK(hipSetDevice(c->device));
+  rio_results &r = res ? *res : c->res;
+  struct Rec {
+    uint64_t off, first;  // span offset of the record, its first item
+  };
+  struct Unp {
+    uint64_t slot, off, len;
+  };
+  std::vector<Rec> recs;
+  std::vector<V1Job> jobs;
+  std::vector<uint64_t> job_rec;
+  std::vector<Unp> unp;
+  rio_error e{};
+  bool err = false;
+  int32_t stop = RIO_STOP_MORE;
+  uint64_t p = 0, items = 0, need = 0;
+  for (;;) {
+    if (p == nbytes) {
+      if (is_file_end) stop = RIO_STOP_EOF;
+      break;
+    }
+    const uint64_t left = nbytes - p;
+    const uint64_t at = file_off + p;
+    if (left < 20) {
+      if (is_file_end) {
+        rio_set_error(&e, RIO_ERR_V1_RECORD, at, "recordio: failed to read header: unexpected EOF");
+        err = true;
+      } else {
+        need = 20;
+      }
+      break;
+    }
+    const uint8_t *h = span + p;
+    uint64_t size;
+    uint32_t crc;
+    memcpy(&size, h + 8, 8);
+    memcpy(&crc, h + 16, 4);
+    const uint32_t ncrc = crc32_host(h + 8, 8);  // unmarshalHeader, recordio.go:324-334
+    if (ncrc != crc) {
+      rio_set_error(&e, RIO_ERR_V1_RECORD, at, "recordio: crc check failed - corrupt record header (%u != %u)?", ncrc,
+                    crc);
+      e.a = ncrc;
+      e.b = crc;
+      err = true;
+      break;
+    }
+    if (size > kV1MaxRecord) {
+      rio_set_error(&e, RIO_ERR_V1_RECORD, at,
+                    "recordio: unreasonably large read record encountered: %" PRIu64 " > %" PRIu64 " bytes", size,
+                    kV1MaxRecord);
+      err = true;
+      break;
+    }
+    if (size > left - 20) {
+      if (!is_file_end) {
+        need = 20 + size;
+      } else if (left == 20) {  // io.ReadFull read nothing: (0, io.EOF), then the length check
+        rio_set_error(&e, RIO_ERR_V1_RECORD, at, "recordio: short/long record: 0 < %" PRIu64, size);
+        err = true;
+      } else {
+        rio_set_error(&e, RIO_ERR_V1_RECORD, at, "recordio: failed to read record: unexpected EOF");
+        err = true;
+      }
+      break;
+    }
+    const uint8_t *pay = h + 20;
+    if (memcmp(h, kV1MagicPacked, 8) == 0) {  // Unpack's checks before the sizes (packer.go:215-229)
+      if (size < 4) {
+        rio_set_error(&e, RIO_ERR_V1_PACKED, at, "recordio: failed to read crc32");
+        err = true;
+        break;
+      }
+      int64_t n;
+      const uint64_t nb = v1_uvarint(pay + 4, size - 4, &n);
+      if (n <= 0) {
+        rio_set_error(&e, RIO_ERR_NITEMS, at, "recordio: failed to read number of packed items: %" PRId64, n);
+        err = true;
+        break;
+      }
+      if (nb > size) {
+        rio_set_error(&e, RIO_ERR_V1_PACKED, at,
+                      "recordio: likely corrupt data, number of packed items exceeds the number of bytes in the "
+                      "record (%" PRIu64 " > %" PRIu64 ")",
+                      nb, size);
+        err = true;
+        break;
+      }
+      job_rec.push_back(recs.size());
+      jobs.push_back(V1Job{p + 20, size, nb, items});
+      recs.push_back(Rec{p, items});
+      items += nb ? nb : 1;
+    } else if (memcmp(h, kV1MagicUnpacked, 8) == 0) {
+      unp.push_back(Unp{items, p + 20, size});
+      recs.push_back(Rec{p, items});
+      items += 1;
+    } else {
+      rio_set_error(&e, RIO_ERR_BAD_MAGIC, at, "recordio: invalid magic number: [%u %u %u %u %u %u %u %u]", h[0],
+                    h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+      err = true;
+      break;
+    }
+    p += 20 + size;
+  }
+  if (err) stop = RIO_STOP_ERROR;
+  if (host_results(r, items, recs.size())) return -1;
+  unsigned long long *h_off = r.items, *h_len = r.items + r.items_cap;
+  float kms = 0;
+  uint64_t nrec = recs.size(), nitems = items, consumed = p;
+  if (!jobs.empty()) {
+    const uint64_t lo = jobs.front().off, hi = jobs.back().off + jobs.back().size;
+    if (dgrow(&c->d_v1, &c->d_v1_cap, hi - lo + 64)) return -1;
+    if (c->d_v1_jobs_cap < jobs.size()) {
+      const uint64_t cap = jobs.size() + jobs.size() / 4 + 64;
+      if (dalloc(&c->d_v1_jobs, cap) || dalloc(&c->d_v1_res, cap)) return -1;
+      c->d_v1_jobs_cap = cap;
+    }
+    if (c->d_v1_items_cap < items) {
+      const uint64_t cap = items + items / 4 + 1024;
+      if (dalloc(&c->d_v1_off, cap) || dalloc(&c->d_v1_len, cap)) return -1;
+      c->d_v1_items_cap = cap;
+    }
+    for (V1Job &j : jobs) j.off -= lo;
+    HIP_OK(hipMemcpyAsync(c->d_v1, span + lo, hi - lo, hipMemcpyHostToDevice, c->st));
+    HIP_OK(hipMemcpyAsync(c->d_v1_jobs, jobs.data(), jobs.size() * sizeof(V1Job), hipMemcpyHostToDevice, c->st));
+    HIP_OK(hipEventRecord(c->ev[kEvStart], c->st));
+    launch_v1_unpack(c->d_v1, lo, c->d_v1_jobs, jobs.size(), c->d_v1_off, c->d_v1_len, c->d_v1_res, c->st);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(c->ev[kEvEnd], c->st));
+    std::vector<V1Res> jr(jobs.size());
+    HIP_OK(hipMemcpyAsync(jr.data(), c->d_v1_res, jr.size() * sizeof(V1Res), hipMemcpyDeviceToHost, c->st));
+    HIP_OK(hipMemcpyAsync(h_off, c->d_v1_off, items * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_OK(hipMemcpyAsync(h_len, c->d_v1_len, items * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_OK(hipStreamSynchronize(c->st));
+    hipEventElapsedTime(&kms, c->ev[kEvStart], c->ev[kEvEnd]);
+    for (size_t k = 0; k < jobs.size(); k++) {  // the first packed record that failed ends the batch there
+      const V1Res &x = jr[k];
+      if (x.status == kV1Ok) continue;
+      const Rec &rc = recs[job_rec[k]];
+      const uint64_t at = file_off + rc.off;
+      memset(&e, 0, sizeof(e));
+      switch (x.status) {
+      case kV1ItemSize:
+        rio_set_error(&e, RIO_ERR_ITEM_SIZE, at,
+                      "recordio: likely corrupt data, failed to read size of packed item %" PRIu64 ": %" PRId64,
+                      (uint64_t)x.a, (int64_t)x.b);
+        break;
+      case kV1Crc:
+        rio_set_error(&e, RIO_ERR_V1_PACKED, at,
+                      "recordio: likely corrupt data, crc check failed - corrupt packed record header (%u != %u)?",
+                      (uint32_t)x.a, (uint32_t)x.b);
+        break;
+      case kV1Offset:
+        rio_set_error(&e, RIO_ERR_V1_PACKED, at,
+                      "recordio: offset greater than buf size (%" PRIu64 " > %" PRIu64
+                      "), likely due to a mismatched transform or a truncated file",
+                      (uint64_t)x.a, (uint64_t)x.b);
+        break;
+      default:  // the reference panics slicing
+        rio_set_error(&e, RIO_ERR_ITEM_RANGE, at, "recordio: corrupt packed record header, item sizes out of range");
+      }
+      e.a = x.a;
+      e.b = x.b;
+      err = true;
+      stop = RIO_STOP_ERROR;
+      nrec = job_rec[k];
+      nitems = rc.first;
+      consumed = rc.off;
+      break;
+    }
+  }
+  for (const Unp &u : unp) {
+    if (u.slot >= nitems) break;
+    h_off[u.slot] = u.off;
+    h_len[u.slot] = u.len;
+  }
+  unsigned long long *first = r.blk, *foff = r.blk + nrec + 1;
+  for (uint64_t i = 0; i < nrec; i++) {
+    first[i] = recs[i].first;
+    foff[i] = file_off + recs[i].off;
+  }
+  first[nrec] = nitems;
+  out->span = span;
+  out->records = nullptr;
+  out->records_len = 0;
+  out->item_off = reinterpret_cast<const uint64_t *>(h_off);
+  out->item_len = reinterpret_cast<const uint64_t *>(h_len);
+  out->n_items = nitems;
+  out->block_first_item = reinterpret_cast<const uint64_t *>(first);
+  out->block_file_off = reinterpret_cast<const uint64_t *>(foff);
+  out->n_blocks = nrec;
+  out->consumed = consumed;
+  out->stop = stop;
+  out->in_bytes = nbytes;
+  out->kernel_ms = kms;
+  if (err) out->err = e;
+  else if (stop == RIO_STOP_MORE && nrec == 0) out->err.a = need;  // the next record needs a span this large
+  return 0;
+}
+
+extern "C" int rio_scan_v1_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
+                                int32_t is_file_end, rio_batch *out) {
+  return rio_scan_v1_span_mode(ctx, span, nbytes, file_off, is_file_end, nullptr, out);
 }

@@ -16,6 +16,9 @@ void rio_results_free(rio_results *r);
 int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
                        int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res,
                        rio_batch *out);
+// v1 records of one span (rio_scan_v1_span) into *res (the ctx's own when null)
+int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
+                          rio_results *res, rio_batch *out);
 uint64_t rio_ctx_max_span(rio_ctx *c);
 // the ctx's pools of pinned buffers and result sets (scanners borrow and return them)
 int rio_ctx_take_buf(rio_ctx *c, uint64_t need, uint8_t **p, uint64_t *cap);

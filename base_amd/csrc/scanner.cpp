@@ -149,6 +149,9 @@ struct rio_scanner {
   bool error_scanner = false;
   std::vector<KV> header;
   int32_t codec = RIO_CODEC_NONE;
+  // a v1 file (legacyScannerAdapter, legacyscanner.go): body spans decode as v1
+  // records (rio_scan_v1_span); off is the next record's offset
+  bool v1 = false;
   // ChunkScanner position
   uint64_t off = 0, limit = UINT64_MAX;
   // current batch: the span (pinned host staging; none-codec items are views
@@ -304,6 +307,7 @@ struct rio_scanner {
       return 0;
     }
     const int is_end = (at + got >= file_size);
+    if (v1 && mode == 0) return rio_scan_v1_span_mode(ctx, *buf, got, at, is_end, rs, out);
     return rio_scan_span_mode(ctx, *buf, got, at, is_end, lim, cdc, mode, rs, out);
   }
   int decode(uint64_t at, uint64_t n, int32_t cdc, int32_t mode, uint64_t lim, rio_batch *out) {
@@ -324,7 +328,8 @@ struct rio_scanner {
       std::swap(span, ra_buf);  // the batch's views will point into this buffer
       std::swap(span_cap, ra_cap);
       const int is_end = (at + n >= file_size);
-      const int rc = rio_scan_span_mode(ctx, base, n, at, is_end, limit, codec, 0, res, out);
+      const int rc = v1 ? rio_scan_v1_span_mode(ctx, base, n, at, is_end, res, out)
+                        : rio_scan_span_mode(ctx, base, n, at, is_end, limit, codec, 0, res, out);
       span_data = base;
       span_at = at;
       span_n = n;
@@ -495,7 +500,26 @@ bool next_batch(rio_scanner *s) {
     } else if (b.stop == RIO_STOP_EOF) {
       s->done = true;
     } else {
-      if (b.consumed == 0) {
+      if (b.consumed == 0 && s->v1 && b.err.a > n) {
+        // a v1 record larger than the span (records run to MaxReadRecordSize,
+        // 512 MiB): the record alone, in a staging buffer of its size
+        const uint64_t need = b.err.a;
+        if (s->decode(s->off, need, RIO_CODEC_NONE, 0, UINT64_MAX, &b) != 0) {
+          s->set_errf(RIO_ERR_HIP, s->off, "%s", rio_last_error());
+          return false;
+        }
+        s->span_data = s->span;
+        s->span_at = s->off;
+        s->span_n = need;
+        if (b.stop == RIO_STOP_ERROR) {
+          s->pending = b.err;
+          s->pending_set = true;
+          s->done = true;
+        } else if (b.stop == RIO_STOP_EOF) {
+          s->done = true;
+        }
+      }
+      if (b.stop == RIO_STOP_MORE && b.consumed == 0) {
         s->set_errf(RIO_ERR_CAPACITY, s->off, "block at offset %" PRIu64 " larger than the GPU span",
                     s->off);
         return false;
@@ -586,11 +610,20 @@ rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int l
     return s;
   }
   if (memcmp(magic, kMagicHeaderBytes, 8) != 0) {
-    s->error_scanner = true;
-    if (start != 0 || limit != 1 || nshard != 1)
+    if (start != 0 || limit != 1 || nshard != 1) {
+      s->error_scanner = true;
       s->set_errf(RIO_ERR_ARG, 0, "legacy record IOs do not support sharding");
-    else
-      s->set_errf(RIO_ERR_LEGACY, 0, "legacy recordio file: decode with recordio.NewScanner");
+      return s;
+    }
+    // newLegacyScannerAdapter (scannerv2.go:232): Header() empty, Trailer() nil
+    if (!ctx) {
+      s->error_scanner = true;
+      s->set_errf(RIO_ERR_ARG, 0, "nil rio_ctx");
+      return s;
+    }
+    s->v1 = true;
+    s->off = 0;
+    s->limit = UINT64_MAX;
     return s;
   }
   if (!ctx) {
@@ -754,6 +787,16 @@ int rio_scanner_trailer(rio_scanner *s, const uint8_t **data, uint64_t *len) {
 
 void rio_scanner_seek(rio_scanner *s, uint64_t block, int64_t item) {
   if (!s || s->error_scanner) return;
+  // v1 Seek (legacyscanner.go:67-82): seekRaw + sc.Reset clear the record
+  // scanner's error (InternalScan's); the adapter's own (Unpack, magic,
+  // location) stays
+  if (s->v1 && s->err_set && s->err.code == RIO_ERR_V1_RECORD) {
+    s->err_set = false;
+    memset(&s->err, 0, sizeof(s->err));
+  }
+  if (s->v1 && !s->err_set && (int64_t)block < 0) {
+    s->set_errf(RIO_ERR_ARG, block, "bytes.Reader.Seek: negative position");
+  }
   if (s->err_set) {  // scanNextBlock clears rawItems, then fails on the sticky error
     s->have_batch = false;
     s->cur = nullptr;
@@ -780,10 +823,7 @@ void rio_scanner_location(rio_scanner *s, uint64_t *block, int64_t *item) {
   *item = s ? s->cur_item : 0;
 }
 
-int rio_scanner_version(rio_scanner *s) {
-  (void)s;
-  return 2;
-}
+int rio_scanner_version(rio_scanner *s) { return (s && s->v1) ? 1 : 2; }
 
 // Gather: the items at n ItemLocations, as n Seek + Scan +
 // Get calls would return them (scannerv2.go:348-361, 390-403), with the
@@ -822,7 +862,7 @@ int64_t rio_scanner_gather(rio_scanner *s, const uint64_t *blocks, const int64_t
     bl[i].off = uniq[i];
     uint8_t hdr[RIO_CHUNK_HEADER_SIZE];
     int st;
-    if (uniq[i] % kCk != 0 || uniq[i] >= s->file_size) continue;  // the exact path reports it
+    if (s->v1 || uniq[i] % kCk != 0 || uniq[i] >= s->file_size) continue;  // the exact path reports it
     s->read_full(hdr, sizeof(hdr), uniq[i], &st);
     if (st != 0) continue;
     uint32_t total, index;

@@ -148,3 +148,49 @@ def chunk_block(magic: bytes, payload: bytes) -> bytes:
         if index == total - 1:
             out += _PAD[:MAX_CHUNK_PAYLOAD - len(part)]
     return bytes(out)
+
+
+# ------------------------------------------------------------------ v1 (legacy)
+# recordio/deprecated/recordio.go:80-86: 8-byte magic, u64 size, crc32 of size
+LEGACY_HEADER_SIZE = 20
+MAX_READ_RECORD_SIZE = 1 << 29  # recordio/internal/magic.go:33
+# recordio/deprecated/packed.go:18-24
+LEGACY_DEFAULT_PACKED_ITEMS = 16 * 1024
+LEGACY_DEFAULT_PACKED_BYTES = 16 * 1024 * 1024
+
+
+def legacy_record(magic: bytes, payload: bytes) -> bytes:
+    """One v1 record: marshalHeader (deprecated/recordio.go:316-322) + payload."""
+    size = len(payload).to_bytes(8, "little")
+    return magic + size + crc32_ieee(size).to_bytes(4, "little") + bytes(payload)
+
+
+def legacy_packed_payload(items) -> bytes:
+    """Packer.Pack (deprecated/packer.go:85-133), no transform: crc32 of the
+    varint header, item count, item sizes, then the items."""
+    hdr = put_uvarint(len(items)) + b"".join(put_uvarint(len(p)) for p in items)
+    return crc32_ieee(hdr).to_bytes(4, "little") + hdr + b"".join(bytes(p) for p in items)
+
+
+def legacy_unpacked_file(items) -> bytes:
+    """NewLegacyWriter + Write per item (deprecated/recordio.go:132-142)."""
+    return b"".join(legacy_record(MAGIC_LEGACY_UNPACKED, p) for p in items)
+
+
+def legacy_packed_file(items, max_items: int = LEGACY_DEFAULT_PACKED_ITEMS,
+                       max_bytes: int = LEGACY_DEFAULT_PACKED_BYTES) -> bytes:
+    """NewLegacyPackedWriter + Write per item + Flush (deprecated/packed.go:
+    119-200): a record is flushed before an item that would exceed max_items
+    or max_bytes."""
+    out, cur, nbytes = [], [], 0
+    for p in items:
+        if len(p) > max_bytes:
+            raise ValueError(f"buffer is too large {len(p)} > {max_bytes}")
+        if cur and (nbytes + len(p) > max_bytes or len(cur) + 1 > max_items):
+            out.append(legacy_record(MAGIC_PACKED, legacy_packed_payload(cur)))
+            cur, nbytes = [], 0
+        cur.append(p)
+        nbytes += len(p)
+    if cur:
+        out.append(legacy_record(MAGIC_PACKED, legacy_packed_payload(cur)))
+    return b"".join(out)

@@ -26,7 +26,9 @@ LIB_PATH = os.environ.get("RIO_GPU_LIB") or os.path.join(_ROOT, "lib", "librio_g
 RIO_CODEC_NONE, RIO_CODEC_FLATE, RIO_CODEC_ZSTD = 0, 1, 2
 RIO_STOP_MORE, RIO_STOP_EOF, RIO_STOP_ERROR = 0, 1, 2
 RIO_ERR_CAPACITY = 98
-RIO_ERR_LEGACY = 20    # v1 file: the reference scanner decodes it (scannerv2.go:228-233)
+RIO_ERR_LEGACY = 20    # (no longer returned: v1 files decode natively)
+RIO_ERR_V1_RECORD = 24  # v1 record header / read errors (deprecated/recordio.go:258-300)
+RIO_ERR_V1_PACKED = 25  # v1 packed-record errors (deprecated/packer.go:214-272)
 RIO_ERR_FALLBACK = 23  # transformer chain / name other than flate, zstd (registry.go:113-148)
 U64_MAX = (1 << 64) - 1
 ITEM_IN_RECORDS = 1 << 63  # RIO_ITEM_IN_RECORDS
@@ -73,7 +75,7 @@ EXPORTS = [
     "rio_scanner_new", "rio_scanner_scan", "rio_scanner_get", "rio_scanner_next_batch", "rio_scanner_err",
     "rio_scanner_header_len", "rio_scanner_header_kv", "rio_scanner_trailer", "rio_scanner_seek",
     "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish", "rio_scanner_gather",
-    "rio_memory_reader",
+    "rio_memory_reader", "rio_scan_v1_span",
 ]
 
 _lib = None
@@ -102,6 +104,8 @@ def load(path: str = LIB_PATH):
                                                  ctypes.POINTER(I32), ctypes.POINTER(RioError)]
         L.rio_scan_span.restype = ctypes.c_int
         L.rio_scan_span.argtypes = [P, P, U64, U64, I32, U64, I32, ctypes.POINTER(RioBatch)]
+        L.rio_scan_v1_span.restype = ctypes.c_int
+        L.rio_scan_v1_span.argtypes = [P, P, U64, U64, I32, ctypes.POINTER(RioBatch)]
         L.rio_scan_device.restype = ctypes.c_int
         L.rio_scan_device.argtypes = [P, P, U64, U64, I32, U64, I32, ctypes.POINTER(RioBatch)]
         L.rio_scan_device_async.restype = ctypes.c_int
@@ -190,6 +194,17 @@ class Context:
         if rc != 0:
             raise RuntimeError("rio_scan_span: " + self.L.rio_last_error().decode())
         out._span_buf = buf  # item views point into it
+        return out
+
+    def scan_v1_span(self, span: bytes, file_off: int = 0, is_file_end: bool = True) -> RioBatch:
+        """rio_scan_v1_span: the v1 (legacy) records of span (legacyscanner.go:84-117)."""
+        out = RioBatch()
+        buf = (ctypes.c_char * max(len(span), 1)).from_buffer_copy(bytes(span) or b"\0")
+        rc = self.L.rio_scan_v1_span(self.h, ctypes.addressof(buf), len(span), file_off, int(is_file_end),
+                                     ctypes.byref(out))
+        if rc != 0:
+            raise RuntimeError("rio_scan_v1_span: " + self.L.rio_last_error().decode())
+        out._span_buf = buf
         return out
 
     def scan_host_ptr(self, host_ptr: int, nbytes: int, file_off: int = 0, is_file_end: bool = True,
@@ -387,11 +402,11 @@ class Scanner:
     """Mirror of the recordio.Scanner interface (scannerv2.go:120-161).
 
     Every scanner owns its staging and result buffers (the C scanner does), so
-    scanners sharing one Context never see each other's records. A file this
-    library does not decode -- v1 (RIO_ERR_LEGACY) or a transformer chain /
-    other registered transformer (RIO_ERR_FALLBACK) -- reports that code from
-    Err(); the Go shim hands such files to recordio.NewShardScanner
-    (INTEGRATION.md)."""
+    scanners sharing one Context never see each other's records. v1 (legacy)
+    files decode natively (Version() == 1, legacyscanner.go). A file this
+    library does not decode -- a transformer chain / other registered
+    transformer (RIO_ERR_FALLBACK) -- reports that code from Err(); the Go shim
+    hands such files to recordio.NewShardScanner."""
 
     def __init__(self, src, opts: ScannerOpts = None, start: int = 0, limit: int = 1, nshard: int = 1,
                  ctx: Optional[Context] = None):

@@ -66,13 +66,25 @@ enum rio_err_code {
     RIO_ERR_TRAILER = 17,       /* trailer lookup errors                       scannerv2.go:316-342 */
     RIO_ERR_TRANSFORMER = 18,   /* "Transformer %s not found"                  registry.go:58 */
     RIO_ERR_ARG = 19,           /* invalid argument / sharding                 scannerv2.go:226 */
-    RIO_ERR_LEGACY = 20,        /* v1 file: decode with the reference scanner  scannerv2.go:228 */
+    RIO_ERR_LEGACY = 20,        /* (unused since v1 files decode natively; kept for ABI stability) */
     RIO_ERR_IO = 21,            /* reader callback failed                      */
     RIO_ERR_LOCATION = 22,      /* "Invalid location %+v, block has only %d items" scannerv2.go:358 */
     RIO_ERR_FALLBACK = 23,      /* transformers this library does not decode: a chain of several, or a
                                    name other than flate/zstd (registry.go:113-148). Decode the file with
                                    recordio.NewShardScanner; msg is the reference's text for the case the
                                    name is not registered there either ("Transformer %s not found") */
+    RIO_ERR_V1_RECORD = 24,     /* v1 record header / read errors (InternalScan): "recordio: crc check
+                                   failed - corrupt record header (%v != %v)?", "recordio: failed to read
+                                   header: unexpected EOF", "recordio: unreasonably large read record
+                                   encountered: %d > %d bytes", "recordio: failed to read record: unexpected
+                                   EOF", "recordio: short/long record: %d < %d"
+                                                                  deprecated/recordio.go:258-300, 324-334 */
+    RIO_ERR_V1_PACKED = 25,     /* v1 packed-record errors (Unpack): "recordio: failed to read crc32",
+                                   "...number of packed items exceeds the number of bytes in the record
+                                   (%v > %v)", "...crc check failed - corrupt packed record header (%v !=
+                                   %v)?", "recordio: offset greater than buf size (%v > %v), ..."
+                                   (item count / size varint errors use RIO_ERR_NITEMS / RIO_ERR_ITEM_SIZE,
+                                   same text as v2)               deprecated/packer.go:214-272 */
     RIO_ERR_CAPACITY = 98,      /* span or output exceeds the ctx capacity      */
     RIO_ERR_HIP = 99,           /* HIP runtime failure                          */
 };
@@ -163,6 +175,19 @@ int rio_scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t f
 int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, uint64_t file_off,
                     int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_batch *out);
 
+/* v1 ("legacy") files (recordio/deprecated; read by the reference through
+ * legacyScannerAdapter, legacyscanner.go:84-117): decode the v1 records in
+ * span = file bytes at file_off, a record boundary. Blocks are records
+ * (block_file_off = the record's offset, ItemLocation.Block for Seek); a
+ * packed record's items are its unpacked items, an unpacked record is one
+ * item. Every item is a view into span. stop: EOF at the file end, MORE at the
+ * last whole record (consumed = its end; when not even the first record fits,
+ * consumed is 0 and err.a holds the span size it needs), ERROR at the first
+ * failing record. No LegacyTransform: a caller that sets one decodes the file
+ * with the reference scanner. */
+int rio_scan_v1_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
+                     int32_t is_file_end, rio_batch *out);
+
 /* Device-resident benchmark entry: like rio_scan_device but asynchronous on the
  * ctx stream and with no host copies; call rio_sync to collect the summary. */
 int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, uint64_t file_off,
@@ -236,7 +261,7 @@ int64_t rio_scanner_gather(rio_scanner *s, const uint64_t *blocks, const int64_t
                            const uint8_t **data, uint64_t *lens, rio_error *err);
 /* ItemLocation of the current record */
 void rio_scanner_location(rio_scanner *s, uint64_t *block, int64_t *item);
-/* Version (scannerv2.go:308): 2 */
+/* Version (scannerv2.go:308, legacyscanner.go:45): 2, or 1 for a v1 file */
 int rio_scanner_version(rio_scanner *s);
 /* Finish (scannerv2.go:414-425): returns Err() code and frees the scanner */
 int rio_scanner_finish(rio_scanner *s, rio_error *err);

@@ -897,10 +897,24 @@ static void res_take_header(orc_result *r, sc_t *s) {
     r->legacy = s->legacy;
 }
 
+/* oracle/legacy.c: the v1 adapter (legacyscanner.go) */
+typedef void (*v1_item_fn)(void *u, const uint8_t *p, int64_t n, uint64_t block, int64_t idx);
+void orc_v1_run(const uint8_t *f, int64_t n, int seek, uint64_t block, int64_t item, v1_item_fn fn, void *u,
+                char *err, size_t errcap);
+static void v1_collect(void *u, const uint8_t *p, int64_t n, uint64_t block, int64_t idx) {
+    res_push_item((orc_result *)u, p, n, block, idx);
+}
+
 orc_result *orc_scan(const uint8_t *f, int64_t n, int start, int limit, int nshard, int flags) {
     sc_t s;
     sc_open(&s, f, n, start, limit, nshard);
     orc_result *r = res_new();
+    if (s.legacy) { /* newLegacyScannerAdapter (scannerv2.go:232): Trailer() is nil */
+        orc_v1_run(f, n, 0, 0, 0, v1_collect, r, r->err, sizeof(r->err));
+        res_take_header(r, &s);
+        sc_close(&s);
+        return r;
+    }
     if ((flags & 1) && !s.error_scanner) r->has_trailer = sc_trailer(&s, &r->trailer);
     const uint8_t *p;
     int64_t len;
@@ -915,7 +929,9 @@ orc_result *orc_seek_get(const uint8_t *f, int64_t n, uint64_t block, int64_t it
     sc_t s;
     sc_open(&s, f, n, 0, 1, 1);
     orc_result *r = res_new();
-    if (!s.error_scanner) {
+    if (s.legacy) {
+        orc_v1_run(f, n, 1, block, item, v1_collect, r, r->err, sizeof(r->err));
+    } else if (!s.error_scanner) {
         /* Seek (scannerv2.go:348-361) */
         cs_seek(&s.cs, (int64_t)block);
         if (sc_next_block(&s)) {
@@ -939,6 +955,15 @@ int64_t orc_scan_count(const uint8_t *f, int64_t n, int64_t *bytes_out, int star
                        int nshard) {
     sc_t s;
     sc_open(&s, f, n, start, limit, nshard);
+    if (s.legacy) {
+        orc_result *r = res_new();
+        orc_v1_run(f, n, 0, 0, 0, v1_collect, r, r->err, sizeof(r->err));
+        int64_t items = r->n_items, bad = r->err[0] != 0;
+        *bytes_out = (int64_t)r->items.n;
+        orc_free(r);
+        sc_close(&s);
+        return bad ? -1 : items;
+    }
     const uint8_t *p;
     int64_t len, items = 0, bytes = 0;
     while (sc_scan(&s, &p, &len)) {

@@ -71,8 +71,9 @@ def test_golden_cases(gpu_ctx, manifest, oracle):
             continue
         data = golden_bytes(case)
         header, items, trailer, err, e = gpu_scan(data, gpu_ctx, read_trailer=case["read_trailer"])
-        if case["name"] == "legacy_magic":
-            assert e is not None and e.code == 20  # RIO_ERR_LEGACY: defer to recordio.NewScanner
+        if case["name"] == "legacy_magic":  # decoded as v1 (legacyscanner.go): the oracle's v1 result
+            ref = oracle.scan(data)
+            assert ref.legacy and e is not None and e.code == 24 and err == ref.err and items == ref.items
             continue
         want_tr = bytes.fromhex(case["trailer"]) if case["trailer"] is not None else None
         got = (err, len(items), sha(items), trailer, hdr_json(header))
@@ -173,9 +174,7 @@ def test_corruption_sweep_matches_oracle(gpu_ctx, oracle, codec):
         d = bytes(b)
         _, items, trailer, err, e = gpu_scan(d, gpu_ctx, read_trailer=False)
         ref = oracle.scan(d, read_trailer=False)
-        if ref.legacy:  # header magic destroyed: the reference switches to its v1 adapter
-            assert e is not None and e.code == 20 and items == []
-            continue
+        # (header magic destroyed: both read the file as v1, legacyscanner.go)
         assert err == ref.err, (trial, kind, o)
         assert items == ref.items, (trial, kind, o)
 

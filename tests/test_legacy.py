@@ -1,0 +1,330 @@
+"""v1 ("legacy") files: the oracle pinned by the reference's own v1 vectors and
+error tables, then the GPU path (rio_scan_v1_span via the scanner) against the
+oracle.
+
+Reference anchors:
+  deprecated/recordio_test.go:41-110   golden record bytes ("", "a", "hello\\n")
+  deprecated/recordio_test.go:138-221  header corruption / short read errors
+  deprecated/recordio_test.go:245-289  multiple records incl. empty ones
+  deprecated/packer_test.go:283-318    Unpack's short-read / corruption errors
+  v2_test.go:49-72                     NewScanner over v1 packed / unpacked files
+The reference's v1 error tests assert substrings (expect.HasSubstr); the oracle
+restates the full texts (deprecated/recordio.go:258-334, packer.go:214-272,
+legacyscanner.go:84-117) and the GPU path must equal the oracle byte for byte.
+"""
+import random
+import struct
+import zlib
+
+import pytest
+
+from base_amd.recordio import format as F
+
+
+def v1_packed_raw(sizes, body: bytes, count=None, crc_ok=True) -> bytes:
+    """A packed record payload with an arbitrary (possibly inconsistent) header."""
+    hdr = F.put_uvarint(len(sizes) if count is None else count) + b"".join(F.put_uvarint(s) for s in sizes)
+    crc = zlib.crc32(hdr) if crc_ok else zlib.crc32(hdr) ^ 1
+    return struct.pack("<I", crc) + hdr + body
+
+
+def packer_record():
+    """packer_test.go:283-291: Pack of "hello", "world" as one record payload."""
+    return F.legacy_packed_payload([b"hello", b"world"])
+
+
+# ---------------------------------------------------------------- oracle (CPU)
+
+def test_oracle_golden_record_bytes(oracle):
+    """recordio_test.go:41-72: the exact bytes of one-record files, read back."""
+    vecs = [(b"", [0, 0, 0, 0, 0, 0, 0, 0, 0x69, 0xDF, 0x22, 0x65]),
+            (b"a", [1, 0, 0, 0, 0, 0, 0, 0, 0xF7, 0xDF, 0x88, 0xA9]),
+            (b"hello\n", [6, 0, 0, 0, 0, 0, 0, 0, 0xEE, 0xD6, 0x4D, 0xA3])]
+    for s, args in vecs:
+        data = F.MAGIC_LEGACY_UNPACKED + bytes(args) + s
+        assert F.legacy_unpacked_file([s]) == data
+        r = oracle.scan(data)
+        assert r.legacy and r.items == [s] and r.err == "" and r.trailer is None and r.header == []
+
+
+def test_oracle_read_v1(oracle):
+    """v2_test.go:49-72 and recordio_test.go:245-289."""
+    for data in (F.legacy_packed_file([b"Foo", b"Baz"]), F.legacy_unpacked_file([b"Foo", b"Baz"])):
+        r = oracle.scan(data)
+        assert r.items == [b"Foo", b"Baz"] and r.err == ""
+    want = [b"", b"hello", b"world", b"", b"last record"]
+    assert oracle.scan(F.legacy_unpacked_file(want)).items == want
+    assert oracle.scan(F.legacy_packed_file(want, max_items=2)).items == want
+
+
+def test_oracle_record_errors(oracle):
+    """recordio_test.go:160-190 (the adapter's texts contain the asserted substrings)."""
+    good = F.legacy_unpacked_file([b"hello\n"])
+    for off, sub in [(0, "invalid magic number"), (10, "crc check failed"), (17, "crc check failed")]:
+        b = bytearray(good)
+        b[off] = 0xFF
+        r = oracle.scan(bytes(b))
+        assert r.items == [] and sub in r.err, (off, r.err)
+    assert oracle.scan(good[:19]).err == "recordio: failed to read header: unexpected EOF"
+    assert oracle.scan(good[:20]).err == "recordio: short/long record: 0 < 6"
+    assert oracle.scan(good[:21]).err == "recordio: failed to read record: unexpected EOF"
+    assert oracle.scan(good[:1]).err == "unexpected EOF"  # NewShardScanner's magic read
+    # size > MaxReadRecordSize (recordio_test.go:206-220 lowers the limit; here the size is raised)
+    size = struct.pack("<Q", (1 << 29) + 1)
+    big = F.MAGIC_LEGACY_UNPACKED + size + struct.pack("<I", zlib.crc32(size)) + b"x"
+    assert oracle.scan(big).err == ("recordio: unreasonably large read record encountered: %d > %d bytes"
+                                    % ((1 << 29) + 1, 1 << 29))
+    r = oracle.scan(F.legacy_unpacked_file([b"a", b"b"]) + F.legacy_record(F.MAGIC_HEADER[:7] + b"\0", b"zz"))
+    assert r.items == [b"a", b"b"] and r.err == "recordio: invalid magic number: [217 225 217 92 194 22 4 0]"
+
+
+def test_oracle_unpack_errors(oracle):
+    """packer_test.go:283-318, each case as a v1 packed record."""
+    rec = packer_record()
+    cases = [(rec[:1], "failed to read crc32"), (rec[:4], "failed to read number of packed items"),
+             (rec[:5], "likely corrupt data, failed to read size of packed item"),
+             (rec[:10], "offset greater than buf size")]
+    for off, sub, ow in [(2, "crc check failed - corrupt packed record header", bytes([rec[2] + 1])),
+                         (4, "likely corrupt data, number of packed items exceeds", b"\x7f"),
+                         (4, "likely corrupt data, failed to read size of packed item", b"\x0f"),
+                         (5, "crc check failed - corrupt packed record header", b"\x7f")]:
+        t = bytearray(rec)
+        t[off:off + len(ow)] = ow
+        cases.append((bytes(t), sub))
+    for payload, sub in cases:
+        r = oracle.scan(F.legacy_record(F.MAGIC_PACKED, payload))
+        assert r.items == [] and sub in r.err, (payload, r.err)
+    # exact texts of two of them
+    r = oracle.scan(F.legacy_record(F.MAGIC_PACKED, rec[:10]))
+    assert r.err == ("recordio: offset greater than buf size (5 > 3), likely due to a mismatched transform or a "
+                     "truncated file")
+    r = oracle.scan(F.legacy_record(F.MAGIC_PACKED, rec[:5]))
+    assert r.err == "recordio: likely corrupt data, failed to read size of packed item 0: 0"
+
+
+def test_oracle_unpack_edges(oracle):
+    """Unpack's slicing: n == 0 yields one empty item; the last item is
+    packed[prev:total], so trailing bytes past the sizes are not an item."""
+    r = oracle.scan(F.legacy_record(F.MAGIC_PACKED, v1_packed_raw([], b"junk")))
+    assert r.items == [b""] and r.err == ""
+    r = oracle.scan(F.legacy_record(F.MAGIC_PACKED, v1_packed_raw([2, 3], b"abcdefgh")))
+    assert r.items == [b"ab", b"cde"] and r.err == ""
+    r = oracle.scan(F.legacy_record(F.MAGIC_PACKED, v1_packed_raw([2, 3], b"abcd")))
+    assert r.items == [] and r.err == "recordio: corrupt packed record header, item sizes out of range"
+
+
+def test_oracle_seek(oracle):
+    data = F.legacy_unpacked_file([b"a", b"bb"]) + F.legacy_packed_file([b"x", b"yy", b"zzz"])
+    r = oracle.scan(data)
+    assert r.items == [b"a", b"bb", b"x", b"yy", b"zzz"]
+    assert r.locations == [(0, 0), (21, 0), (43, 0), (43, 1), (43, 2)]
+    assert oracle.seek_get(data, 43, 2).items == [b"zzz"]
+    s = oracle.seek_get(data, 43, 3)
+    assert s.items == [] and s.err == "Invalid location {Block:43 Item:3}, block has only 3 items"
+
+
+# ---------------------------------------------------------------- GPU
+
+def gpu_read(data, ctx):
+    from base_amd.recordio import gpu
+    sc = gpu.NewScanner(data, ctx=ctx)
+    assert sc.Version() == (1 if data[:8] != F.MAGIC_HEADER and len(data) >= 8 else 2)
+    assert sc.Header() == [] and sc.Trailer() is None
+    items, locs = [], []
+    while sc.Scan():
+        items.append(sc.Get())
+        locs.append(sc.Location())
+    assert not sc.Scan()
+    err = sc.Finish()
+    return items, locs, ("" if err is None else str(err)), err
+
+
+def check(data, ctx, oracle, tag=None):
+    items, locs, err, e = gpu_read(data, ctx)
+    ref = oracle.scan(data)
+    assert err == ref.err, (tag, err, ref.err)
+    assert items == ref.items, tag
+    assert [(x.Block, x.Item) for x in locs] == ref.locations, tag
+    return ref
+
+
+def random_v1_file(rng, n=None):
+    n = rng.randrange(0, 400) if n is None else n
+    items = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 5, 40, 300, 3000])))
+             for _ in range(n)]
+    kind = rng.randrange(3)
+    if kind == 0:
+        return F.legacy_unpacked_file(items)
+    if kind == 1:
+        return F.legacy_packed_file(items, max_items=rng.choice([1, 3, 64, 16384]),
+                                    max_bytes=rng.choice([1 << 12, 1 << 16, 16 << 20]))
+    out = b""
+    while items:  # mixed records
+        k = rng.randrange(1, 20)
+        chunk, items = items[:k], items[k:]
+        out += F.legacy_packed_file(chunk) if rng.random() < 0.5 else F.legacy_unpacked_file(chunk)
+    return out
+
+
+@pytest.mark.gpu
+def test_gpu_v1_reference_cases(gpu_ctx, oracle):
+    """Every reference-pinned case above, through the GPU scanner."""
+    good = F.legacy_unpacked_file([b"hello\n"])
+    datas = [F.legacy_packed_file([b"Foo", b"Baz"]), F.legacy_unpacked_file([b"Foo", b"Baz"]),
+             F.legacy_unpacked_file([b"", b"hello", b"world", b"", b"last record"]),
+             F.legacy_packed_file([b"", b"hello", b"world", b"", b"last record"], max_items=2),
+             good[:19], good[:20], good[:21], b""]
+    for off in (0, 10, 17):
+        b = bytearray(good)
+        b[off] = 0xFF
+        datas.append(bytes(b))
+    rec = packer_record()
+    for k in (1, 4, 5, 10):
+        datas.append(F.legacy_record(F.MAGIC_PACKED, rec[:k]))
+    for off, ow in [(2, bytes([rec[2] + 1])), (4, b"\x7f"), (4, b"\x0f"), (5, b"\x7f")]:
+        t = bytearray(rec)
+        t[off:off + len(ow)] = ow
+        datas.append(F.legacy_record(F.MAGIC_PACKED, bytes(t)))
+    size = struct.pack("<Q", (1 << 29) + 1)
+    datas.append(F.MAGIC_LEGACY_UNPACKED + size + struct.pack("<I", zlib.crc32(size)) + b"x")
+    datas.append(F.legacy_unpacked_file([b"a", b"b"]) + F.legacy_record(F.MAGIC_HEADER[:7] + b"\0", b"zz"))
+    for i, d in enumerate(datas):
+        if len(d) < 8:
+            continue  # the magic read itself fails: errorScanner (covered by test_gpu_parity)
+        check(d, gpu_ctx, oracle, i)
+
+
+@pytest.mark.gpu
+def test_gpu_v1_unpack_edges(gpu_ctx, oracle):
+    """Header shapes for the GPU kernel: n == 0, trailing bytes, 10/11-byte
+    varints, wrapped sizes, headers across several 1 KiB windows, bad CRC."""
+    P = F.MAGIC_PACKED
+    big = [1 + (i * 7919) % 300 for i in range(5000)]  # ~7.5 KiB of size varints
+    body = bytes(i & 0xFF for i in range(sum(big)))
+    payloads = [
+        v1_packed_raw([], b"junk"), v1_packed_raw([], b""), v1_packed_raw([2, 3], b"abcdefgh"),
+        v1_packed_raw([2, 3], b"abcd"), v1_packed_raw([5, (1 << 64) - 2], b"abcdefgh"),
+        v1_packed_raw([(1 << 64) - 1, 5], b"abcdefgh"), v1_packed_raw(big, body),
+        v1_packed_raw(big, body, crc_ok=False), v1_packed_raw(big, body[:-1]),
+        v1_packed_raw([1] * 3000, b"x" * 3000),
+        # 10-byte varint with a final byte > 1, and an 11-byte one (binary.Uvarint overflow)
+        struct.pack("<I", 0) + b"\x02" + b"\x81" * 9 + b"\x02" + b"\x01",
+        struct.pack("<I", 0) + b"\x02\x01" + b"\x80" * 10 + b"\x00",
+        # the sizes run off the end of the record
+        struct.pack("<I", 0) + b"\x05\x01\x01",
+    ]
+    for i, p in enumerate(payloads):
+        check(F.legacy_record(P, p), gpu_ctx, oracle, ("edge", i))
+        # after a good record, and followed by one
+        check(F.legacy_unpacked_file([b"pre"]) + F.legacy_record(P, p) + F.legacy_unpacked_file([b"post"]),
+              gpu_ctx, oracle, ("edge-ctx", i))
+
+
+@pytest.mark.gpu
+def test_gpu_v1_random(gpu_ctx, oracle):
+    rng = random.Random(11)
+    for t in range(40):
+        check(random_v1_file(rng), gpu_ctx, oracle, t)
+
+
+@pytest.mark.gpu
+def test_gpu_v1_mutations(gpu_ctx, oracle):
+    """Bit flips and truncations of v1 files: items and error text equal the oracle's."""
+    rng = random.Random(12)
+    for t in range(150):
+        d = bytearray(random_v1_file(rng, rng.randrange(1, 60)))
+        if not d:
+            continue
+        if rng.random() < 0.3:
+            del d[rng.randrange(8, len(d) + 1):]
+        else:
+            for _ in range(rng.choice([1, 2])):
+                d[rng.randrange(8, len(d)) if len(d) > 8 else 0] ^= 1 << rng.randrange(8)
+        if len(d) >= 8:
+            check(bytes(d), gpu_ctx, oracle, t)
+
+
+@pytest.mark.gpu
+def test_gpu_v1_spans(oracle):
+    """A small span: records larger than it (the one-record staging path) and
+    many spans of records (the read-ahead path)."""
+    from base_amd.recordio import gpu
+    rng = random.Random(13)
+    ctx = gpu.Context(0, max_span_bytes=64 << 10)
+    try:
+        items = [bytes([i & 0xFF]) * rng.choice([10, 1000, 70000, 200000]) for i in range(40)]
+        for data in (F.legacy_unpacked_file(items), F.legacy_packed_file(items, max_items=3),
+                     F.legacy_packed_file([b"q" * 50] * 20000)):
+            check(data, ctx, oracle)
+            # truncated inside a large record
+            check(data[:len(data) - 7], ctx, oracle)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_v1_seek(gpu_ctx, oracle):
+    """Seek (legacyscanner.go:67-82): random locations against a fresh oracle
+    Seek; a record-header error is cleared by Seek (sc.Reset), an adapter
+    error (Unpack, magic, location) is not."""
+    from base_amd.recordio import gpu
+    from base_amd.recordio.writer import ItemLocation
+    rng = random.Random(14)
+    data = random_v1_file(random.Random(5), 300)
+    ref = oracle.scan(data)
+    assert ref.err == "" and ref.items
+    sc = gpu.NewScanner(data, ctx=gpu_ctx)
+    for _ in range(60):
+        k = rng.randrange(len(ref.items))
+        blk, it = ref.locations[k][0], ref.locations[k][1] + (rng.random() < 0.1) * 10**6
+        want = oracle.seek_get(data, blk, it)
+        sc2 = gpu.NewScanner(data, ctx=gpu_ctx)
+        sc2.Seek(ItemLocation(blk, it))
+        got = [sc2.Get()] if sc2.Scan() else []
+        e = sc2.Finish()
+        assert got == want.items and ("" if e is None else str(e)) == want.err
+        if not want.err:
+            sc.Seek(ItemLocation(blk, it))
+            assert sc.Scan() and sc.Get() == ref.items[k]
+    sc.Finish()
+    # header CRC error, then Seek past it: scanning resumes
+    recs = [F.legacy_record(F.MAGIC_LEGACY_UNPACKED, bytes([65 + i]) * 3) for i in range(4)]
+    bad = bytearray(recs[1])
+    bad[9] ^= 1
+    data = recs[0] + bytes(bad) + recs[2] + recs[3]
+    sc = gpu.NewScanner(data, ctx=gpu_ctx)
+    got = []
+    while sc.Scan():
+        got.append(sc.Get())
+    assert got == [b"AAA"] and "crc check failed - corrupt record header" in str(sc.Err())
+    sc.Seek(ItemLocation(2 * 23, 0))
+    assert sc.Err() is None
+    got = []
+    while sc.Scan():
+        got.append(sc.Get())
+    assert got == [b"CCC", b"DDD"] and sc.Finish() is None
+    # invalid magic is sticky
+    data = recs[0] + F.legacy_record(F.MAGIC_TRAILER, b"t") + recs[2]
+    sc = gpu.NewScanner(data, ctx=gpu_ctx)
+    while sc.Scan():
+        pass
+    assert "invalid magic number" in str(sc.Err())
+    sc.Seek(ItemLocation(2 * 23 - 1, 0))
+    assert not sc.Scan() and "invalid magic number" in str(sc.Finish())
+
+
+@pytest.mark.gpu
+def test_gpu_v1_batch_layer(gpu_ctx, oracle):
+    """rio_scan_v1_span directly: a span cut mid-record stops at the last whole
+    record (MORE), a span too small for its first record says what it needs."""
+    from base_amd.recordio import gpu
+    data = F.legacy_packed_file([b"a" * 100] * 50, max_items=10)  # 5 records of 1000+ bytes
+    rec_len = len(data) // 5
+    b = gpu_ctx.scan_v1_span(data[:rec_len * 2 + 30], is_file_end=False)
+    assert b.stop == gpu.RIO_STOP_MORE and b.consumed == 2 * rec_len and b.n_blocks == 2 and b.n_items == 20
+    assert gpu.batch_items(b) == [b"a" * 100] * 20
+    b = gpu_ctx.scan_v1_span(data[:100], is_file_end=False)
+    assert b.stop == gpu.RIO_STOP_MORE and b.consumed == 0 and b.n_items == 0 and b.err.a == rec_len
+    b = gpu_ctx.scan_v1_span(data, file_off=0, is_file_end=True)
+    assert b.stop == gpu.RIO_STOP_EOF and b.n_items == 50 and b.consumed == len(data)
+    assert [b.block_file_off[i] for i in range(5)] == [i * rec_len for i in range(5)]
