@@ -12,6 +12,16 @@ struct V1Job {
   unsigned long long size;       // payload length
   unsigned long long nbufs;      // item count (the first varint, checked on the host)
   unsigned long long item_base;  // its first item slot in the batch
+  unsigned long long hbytes;     // payload bytes staged: the header's bound, or all of it
+  unsigned long long span_off;   // the payload's offset in the caller's span (item views)
+};
+
+// host-side record table of a v1 span (pipeline.cpp)
+struct V1Rec {
+  uint64_t off, first;  // span offset of the record, its first item slot
+};
+struct V1Unp {
+  uint64_t slot, off, len;  // an unpacked record's item
 };
 
 enum V1Status : uint32_t {
@@ -20,6 +30,7 @@ enum V1Status : uint32_t {
   kV1Crc = 2,       // "crc check failed - corrupt packed record header" a = computed, b = stored
   kV1Offset = 3,    // "offset greater than buf size (%v > %v)"          a = end, b = max
   kV1Range = 4,     // item sizes the reference would panic slicing
+  kV1More = 5,      // the header runs past the staged bytes: restage the whole record
 };
 
 struct V1Res {
@@ -29,7 +40,7 @@ struct V1Res {
   unsigned long long pad2;
 };
 
-void launch_v1_unpack(const uint8_t *dspan, uint64_t span_lo, const V1Job *jobs, uint64_t njobs,
+void launch_v1_unpack(const uint8_t *dstage, const V1Job *jobs, uint64_t njobs,
                       unsigned long long *item_off, unsigned long long *item_len, V1Res *res, hipStream_t st);
 
 }  // namespace rio

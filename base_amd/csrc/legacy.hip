@@ -16,7 +16,10 @@
 //   pass 1: (header valid) the sizes again -> item offsets by a wave prefix
 //           sum with a running carry, Unpack's bounds checks, item views
 //           written coalesced-ish (consecutive items -> consecutive slots).
-// Item views are span offsets: items stay in the caller's host span.
+// Only each packed record's header bound (crc, count, 10 bytes per size
+// varint) is staged to the device; a header that runs past it (a size varint
+// of more than 10 bytes, an error) is restaged whole and run again. Item views
+// are span offsets: items stay in the caller's host span.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -81,7 +84,7 @@ __device__ __forceinline__ uint32_t v1_term_mask(const uint32_t (&w)[4]) {
   return term4(w[0]) | (term4(w[1]) << 4) | (term4(w[2]) << 8) | (term4(w[3]) << 12);
 }
 
-__global__ void __launch_bounds__(256) k_v1_unpack(const uint8_t *__restrict__ dspan, uint64_t span_lo,
+__global__ void __launch_bounds__(256) k_v1_unpack(const uint8_t *__restrict__ dstage,
                                                    const V1Job *__restrict__ jobs, uint64_t njobs,
                                                    unsigned long long *__restrict__ item_off,
                                                    unsigned long long *__restrict__ item_len, V1Res *res) {
@@ -102,11 +105,11 @@ __global__ void __launch_bounds__(256) k_v1_unpack(const uint8_t *__restrict__ d
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   for (uint64_t j = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; j < njobs; j += nwaves) {
     const V1Job jb = jobs[j];
-    const uint8_t *p = dspan + jb.off;  // the record payload
+    const uint8_t *p = dstage + jb.off;  // the record payload's staged prefix
     const int64_t len = (int64_t)jb.size;
     const uint64_t nb = jb.nbufs;
     const uint8_t *h = p + 4;  // header varints: ordinal 0 = item count, 1..nb = sizes
-    const int64_t hlen = len - 4;
+    const int64_t hlen = (int64_t)jb.hbytes - 4;
     V1Res r{kV1Ok, 0, 0, 0, 0};
     // ---- pass 0: header end, first bad size varint, CRC of h[0, hend)
     uint64_t ord_base = 0;
@@ -182,10 +185,14 @@ __global__ void __launch_bounds__(256) k_v1_unpack(const uint8_t *__restrict__ d
       const long long wl = __shfl(lmax, 63, 64);
       if (wl > prev_term) prev_term = wl;
     }
-    if (r.status == kV1Ok && hend < 0) {  // the record ended first: n == 0
-      r.status = kV1ItemSize;
-      r.a = ord_base == 0 ? 0 : ord_base - 1;
-      r.b = 0;
+    if (r.status == kV1Ok && hend < 0) {
+      if (jb.hbytes < jb.size) {  // (a varint longer than 10 bytes) past the staged bound
+        r.status = kV1More;
+      } else {  // the record ended first: n == 0
+        r.status = kV1ItemSize;
+        r.a = ord_base == 0 ? 0 : ord_base - 1;
+        r.b = 0;
+      }
     }
     if (r.status == kV1Ok) {
       const uint64_t m = (uint64_t)hend;
@@ -203,7 +210,7 @@ __global__ void __launch_bounds__(256) k_v1_unpack(const uint8_t *__restrict__ d
     if (r.status == kV1Ok) {
       const uint64_t pend = 4 + (uint64_t)hend;  // packed = payload[pend:]
       const uint64_t max = (uint64_t)len - pend;
-      const uint64_t vbase = span_lo + jb.off + pend;
+      const uint64_t vbase = jb.span_off + pend;
       if (nb == 0) {  // packed[0:0]: one empty item
         if (l == 0) {
           item_off[jb.item_base] = vbase;
@@ -289,13 +296,13 @@ __global__ void __launch_bounds__(256) k_v1_unpack(const uint8_t *__restrict__ d
   }
 }
 
-void launch_v1_unpack(const uint8_t *dspan, uint64_t span_lo, const V1Job *jobs, uint64_t njobs,
+void launch_v1_unpack(const uint8_t *dstage, const V1Job *jobs, uint64_t njobs,
                       unsigned long long *item_off, unsigned long long *item_len, V1Res *res, hipStream_t st) {
   uint64_t g = (njobs + 3) / 4;
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(k_v1_unpack, dim3((unsigned)g), dim3(256), 0, st, dspan, span_lo, jobs, njobs, item_off,
-                     item_len, res);
+  hipLaunchKernelGGL(k_v1_unpack, dim3((unsigned)g), dim3(256), 0, st, dstage, jobs, njobs, item_off, item_len,
+                     res);
 }
 
 }  // namespace rio

@@ -120,7 +120,15 @@ struct rio_ctx {
   Ctl *h_ctl = nullptr;  // pinned copy of the control block
   rio_results res;       // host results of rio_scan_span (scanners bring their own)
   uint8_t *h_stage = nullptr;  // pinned staging of rio_decode_block's chunk stream
-  // v1 (legacy) spans: device staging of the packed records, jobs, views
+  // v1 (legacy) spans: the record table (host), packed-record headers staged
+  // (pinned host + device), jobs, views
+  std::vector<V1Rec> v1_recs;
+  std::vector<V1Job> v1_jobs;
+  std::vector<uint64_t> v1_job_rec;
+  std::vector<V1Unp> v1_unp;
+  std::vector<V1Res> v1_res;
+  uint8_t *h_v1 = nullptr;
+  uint64_t h_v1_cap = 0;
   uint8_t *d_v1 = nullptr;
   uint64_t d_v1_cap = 0;
   V1Job *d_v1_jobs = nullptr;
@@ -185,6 +193,7 @@ static void free_all(rio_ctx *c) {
   if (c->h_ctl) hipHostFree(c->h_ctl);
   c->res.release();
   if (c->h_stage) hipHostFree(c->h_stage);
+  if (c->h_v1) hipHostFree(c->h_v1);
   for (hipEvent_t e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->evA) hipEventDestroy(c->evA);
@@ -866,6 +875,30 @@ uint64_t v1_uvarint(const uint8_t *p, uint64_t n, int64_t *cnt) {  // binary.Uva
   return 0;
 }
 
+// CRC32-IEEE of the 8 bytes of a record header's size field: slicing-by-8
+uint32_t v1_crc8(const uint8_t *p) {
+  static const std::vector<uint32_t> tab = [] {
+    std::vector<uint32_t> t(8 * 256);
+    for (uint32_t b = 0; b < 256; b++) {
+      uint32_t c = b;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? kPoly ^ (c >> 1) : c >> 1;
+      t[b] = c;
+    }
+    for (int s = 1; s < 8; s++)
+      for (uint32_t b = 0; b < 256; b++) t[s * 256 + b] = (t[(s - 1) * 256 + b] >> 8) ^ t[t[(s - 1) * 256 + b] & 0xff];
+    return t;
+  }();
+  uint32_t lo, hi;
+  memcpy(&lo, p, 4);
+  memcpy(&hi, p + 4, 4);
+  lo ^= 0xFFFFFFFFu;
+  const uint32_t *T = tab.data();
+  const uint32_t c = T[7 * 256 + (lo & 0xff)] ^ T[6 * 256 + ((lo >> 8) & 0xff)] ^ T[5 * 256 + ((lo >> 16) & 0xff)] ^
+                     T[4 * 256 + (lo >> 24)] ^ T[3 * 256 + (hi & 0xff)] ^ T[2 * 256 + ((hi >> 8) & 0xff)] ^
+                     T[1 * 256 + ((hi >> 16) & 0xff)] ^ T[hi >> 24];
+  return ~c;
+}
+
 int dgrow(uint8_t **p, uint64_t *cap, uint64_t n) {
   if (*cap >= n) return 0;
   const uint64_t c = n + n / 4 + 64;
@@ -898,20 +931,18 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
   memset(out, 0, sizeof(*out));
   HIP_OK(hipSetDevice(c->device));
   rio_results &r = res ? *res : c->res;
-  struct Rec {
-    uint64_t off, first;  // span offset of the record, its first item
-  };
-  struct Unp {
-    uint64_t slot, off, len;
-  };
-  std::vector<Rec> recs;
-  std::vector<V1Job> jobs;
-  std::vector<uint64_t> job_rec;
-  std::vector<Unp> unp;
+  std::vector<V1Rec> &recs = c->v1_recs;
+  std::vector<V1Job> &jobs = c->v1_jobs;
+  std::vector<uint64_t> &job_rec = c->v1_job_rec;
+  std::vector<V1Unp> &unp = c->v1_unp;
+  recs.clear();
+  jobs.clear();
+  job_rec.clear();
+  unp.clear();
   rio_error e{};
   bool err = false;
   int32_t stop = RIO_STOP_MORE;
-  uint64_t p = 0, items = 0, need = 0;
+  uint64_t p = 0, items = 0, need = 0, staged = 0;
   for (;;) {
     if (p == nbytes) {
       if (is_file_end) stop = RIO_STOP_EOF;
@@ -933,7 +964,7 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
     uint32_t crc;
     memcpy(&size, h + 8, 8);
     memcpy(&crc, h + 16, 4);
-    const uint32_t ncrc = crc32_host(h + 8, 8);  // unmarshalHeader, recordio.go:324-334
+    const uint32_t ncrc = v1_crc8(h + 8);  // unmarshalHeader, recordio.go:324-334
     if (ncrc != crc) {
       rio_set_error(&e, RIO_ERR_V1_RECORD, at, "recordio: crc check failed - corrupt record header (%u != %u)?", ncrc,
                     crc);
@@ -983,13 +1014,17 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
         err = true;
         break;
       }
+      // a valid header fits in crc + count + 10 bytes per size varint
+      const uint64_t bound = 4 + (uint64_t)n + 10 * nb;
+      const uint64_t hb = bound < size ? bound : size;
       job_rec.push_back(recs.size());
-      jobs.push_back(V1Job{p + 20, size, nb, items});
-      recs.push_back(Rec{p, items});
+      jobs.push_back(V1Job{staged, size, nb, items, hb, p + 20});
+      staged += (hb + 15) & ~15ull;
+      recs.push_back(V1Rec{p, items});
       items += nb ? nb : 1;
     } else if (memcmp(h, kV1MagicUnpacked, 8) == 0) {
-      unp.push_back(Unp{items, p + 20, size});
-      recs.push_back(Rec{p, items});
+      unp.push_back(V1Unp{items, p + 20, size});
+      recs.push_back(V1Rec{p, items});
       items += 1;
     } else {
       rio_set_error(&e, RIO_ERR_BAD_MAGIC, at, "recordio: invalid magic number: [%u %u %u %u %u %u %u %u]", h[0],
@@ -1005,8 +1040,6 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
   float kms = 0;
   uint64_t nrec = recs.size(), nitems = items, consumed = p;
   if (!jobs.empty()) {
-    const uint64_t lo = jobs.front().off, hi = jobs.back().off + jobs.back().size;
-    if (dgrow(&c->d_v1, &c->d_v1_cap, hi - lo + 64)) return -1;
     if (c->d_v1_jobs_cap < jobs.size()) {
       const uint64_t cap = jobs.size() + jobs.size() / 4 + 64;
       if (dalloc(&c->d_v1_jobs, cap) || dalloc(&c->d_v1_res, cap)) return -1;
@@ -1017,23 +1050,63 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
       if (dalloc(&c->d_v1_off, cap) || dalloc(&c->d_v1_len, cap)) return -1;
       c->d_v1_items_cap = cap;
     }
-    for (V1Job &j : jobs) j.off -= lo;
-    HIP_OK(hipMemcpyAsync(c->d_v1, span + lo, hi - lo, hipMemcpyHostToDevice, c->st));
-    HIP_OK(hipMemcpyAsync(c->d_v1_jobs, jobs.data(), jobs.size() * sizeof(V1Job), hipMemcpyHostToDevice, c->st));
-    HIP_OK(hipEventRecord(c->ev[kEvStart], c->st));
-    launch_v1_unpack(c->d_v1, lo, c->d_v1_jobs, jobs.size(), c->d_v1_off, c->d_v1_len, c->d_v1_res, c->st);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(c->ev[kEvEnd], c->st));
-    std::vector<V1Res> jr(jobs.size());
-    HIP_OK(hipMemcpyAsync(jr.data(), c->d_v1_res, jr.size() * sizeof(V1Res), hipMemcpyDeviceToHost, c->st));
+    std::vector<V1Res> &jr = c->v1_res;
+    jr.resize(jobs.size());
+    // round 0: every packed record's header bound; round 1: the records whose
+    // header ran past it, whole (their error is then exact)
+    std::vector<V1Job> run;
+    std::vector<uint64_t> sel;
+    for (int round = 0; round < 2; round++) {
+      if (round == 1) {
+        run.clear();
+        uint64_t at = 0;
+        for (size_t k = 0; k < jobs.size(); k++) {
+          if (jr[k].status != kV1More) continue;
+          V1Job j = jobs[k];
+          j.off = at;
+          j.hbytes = j.size;
+          at += (j.size + 15) & ~15ull;
+          run.push_back(j);
+          sel.push_back(k);
+        }
+        if (run.empty()) break;
+        staged = at;
+      }
+      const std::vector<V1Job> &rj = round == 0 ? jobs : run;
+      if (c->h_v1_cap < staged + 64) {
+        if (c->h_v1) hipHostFree(c->h_v1);
+        c->h_v1 = nullptr;
+        c->h_v1_cap = staged + staged / 4 + 4096;
+        HIP_OK(hipHostMalloc((void **)&c->h_v1, c->h_v1_cap, hipHostMallocDefault));
+      }
+      if (dgrow(&c->d_v1, &c->d_v1_cap, staged + 64)) return -1;
+      for (const V1Job &j : rj) memcpy(c->h_v1 + j.off, span + j.span_off, j.hbytes);
+      HIP_OK(hipMemcpyAsync(c->d_v1, c->h_v1, staged, hipMemcpyHostToDevice, c->st));
+      HIP_OK(hipMemcpyAsync(c->d_v1_jobs, rj.data(), rj.size() * sizeof(V1Job), hipMemcpyHostToDevice, c->st));
+      HIP_OK(hipEventRecord(c->ev[kEvStart], c->st));
+      launch_v1_unpack(c->d_v1, c->d_v1_jobs, rj.size(), c->d_v1_off, c->d_v1_len, c->d_v1_res, c->st);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipEventRecord(c->ev[kEvEnd], c->st));
+      if (round == 0) {
+        HIP_OK(hipMemcpyAsync(jr.data(), c->d_v1_res, jr.size() * sizeof(V1Res), hipMemcpyDeviceToHost, c->st));
+        HIP_OK(hipStreamSynchronize(c->st));
+      } else {
+        std::vector<V1Res> r1(rj.size());
+        HIP_OK(hipMemcpyAsync(r1.data(), c->d_v1_res, r1.size() * sizeof(V1Res), hipMemcpyDeviceToHost, c->st));
+        HIP_OK(hipStreamSynchronize(c->st));
+        for (size_t q = 0; q < sel.size(); q++) jr[sel[q]] = r1[q];
+      }
+      float ms = 0;
+      hipEventElapsedTime(&ms, c->ev[kEvStart], c->ev[kEvEnd]);
+      kms += ms;
+    }
     HIP_OK(hipMemcpyAsync(h_off, c->d_v1_off, items * 8, hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipMemcpyAsync(h_len, c->d_v1_len, items * 8, hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipStreamSynchronize(c->st));
-    hipEventElapsedTime(&kms, c->ev[kEvStart], c->ev[kEvEnd]);
     for (size_t k = 0; k < jobs.size(); k++) {  // the first packed record that failed ends the batch there
       const V1Res &x = jr[k];
       if (x.status == kV1Ok) continue;
-      const Rec &rc = recs[job_rec[k]];
+      const V1Rec &rc = recs[job_rec[k]];
       const uint64_t at = file_off + rc.off;
       memset(&e, 0, sizeof(e));
       switch (x.status) {
@@ -1053,8 +1126,11 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
                       "), likely due to a mismatched transform or a truncated file",
                       (uint64_t)x.a, (uint64_t)x.b);
         break;
-      default:  // the reference panics slicing
+      case kV1Range:  // the reference panics slicing
         rio_set_error(&e, RIO_ERR_ITEM_RANGE, at, "recordio: corrupt packed record header, item sizes out of range");
+        break;
+      default:
+        rio_set_error(&e, RIO_ERR_HIP, at, "internal: v1 record status %u", x.status);
       }
       e.a = x.a;
       e.b = x.b;
@@ -1066,7 +1142,7 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
       break;
     }
   }
-  for (const Unp &u : unp) {
+  for (const V1Unp &u : unp) {
     if (u.slot >= nitems) break;
     h_off[u.slot] = u.off;
     h_len[u.slot] = u.len;

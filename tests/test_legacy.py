@@ -212,6 +212,8 @@ def test_gpu_v1_unpack_edges(gpu_ctx, oracle):
         struct.pack("<I", 0) + b"\x02\x01" + b"\x80" * 10 + b"\x00",
         # the sizes run off the end of the record
         struct.pack("<I", 0) + b"\x05\x01\x01",
+        # a 25-byte size varint in a long record: past the staged header bound, restaged whole
+        struct.pack("<I", 0) + b"\x02" + b"\x80" * 24 + b"\x01" + b"\x01" + b"z" * 1000,
     ]
     for i, p in enumerate(payloads):
         check(F.legacy_record(P, p), gpu_ctx, oracle, ("edge", i))
