@@ -110,7 +110,9 @@ class Writer:
         if self.cur is None:
             self.cur = []
         self.cur.append(v)
-        if len(self.cur) >= self.opts.MaxItems:
+        # a block's object slice has capacity MaxItems + 1 and is flushed when
+        # full (writerv2.go:315, 366-368): MaxItems + 1 items per block
+        if len(self.cur) >= self.opts.MaxItems + 1:
             self._flush_body()
 
     def Flush(self):

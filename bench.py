@@ -2,7 +2,9 @@
 
 Workload (BASELINE.json configs[1]): uncompressed ('none')
 recordio, 1,000,000 x 256 B records (splitmix64 bytes, seed 0x5EED0001),
-MaxItems=253 -> 3,953 blocks of exactly 2 chunks (64 KiB); the 7,906 body
+253 records per block (the writer packs MaxItems + 1 per block,
+writerv2.go:315, 366-368: MaxItems=252) -> 3,953 blocks of exactly 2 chunks
+(64 KiB); the 7,906 body
 chunks are replicated 64x device-resident (~16.1 GiB, 64M records) behind one
 header chunk. One step = one pass of the scan hot path over that whole file:
 chunk CRC32 verify + block structure + varint unpack -> one (offset, length)
@@ -53,8 +55,9 @@ def c2_records() -> np.ndarray:
 
 def make_c2_file(max_items: int = MAX_ITEMS):
     """C2 file bytes (header chunk + 3,953 two-chunk blocks) and the record count.
-    max_items=16384 (the writer default, writerv2.go:28-29) gives the C1 file:
-    62 blocks of 130 chunks."""
+    max_items = records per block = the writer's MaxItems + 1 (writerv2.go:315,
+    366-368); 16385 (the default MaxItems = 16384, writerv2.go:28-29) gives the
+    C1 file: 62 blocks of 130 chunks."""
     from base_amd.recordio import format as F
     recs = c2_records()
     out = [F.chunk_block(F.MAGIC_HEADER, F.packed_block_payload([F.marshal_header([])]))]
@@ -69,7 +72,7 @@ def make_c2_file(max_items: int = MAX_ITEMS):
 
 def make_c1_file():
     """C1 (configs[0]): the same records at the default MaxItems = 16384."""
-    return make_c2_file(16384)
+    return make_c2_file(16385)
 
 
 PMC_FILE = os.path.join(ROOT, "profiles", "r02_c2_pmc.json")
@@ -405,7 +408,7 @@ def main():
            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-           "config": {"workload": "C2: none codec, 1e6 x 256 B records x %d replicas, MaxItems=253 "
+           "config": {"workload": "C2: none codec, 1e6 x 256 B records x %d replicas, 253 per block (MaxItems=252) "
                                   "(64 KiB blocks), chunk CRC32 + packed-unpack" % args.replicas,
                       "records_per_gpu": int(n_items), "record_bytes": RECORD_SIZE,
                       "parallelism": f"{world} GPU(s), independent replica sets",

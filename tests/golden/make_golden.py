@@ -337,7 +337,7 @@ def main():
         note="partial last chunk beyond ChunkScanner.limit is never read")
     # a partial chunk inside a block -> unexpected EOF (chunk.go:318-322)
     recs2 = [rnd_bytes(rng, 20000) for _ in range(4)]
-    d2 = write_file(recs2, WriterOpts(MaxItems=2))  # blocks of 2 chunks
+    d2 = write_file(recs2, WriterOpts(MaxItems=1))  # 2 items (MaxItems + 1) = 2 chunks per block
     add("err_truncated", d2[:-5000], recs2[:2], err="unexpected EOF")
     # file ending at a chunk boundary inside a block: silent end (io.EOF ignored)
     last_c0, last_t = blks[-1]

@@ -1,7 +1,7 @@
 """BASELINE.json configs at full size on the GPU (pytest -m gpu), plus the
 reference's randomized sharding tests restated (recordio/v2_test.go:458-591).
 
-- C1 (configs[0]): 1M x 256 B at the writer's default MaxItems = 16384
+- C1 (configs[0]): 1M x 256 B at the writer's default MaxItems = 16384 (16,385 per block)
   (130-chunk blocks, 32 KiB varint headers: the general parser's path), every
   record byte-exact against the generator and against the oracle's scan;
 - C4 (configs[3]): the zstd workload's base file (tools/c4_data.py: record sizes
@@ -58,7 +58,8 @@ def _views_to_array(b, span, nrec, rec_len):
 
 def test_full_size_c1(oracle):
     """configs[0] at full size: 1,000,000 x 256 B, MaxItems 16384 -> 62 blocks of
-    130 chunks (last block 576 items in 5 chunks), SURVEY.md §8(a)."""
+    16,385 items (MaxItems + 1, writerv2.go:315, 366-368) in 130 chunks (last
+    block 515 items in 5 chunks), SURVEY.md §8(a)."""
     import bench
     from base_amd.recordio import gpu
     data, nrec = bench.make_c1_file()
@@ -68,7 +69,7 @@ def test_full_size_c1(oracle):
     assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
     assert b.n_items == nrec and b.n_blocks == 62
     first = np.ctypeslib.as_array(b.block_first_item, shape=(b.n_blocks + 1,)).astype(np.int64)
-    assert np.all(np.diff(first)[:-1] == 16384) and first[-1] - first[-2] == 576
+    assert np.all(np.diff(first)[:-1] == 16385) and first[-1] - first[-2] == 515
     span = np.frombuffer(data, dtype=np.uint8)[32768:]
     got = _views_to_array(b, span, nrec, 256)
     recs = bench.c2_records()
