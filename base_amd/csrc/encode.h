@@ -1,0 +1,34 @@
+// Writer encode path (encode.hip, deflate_enc.hip; driver in pipeline.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rio {
+
+struct EncArgs {
+  const uint8_t *data;                  // item bytes, back to back
+  const unsigned long long *item_end;   // exclusive ends (n_items)
+  uint64_t n_items;
+  uint64_t per_block;                   // items per block (the writer's MaxItems + 1)
+  uint64_t nblocks;
+  int32_t codec;
+  int32_t level;
+  unsigned long long magic;             // block magic, little-endian
+  // per block (nblocks + 1)
+  unsigned long long *hdr_len, *hdr_off, *pay_len, *nck, *ck0, *comp_off;
+  uint8_t *hdr;                         // varint headers
+  uint8_t *comp;                        // transformed payloads (flate)
+  // per chunk
+  uint32_t *ck_block, *ck_size;
+  uint8_t *out;
+};
+
+void launch_enc_count(const EncArgs &a, hipStream_t st);
+void launch_enc_header(const EncArgs &a, hipStream_t st);
+void launch_enc_nck(const EncArgs &a, hipStream_t st);
+void launch_enc_ckmap(const EncArgs &a, hipStream_t st);
+void launch_enc_chunks(const EncArgs &a, uint64_t nchunks, hipStream_t st);
+void launch_enc_boff(const unsigned long long *ck0, unsigned long long *boff, uint64_t nblocks, hipStream_t st);
+void launch_enc_crc(uint8_t *out, const uint32_t *ck_crc, uint64_t nchunks, hipStream_t st);
+
+}  // namespace rio

@@ -20,6 +20,7 @@
 #include <utility>
 #include <vector>
 
+#include "encode.h"
 #include "legacy.h"
 #include "pipeline.h"
 #include "rio_internal.h"
@@ -129,6 +130,14 @@ struct rio_ctx {
   std::vector<V1Res> v1_res;
   uint8_t *h_v1 = nullptr;
   uint64_t h_v1_cap = 0;
+  // writer encode path: per-block arrays (6 x (n + 1)), varint headers,
+  // transformed payloads; host-path staging of items, ends and output
+  unsigned long long *e_blk = nullptr;
+  uint64_t e_blk_cap = 0;
+  uint8_t *e_hdr = nullptr, *e_comp = nullptr, *e_data = nullptr, *e_out = nullptr;
+  uint64_t e_hdr_cap = 0, e_comp_cap = 0, e_data_cap = 0, e_out_cap = 0;
+  unsigned long long *e_ends = nullptr, *e_boff = nullptr;
+  uint64_t e_ends_cap = 0, e_boff_cap = 0;
   uint8_t *d_v1 = nullptr;
   uint64_t d_v1_cap = 0;
   V1Job *d_v1_jobs = nullptr;
@@ -187,7 +196,8 @@ static void free_all(rio_ctx *c) {
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.cmp, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
-                c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len};
+                c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len,
+                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff};
   for (void *p : ps)
     if (p) hipFree(p);
   if (c->h_ctl) hipHostFree(c->h_ctl);
@@ -1174,4 +1184,146 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
 extern "C" int rio_scan_v1_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
                                 int32_t is_file_end, rio_batch *out) {
   return rio_scan_v1_span_mode(ctx, span, nbytes, file_off, is_file_end, nullptr, out);
+}
+
+// ------------------------------------------------------------ writer encode
+// the blocks of a v2 file from items, on the GPU (encode.hip).
+namespace {
+
+const unsigned long long kMagicBody = 0x2e3c0734eb47762eull;     // MagicPacked, little-endian
+const unsigned long long kMagicHdr = 0xf70416c25cd9e1d9ull;      // MagicHeader
+const unsigned long long kMagicTrl = 0x3a75dfcbd71abafeull;      // MagicTrailer
+
+template <class T>
+int egrow(T **p, uint64_t *cap, uint64_t n) {
+  if (*cap >= n) return 0;
+  const uint64_t c = n + n / 4 + 256;
+  if (dalloc(p, c)) return -1;
+  *cap = c;
+  return 0;
+}
+
+}  // namespace
+
+static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data, const unsigned long long *ends,
+                      uint8_t *out, uint64_t out_cap, uint64_t *out_len, unsigned long long *boff, rio_error *err) {
+  DevBufs &d = c->d;
+  hipStream_t st = c->st;
+  const uint64_t per = a->items_per_block ? a->items_per_block : 16385;  // DefaultPackedItems + 1
+  const uint64_t nb = a->n_items ? (a->n_items + per - 1) / per : 0;
+  *out_len = 0;
+  if (nb == 0) return 0;
+  if (nb > c->max_chunks) {
+    rio_set_error(err, RIO_ERR_CAPACITY, 0, "%" PRIu64 " blocks exceed the ctx's %" PRIu64 " chunks", nb,
+                  c->max_chunks);
+    return RIO_ERR_CAPACITY;
+  }
+  if (egrow(&c->e_blk, &c->e_blk_cap, 6 * (nb + 1))) return -1;
+  EncArgs ea{};
+  ea.data = data;
+  ea.item_end = ends;
+  ea.n_items = a->n_items;
+  ea.per_block = per;
+  ea.nblocks = nb;
+  ea.codec = a->codec;
+  ea.level = a->level;
+  ea.magic = a->kind == RIO_BLOCK_HEADER ? kMagicHdr : a->kind == RIO_BLOCK_TRAILER ? kMagicTrl : kMagicBody;
+  ea.hdr_len = c->e_blk;
+  ea.hdr_off = c->e_blk + (nb + 1);
+  ea.pay_len = c->e_blk + 2 * (nb + 1);
+  ea.nck = c->e_blk + 3 * (nb + 1);
+  ea.ck0 = c->e_blk + 4 * (nb + 1);
+  ea.comp_off = c->e_blk + 5 * (nb + 1);
+  HIP_OK(hipEventRecord(c->ev[kEvStart], st));
+  launch_enc_count(ea, st);
+  launch_chunk_scan(ea.hdr_len, ea.hdr_off, d.scan_tmp, nb, st);
+  unsigned long long hdr_total = 0;
+  HIP_OK(hipMemcpyAsync(&hdr_total, ea.hdr_off + nb, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (egrow(&c->e_hdr, &c->e_hdr_cap, hdr_total + 16)) return -1;
+  ea.hdr = c->e_hdr;
+  launch_enc_header(ea, st);
+  launch_enc_nck(ea, st);
+  launch_chunk_scan(ea.nck, ea.ck0, d.scan_tmp, nb, st);
+  unsigned long long nchunks = 0;
+  HIP_OK(hipMemcpyAsync(&nchunks, ea.ck0 + nb, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  *out_len = nchunks * kChunk;
+  if (nchunks > c->max_chunks) {
+    rio_set_error(err, RIO_ERR_CAPACITY, 0, "%llu chunks exceed the ctx's %" PRIu64, nchunks, c->max_chunks);
+    return RIO_ERR_CAPACITY;
+  }
+  if (out && *out_len > out_cap) {
+    rio_set_error(err, RIO_ERR_CAPACITY, 0, "output too small: need %" PRIu64 " bytes", *out_len);
+    return RIO_ERR_CAPACITY;
+  }
+  if (!out) return 0;  // sizing only
+  ea.ck_block = d.ck_block;
+  ea.ck_size = d.ck_size;
+  ea.out = out;
+  launch_enc_ckmap(ea, st);
+  launch_enc_chunks(ea, nchunks, st);
+  launch_crc(out, nchunks, d, CrcArgs{0, 0}, c->ncu, st, nullptr);
+  launch_enc_crc(out, d.ck_crc, nchunks, st);
+  if (boff) launch_enc_boff(ea.ck0, boff, nb, st);
+  HIP_OK(hipEventRecord(c->ev[kEvEnd], st));
+  HIP_OK(hipStreamSynchronize(st));
+  return 0;
+}
+
+static int encode_check(rio_ctx *ctx, const rio_encode_args *a, rio_error *err) {
+  if (!ctx || !a) return -1;
+  if (a->codec != RIO_CODEC_NONE) {
+    rio_set_error(err, RIO_ERR_ARG, 0, "encode: codec %d not supported", a->codec);
+    return RIO_ERR_ARG;
+  }
+  if (a->kind < RIO_BLOCK_BODY || a->kind > RIO_BLOCK_TRAILER) {
+    rio_set_error(err, RIO_ERR_ARG, 0, "encode: unknown block kind %d", a->kind);
+    return RIO_ERR_ARG;
+  }
+  if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+  return 0;
+}
+
+extern "C" int rio_encode_device(rio_ctx *ctx, const rio_encode_args *a, void *out, uint64_t out_cap,
+                                 uint64_t *out_len, uint64_t *block_off, rio_error *err) {
+  rio_error scratch;
+  if (!err) err = &scratch;
+  memset(err, 0, sizeof(*err));
+  if (!out_len) return -1;
+  if (int rc = encode_check(ctx, a, err)) return rc;
+  return encode_dev(ctx, a, (const uint8_t *)a->data, (const unsigned long long *)a->item_end, (uint8_t *)out,
+                    out_cap, out_len, (unsigned long long *)block_off, err);
+}
+
+extern "C" int rio_encode(rio_ctx *ctx, const rio_encode_args *a, uint8_t *out, uint64_t out_cap, uint64_t *out_len,
+                          uint64_t *block_off, rio_error *err) {
+  rio_error scratch;
+  if (!err) err = &scratch;
+  memset(err, 0, sizeof(*err));
+  if (!out_len) return -1;
+  if (int rc = encode_check(ctx, a, err)) return rc;
+  rio_ctx *c = ctx;
+  const uint64_t n = a->n_items;
+  const uint64_t bytes = n ? a->item_end[n - 1] : 0;
+  if (egrow(&c->e_data, &c->e_data_cap, bytes + 64) || egrow(&c->e_ends, &c->e_ends_cap, n + 1)) return -1;
+  if (bytes) HIP_OK(hipMemcpyAsync(c->e_data, a->data, bytes, hipMemcpyHostToDevice, c->st));
+  if (n) HIP_OK(hipMemcpyAsync(c->e_ends, a->item_end, n * 8, hipMemcpyHostToDevice, c->st));
+  const uint64_t per = a->items_per_block ? a->items_per_block : 16385;
+  const uint64_t nb = n ? (n + per - 1) / per : 0;
+  // size first, then encode into the ctx's device output and copy back
+  int rc = encode_dev(c, a, c->e_data, c->e_ends, nullptr, 0, out_len, nullptr, err);
+  if (rc) return rc;
+  if (*out_len > out_cap) {
+    rio_set_error(err, RIO_ERR_CAPACITY, 0, "output too small: need %" PRIu64 " bytes", *out_len);
+    return RIO_ERR_CAPACITY;
+  }
+  if (*out_len == 0) return 0;
+  if (egrow(&c->e_out, &c->e_out_cap, *out_len) || egrow(&c->e_boff, &c->e_boff_cap, nb + 1)) return -1;
+  rc = encode_dev(c, a, c->e_data, c->e_ends, c->e_out, c->e_out_cap, out_len, c->e_boff, err);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(out, c->e_out, *out_len, hipMemcpyDeviceToHost, c->st));
+  if (block_off) HIP_OK(hipMemcpyAsync(block_off, c->e_boff, nb * 8, hipMemcpyDeviceToHost, c->st));
+  HIP_OK(hipStreamSynchronize(c->st));
+  return 0;
 }

@@ -64,6 +64,15 @@ class RioReader(ctypes.Structure):
     _fields_ = [("user", ctypes.c_void_p), ("read_at", READ_AT), ("size", ctypes.c_int64)]
 
 
+class RioEncodeArgs(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("item_end", ctypes.c_void_p), ("n_items", ctypes.c_uint64),
+                ("items_per_block", ctypes.c_uint64), ("codec", ctypes.c_int32), ("kind", ctypes.c_int32),
+                ("level", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+RIO_BLOCK_BODY, RIO_BLOCK_HEADER, RIO_BLOCK_TRAILER = 0, 1, 2
+
+
 class RioMemory(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("size", ctypes.c_uint64)]
 
@@ -75,7 +84,7 @@ EXPORTS = [
     "rio_scanner_new", "rio_scanner_scan", "rio_scanner_get", "rio_scanner_next_batch", "rio_scanner_err",
     "rio_scanner_header_len", "rio_scanner_header_kv", "rio_scanner_trailer", "rio_scanner_seek",
     "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish", "rio_scanner_gather",
-    "rio_memory_reader", "rio_scan_v1_span",
+    "rio_memory_reader", "rio_scan_v1_span", "rio_encode", "rio_encode_device",
 ]
 
 _lib = None
@@ -106,6 +115,12 @@ def load(path: str = LIB_PATH):
         L.rio_scan_span.argtypes = [P, P, U64, U64, I32, U64, I32, ctypes.POINTER(RioBatch)]
         L.rio_scan_v1_span.restype = ctypes.c_int
         L.rio_scan_v1_span.argtypes = [P, P, U64, U64, I32, ctypes.POINTER(RioBatch)]
+        L.rio_encode.restype = ctypes.c_int
+        L.rio_encode.argtypes = [P, ctypes.POINTER(RioEncodeArgs), P, U64, ctypes.POINTER(U64), P,
+                                 ctypes.POINTER(RioError)]
+        L.rio_encode_device.restype = ctypes.c_int
+        L.rio_encode_device.argtypes = [P, ctypes.POINTER(RioEncodeArgs), P, U64, ctypes.POINTER(U64), P,
+                                        ctypes.POINTER(RioError)]
         L.rio_scan_device.restype = ctypes.c_int
         L.rio_scan_device.argtypes = [P, P, U64, U64, I32, U64, I32, ctypes.POINTER(RioBatch)]
         L.rio_scan_device_async.restype = ctypes.c_int
@@ -206,6 +221,41 @@ class Context:
             raise RuntimeError("rio_scan_v1_span: " + self.L.rio_last_error().decode())
         out._span_buf = buf
         return out
+
+    def encode(self, items, items_per_block: int = 0, kind: int = RIO_BLOCK_BODY,
+               codec: int = RIO_CODEC_NONE, level: int = 0):
+        """rio_encode: the chunk stream of the blocks holding `items` (a list of
+        bytes) and each block's offset in it (writerv2.go:388-442, chunk.go:100-141)."""
+        import numpy as np
+        n = len(items)
+        lens = np.fromiter((len(x) for x in items), dtype=np.uint64, count=n)
+        ends = np.cumsum(lens, dtype=np.uint64) if n else np.zeros(0, dtype=np.uint64)
+        blob = b"".join(bytes(x) for x in items)
+        return self.encode_arrays(blob, ends, items_per_block, kind, codec, level)
+
+    def encode_arrays(self, blob, ends, items_per_block: int = 0, kind: int = RIO_BLOCK_BODY,
+                      codec: int = RIO_CODEC_NONE, level: int = 0):
+        """rio_encode over item bytes `blob` (buffer protocol) and exclusive ends."""
+        import numpy as np
+        ends = np.ascontiguousarray(ends, dtype=np.uint64)
+        data = np.frombuffer(blob, dtype=np.uint8) if len(blob) else np.zeros(1, dtype=np.uint8)
+        n = int(ends.size)
+        per = items_per_block or 16385
+        nb = (n + per - 1) // per
+        a = RioEncodeArgs(data.ctypes.data, ends.ctypes.data if n else None, n, items_per_block, codec, kind,
+                          level, 0)
+        err = RioError()
+        olen = ctypes.c_uint64()
+        boff = np.zeros(max(nb, 1), dtype=np.uint64)
+        cap = 32768 * (nb + (len(blob) + 10 * (n + nb)) // 32740 + 2)  # >= the chunk stream
+        out = np.empty(cap, dtype=np.uint8)
+        rc = self.L.rio_encode(self.h, ctypes.byref(a), out.ctypes.data, cap, ctypes.byref(olen),
+                               boff.ctypes.data, ctypes.byref(err))
+        if rc < 0:
+            raise RuntimeError("rio_encode: " + self.L.rio_last_error().decode())
+        if rc != 0:
+            raise _err(err)
+        return out[:olen.value].tobytes(), [int(x) for x in boff[:nb]]
 
     def scan_host_ptr(self, host_ptr: int, nbytes: int, file_off: int = 0, is_file_end: bool = True,
                       limit_off: int = U64_MAX, codec: int = RIO_CODEC_NONE) -> RioBatch:

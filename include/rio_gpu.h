@@ -212,6 +212,43 @@ int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, const uint32_
                      int32_t codec, uint8_t *scratch, uint64_t cap, uint64_t *out_len,
                      rio_error *err);
 
+/* ---- writer encode path ----
+ * The blocks of a v2 file encoded on the GPU, byte for byte what
+ * recordio.NewWriter writes for the same items (none transformer):
+ * items_per_block items per block (the writer packs MaxItems + 1 per block:
+ * its object slice has capacity MaxItems + 1 and is flushed when full,
+ * writerv2.go:315, 366-368; the last block takes the rest; 0 = the default
+ * MaxItems 16384 + 1), each block generatePackedHeaderv2 + items
+ * (writerv2.go:388-442), framed by ChunkWriter.Write (internal/chunk.go:100-141:
+ * 28-byte headers, CRC32-IEEE over [12, 28 + size), 0xdeadbeef padding).
+ * kind picks the magic: body blocks (MagicPacked), the header block or the
+ * trailer block (one item each: the marshalled header / the trailer bytes,
+ * writerv2.go:327-335, 510-536). */
+enum rio_block_kind { RIO_BLOCK_BODY = 0, RIO_BLOCK_HEADER = 1, RIO_BLOCK_TRAILER = 2 };
+typedef struct rio_encode_args {
+    const void *data;          /* item bytes back to back */
+    const uint64_t *item_end;  /* n_items exclusive ends: item i = data[end[i-1], end[i]) */
+    uint64_t n_items;
+    uint64_t items_per_block;  /* MaxItems + 1; 0 = 16385 */
+    int32_t codec;             /* RIO_CODEC_NONE */
+    int32_t kind;              /* enum rio_block_kind */
+    int32_t level;             /* reserved (transformer level), 0 */
+    int32_t reserved;
+} rio_encode_args;
+/* Host memory in and out: writes the chunk stream to out (out_cap bytes) and
+ * each block's offset in it (ItemLocation.Block minus the stream's file
+ * offset) to block_off (ceil(n_items / items_per_block) entries, may be NULL).
+ * Returns 0 with *out_len; RIO_ERR_CAPACITY with the needed *out_len when out
+ * is too small, or when the stream exceeds the ctx's span capacity; < 0 on a
+ * runtime failure. */
+int rio_encode(rio_ctx *ctx, const rio_encode_args *a, uint8_t *out, uint64_t out_cap, uint64_t *out_len,
+               uint64_t *block_off, rio_error *err);
+/* The same with data, item_end, out and block_off in device memory (the
+ * device-resident producer of a scan: rio_scan_device reads what this wrote).
+ * out = NULL only sizes the stream (*out_len). */
+int rio_encode_device(rio_ctx *ctx, const rio_encode_args *a, void *out, uint64_t out_cap, uint64_t *out_len,
+                      uint64_t *block_off, rio_error *err);
+
 /* ---- scanner layer ---- */
 typedef struct rio_reader {
     void *user;

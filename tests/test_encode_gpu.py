@@ -1,0 +1,119 @@
+"""Writer encode path on the GPU (rio_encode): the chunk
+stream must be byte-identical to the writer restatement (base_amd/recordio/
+writer.py: writerv2.go + chunk.go) for the none transformer -- the writer is
+deterministic there -- and scan back through both the GPU scanner and the
+oracle to the records written."""
+import io
+import random
+
+import numpy as np
+import pytest
+
+from base_amd.recordio import format as F
+from base_amd.recordio.writer import WriterOpts, write_file, Writer
+
+
+def gpu_write(records, opts, header=(), trailer=None, flush_every=0, ctx=None, batch_bytes=64 << 20):
+    from base_amd.recordio.gpu_writer import GpuWriter
+    import dataclasses
+    buf = io.BytesIO()
+    opts = dataclasses.replace(opts)
+    if trailer is not None:
+        opts.KeyTrailer = True
+    w = GpuWriter(buf, opts, ctx=ctx, batch_bytes=batch_bytes)
+    for k, v in header:
+        w.AddHeader(k, v)
+    for i, r in enumerate(records):
+        w.Append(r)
+        if flush_every and i % flush_every == flush_every - 1:
+            w.Flush()
+    if trailer is not None:
+        w.SetTrailer(trailer)
+    assert w.Finish() is None
+    return buf.getvalue()
+
+
+def records(rng, n, sizes=(0, 1, 7, 100, 256, 3000, 40000)):
+    return [bytes(rng.getrandbits(8) for _ in range(rng.choice(sizes))) if rng.random() < 0.3 else
+            rng.randbytes(rng.choice(sizes)) for _ in range(n)]
+
+
+@pytest.mark.gpu
+def test_encode_matches_writer(gpu_ctx, oracle):
+    rng = random.Random(3)
+    cases = [
+        (records(rng, 0), WriterOpts(), {}),
+        (records(rng, 1), WriterOpts(), {}),
+        (records(rng, 200), WriterOpts(MaxItems=7), {}),
+        (records(rng, 500), WriterOpts(MaxItems=1), {"trailer": b"T" * 70000}),
+        (records(rng, 300, (0,)), WriterOpts(MaxItems=100), {}),  # empty items only
+        (records(rng, 120, (33000, 70000)), WriterOpts(MaxItems=3), {}),  # items over chunks
+        (records(rng, 700), WriterOpts(MaxItems=64), {"flush_every": 13}),
+        (records(rng, 400), WriterOpts(SkipHeader=True, MaxItems=50), {}),
+        (records(rng, 50), WriterOpts(MaxItems=5), {"header": [("k", "v"), ("n", -3), ("b", False)]}),
+        (records(rng, 5000, (0, 1, 2, 200)), WriterOpts(), {}),  # one block of 5000 items
+    ]
+    for i, (recs, opts, kw) in enumerate(cases):
+        want = write_file(recs, opts, header=kw.get("header", ()), trailer=kw.get("trailer"),
+                          flush_every=kw.get("flush_every", 0))
+        got = gpu_write(recs, opts, header=kw.get("header", ()), trailer=kw.get("trailer"),
+                        flush_every=kw.get("flush_every", 0), ctx=gpu_ctx, batch_bytes=1 << 16)
+        assert got == want, i
+        if not opts.SkipHeader:
+            ref = oracle.scan(got)
+            assert ref.err == "" and ref.items == recs, i
+
+
+@pytest.mark.gpu
+def test_encode_index_locations(gpu_ctx):
+    """IndexFunc (writerv2.go:40-43): every item's ItemLocation, as the writer reports it."""
+    from base_amd.recordio import gpu
+    rng = random.Random(4)
+    recs = records(rng, 400)
+    got_w, got_g = [], []
+    opts = WriterOpts(MaxItems=9, Index=lambda loc, v: got_w.append((loc, v)))
+    write_file(recs, opts, flush_every=31)
+    opts = WriterOpts(MaxItems=9, Index=lambda loc, v: got_g.append((loc, v)))
+    data = gpu_write(recs, opts, flush_every=31, ctx=gpu_ctx, batch_bytes=1 << 12)
+    assert got_g == got_w and len(got_g) == len(recs)
+    sc = gpu.NewScanner(data, ctx=gpu_ctx)
+    for loc, v in got_g[::17]:
+        sc.Seek(loc)
+        assert sc.Scan() and sc.Get() == v
+    assert sc.Finish() is None
+
+
+@pytest.mark.gpu
+def test_encode_c2_round_trip(gpu_ctx):
+    """The C2 record set (1e6 x 256 B, 253 per block): encode equals the bench's
+    C2 file byte for byte, and the GPU scan of the encoded bytes gives the records."""
+    import bench
+    from base_amd.recordio import gpu
+    recs = bench.c2_records()
+    want, n = bench.make_c2_file()
+    ctx = gpu.Context(0, max_span_bytes=len(want) + (1 << 20))
+    try:
+        hdr, _ = ctx.encode([F.marshal_header([])], 1, gpu.RIO_BLOCK_HEADER)
+        ends = np.arange(1, n + 1, dtype=np.uint64) * 256
+        body, boff = ctx.encode_arrays(recs.tobytes(), ends, 253)
+        assert hdr + body == want
+        assert boff[:3] == [0, 65536, 131072] and len(boff) == 3953
+        b = ctx.scan_span(body, file_off=len(hdr), is_file_end=True)
+        assert b.stop == gpu.RIO_STOP_EOF and b.n_items == n
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_encode_capacity(gpu_ctx):
+    """A stream larger than the ctx's span reports RIO_ERR_CAPACITY."""
+    from base_amd.recordio import gpu
+    ctx = gpu.Context(0, max_span_bytes=1 << 20)
+    try:
+        with pytest.raises(gpu.RecordioError) as e:
+            ctx.encode([b"x" * 200000] * 10, 1)
+        assert e.value.code == gpu.RIO_ERR_CAPACITY
+        data, boff = ctx.encode([b"x" * 200000] * 3, 1)  # 3 blocks x 7 chunks fit
+        assert len(data) == 21 * 32768 and boff == [0, 7 * 32768, 14 * 32768]
+    finally:
+        ctx.close()
