@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc_fold.h"
 #include "device_common.h"
 #include "parse_block.h"
 #include "rio_internal.h"
@@ -43,45 +44,6 @@ namespace rio {
 #define RIO_CRC_WAVES 16
 #endif
 constexpr int kCrcWaves = RIO_CRC_WAVES;  // waves per workgroup (one workgroup per CU: 156 KiB LDS at 32 copies)
-
-__device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
-  uint32_t p = 0;
-#pragma unroll
-  for (int i = 31; i >= 0; i--) {
-    p ^= b & (0u - ((a >> i) & 1u));
-    b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));
-  }
-  return p;
-}
-
-// keep the bytes of dword v (at chunk offset off) that lie below chunk offset hi
-__device__ __forceinline__ uint32_t mask_dword(uint32_t v, int off, int hi) {
-  int keep = hi - off;
-  keep = keep < 0 ? 0 : (keep > 4 ? 4 : keep);
-  const uint32_t m = keep >= 4 ? 0xffffffffu : ((1u << (8 * keep)) - 1u);
-  return v & m;
-}
-
-// one Horner step of the lane's 4 dword streams: 16 independent lookups in the
-// lane's private table copies
-__device__ __forceinline__ void fold_row(const char *__restrict__ tab, uint32_t lb, uint4 v, uint32_t (&s)[4]) {
-  const uint32_t d[4] = {v.x ^ s[0], v.y ^ s[1], v.z ^ s[2], v.w ^ s[3]};
-  uint32_t t[4][4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t a = (((d[k] >> (8 * j)) & 0xffu) << kFoldShift) | lb;
-      t[k][j] = *reinterpret_cast<const uint32_t *>(tab + j * (256 * 4 * kFoldCopies) + a);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 4; k++) s[k] = t[k][0] ^ t[k][1] ^ t[k][2] ^ t[k][3];
-}
-
-__device__ __forceinline__ uint32_t mul_const(const uint32_t *__restrict__ T, uint32_t v) {
-  return T[v & 0xff] ^ T[256 + ((v >> 8) & 0xff)] ^ T[512 + ((v >> 16) & 0xff)] ^ T[768 + (v >> 24)];
-}
 
 constexpr int kRows = 4;   // rows per pipeline stage (4 KiB per wave)
 constexpr int kBufs = 4;   // register buffers: kBufs - 1 stages in flight during a fold
@@ -214,7 +176,8 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
       const uint32_t t = full ? v : gf_mul_dev(v, fb);
       const uint32_t crc = ~(fa ^ t);
       d.ck_crc[c] = crc;
-      if (crc != stored && fold) atomicMin(&d.ctl->first_crc_err, (unsigned long long)c);
+      // (flags & 2: the encode path computes CRCs of chunks it is writing -- no compare)
+      if (crc != stored && fold && !(ca.flags & 2)) atomicMin(&d.ctl->first_crc_err, (unsigned long long)c);
     }
     if (kParse && starts) {
       const uint32_t b = pin.ck_block[c];

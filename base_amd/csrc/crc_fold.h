@@ -1,0 +1,53 @@
+// The chunk CRC fold of k_crc (crc.hip) as device helpers, shared with the
+// writer's fused chunk encoder (encode.hip): GF(2) products in the reflected
+// CRC-32 representation, masking of a dword to the covered bytes, one row
+// step of a lane's 4 dword streams through the bank-private LDS fold tables,
+// and multiply-by-constant through the 4-byte multiply tables.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rio_internal.h"
+
+namespace rio {
+
+__device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 31; i >= 0; i--) {
+    p ^= b & (0u - ((a >> i) & 1u));
+    b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+// keep the bytes of dword v (at chunk offset off) that lie below chunk offset hi
+__device__ __forceinline__ uint32_t mask_dword(uint32_t v, int off, int hi) {
+  int keep = hi - off;
+  keep = keep < 0 ? 0 : (keep > 4 ? 4 : keep);
+  const uint32_t m = keep >= 4 ? 0xffffffffu : ((1u << (8 * keep)) - 1u);
+  return v & m;
+}
+
+// one Horner step of the lane's 4 dword streams: 16 independent lookups in the
+// lane's private table copies
+__device__ __forceinline__ void fold_row(const char *__restrict__ tab, uint32_t lb, uint4 v, uint32_t (&s)[4]) {
+  const uint32_t d[4] = {v.x ^ s[0], v.y ^ s[1], v.z ^ s[2], v.w ^ s[3]};
+  uint32_t t[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t a = (((d[k] >> (8 * j)) & 0xffu) << kFoldShift) | lb;
+      t[k][j] = *reinterpret_cast<const uint32_t *>(tab + j * (256 * 4 * kFoldCopies) + a);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) s[k] = t[k][0] ^ t[k][1] ^ t[k][2] ^ t[k][3];
+}
+
+__device__ __forceinline__ uint32_t mul_const(const uint32_t *__restrict__ T, uint32_t v) {
+  return T[v & 0xff] ^ T[256 + ((v >> 8) & 0xff)] ^ T[512 + ((v >> 16) & 0xff)] ^ T[768 + (v >> 24)];
+}
+
+}  // namespace rio

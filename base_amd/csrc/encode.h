@@ -19,7 +19,7 @@ struct EncArgs {
   uint8_t *hdr;                         // varint headers
   uint8_t *comp;                        // transformed payloads (flate)
   // per chunk
-  uint32_t *ck_block, *ck_size;
+  uint32_t *ck_block;
   uint8_t *out;
 };
 
@@ -27,8 +27,11 @@ void launch_enc_count(const EncArgs &a, hipStream_t st);
 void launch_enc_header(const EncArgs &a, hipStream_t st);
 void launch_enc_nck(const EncArgs &a, hipStream_t st);
 void launch_enc_ckmap(const EncArgs &a, hipStream_t st);
-void launch_enc_chunks(const EncArgs &a, uint64_t nchunks, hipStream_t st);
+// k_crc's tables (DevBufs::crc_*)
+struct CrcTabs {
+  const uint32_t *fold, *mul, *fix_a, *fix_b;
+};
+void launch_enc_chunks(const EncArgs &a, uint64_t nchunks, const CrcTabs &t, int ncu, hipStream_t st);
 void launch_enc_boff(const unsigned long long *ck0, unsigned long long *boff, uint64_t nblocks, hipStream_t st);
-void launch_enc_crc(uint8_t *out, const uint32_t *ck_crc, uint64_t nchunks, hipStream_t st);
 
 }  // namespace rio

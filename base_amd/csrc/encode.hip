@@ -13,12 +13,12 @@
 //   (scan)        first chunk per block
 //   k_enc_ckmap   chunk -> block
 //   k_enc_chunks  wave per chunk: header fields, payload (16 B per lane from
-//                 aligned loads + funnel shift), padding; 16 B stores
-//   k_crc         the scan's own CRC kernel over the written chunks
-//   k_enc_crc     the CRCs into the chunk headers
+//                 aligned loads + funnel shift), padding; 16 B stores, each row
+//                 folded into the chunk CRC on the way (k_crc's tables)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc_fold.h"
 #include "device_common.h"
 #include "encode.h"
 #include "rio_internal.h"
@@ -133,80 +133,153 @@ __device__ __forceinline__ uint32_t pay_byte(const PaySrc &s, unsigned long long
   return p < s.hlen ? s.hdr[p] : s.data[p - s.hlen];
 }
 
-__global__ void __launch_bounds__(256) k_enc_chunks(EncArgs a, uint64_t nchunks) {
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  const int l = lane_id();
-  for (uint64_t c = wave; c < nchunks; c += nwaves) {
-    const uint32_t b = a.ck_block[c];
-    const unsigned long long c0 = a.ck0[b], total = a.nck[b], idx = c - c0;
-    PaySrc s;
-    if (a.codec == RIO_CODEC_NONE) {
-      const uint64_t f = enc_first(a, b);
-      s.hdr = a.hdr + a.hdr_off[b];
-      s.hlen = a.hdr_len[b];
-      s.data = a.data + item_start(a, f);
-    } else {
-      s.hdr = a.comp + a.comp_off[b];
-      s.hlen = ~0ull;
-      s.data = nullptr;
+struct ChunkCtx {
+  PaySrc s;
+  unsigned long long p0, total, idx;
+  uint32_t size, end;
+};
+
+__device__ __forceinline__ ChunkCtx chunk_ctx(const EncArgs &a, uint64_t c) {
+  ChunkCtx x;
+  const uint32_t b = a.ck_block[c];
+  const unsigned long long c0 = a.ck0[b];
+  x.total = a.nck[b];
+  x.idx = c - c0;
+  if (a.codec == RIO_CODEC_NONE) {
+    const uint64_t f = enc_first(a, b);
+    x.s.hdr = a.hdr + a.hdr_off[b];
+    x.s.hlen = a.hdr_len[b];
+    x.s.data = a.data + item_start(a, f);
+  } else {
+    x.s.hdr = a.comp + a.comp_off[b];
+    x.s.hlen = ~0ull;
+    x.s.data = nullptr;
+  }
+  x.s.len = a.pay_len[b];
+  x.p0 = x.idx * kMaxPayload;
+  const unsigned long long left = x.s.len - x.p0;
+  x.size = (uint32_t)(left < (unsigned long long)kMaxPayload ? left : (unsigned long long)kMaxPayload);
+  x.end = kChunkHdr + x.size;
+  return x;
+}
+
+// the 16 chunk bytes at offset q0 byte by byte (header fields with CRC 0, the
+// payload's ends, the start of the padding): the few units at a boundary
+__device__ __noinline__ uint4 unit_words_slow(const EncArgs &a, const ChunkCtx &x, uint32_t q0) {
+  uint32_t w[4];
+  for (int k = 0; k < 4; k++) {
+    uint32_t v = 0;
+    for (int j = 0; j < 4; j++) {
+      const uint32_t q = q0 + 4 * k + j;
+      uint32_t bv;
+      if (q < 8) bv = (uint32_t)(a.magic >> (8 * q)) & 0xff;
+      else if (q < 16) bv = 0;  // the CRC (filled in last) and the flag
+      else if (q < 20) bv = (x.size >> (8 * (q - 16))) & 0xff;
+      else if (q < 24) bv = (uint32_t)(x.total >> (8 * (q - 20))) & 0xff;
+      else if (q < 28) bv = (uint32_t)(x.idx >> (8 * (q - 24))) & 0xff;
+      else if (q < x.end) bv = pay_byte(x.s, x.p0 + (q - kChunkHdr));
+      else bv = (0xefbeaddeu >> (8 * ((q - x.end) & 3))) & 0xff;
+      v |= bv << (8 * j);
     }
-    s.len = a.pay_len[b];
-    const unsigned long long p0 = idx * kMaxPayload;
-    const unsigned long long left = s.len - p0;
-    const uint32_t size = (uint32_t)(left < (unsigned long long)kMaxPayload ? left : (unsigned long long)kMaxPayload);
-    const uint32_t end = kChunkHdr + size;
-    uint8_t *ck = a.out + c * kChunk;
-    if (l == 0) a.ck_size[c] = size;
-    for (uint32_t u = l; u < kChunk / 16; u += 64) {
-      const uint32_t q0 = 16 * u;
-      uint32_t w[4];
-      if (q0 >= kChunkHdr && q0 + 16 <= end) {  // payload only
-        const unsigned long long p = p0 + (q0 - kChunkHdr);
-        if (p + 16 <= s.hlen) load16_any(s.hdr + p, w);
-        else if (p >= s.hlen) load16_any(s.data + (p - s.hlen), w);
-        else {
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            uint32_t x = 0;
-            for (int j = 0; j < 4; j++) x |= pay_byte(s, p + 4 * k + j) << (8 * j);
-            w[k] = x;
-          }
-        }
-      } else if (q0 >= end) {  // padding: de ad be ef from the payload end
-        const uint32_t r = (q0 - end) & 3;
-        const uint32_t pat = 0xefbeaddeu;  // bytes de ad be ef
-        const uint32_t v = r ? (pat >> (8 * r)) | (pat << (32 - 8 * r)) : pat;
-        w[0] = w[1] = w[2] = w[3] = v;
-      } else {  // header fields, the payload's ends, padding start: byte by byte
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          uint32_t x = 0;
-          for (int j = 0; j < 4; j++) {
-            const uint32_t q = q0 + 4 * k + j;
-            uint32_t v;
-            if (q < 8) v = (uint32_t)(a.magic >> (8 * q)) & 0xff;
-            else if (q < 12) v = 0;  // the CRC, written by k_enc_crc
-            else if (q < 16) v = 0;  // flag
-            else if (q < 20) v = (size >> (8 * (q - 16))) & 0xff;
-            else if (q < 24) v = (uint32_t)(total >> (8 * (q - 20))) & 0xff;
-            else if (q < 28) v = (uint32_t)(idx >> (8 * (q - 24))) & 0xff;
-            else if (q < end) v = pay_byte(s, p0 + (q - kChunkHdr));
-            else v = (0xefbeaddeu >> (8 * ((q - end) & 3))) & 0xff;
-            x |= v << (8 * j);
-          }
-          w[k] = x;
-        }
-      }
-      *reinterpret_cast<uint4 *>(ck + q0) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
+    w[k] = v;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// the 16 chunk bytes at offset q0: payload (aligned loads + funnel shift),
+// padding, or the slow path
+__device__ __forceinline__ void unit_words(const EncArgs &a, const ChunkCtx &x, uint32_t q0, uint32_t (&w)[4]) {
+  const unsigned long long p = x.p0 + (q0 - kChunkHdr);
+  if (q0 >= kChunkHdr && q0 + 16 <= x.end && (p + 16 <= x.s.hlen || p >= x.s.hlen)) {  // one source
+    load16_any(p < x.s.hlen ? x.s.hdr + p : x.s.data + (p - x.s.hlen), w);
+  } else if (q0 >= x.end) {  // padding: de ad be ef from the payload end
+    const uint32_t r = (q0 - x.end) & 3;
+    const uint32_t pat = 0xefbeaddeu;  // bytes de ad be ef
+    const uint32_t v = r ? (pat >> (8 * r)) | (pat << (32 - 8 * r)) : pat;
+    w[0] = w[1] = w[2] = w[3] = v;
+  } else {
+    const uint4 u = unit_words_slow(a, x, q0);
+    w[0] = u.x;
+    w[1] = u.y;
+    w[2] = u.z;
+    w[3] = u.w;
   }
 }
 
-__global__ void k_enc_crc(uint8_t *out, const uint32_t *ck_crc, uint64_t nchunks) {
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks;
-       c += (uint64_t)gridDim.x * blockDim.x)
-    *reinterpret_cast<uint32_t *>(out + c * kChunk + 8) = ck_crc[c];
+// Wave per chunk, k_crc's layout (lane l owns bytes 1024 i + 16 l of row i):
+// every row is built, stored (16 B per lane, 1 KiB per instruction) and folded
+// into the lane's 4 CRC streams (crc_fold.h) in the same pass, rows
+// software-pipelined in groups of 4 (the next group's loads in flight while one
+// is stored and folded). The CRC goes into the header at the end: the chunk
+// stream is written once and never read back.
+constexpr int kEncWaves = 16;
+constexpr int kEncGroup = 4;
+
+__global__ void __launch_bounds__(64 * kEncWaves) k_enc_chunks(EncArgs a, uint64_t nchunks, CrcTabs t) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_fold[kFoldWords];
+  __shared__ __attribute__((aligned(16))) uint32_t s_mul[kMulTables * 1024];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(t.fold);
+    uint4 *dst = reinterpret_cast<uint4 *>(s_fold);
+    for (int i = threadIdx.x; i < kFoldWords / 4; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < kMulTables * 1024; i += blockDim.x) s_mul[i] = t.mul[i];
+  }
+  __syncthreads();
+  const int l = lane_id();
+  const uint32_t lb = (uint32_t)(l & (kFoldCopies - 1)) << 2;
+  const char *tab = reinterpret_cast<const char *>(s_fold);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kEncWaves;
+  for (uint64_t c = (uint64_t)blockIdx.x * kEncWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < nchunks;
+       c += nwaves) {
+    const ChunkCtx x = chunk_ctx(a, c);
+    uint8_t *ck = a.out + c * kChunk;
+    uint32_t s[4] = {0, 0, 0, 0};
+    uint32_t wa[kEncGroup][4], wb[kEncGroup][4];
+#pragma unroll
+    for (int r = 0; r < kEncGroup; r++) unit_words(a, x, 1024 * r + 16 * l, wa[r]);
+#pragma unroll 1
+    for (int g = 0; g < 32 / kEncGroup; g++) {
+      if (g + 1 < 32 / kEncGroup) {
+#pragma unroll
+        for (int r = 0; r < kEncGroup; r++) unit_words(a, x, 1024 * (kEncGroup * (g + 1) + r) + 16 * l, wb[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < kEncGroup; r++) {
+        const int row = kEncGroup * g + r;
+        const uint32_t q0 = 1024 * row + 16 * l;
+        *reinterpret_cast<uint4 *>(ck + q0) = make_uint4(wa[r][0], wa[r][1], wa[r][2], wa[r][3]);
+        uint4 v = make_uint4(wa[r][0], wa[r][1], wa[r][2], wa[r][3]);
+        if (row == 0 && l == 0) v.x = v.y = v.z = 0;  // magic and CRC are not covered
+        if (1024 * (row + 1) > (int)x.end) {
+          v.x = mask_dword(v.x, q0, x.end);
+          v.y = mask_dword(v.y, q0 + 4, x.end);
+          v.z = mask_dword(v.z, q0 + 8, x.end);
+          v.w = mask_dword(v.w, q0 + 12, x.end);
+        }
+        fold_row(tab, lb, v, s);
+      }
+#pragma unroll
+      for (int r = 0; r < kEncGroup; r++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) wa[r][k] = wb[r][k];
+    }
+    // lane: V_t = s0 + s1 x^-32 + s2 x^-64 + s3 x^-96; lanes: V = sum_t V_t x^-128t
+    uint32_t v = mul_const(s_mul, s[3]) ^ s[2];
+    v = mul_const(s_mul, v) ^ s[1];
+    v = mul_const(s_mul, v) ^ s[0];
+#pragma unroll
+    for (int lv = 0; lv < 6; lv++) {
+      const uint32_t m = mul_const(s_mul + (lv + 1) * 1024, v);
+      const int step = 1 << lv;
+      const uint32_t o = __shfl(m, (l + step) & 63, 64);
+      v ^= (l + step < 64) ? o : 0u;
+    }
+    if (l == 0) {
+      const uint32_t fa = t.fix_a[x.size], fb = t.fix_b[x.size];
+      const uint32_t crc = ~(fa ^ (x.size == (uint32_t)kMaxPayload ? v : gf_mul_dev(v, fb)));
+      *reinterpret_cast<uint32_t *>(ck + 8) = crc;
+    }
+  }
 }
 
 __global__ void k_enc_boff(const unsigned long long *ck0, unsigned long long *boff, uint64_t nblocks) {
@@ -233,14 +306,14 @@ void launch_enc_nck(const EncArgs &a, hipStream_t st) {
 void launch_enc_ckmap(const EncArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(k_enc_ckmap, dim3(enc_grid(a.nblocks, 4)), dim3(256), 0, st, a);
 }
-void launch_enc_chunks(const EncArgs &a, uint64_t nchunks, hipStream_t st) {
-  hipLaunchKernelGGL(k_enc_chunks, dim3(enc_grid(nchunks, 4)), dim3(256), 0, st, a, nchunks);
+void launch_enc_chunks(const EncArgs &a, uint64_t nchunks, const CrcTabs &t, int ncu, hipStream_t st) {
+  uint64_t g = (nchunks + kEncWaves - 1) / kEncWaves;
+  const uint64_t cap = (uint64_t)(ncu > 0 ? ncu : 256);
+  if (g > cap) g = cap;
+  hipLaunchKernelGGL(k_enc_chunks, dim3((unsigned)(g ? g : 1)), dim3(64 * kEncWaves), 0, st, a, nchunks, t);
 }
 void launch_enc_boff(const unsigned long long *ck0, unsigned long long *boff, uint64_t nblocks, hipStream_t st) {
   hipLaunchKernelGGL(k_enc_boff, dim3(enc_grid(nblocks, 256)), dim3(256), 0, st, ck0, boff, nblocks);
-}
-void launch_enc_crc(uint8_t *out, const uint32_t *ck_crc, uint64_t nchunks, hipStream_t st) {
-  hipLaunchKernelGGL(k_enc_crc, dim3(enc_grid(nchunks, 256)), dim3(256), 0, st, out, ck_crc, nchunks);
 }
 
 }  // namespace rio

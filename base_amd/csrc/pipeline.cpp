@@ -1259,12 +1259,9 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
   }
   if (!out) return 0;  // sizing only
   ea.ck_block = d.ck_block;
-  ea.ck_size = d.ck_size;
   ea.out = out;
   launch_enc_ckmap(ea, st);
-  launch_enc_chunks(ea, nchunks, st);
-  launch_crc(out, nchunks, d, CrcArgs{0, 0}, c->ncu, st, nullptr);
-  launch_enc_crc(out, d.ck_crc, nchunks, st);
+  launch_enc_chunks(ea, nchunks, CrcTabs{d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b}, c->ncu, st);
   if (boff) launch_enc_boff(ea.ck0, boff, nb, st);
   HIP_OK(hipEventRecord(c->ev[kEvEnd], st));
   HIP_OK(hipStreamSynchronize(st));
