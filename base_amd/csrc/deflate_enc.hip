@@ -1,0 +1,273 @@
+// DEFLATE encoder of the writer's "flate" transformer on the GPU (SURVEY.md
+// §8(f) 1: the mirror of recordioflate's FlateUncompress; the reference
+// compresses with klauspost/compress flate, recordioflate.go:31-52). The
+// output need not equal klauspost's bytes -- any valid raw DEFLATE stream
+// that the reference's inflater decodes to the payload is a correct "flate"
+// block (decode parity is what tests/test_encode_gpu.py checks, with the GPU
+// scanner, the oracle's inflater and zlib).
+//
+// One wave per block, the block payload (varint header + items, the writer
+// transforms the whole payload, writerv2.go:432-441) in rounds of 64
+// positions:
+//   - a 4,096-entry hash table of 4-byte prefixes in LDS (position of the
+//     last occurrence); every lane looks up its position, then inserts it
+//     (candidates come from earlier rounds, so a round never matches itself);
+//   - lanes at or after the parse cursor extend their candidate's match
+//     (4 bytes per step, <= 258, distance <= 32 KiB);
+//   - greedy parse of the round by the wave: from the cursor, a match if one
+//     was found at that position, else a literal (a scalar walk of <= 64
+//     steps over readlane'd lengths);
+//   - the chosen tokens' fixed-Huffman codes (RFC 1951 3.2.6: <= 31 bits each)
+//     placed by a wave prefix sum of their bit lengths and OR-ed into a
+//     128-dword LDS ring (ds_or: tokens share dwords); completed dwords are
+//     written out coalesced after every round.
+// One final block (BFINAL 1, BTYPE 01), end-of-block code 0000000.
+// Level 0 emits stored blocks instead (BTYPE 00, <= 65,535 bytes each), like
+// flate.NoCompression.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_common.h"
+#include "encode.h"
+#include "rio_internal.h"
+
+namespace rio {
+
+constexpr int kDHashBits = 12;
+constexpr uint32_t kDNone = 0xffffffffu;
+constexpr int kDRing = 128;        // output staging dwords per wave
+constexpr int kDWaves = 4;         // waves per workgroup
+
+// 4 payload bytes at p (p + 4 <= len): hdr scratch then items, or one buffer
+struct DSrc {
+  const uint8_t *hdr;
+  unsigned long long hlen;
+  const uint8_t *data;
+  unsigned long long len;
+  __device__ __forceinline__ uint32_t byte(unsigned long long p) const { return p < hlen ? hdr[p] : data[p - hlen]; }
+  __device__ __forceinline__ uint32_t load4(unsigned long long p) const {
+    const uint8_t *q;
+    if (p + 4 <= hlen) q = hdr + p;
+    else if (p >= hlen) q = data + (p - hlen);
+    else return byte(p) | (byte(p + 1) << 8) | (byte(p + 2) << 16) | (byte(p + 3) << 24);
+    const uintptr_t a = (uintptr_t)q;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    return sh ? (w[0] >> sh) | (w[1] << (32 - sh)) : w[0];
+  }
+};
+
+__device__ __forceinline__ uint32_t rev_bits(uint32_t code, uint32_t n) { return __brev(code) >> (32 - n); }
+
+// fixed-Huffman bits (LSB first) of a literal byte
+__device__ __forceinline__ void lit_bits(uint32_t b, uint32_t &bits, uint32_t &n) {
+  if (b < 144) {
+    bits = rev_bits(0x30 + b, 8);
+    n = 8;
+  } else {
+    bits = rev_bits(0x190 + (b - 144), 9);
+    n = 9;
+  }
+}
+
+// fixed-Huffman bits of a match (length 3..258, distance 1..32768): <= 31 bits
+__device__ __forceinline__ void match_bits(uint32_t m, uint32_t d, uint32_t &bits, uint32_t &n) {
+  uint32_t lcode, lext = 0, lval = 0;
+  const uint32_t x = m - 3;
+  if (m == 258) {
+    lcode = 285;
+  } else if (x < 8) {
+    lcode = 257 + x;
+  } else {
+    const uint32_t k = 31 - __clz(x);  // >= 3
+    lcode = 257 + 4 * (k - 1) + ((x >> (k - 2)) & 3);
+    lext = k - 2;
+    lval = x & ((1u << lext) - 1);
+  }
+  uint32_t hc, hn;
+  if (lcode <= 279) {
+    hc = lcode - 256;
+    hn = 7;
+  } else {
+    hc = 0xC0 + (lcode - 280);
+    hn = 8;
+  }
+  uint32_t dcode, dext = 0, dval = 0;
+  const uint32_t y = d - 1;
+  if (y < 4) {
+    dcode = y;
+  } else {
+    const uint32_t k = 31 - __clz(y);  // >= 2
+    dcode = 2 * k + ((y >> (k - 1)) & 1);
+    dext = k - 1;
+    dval = y & ((1u << dext) - 1);
+  }
+  bits = rev_bits(hc, hn);
+  n = hn;
+  bits |= lval << n;
+  n += lext;
+  bits |= rev_bits(dcode, 5) << n;
+  n += 5;
+  bits |= dval << n;
+  n += dext;
+}
+
+__device__ __forceinline__ DSrc dsrc_of(const EncArgs &a, uint64_t b) {
+  DSrc s;
+  const uint64_t f0 = b * a.per_block;
+  const uint64_t f = f0 < a.n_items ? f0 : a.n_items;
+  s.hdr = a.hdr + a.hdr_off[b];
+  s.hlen = a.hdr_len[b];
+  s.data = a.data + (f == 0 ? 0ull : a.item_end[f - 1]);
+  s.len = a.pay_len[b];
+  return s;
+}
+
+__global__ void __launch_bounds__(64 * kDWaves) k_deflate(EncArgs a) {
+  __shared__ uint32_t s_hash[kDWaves][1 << kDHashBits];
+  __shared__ uint32_t s_ring[kDWaves][kDRing];
+  const int wv = threadIdx.x >> 6;
+  uint32_t *hash = s_hash[wv];
+  uint32_t *ring = s_ring[wv];
+  const int l = lane_id();
+  const uint64_t nwaves = (uint64_t)gridDim.x * kDWaves;
+  for (uint64_t b = (uint64_t)blockIdx.x * kDWaves + wv; b < a.nblocks; b += nwaves) {
+    const DSrc s = dsrc_of(a, b);
+    const unsigned long long L = s.len;
+    uint32_t *out = reinterpret_cast<uint32_t *>(a.comp + a.comp_off[b]);
+    for (int i = l; i < (1 << kDHashBits); i += 64) hash[i] = kDNone;
+    for (int i = l; i < kDRing; i += 64) ring[i] = 0;
+    wave_lds_sync();
+    if (l == 0) ring[0] = 3;  // BFINAL 1, BTYPE 01 (fixed Huffman)
+    unsigned long long bitpos = 3, flushed = 0, cur = 0;
+    for (unsigned long long base = 0; base < L; base += 64) {
+      const unsigned long long p = base + l;
+      const bool has4 = p + 4 <= L;
+      const uint32_t v4 = has4 ? s.load4(p) : 0u;
+      const uint32_t h = (v4 * 0x9E3779B1u) >> (32 - kDHashBits);
+      const uint32_t cand = has4 ? hash[h] : kDNone;
+      wave_lds_sync();
+      if (has4) hash[h] = (uint32_t)p;  // (positions < 2^32: blocks are smaller)
+      // match length at p (only where the parse can land)
+      uint32_t m = 0;
+      if (has4 && p >= cur && cand != kDNone && p - cand <= 32768 && s.load4(cand) == v4) {
+        const unsigned long long room = L - p;
+        const uint32_t maxm = room < 258 ? (uint32_t)room : 258u;
+        m = 4;
+        while (m < maxm) {
+          if (m + 4 <= maxm) {
+            const uint32_t x = s.load4(cand + m) ^ s.load4(p + m);
+            if (x) {
+              m += (uint32_t)((__ffs(x) - 1) >> 3);  // the first differing byte
+              break;
+            }
+            m += 4;
+          } else {
+            if (s.byte(cand + m) != s.byte(p + m)) break;
+            m++;
+          }
+        }
+      }
+      // greedy parse of this round from the cursor (wave-uniform walk)
+      unsigned long long chosen = 0;
+      unsigned long long pos = cur;
+      const unsigned long long rend = base + 64 < L ? base + 64 : L;
+      while (pos < rend) {
+        const uint32_t lane = (uint32_t)(pos - base);
+        const uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)m, (int)lane);
+        chosen |= 1ull << lane;
+        pos += ml >= 4 ? ml : 1;
+      }
+      cur = pos;
+      // this lane's token
+      uint32_t bits = 0, nb = 0;
+      if ((chosen >> l) & 1) {
+        if (m >= 4) match_bits(m, (uint32_t)(p - cand), bits, nb);
+        else lit_bits(has4 ? (v4 & 0xff) : s.byte(p), bits, nb);
+      }
+      const uint32_t incl = wave_incl_sum<uint32_t>(nb);
+      const uint32_t tot = __shfl(incl, 63, 64);
+      if (nb) {
+        const unsigned long long o = bitpos + (incl - nb);
+        const uint32_t k = (uint32_t)(o >> 5), sh = (uint32_t)(o & 31);
+        atomicOr(&ring[k & (kDRing - 1)], bits << sh);
+        if (sh + nb > 32) atomicOr(&ring[(k + 1) & (kDRing - 1)], bits >> (32 - sh));
+      }
+      bitpos += tot;
+      wave_lds_sync();
+      // completed dwords out (coalesced), their ring slots cleared
+      const unsigned long long done = bitpos >> 5;
+      if (flushed + l < done) {
+        const uint32_t slot = (uint32_t)((flushed + l) & (kDRing - 1));
+        out[flushed + l] = ring[slot];
+        ring[slot] = 0;
+      }
+      flushed = done;
+      wave_lds_sync();
+    }
+    bitpos += 7;  // end of block: code 256 = 0000000
+    const unsigned long long nd = (bitpos + 31) >> 5;
+    for (unsigned long long k = flushed + l; k < nd; k += 64) {
+      const uint32_t slot = (uint32_t)(k & (kDRing - 1));
+      out[k] = ring[slot];
+      ring[slot] = 0;
+    }
+    wave_lds_sync();
+    if (l == 0) a.pay_len[b] = (bitpos + 7) >> 3;
+  }
+}
+
+// flate.NoCompression: stored blocks of <= 65,535 bytes (RFC 1951 3.2.4)
+__global__ void __launch_bounds__(256) k_deflate_stored(EncArgs a) {
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const int l = lane_id();
+  for (uint64_t b = wave; b < a.nblocks; b += nwaves) {
+    const DSrc s = dsrc_of(a, b);
+    const unsigned long long L = s.len;
+    uint8_t *out = a.comp + a.comp_off[b];
+    const unsigned long long np = L == 0 ? 1 : (L + 65534) / 65535;
+    for (unsigned long long k = 0; k < np; k++) {
+      const unsigned long long p0 = k * 65535;
+      const uint32_t n = (uint32_t)((L - p0) < 65535 ? (L - p0) : 65535);
+      uint8_t *o = out + k * 65540;
+      if (l == 0) {
+        o[0] = (k + 1 == np) ? 1 : 0;  // BFINAL, BTYPE 00, then the byte boundary
+        o[1] = n & 0xff;
+        o[2] = n >> 8;
+        o[3] = ~n & 0xff;
+        o[4] = (~n >> 8) & 0xff;
+      }
+      for (uint32_t i = l; i < n; i += 64) o[5 + i] = (uint8_t)s.byte(p0 + i);
+    }
+    if (l == 0) a.pay_len[b] = L + 5 * np;
+  }
+}
+
+// per block: the compressed region's bound (into nck, scanned into comp_off)
+__global__ void k_deflate_bound(EncArgs a) {
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < a.nblocks;
+       b += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long L = a.pay_len[b];
+    const unsigned long long stored = L + 5 * (L / 65535 + 1);
+    const unsigned long long fixed = L + L / 8 + 16;
+    a.nck[b] = ((stored > fixed ? stored : fixed) + 64 + 15) & ~15ull;
+  }
+}
+
+void launch_deflate_bound(const EncArgs &a, hipStream_t st) {
+  uint64_t g = (a.nblocks + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(k_deflate_bound, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, a);
+}
+
+void launch_deflate(const EncArgs &a, hipStream_t st) {
+  uint64_t g = (a.nblocks + kDWaves - 1) / kDWaves;
+  if (g > 8192) g = 8192;
+  if (a.level == 0)
+    hipLaunchKernelGGL(k_deflate_stored, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_deflate, dim3((unsigned)(g ? g : 1)), dim3(64 * kDWaves), 0, st, a);
+}
+
+}  // namespace rio

@@ -32,6 +32,8 @@ struct CrcTabs {
   const uint32_t *fold, *mul, *fix_a, *fix_b;
 };
 void launch_enc_chunks(const EncArgs &a, uint64_t nchunks, const CrcTabs &t, int ncu, hipStream_t st);
+void launch_deflate_bound(const EncArgs &a, hipStream_t st);
+void launch_deflate(const EncArgs &a, hipStream_t st);
 void launch_enc_boff(const unsigned long long *ck0, unsigned long long *boff, uint64_t nblocks, hipStream_t st);
 
 }  // namespace rio

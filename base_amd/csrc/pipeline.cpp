@@ -1225,7 +1225,7 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
   ea.n_items = a->n_items;
   ea.per_block = per;
   ea.nblocks = nb;
-  ea.codec = a->codec;
+  ea.codec = a->kind == RIO_BLOCK_HEADER ? RIO_CODEC_NONE : a->codec;  // the header block is never transformed
   ea.level = a->level;
   ea.magic = a->kind == RIO_BLOCK_HEADER ? kMagicHdr : a->kind == RIO_BLOCK_TRAILER ? kMagicTrl : kMagicBody;
   ea.hdr_len = c->e_blk;
@@ -1243,6 +1243,16 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
   if (egrow(&c->e_hdr, &c->e_hdr_cap, hdr_total + 16)) return -1;
   ea.hdr = c->e_hdr;
   launch_enc_header(ea, st);
+  if (ea.codec == RIO_CODEC_FLATE) {  // the payloads compressed into comp (deflate_enc.hip)
+    launch_deflate_bound(ea, st);
+    launch_chunk_scan(ea.nck, ea.comp_off, d.scan_tmp, nb, st);
+    unsigned long long comp_total = 0;
+    HIP_OK(hipMemcpyAsync(&comp_total, ea.comp_off + nb, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (egrow(&c->e_comp, &c->e_comp_cap, comp_total + 64)) return -1;
+    ea.comp = c->e_comp;
+    launch_deflate(ea, st);
+  }
   launch_enc_nck(ea, st);
   launch_chunk_scan(ea.nck, ea.ck0, d.scan_tmp, nb, st);
   unsigned long long nchunks = 0;
@@ -1270,8 +1280,8 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
 
 static int encode_check(rio_ctx *ctx, const rio_encode_args *a, rio_error *err) {
   if (!ctx || !a) return -1;
-  if (a->codec != RIO_CODEC_NONE) {
-    rio_set_error(err, RIO_ERR_ARG, 0, "encode: codec %d not supported", a->codec);
+  if (a->codec != RIO_CODEC_NONE && a->codec != RIO_CODEC_FLATE) {
+    rio_set_error(err, RIO_ERR_ARG, 0, "encode: codec %d not supported (none, flate)", a->codec);
     return RIO_ERR_ARG;
   }
   if (a->kind < RIO_BLOCK_BODY || a->kind > RIO_BLOCK_TRAILER) {

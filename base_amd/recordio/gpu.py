@@ -247,10 +247,14 @@ class Context:
         err = RioError()
         olen = ctypes.c_uint64()
         boff = np.zeros(max(nb, 1), dtype=np.uint64)
-        cap = 32768 * (nb + (len(blob) + 10 * (n + nb)) // 32740 + 2)  # >= the chunk stream
-        out = np.empty(cap, dtype=np.uint8)
-        rc = self.L.rio_encode(self.h, ctypes.byref(a), out.ctypes.data, cap, ctypes.byref(olen),
-                               boff.ctypes.data, ctypes.byref(err))
+        cap = 32768 * (2 * nb + (len(blob) * 9 // 8 + 11 * (n + nb)) // 32740 + 2)  # >= the chunk stream
+        for _ in range(2):
+            out = np.empty(cap, dtype=np.uint8)
+            rc = self.L.rio_encode(self.h, ctypes.byref(a), out.ctypes.data, cap, ctypes.byref(olen),
+                                   boff.ctypes.data, ctypes.byref(err))
+            if rc != RIO_ERR_CAPACITY or olen.value <= cap:
+                break
+            cap = olen.value  # the exact size, once
         if rc < 0:
             raise RuntimeError("rio_encode: " + self.L.rio_last_error().decode())
         if rc != 0:

@@ -3,7 +3,8 @@ the block serialisation, chunk framing and CRC32 on the GPU (rio_encode,
 SURVEY.md §8(f) 1).
 
 Same state machine, header order and bytes as the reference for the none
-transformer. The reference serialises each block on a goroutine as it fills
+transformer; "flate" blocks are valid DEFLATE streams of the same payloads
+(GPU-encoded, deflate_enc.hip), so they decode to the same records. The reference serialises each block on a goroutine as it fills
 (MaxItems + 1 items, writerv2.go:315, 366-368) and writes blocks in sequence;
 here the items between two block-ending calls (Flush, SetTrailer, Finish) are
 kept and encoded by one rio_encode call -- once a run holds `batch_bytes`, its
@@ -31,8 +32,14 @@ class GpuWriter:
         if opts.MaxItems == 0:
             opts.MaxItems = F.DEFAULT_PACKED_ITEMS
         opts.MaxItems = min(opts.MaxItems, F.MAX_PACKED_ITEMS)
+        # transformers: none, or one "flate" / "flate N" (recordioflate.go:31-52)
+        self.codec, self.level = gpu.RIO_CODEC_NONE, 0
         if opts.Transformers:
-            raise ValueError("GpuWriter encodes the none transformer (got %r)" % (opts.Transformers,))
+            name, _, arg = opts.Transformers[0].partition(" ")
+            if len(opts.Transformers) != 1 or name != "flate":
+                raise ValueError("GpuWriter encodes none or one flate transformer (got %r)" % (opts.Transformers,))
+            self.codec = gpu.RIO_CODEC_FLATE
+            self.level = int(arg) if arg.strip() else -1
         self.opts = opts
         self.out = out
         self.ctx = ctx or gpu.default_context()
@@ -41,6 +48,9 @@ class GpuWriter:
         self.err: Optional[Exception] = None
         self.header = []
         self.state = _BODY if opts.SkipHeader else _INITIAL
+        if not opts.SkipHeader:
+            for t in opts.Transformers:
+                self.header.append((F.KEY_TRANSFORMER, t))
         if opts.KeyTrailer:
             self.header.append((F.KEY_TRAILER, True))
         self.run_objs = []   # the current run's objects
@@ -59,7 +69,7 @@ class GpuWriter:
         del self.run_objs[:n], self.run_items[:n]
         self.run_bytes -= sum(len(x) for x in items)
         per = self.opts.MaxItems + 1
-        data, boff = self.ctx.encode(items, per)
+        data, boff = self.ctx.encode(items, per, gpu.RIO_BLOCK_BODY, self.codec, self.level)
         base = self.n_written
         if self.opts.Index is not None:
             for i, v in enumerate(objs):
@@ -106,7 +116,7 @@ class GpuWriter:
         else:
             raise RuntimeError(f"SetTrailer: wrong state: {self.state}")
         self.state = _TRAILER
-        enc, _ = self.ctx.encode([bytes(data)], 1, gpu.RIO_BLOCK_TRAILER)
+        enc, _ = self.ctx.encode([bytes(data)], 1, gpu.RIO_BLOCK_TRAILER, self.codec, self.level)
         self._write(enc)
 
     def Err(self):

@@ -214,7 +214,8 @@ int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, const uint32_
 
 /* ---- writer encode path ----
  * The blocks of a v2 file encoded on the GPU, byte for byte what
- * recordio.NewWriter writes for the same items (none transformer):
+ * recordio.NewWriter writes for the same items with the none transformer
+ * (flate: a valid DEFLATE stream of the same payload):
  * items_per_block items per block (the writer packs MaxItems + 1 per block:
  * its object slice has capacity MaxItems + 1 and is flushed when full,
  * writerv2.go:315, 366-368; the last block takes the rest; 0 = the default
@@ -230,9 +231,12 @@ typedef struct rio_encode_args {
     const uint64_t *item_end;  /* n_items exclusive ends: item i = data[end[i-1], end[i]) */
     uint64_t n_items;
     uint64_t items_per_block;  /* MaxItems + 1; 0 = 16385 */
-    int32_t codec;             /* RIO_CODEC_NONE */
+    int32_t codec;             /* RIO_CODEC_NONE, or RIO_CODEC_FLATE: a raw DEFLATE stream per
+                                  block ("flate N" transformer, recordioflate.go:31-52; any valid
+                                  stream decodes alike -- the bytes are not klauspost's) */
     int32_t kind;              /* enum rio_block_kind */
-    int32_t level;             /* reserved (transformer level), 0 */
+    int32_t level;             /* flate: 0 stored blocks (NoCompression), otherwise one
+                                  fixed-Huffman block with greedy hash-chain matches */
     int32_t reserved;
 } rio_encode_args;
 /* Host memory in and out: writes the chunk stream to out (out_cap bytes) and

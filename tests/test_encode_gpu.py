@@ -117,3 +117,54 @@ def test_encode_capacity(gpu_ctx):
         assert len(data) == 21 * 32768 and boff == [0, 7 * 32768, 14 * 32768]
     finally:
         ctx.close()
+
+
+def fastq_records(rng, n):
+    """C3-style text records: compressible, with repeats at all distances."""
+    bases = b"ACGT"
+    out = []
+    for i in range(n):
+        seq = bytes(rng.choice(bases) for _ in range(rng.randrange(50, 150)))
+        qual = bytes(rng.choice(b"FFFF:,") for _ in range(len(seq)))
+        out.append(b"@read%d/1\n" % i + seq + b"\n+\n" + qual + b"\n")
+    return out
+
+
+@pytest.mark.gpu
+def test_encode_flate_decodes(gpu_ctx, oracle):
+    """flate blocks from the GPU encoder (fixed Huffman + greedy matches, and
+    level 0 stored blocks) decode -- GPU scanner, the oracle's Go-semantics
+    inflater, zlib -- to the records written; text compresses."""
+    import zlib
+    from base_amd.recordio import gpu
+    rng = random.Random(5)
+    sets = [fastq_records(rng, 3000), records(rng, 300), [b""] * 50, [b"x" * 100000] * 3,
+            [bytes([i % 7]) * rng.randrange(0, 600) for i in range(2000)]]
+    for level in ("flate", "flate 0", "flate 5"):
+        for i, recs in enumerate(sets):
+            data = gpu_write(recs, WriterOpts(Transformers=[level], MaxItems=rng.choice([1, 50, 1000])),
+                             trailer=b"trail" * 3, ctx=gpu_ctx, batch_bytes=1 << 18)
+            ref = oracle.scan(data)
+            assert ref.err == "" and ref.items == recs and ref.trailer == b"trail" * 3, (level, i)
+            sc = gpu.NewScanner(data, ctx=gpu_ctx)
+            got = []
+            while sc.Scan():
+                got.append(sc.Get())
+            assert sc.Finish() is None and got == recs, (level, i)
+    # every block's payload is a raw DEFLATE stream zlib inflates to the packed payload
+    recs = fastq_records(rng, 500)
+    data = gpu_write(recs, WriterOpts(Transformers=["flate"], MaxItems=99), ctx=gpu_ctx)
+    off, k, comp, plain = 32768, 0, 0, 0
+    while off < len(data):
+        total = int.from_bytes(data[off + 20:off + 24], "little")
+        pay = b"".join(data[off + c * 32768 + 28: off + c * 32768 + 28 +
+                            int.from_bytes(data[off + c * 32768 + 16:off + c * 32768 + 20], "little")]
+                       for c in range(total))
+        blk = recs[k * 100:(k + 1) * 100]
+        assert zlib.decompress(pay, -15) == F.packed_block_payload(blk)
+        comp += len(pay)
+        plain += len(F.packed_block_payload(blk))
+        off += total * 32768
+        k += 1
+    assert k == 5
+    assert comp < 0.75 * plain, (comp, plain)  # fixed Huffman + greedy matches on FASTQ-like text
