@@ -18,21 +18,34 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--replicas", type=int, default=32)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--codec", type=int, default=0)
+    ap.add_argument("--codec", type=int, default=0)  # 0 none (C2 records), 1 flate (C3 records)
     a = ap.parse_args()
     import numpy as np
     import torch
     import bench
     from base_amd.recordio import gpu
-    recs = bench.c2_records()
-    n1 = recs.shape[0]
     R = a.replicas
-    n = n1 * R
-    data = torch.from_numpy(np.ascontiguousarray(recs).reshape(-1)).cuda().repeat(R)
-    ends = (torch.arange(1, n + 1, dtype=torch.int64, device="cuda") * 256)
-    per = 253
+    if a.codec == 0:  # C2: 1e6 x 256 B, 253 per block
+        recs = bench.c2_records()
+        n1 = recs.shape[0]
+        n = n1 * R
+        data = torch.from_numpy(np.ascontiguousarray(recs).reshape(-1)).cuda().repeat(R)
+        ends = (torch.arange(1, n + 1, dtype=torch.int64, device="cuda") * 256)
+        per = 253
+    else:  # C3: FASTQ-like records (tools/c3_data.py), 1,024 per block, flate
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import c3_data
+        recs = c3_data.records(0, 1 << 17)
+        n1 = len(recs)
+        n = n1 * R
+        blob = np.frombuffer(b"".join(recs), dtype=np.uint8)
+        lens = np.fromiter((len(r) for r in recs), dtype=np.int64, count=n1)
+        data = torch.from_numpy(blob.copy()).cuda().repeat(R)
+        e1 = torch.from_numpy(np.cumsum(lens)).cuda()
+        ends = torch.cat([e1 + k * int(blob.size) for k in range(R)])
+        per = 1024
     nb = (n + per - 1) // per
-    cap = 32768 * (nb * 2 + 16)
+    cap = 32768 * (nb * 2 + int(data.numel()) * 9 // 8 // 32740 + 16)  # >= any stream (flate: <= 9/8)
     out = torch.empty(cap, dtype=torch.uint8, device="cuda")
     boff = torch.empty(nb, dtype=torch.int64, device="cuda")
     ctx = gpu.Context(0, max_span_bytes=cap)
@@ -55,14 +68,16 @@ def main():
     # parity: scan the encoded stream back on the device
     b = ctx.scan_device(out.data_ptr(), out_len, 32768, True, a.codec)
     ok = b.stop == gpu.RIO_STOP_EOF and b.n_items == n
-    detail = {"stop": int(b.stop), "n_items": int(b.n_items), "err": b.err.msg.decode()}
+    detail = {"stop": int(b.stop), "n_items": int(b.n_items), "err": b.err.msg.decode(),
+              "ratio": round(int(data.numel()) / out_len, 3)}
     if a.codec == 0:  # the first 3,952 blocks (whole 253-record blocks) equal the bench's C2 file
         want = bench.make_c2_file()[0][32768:32768 + 3952 * 65536]
         detail["bytes_equal"] = out[:len(want)].cpu().numpy().tobytes() == want
         ok = ok and detail["bytes_equal"]
-    rec_bytes = n * 256
+    rec_bytes = int(data.numel())
     GiB = float(1 << 30)
-    res = {"workload": "encode C2 records x %d (%d records, 253 per block), codec %d" % (R, n, a.codec),
+    res = {"workload": "encode %s records x %d (%d records, %d per block), codec %d" %
+           ("C2" if a.codec == 0 else "C3", R, n, per, a.codec),
            "record_bytes": rec_bytes, "out_bytes": out_len, "ms": round(dt * 1e3, 3),
            "records_GiBps": round(rec_bytes / dt / GiB, 1),
            "hbm_alg_GBps": round((rec_bytes + out_len) / dt / 1e9, 1),  # records read + stream written
