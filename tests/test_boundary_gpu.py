@@ -229,14 +229,14 @@ def test_trailer_error_mid_scan(gpu_ctx):
     w.Finish()
     sc = gpu.NewScanner(buf.getvalue(), ctx=gpu_ctx)
     got = []
-    for _ in range(35):  # into the second block (items 30..59)
+    for _ in range(35):  # into the second block (items 31..61: MaxItems + 1 per block)
         assert sc.Scan()
         got.append(sc.Get())
     assert sc.Trailer() is None
     err = str(sc.Err())
     assert err.startswith("Missing magic trailer; found ["), err
     got += _scan_all(sc)
-    assert got == recs[:60]  # the rest of block 2, then the sticky error
+    assert got == recs[:62]  # the rest of block 2, then the sticky error
     assert str(sc.Finish()) == err
 
 

@@ -117,7 +117,7 @@ def test_token_region_yield_and_resume(gpu_lib, cap):
     # at 128 tokens a block needs more than the 6 launched rounds and the host
     # retries with more
     recs = mixed_records(cap, 300)
-    data = write(recs, 6, "go", max_items=50)
+    data = write(recs, 6, "go", max_items=49)  # 50 records per block
     c = make_ctx({"RIO_FL_TOKCAP": cap})
     try:
         items, err = scan_all(data, c)

@@ -200,7 +200,7 @@ def test_batch_api_c2_like(gpu_ctx, oracle):
     from base_amd.recordio.writer import write_file, WriterOpts
     rng = np.random.default_rng(1)
     recs = [bytes(r) for r in rng.integers(0, 256, size=(20000, 256), dtype=np.uint8)]
-    data = write_file(recs, WriterOpts(MaxItems=253))
+    data = write_file(recs, WriterOpts(MaxItems=252))  # 253 per block (MaxItems + 1)
     hdr = 32768
     b = gpu_ctx.scan_span(data[hdr:], file_off=hdr, is_file_end=True)
     assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0
