@@ -55,7 +55,48 @@ struct DSrc {
     const uint32_t sh = (uint32_t)(a & 3) * 8;
     return sh ? (w[0] >> sh) | (w[1] << (32 - sh)) : w[0];
   }
+  // 16 bytes at p; bytes at or past len read as 0 (and are never loaded)
+  __device__ __forceinline__ void load16(unsigned long long p, uint32_t (&w)[4]) const {
+    const uint8_t *q = nullptr;
+    if (p + 16 <= len) {
+      if (p + 16 <= hlen) q = hdr + p;
+      else if (p >= hlen) q = data + (p - hlen);
+    }
+    if (q) {
+      const uintptr_t a = (uintptr_t)q;
+      const uint32_t *d = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(a & 3) * 8;
+      if (sh == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) w[k] = d[k];
+      } else {
+        uint32_t e[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) e[k] = d[k];  // the 5th dword holds byte 15: inside the payload
+#pragma unroll
+        for (int k = 0; k < 4; k++) w[k] = (e[k] >> sh) | (e[k + 1] << (32 - sh));
+      }
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t v = 0;
+      for (int j = 0; j < 4; j++)
+        if (p + 4 * k + j < len) v |= byte(p + 4 * k + j) << (8 * j);
+      w[k] = v;
+    }
+  }
 };
+
+// bytes equal from the start of two 16-byte groups (16: all)
+__device__ __forceinline__ uint32_t common16(const uint32_t (&a)[4], const uint32_t (&b)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t x = a[k] ^ b[k];
+    if (x) return 4 * k + ((__ffs(x) - 1) >> 3);
+  }
+  return 16;
+}
 
 __device__ __forceinline__ uint32_t rev_bits(uint32_t code, uint32_t n) { return __brev(code) >> (32 - n); }
 
@@ -140,33 +181,36 @@ __global__ void __launch_bounds__(64 * kDWaves) k_deflate(EncArgs a) {
     wave_lds_sync();
     if (l == 0) ring[0] = 3;  // BFINAL 1, BTYPE 01 (fixed Huffman)
     unsigned long long bitpos = 3, flushed = 0, cur = 0;
+    uint32_t nx[4];  // the next round's 16 bytes at this lane's position (prefetched)
+    s.load16(l, nx);
     for (unsigned long long base = 0; base < L; base += 64) {
       const unsigned long long p = base + l;
+      uint32_t cw[4] = {nx[0], nx[1], nx[2], nx[3]};
+      if (base + 64 < L) s.load16(p + 64, nx);
       const bool has4 = p + 4 <= L;
-      const uint32_t v4 = has4 ? s.load4(p) : 0u;
+      const uint32_t v4 = cw[0];
       const uint32_t h = (v4 * 0x9E3779B1u) >> (32 - kDHashBits);
       const uint32_t cand = has4 ? hash[h] : kDNone;
       wave_lds_sync();
       if (has4) hash[h] = (uint32_t)p;  // (positions < 2^32: blocks are smaller)
-      // match length at p (only where the parse can land)
+      // match length at p (only where the parse can land): 16 bytes per step
       uint32_t m = 0;
-      if (has4 && p >= cur && cand != kDNone && p - cand <= 32768 && s.load4(cand) == v4) {
+      if (has4 && p >= cur && cand != kDNone && p - cand <= 32768) {
         const unsigned long long room = L - p;
         const uint32_t maxm = room < 258 ? (uint32_t)room : 258u;
-        m = 4;
-        while (m < maxm) {
-          if (m + 4 <= maxm) {
-            const uint32_t x = s.load4(cand + m) ^ s.load4(p + m);
-            if (x) {
-              m += (uint32_t)((__ffs(x) - 1) >> 3);  // the first differing byte
-              break;
-            }
-            m += 4;
-          } else {
-            if (s.byte(cand + m) != s.byte(p + m)) break;
-            m++;
-          }
+        uint32_t cc[4];
+        s.load16(cand, cc);
+        m = common16(cc, cw);
+        while (m == 16 * ((m + 15) / 16) && m > 0 && m < maxm) {  // all equal so far
+          uint32_t a16[4], b16[4];
+          s.load16(cand + m, a16);
+          s.load16(p + m, b16);
+          const uint32_t k = common16(a16, b16);
+          m += k;
+          if (k < 16) break;
         }
+        if (m > maxm) m = maxm;
+        if (m < 4) m = 0;
       }
       // greedy parse of this round from the cursor (wave-uniform walk)
       unsigned long long chosen = 0;
@@ -183,7 +227,7 @@ __global__ void __launch_bounds__(64 * kDWaves) k_deflate(EncArgs a) {
       uint32_t bits = 0, nb = 0;
       if ((chosen >> l) & 1) {
         if (m >= 4) match_bits(m, (uint32_t)(p - cand), bits, nb);
-        else lit_bits(has4 ? (v4 & 0xff) : s.byte(p), bits, nb);
+        else lit_bits(cw[0] & 0xff, bits, nb);
       }
       const uint32_t incl = wave_incl_sum<uint32_t>(nb);
       const uint32_t tot = __shfl(incl, 63, 64);
