@@ -30,31 +30,35 @@ constexpr int kBatch = RIO_PARSE_BATCH;  // blocks per wave iteration: their loa
 // (scannerv2.go:53-97) and one view per item (cumSize, scannerv2.go:83-91)
 // into the item slots reserved by the block scan.
 __global__ void __launch_bounds__(256) k_parse(DevBufs d, ParseArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_win[4][1024];
-  __shared__ uint16_t s_tpos[4][1024];
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[4][1040];  // 1 KiB window + room for lds_bytes4
+  __shared__ __attribute__((aligned(16))) uint16_t s_tpos[4][1024];
   uint8_t *lwin = s_win[threadIdx.x >> 6];
   uint16_t *ltpos = s_tpos[threadIdx.x >> 6];
-  const uint64_t nb = *a.nblocks;
+  const uint64_t nb = a.list ? *a.list_n : *a.nblocks;  // list: the blocks k_parse_lean declined
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const int l = lane_id();
   for (uint64_t b0 = wave * kBatch; b0 < nb; b0 += nwaves * kBatch) {
     // round 1: descriptors of the batch (lane j: block b0 + j)
-    unsigned long long m_c0 = 0, m_meta = 0, m_len = 0, m_base = 0;
+    unsigned long long m_b = 0, m_c0 = 0, m_meta = 0, m_len = 0, m_base = 0, m_pay0 = 0;
     if (l < kBatch && b0 + l < nb) {
-      const uint64_t b = b0 + l;
+      const uint64_t b = a.list ? a.list[b0 + l] : b0 + l;
+      m_b = b;
       m_c0 = d.blk_c0[b];
       m_meta = d.blk_meta[b];
       m_len = (a.codec == RIO_CODEC_NONE) ? d.blk_len[b] : d.blk_out_len[b];
       m_base = d.blk_item_base[b];
+      if (a.codec == RIO_CODEC_NONE) m_pay0 = d.ck_pay[m_c0];
     }
-    unsigned long long c0s[kBatch], metas[kBatch], lens[kBatch], bases[kBatch];
+    unsigned long long bs[kBatch], c0s[kBatch], metas[kBatch], lens[kBatch], bases[kBatch], pay0s[kBatch];
 #pragma unroll
     for (int j = 0; j < kBatch; j++) {  // wave-uniform: scalar registers
+      bs[j] = readlane_u64(m_b, j);
       c0s[j] = readlane_u64(m_c0, j);
       metas[j] = readlane_u64(m_meta, j);
       lens[j] = readlane_u64(m_len, j);
       bases[j] = readlane_u64(m_base, j);
+      pay0s[j] = readlane_u64(m_pay0, j);
     }
     // round 2: the first 1 KiB of every block payload (16 B per lane)
     uint32_t win[kBatch][4];
@@ -64,7 +68,7 @@ __global__ void __launch_bounds__(256) k_parse(DevBufs d, ParseArgs a) {
       if (b0 + j >= nb || !(metas[j] & kMetaComplete)) continue;
       const uint64_t p = 16ull * l;
       if (a.codec != RIO_CODEC_NONE) {
-        const uint64_t b = b0 + j;
+        const uint64_t b = bs[j];
         if (p + 16 <= lens[j]) {
 #ifdef RIO_CHECKED
           if (d.blk_dec_off[b] + p + 16 > d.dec_cap) {
@@ -91,10 +95,133 @@ __global__ void __launch_bounds__(256) k_parse(DevBufs d, ParseArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < kBatch; j++) {
+      if (b0 + j >= nb) break;
+      parse_block(d, a, bs[j], c0s[j], metas[j], lens[j], bases[j], pay0s[j], win[j], lwin, ltpos);
+    }
+  }
+}
+
+// The none codec's common block shape in a lean kernel (run before k_parse,
+// which then takes only the blocks listed here): a complete packed body block
+// of regular chunks, its header inside the first 1 KiB of payload, at most 256
+// sizes of at most 4 bytes each, consistent with the block. Wave per block,
+// kLeanBatch blocks per iteration with every load of the batch issued
+// together: the header window and, for a block of >= 2 chunks, the 1 KiB
+// around its first chunk boundary, so the straddler there is written from
+// registers. Anything else -- and any header that is not valid -- is appended
+// to the list for k_parse, untouched (nothing here writes before the checks).
+#ifndef RIO_LEAN_BATCH
+#define RIO_LEAN_BATCH 2
+#endif
+constexpr int kLeanBatch = RIO_LEAN_BATCH;
+
+__global__ void __launch_bounds__(256) k_parse_lean(DevBufs d, ParseArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[4][1040];
+  __shared__ __attribute__((aligned(16))) uint16_t s_tpos[4][264];
+  uint8_t *lwin = s_win[threadIdx.x >> 6];
+  uint16_t *ltpos = s_tpos[threadIdx.x >> 6];
+  const uint64_t nb = *a.nblocks;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const int l = lane_id();
+  for (uint64_t b0 = wave * kLeanBatch; b0 < nb; b0 += nwaves * kLeanBatch) {
+    unsigned long long m_c0 = 0, m_meta = 0, m_len = 0, m_base = 0;
+    if (l < kLeanBatch && b0 + l < nb) {
+      const uint64_t b = b0 + l;
+      m_c0 = d.blk_c0[b];
+      m_meta = d.blk_meta[b];
+      m_len = d.blk_len[b];
+      m_base = d.blk_item_base[b];
+    }
+    unsigned long long c0s[kLeanBatch], metas[kLeanBatch], lens[kLeanBatch], bases[kLeanBatch];
+    bool ok[kLeanBatch];
+#pragma unroll
+    for (int j = 0; j < kLeanBatch; j++) {
+      c0s[j] = readlane_u64(m_c0, j);
+      metas[j] = readlane_u64(m_meta, j);
+      lens[j] = readlane_u64(m_len, j);
+      bases[j] = readlane_u64(m_base, j);
+      const uint32_t cls = (uint32_t)(metas[j] >> kMetaClsShift) & 0xffu;
+      ok[j] = b0 + j < nb && (metas[j] & kMetaComplete) && (metas[j] & kMetaRegular) && cls == kMagicPacked &&
+              c0s[j] < a.limit_chunk && lens[j] < (1ull << 32);
+    }
+    uint32_t win[kLeanBatch][4], bnd[kLeanBatch][4];
+#pragma unroll
+    for (int j = 0; j < kLeanBatch; j++) {
+      win[j][0] = win[j][1] = win[j][2] = win[j][3] = 0x80808080u;
+      bnd[j][0] = bnd[j][1] = bnd[j][2] = bnd[j][3] = 0;
+      if (!ok[j]) continue;
+      const uint8_t *ck = a.span + c0s[j] * kChunk;
+      const uint64_t size0 = lens[j] < (uint64_t)kMaxPayload ? lens[j] : (uint64_t)kMaxPayload;
+      if (16ull * l + 16 <= size0) {  // 4-byte aligned: 28 + 16 l
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(ck + kChunkHdr + 16 * l);
+        win[j][0] = q[0];
+        win[j][1] = q[1];
+        win[j][2] = q[2];
+        win[j][3] = q[3];
+      }
+      if ((metas[j] & kMetaTotalMask) >= 2) {  // payload kBndW0 + 16 l: chunk c0's tail, then c0 + 1's head
+        const uint8_t *src = (l < 32) ? ck + kChunkHdr + kBndW0 + 16 * l : ck + kChunk + kChunkHdr + 16 * (l - 32);
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(src);
+        bnd[j][0] = q[0];
+        bnd[j][1] = q[1];
+        bnd[j][2] = q[2];
+        bnd[j][3] = q[3];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kLeanBatch; j++) {
+      if (b0 + j >= nb) break;
       const uint64_t b = b0 + j;
-      if (b >= nb) break;
-      const unsigned long long pay0 = (a.codec == RIO_CODEC_NONE) ? d.ck_pay[c0s[j]] : 0;
-      parse_block(d, a, b, c0s[j], metas[j], lens[j], bases[j], pay0, win[j], lwin, ltpos);
+      bool done = false;
+      uint32_t hdr = 0;
+      if (ok[j]) {
+        const uint32_t(&w)[4] = win[j];
+        const uint32_t tmask = term4(w[0]) | (term4(w[1]) << 4) | (term4(w[2]) << 8) | (term4(w[3]) << 12);
+        const uint32_t cnt = __popc(tmask);
+        const uint32_t incl = wave_incl_sum_dpp(cnt);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        *reinterpret_cast<uint4 *>(lwin + 16 * l) = make_uint4(w[0], w[1], w[2], w[3]);
+        {  // terminator positions of ordinals 0..263 (a header of <= 256 sizes ends by then)
+          uint32_t m = (incl - cnt < 264u) ? tmask : 0u, o = incl - cnt;
+          while (m && o < 264u) {
+            const uint32_t i = __ffs(m) - 1;
+            m &= m - 1;
+            ltpos[o++] = (uint16_t)(16 * l + i);
+          }
+        }
+        wave_lds_sync();
+        const uint32_t p0 = ltpos[0];
+        if (total > 0 && p0 < 2) {  // item count: one or two bytes
+          const uint32_t nitems = uvarint4(lds_bytes4(lwin, 0), p0 + 1);
+          if (nitems <= 256 && nitems < total) {
+            hdr = (uint32_t)ltpos[nitems] + 1;
+            Payload pl = desc_payload(a.span, d, c0s[j], metas[j], lens[j], 0);
+            ParseOut po;
+            po.item_off = d.item_off;
+            po.item_len = d.item_len;
+            po.item_base = bases[j];
+            po.item_cap = a.item_cap;
+            po.view_base = 0;
+            po.strad = d.strad;
+            po.ssz = d.ck_ssz;
+            po.c0 = c0s[j];
+            po.overflow = &d.ctl->out_overflow;
+            done = small_header<true>(pl, po, lwin, ltpos, nitems, hdr, a.sparse ? d.side : nullptr, bnd[j]) == 1;
+          }
+        }
+        wave_lds_sync();  // the next block's window reuses lwin / ltpos
+      }
+      if (l == 0) {
+        if (done) {
+          d.blk_status[b] = kBlkOk;
+          d.blk_a[b] = 0;
+          d.blk_b[b] = 0;
+          d.blk_hdr[b] = hdr;
+        } else {
+          d.blk_coff[atomicAdd(&d.ctl->n_retry, 1ull)] = b;
+        }
+      }
     }
   }
 }
@@ -394,6 +521,20 @@ static inline unsigned grid_of(uint64_t n, unsigned per, unsigned cap) {
 
 void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
   hipLaunchKernelGGL(k_parse, dim3(grid_of(max_blocks, 4 * kBatch, RIO_PARSE_GRID)), dim3(256), 0, st, d, a);
+}
+
+void launch_parse_lean(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
+  // one resident round: workgroups per CU at this build's occupancy x CUs
+  static unsigned cap = 0;
+  if (!cap) {
+    int per_cu = 0, dev = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_parse_lean, 256, 0) != hipSuccess || per_cu < 1)
+      per_cu = 4;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+      ncu = 256;
+    cap = (unsigned)(per_cu * ncu);
+  }
+  hipLaunchKernelGGL(k_parse_lean, dim3(grid_of(max_blocks, 4 * kLeanBatch, cap)), dim3(256), 0, st, d, a);
 }
 
 void launch_parse_slow(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {

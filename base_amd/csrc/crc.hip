@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
   __shared__ __attribute__((aligned(16))) uint32_t s_fold[kFoldWords];
   __shared__ __attribute__((aligned(16))) uint32_t s_mul[kMulTables * 1024];
   __shared__ __attribute__((aligned(16))) uint8_t s_stage[kParse ? kCrcWaves : 1][kParse ? kStageBytes : 16];
-  __shared__ uint16_t s_tpos[kParse ? kCrcWaves : 1][kParse ? 1024 : 1];
+  __shared__ __attribute__((aligned(16))) uint16_t s_tpos[kParse ? kCrcWaves : 1][kParse ? 1024 : 1];
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(d.crc_fold);
     uint4 *dst = reinterpret_cast<uint4 *>(s_fold);

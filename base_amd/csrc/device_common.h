@@ -465,6 +465,146 @@ __device__ __forceinline__ void copy_straddler(const Payload &pl, uint8_t *side,
   }
 }
 
+// 4 bytes of the LDS window from byte s (the window is dword-aligned, with room
+// for one dword past its 1 KiB)
+__device__ __forceinline__ uint32_t lds_bytes4(const uint8_t *lwin, uint32_t s) {
+  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(lwin);
+  const uint32_t a = s >> 2;
+  return __builtin_amdgcn_alignbyte(w32[a + 1], w32[a], s & 3u);
+}
+
+// the uvarint of the n <= 4 bytes in x (only its last byte is a terminator)
+__device__ __forceinline__ uint32_t uvarint4(uint32_t x, uint32_t n) {
+  const uint32_t v = (x & 0x7fu) | ((x >> 1) & 0x3f80u) | ((x >> 2) & 0x1fc000u) | ((x >> 3) & 0xfe00000u);
+  return n >= 4 ? v : v & ((1u << (7 * n)) - 1u);
+}
+
+// The fast path's passes for a header of at most 256 sizes (C2's 253, C4's
+// ~100): lane l owns items 4l+1 .. 4l+4, so one wave scan places them all; the
+// sizes stay in registers between the checks and the writes, sums are u32
+// (every valid prefix is below plen < 2^32). Returns 1 (views written), 0 (not
+// a valid header: nothing written, the caller declines) or -1 (a size varint
+// longer than 4 bytes: the generic passes below take the block).
+// kBnd: `bnd` holds payload bytes [kBndW0 + 16 l, +16) -- 512 bytes either side of
+// the first chunk boundary, loaded with the header window (k_parse_lean) --
+// and a straddler inside that range is written from it, with no load.
+constexpr uint32_t kBndW0 = (uint32_t)kMaxPayload - 512;
+
+// straddler [S, S + v) (payload bytes, inside the boundary window) to side + phys,
+// in whole dwords: phys = S (mod 4), so every dword lands aligned; the up to 3
+// bytes before / after it belong to no straddler (the next one starts a chunk
+// later), and side bytes outside straddlers are never read
+__device__ __forceinline__ void straddler_from_regs(const uint32_t (&bnd)[4], uint8_t *side, uint32_t S, uint32_t v,
+                                                    unsigned long long phys) {
+  const int l = lane_id();
+  const uint32_t E = S + v;
+  uint32_t *dst = reinterpret_cast<uint32_t *>(side + (phys - (S & 3u)));  // the dword holding byte S
+  const uint32_t S4 = S & ~3u;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t P = kBndW0 + 16u * (uint32_t)l + 4u * i;
+    if (P + 4 > S && P < E) dst[(P - S4) >> 2] = bnd[i];
+  }
+}
+
+template <bool kBnd>
+__device__ __forceinline__ int small_header(const Payload &pl, const ParseOut &po, const uint8_t *lwin,
+                                            const uint16_t *ltpos, uint32_t nitems, uint32_t hdr,
+                                            uint8_t *sparse_side, const uint32_t (&bnd)[4]) {
+  const int l = lane_id();
+  const uint32_t plen = (uint32_t)pl.len;
+  uint32_t v[4], st[4];
+  bool lng = false, bad = false;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    v[k] = 0;
+    const uint32_t o = 64u * k + (uint32_t)l + 1;
+    if (o <= nitems) {
+      const uint32_t e = ltpos[o], n = e - ltpos[o - 1];  // varint o: bytes e-n+1 .. e
+      if (n > 4) {
+        lng = true;
+      } else {
+        v[k] = uvarint4(lds_bytes4(lwin, e + 1 - n), n);
+        if (v[k] > plen) bad = true;
+      }
+    }
+  }
+  if (__ballot(lng)) return -1;
+  if (__ballot(bad)) return 0;
+  // item starts: one u32 scan per 64 items; steps are below 2^28, so the first
+  // wrap of a scan leaves incl < v, and a carry past plen is already invalid
+  unsigned long long carry = hdr;
+  bool wrap = false;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t incl = wave_incl_sum_dpp(v[k]);
+    wrap |= incl < v[k];
+    st[k] = (uint32_t)carry + incl - v[k];
+    carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (carry > pl.len) break;
+  }
+  if (__ballot(wrap) || carry != pl.len) return 0;
+  const bool chunks = !pl.contig && pl.total > 1;
+  if (kBnd && chunks) {  // every straddler must lie in the boundary window (else: declined, untouched)
+    bool far = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t st_ = st[k], vk = v[k];
+      if (64u * k + (uint32_t)l + 1 <= nitems && vk > 0 && st_ / (uint32_t)kMaxPayload != (st_ + vk - 1) / (uint32_t)kMaxPayload)
+        far |= !(st_ >= kBndW0 && st_ + vk <= kBndW0 + 1024);
+    }
+    if (__ballot(far)) return 0;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t o = 64u * k + (uint32_t)l + 1, sk = st[k], vk = v[k];
+    bool sd = false;
+    unsigned long long phys = 0;
+    if (o <= nitems) {
+      const uint64_t slot = po.item_base + (o - 1);
+      if (slot < po.item_cap) {
+        po.item_len[slot] = vk;
+        if (pl.contig) {
+          po.item_off[slot] = po.view_base + sk;
+        } else {
+          const uint32_t j = sk / (uint32_t)kMaxPayload;
+          phys = (pl.c0 + j) * (unsigned long long)kChunk + kChunkHdr + (sk - j * (uint32_t)kMaxPayload);
+          sd = chunks && vk > 0 && j != (sk + vk - 1) / (uint32_t)kMaxPayload;
+          if (sd && sparse_side) {
+            po.item_off[slot] = kItemInRecords | phys;
+          } else if (sd) {
+            StradDesc dsc;
+            dsc.c0 = pl.c0;
+            dsc.src = sk;
+            dsc.len = vk;
+            dsc.item = slot;
+            po.strad[pl.c0 + j] = dsc;
+            po.ssz[pl.c0 + j] = pad16(vk);
+          } else {
+            po.item_off[slot] = (vk == 0 && sk >= plen) ? 0ull : phys;
+          }
+        }
+      } else {
+        atomicOr(po.overflow, 1ull);
+      }
+    }
+    if (sparse_side) {
+      unsigned long long sm = __ballot(sd);
+      while (sm) {
+        const int L = __ffsll((long long)sm) - 1;
+        sm &= sm - 1;
+        const uint32_t S = (uint32_t)__shfl(sk, L, 64), V = (uint32_t)__shfl(vk, L, 64);
+        const unsigned long long ph = __shfl(phys, L, 64);
+        if (kBnd)
+          straddler_from_regs(bnd, sparse_side, S, V, ph);  // (checked above: inside the window)
+        else
+          copy_straddler(pl, sparse_side, S, V, ph);
+      }
+    }
+  }
+  return 1;
+}
+
 // window w = payload bytes [16*lane, 16*lane + 16) (0x80 past the payload);
 // writes the block's item views like parse_header<kParseWrite> and returns
 // nitems / hdr_len in r, or returns false (nothing written).
@@ -478,8 +618,8 @@ __device__ bool fast_header(const Payload &pl, const uint32_t (&w)[4], HdrResult
   if (!pl.contig && !pl.regular) return false;
   const uint32_t tmask = term4(w[0]) | (term4(w[1]) << 4) | (term4(w[2]) << 8) | (term4(w[3]) << 12);
   const uint32_t cnt = __popc(tmask);
-  const uint32_t incl = wave_incl_sum<uint32_t>(cnt);
-  const uint32_t total = __shfl(incl, 63, 64);
+  const uint32_t incl = wave_incl_sum_dpp(cnt);
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (total == 0) return false;
   *reinterpret_cast<uint4 *>(lwin + 16 * l) = make_uint4(w[0], w[1], w[2], w[3]);
   {
@@ -497,6 +637,17 @@ __device__ bool fast_header(const Payload &pl, const uint32_t (&w)[4], HdrResult
   const unsigned long long nitems = lds_uvarint(lwin, 0, p0);
   if (nitems >= total) return false;  // header not inside the window
   const uint32_t hdr = (uint32_t)ltpos[nitems] + 1;
+  if (nitems <= 256) {
+    const uint32_t none[4] = {0, 0, 0, 0};
+    const int res = small_header<false>(pl, po, lwin, ltpos, (uint32_t)nitems, hdr, sparse_side, none);
+    if (res >= 0) {
+      if (!res) return false;
+      r.status = kBlkOk;
+      r.nitems = nitems;
+      r.hdr_len = hdr;
+      return true;
+    }
+  }
   // pass A: validity, range, sum
   int bad = 0;
   unsigned long long lsum = 0;

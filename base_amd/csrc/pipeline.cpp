@@ -36,6 +36,7 @@ void launch_block_scan(const unsigned long long *in, unsigned long long *out, un
                        const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 // blocks.hip
 void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
+void launch_parse_lean(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
 void launch_parse_slow(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
 void launch_dec_nitems(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st);
 void launch_strad(const uint8_t *span, const DevBufs &d, uint64_t nslots, uint64_t side_cap, int32_t sparse,
@@ -394,7 +395,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
 #ifdef RIO_ZPROF
   HIP_OK(hipMemsetAsync(d.ctl->zprof, 0, sizeof(d.ctl->zprof), st));
 #endif
-  HIP_OK(hipMemsetAsync(&d.ctl->flstat_esc, 0, sizeof(unsigned long long), st));
+  HIP_OK(hipMemsetAsync(&d.ctl->flstat_esc, 0, 2 * sizeof(unsigned long long), st));  // + n_retry
   if (attempt == 0 && codec != RIO_CODEC_NONE && nchunks > 0)
     HIP_OK(hipMemsetAsync(d.blk_need, 0, nchunks * sizeof(unsigned long long), st));
   HIP_OK(hipMemsetAsync(c->nblocks_dev, 0, 2 * sizeof(unsigned long long), st));
@@ -437,6 +438,13 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
       HIP_OK(hipEventRecord(c->ev[kEvCrc0], st2));
       launch_crc(span, nchunks, d, ca, c->ncu, st2, &pa);
       HIP_OK(hipEventRecord(c->ev[kEvCrc1], st2));
+    } else if (codec == RIO_CODEC_NONE && mode == kModeBody) {
+      // the common block shape in a lean kernel, the rest listed for k_parse
+      launch_parse_lean(d, pa, max_blocks, st2);
+      ParseArgs pl = pa;
+      pl.list = d.blk_coff;
+      pl.list_n = &d.ctl->n_retry;
+      launch_parse(d, pl, max_blocks, st2);
     } else {
       launch_parse(d, pa, max_blocks, st2);
     }

@@ -96,6 +96,7 @@ struct Ctl {
   unsigned long long consumed_chunks;
   unsigned long long mag_cur, mag_prev, mag_blk;  // little-endian magic bytes
   unsigned long long flstat_esc;                  // (RIO_FLSTAT builds: flate escapes)
+  unsigned long long n_retry;                     // blocks k_parse_lean left to k_parse (listed in blk_coff)
   unsigned long long zprof[4];                    // (RIO_ZPROF builds: zstd entropy-pass cycles per phase)
   unsigned long long zjob_n;                      // zstd jobs made (k_zstd_ent)
 };
@@ -208,6 +209,9 @@ struct ParseArgs {
   uint64_t item_cap, side_cap;
   int32_t sparse;  // straddlers go to a span-shaped side buffer at their own span offset
   int32_t pad;
+  // k_parse over a list of blocks (the ones k_parse_lean declined) instead of all
+  const unsigned long long *list;
+  const unsigned long long *list_n;
 };
 struct CrcArgs {
   int32_t flags;  // RIO_ABLATE of ablation builds (1 no CRC fold); 0 in the shipped library
