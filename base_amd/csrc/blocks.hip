@@ -533,6 +533,9 @@ void launch_parse_lean(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
       ncu = 256;
     cap = (unsigned)(per_cu * ncu);
+#ifdef RIO_LEAN_GRID
+    cap = RIO_LEAN_GRID;  // (experiments: leave CUs to a concurrent k_crc)
+#endif
   }
   hipLaunchKernelGGL(k_parse_lean, dim3(grid_of(max_blocks, 4 * kLeanBatch, cap)), dim3(256), 0, st, d, a);
 }

@@ -2028,16 +2028,41 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
     const uint32_t *lit32 = reinterpret_cast<const uint32_t *>(region + lit0);    // 16-aligned
     uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
     uint32_t olen = 0, litpos = 0, flushed = 0, fstart = 0, zerr = 0;
+    // one group ahead: its 64 entries and the first 256 bytes of its literals
+    // (from dword-aligned pf_nx; ~0: not prefetched), so a group usually
+    // starts without waiting for memory
+    uint64_t e_nx = (uint32_t)l < ntok ? ents[-1 - (int64_t)l] : 0ull;
+    uint32_t pf_nx = ~0u, lit_nx = 0;
+    if (lit0 + 256 <= ent_end) {
+      pf_nx = 0;
+      lit_nx = lit32[l];
+    }
     wave_lds_sync();
     for (uint32_t g0 = 0; g0 < ntok && !zerr; g0 += 64) {
       const uint32_t n = ntok - g0 < 64 ? ntok - g0 : 64;
-      const uint64_t e = (uint32_t)l < n ? ents[-1 - (int64_t)(g0 + l)] : 0ull;
+      const uint64_t e = e_nx;
+      uint32_t lit_at = ~0u;  // litbuf holds literal bytes [lit_at, lit_at + 256)
+      if (pf_nx != ~0u) {
+        wave_lds_sync();
+        litbuf[l] = lit_nx;
+        lit_at = pf_nx;
+      }
+      if (g0 + 64 < ntok)
+        e_nx = (uint32_t)l < ntok - g0 - 64 ? ents[-1 - (int64_t)(g0 + 64 + l)] : 0ull;
       const uint32_t ll0 = (uint32_t)e & 0xffffu, ml0 = (uint32_t)(e >> 16) & 0xffffu, off = (uint32_t)(e >> 32);
       const bool mark = ll0 == kZMark;
       const uint32_t len = mark ? 0u : ll0 + ml0, lits = mark ? 0u : ll0;
       const uint32_t incl = wave_incl_sum_dpp(len), lincl = wave_incl_sum_dpp(lits);
       const uint32_t excl = incl - len, lexcl = lincl - lits;
       const unsigned long long marks = __ballot(mark);
+      {  // the next group's literals start where this group's end
+        const uint32_t na = (litpos + zrl(lincl, n - 1)) & ~3u;
+        pf_nx = ~0u;
+        if (g0 + 64 < ntok && lit0 + na + 256 <= ent_end) {
+          pf_nx = na;
+          lit_nx = lit32[(na >> 2) + l];
+        }
+      }
       uint32_t s = 0;
       while (s < n) {
         const uint32_t bs = zrl(excl, s), ls = zrl(lexcl, s);
@@ -2054,8 +2079,11 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
           const uint32_t myll = mine ? ll0 : 0u, myml = mine ? ml0 : 0u;
           if (Ls) {  // literals: stage the part's run of the literal area, then scatter
             const uint32_t a0 = litpos & ~3u, nd = (litpos + Ls - a0 + 3) >> 2;
-            wave_lds_sync();
-            for (uint32_t j = l; j < nd; j += 64) litbuf[j] = lit32[(a0 >> 2) + j];
+            if (a0 != lit_at || nd > 64) {  // not the prefetched bytes
+              wave_lds_sync();
+              for (uint32_t j = l; j < nd; j += 64) litbuf[j] = lit32[(a0 >> 2) + j];
+              lit_at = ~0u;
+            }
             wave_lds_sync();
             const uint8_t *lb = reinterpret_cast<const uint8_t *>(litbuf) + (litpos - a0);
             const uint32_t lp = lexcl - ls;
