@@ -1780,6 +1780,31 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
   }
 }
 
+// One step of the repeat-offset history scan (k_zstd_fix): compose this
+// lane's op (src, c) after the op of the DPP source lane (g o f); lanes the
+// DPP pattern gives no source keep the identity op (slot k <- slot k, + 0).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void z_hist_step(uint32_t &src, uint32_t &c0, uint32_t &c1, uint32_t &c2) {
+  constexpr int kIdSrc = 0 | (1 << 2) | (2 << 4);
+  const uint32_t fs = (uint32_t)__builtin_amdgcn_update_dpp(kIdSrc, (int)src, kCtrl, kRowMask, 0xf, false);
+  const uint32_t f0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c0, kCtrl, kRowMask, 0xf, false);
+  const uint32_t f1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1, kCtrl, kRowMask, 0xf, false);
+  const uint32_t f2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c2, kCtrl, kRowMask, 0xf, false);
+  uint32_t ns = 0, nc[3];
+  const uint32_t cc[3] = {c0, c1, c2};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint32_t gs = (src >> (2 * k)) & 3u;
+    const uint32_t fsel = gs == 0 ? f0 : (gs == 1 ? f1 : f2);
+    ns |= (gs == 3 ? 3u : (fs >> (2 * gs)) & 3u) << (2 * k);
+    nc[k] = gs == 3 ? cc[k] : fsel + cc[k];
+  }
+  src = ns;
+  c0 = nc[0];
+  c1 = nc[1];
+  c2 = nc[2];
+}
+
 // ---------------------------------------------------------------- k_zstd_fix
 // In file order, one wave per recordio block: every job's raw sequences 64 at
 // a time -- repeat offsets resolved by a wave scan of history ops, the serial decoder's
@@ -1847,10 +1872,12 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
           break;
         }
         const uint64_t *raw = reinterpret_cast<const uint64_t *>(tok8 + raw_off);
+        uint64_t rv_nx = (uint32_t)l < nseq ? raw[l] : 0ull;  // one group ahead
         for (uint32_t g0 = 0; g0 < nseq; g0 += 64) {
           const uint32_t cnt = nseq - g0 < 64 ? nseq - g0 : 64;
           const bool v = (uint32_t)l < cnt;
-          const uint64_t rv = v ? raw[g0 + l] : 0ull;
+          const uint64_t rv = rv_nx;
+          if (g0 + 64 < nseq) rv_nx = (uint32_t)l < nseq - g0 - 64 ? raw[g0 + 64 + l] : 0ull;
           const uint32_t ll = (uint32_t)rv & 0x1FFFFu, ml = (uint32_t)(rv >> 17) & 0x3FFFFu;
           const uint32_t ofv = (uint32_t)(rv >> 35);
           // Repeat offsets: a sequence maps the offset history (rep0, rep1, rep2)
@@ -1877,26 +1904,14 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
               c0 = ~0u;
             }
           }
-#pragma unroll
-          for (int dd = 1; dd < 64; dd <<= 1) {
-            const uint32_t fs = (uint32_t)__shfl_up((int)src, dd), f0 = (uint32_t)__shfl_up((int)c0, dd),
-                           f1 = (uint32_t)__shfl_up((int)c1, dd), f2 = (uint32_t)__shfl_up((int)c2, dd);
-            if (l >= dd) {  // this lane's op after the earlier lanes' (g o f)
-              uint32_t ns = 0, nc[3];
-              const uint32_t cc[3] = {c0, c1, c2};
-#pragma unroll
-              for (int k = 0; k < 3; k++) {
-                const uint32_t gs = (src >> (2 * k)) & 3u;
-                const uint32_t fsel = gs == 0 ? f0 : (gs == 1 ? f1 : f2);
-                ns |= (gs == 3 ? 3u : (fs >> (2 * gs)) & 3u) << (2 * k);
-                nc[k] = gs == 3 ? cc[k] : fsel + cc[k];
-              }
-              src = ns;
-              c0 = nc[0];
-              c1 = nc[1];
-              c2 = nc[2];
-            }
-          }
+          // inclusive scan by DPP (row shifts, then the row broadcasts, as
+          // wave_incl_sum_dpp); lanes without a source lane compose the identity
+          z_hist_step<0x111, 0xf>(src, c0, c1, c2);  // row_shr:1
+          z_hist_step<0x112, 0xf>(src, c0, c1, c2);  // row_shr:2
+          z_hist_step<0x114, 0xf>(src, c0, c1, c2);  // row_shr:4
+          z_hist_step<0x118, 0xf>(src, c0, c1, c2);  // row_shr:8
+          z_hist_step<0x142, 0xa>(src, c0, c1, c2);  // row_bcast:15
+          z_hist_step<0x143, 0xc>(src, c0, c1, c2);  // row_bcast:31
           auto apply = [&](uint32_t sk, uint32_t ck) {
             return sk == 3 ? ck : (sk == 0 ? rep0 : (sk == 1 ? rep1 : rep2)) + ck;
           };
