@@ -1807,7 +1807,13 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
 // gfx9 wave's vector memory operations complete in issue order, so the stores
 // are done. Sources are read with agent-scope loads (from L2, never a stale L1
 // line).
-__global__ void __launch_bounds__(64) k_flate_lz2(DevBufs d, const unsigned long long *nblocks, int round) {
+// Registers for 5 waves per SIMD (96 VGPRs, 4 spilled; the compiler alone takes
+// 125: 4 waves): C3 45.6 -> 47.7 GiB/s; 6 waves (80 VGPRs, 31 spilled) 34.3.
+#ifndef RIO_LZ2_WPE
+#define RIO_LZ2_WPE 5
+#endif
+#define RIO_LZ2_ATTR __attribute__((amdgpu_waves_per_eu(RIO_LZ2_WPE)))
+__global__ void __launch_bounds__(64) RIO_LZ2_ATTR k_flate_lz2(DevBufs d, const unsigned long long *nblocks, int round) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[kL2Ring];
   const int l = lane_id();
   if (round > 0 && uni64(d.fl_more[round - 1]) == 0) return;

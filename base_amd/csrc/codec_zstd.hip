@@ -52,7 +52,10 @@ enum ZErr : uint32_t {
 constexpr uint32_t kZMagic = 0xFD2FB528u;
 constexpr int kZBlockMax = 128 * 1024;
 constexpr uint64_t kZLitStride = kZBlockMax + 256;  // per-wave literal buffer
-constexpr int kZWaves = 12;                          // resident zstd waves per CU (LDS ~10 KiB each)
+#ifndef RIO_ZWAVES
+#define RIO_ZWAVES 12
+#endif
+constexpr int kZWaves = RIO_ZWAVES;  // resident zstd waves per CU (LDS ~10 KiB each)
 constexpr int kZSeqWaves = 8;                        // k_zstd_seq waves per CU (64 jobs each; every job of a C4 span in flight)
 constexpr int kZFixWaves = 8;                        // k_zstd_fix waves per CU
 #ifndef RIO_ZSTD_SEQ2
@@ -1304,7 +1307,14 @@ __device__ __forceinline__ void z_flatten(const uint8_t *span, const DevBufs &d,
 // block becomes a job (ZJob) for k_zstd_seq. Region of block b (512 KiB per
 // chunk): flattened input | literals (up) ... execution entries (down from
 // the middle) | jobs (from the middle up).
-__global__ void __launch_bounds__(64) k_zstd_ent(const uint8_t *__restrict__ span, DevBufs d,
+// Registers for 3 waves per SIMD (12 per CU, the LDS's limit at ~12 KiB each):
+// left to itself the compiler takes 205 VGPRs (2 waves per SIMD) and 1/3 of the
+// launched waves wait; at 168 VGPRs (28 spilled, cold paths) C4 177.6 -> 161.4 ms.
+#ifndef RIO_ZENT_WPE
+#define RIO_ZENT_WPE 3
+#endif
+#define RIO_ZENT_ATTR __attribute__((amdgpu_waves_per_eu(RIO_ZENT_WPE)))
+__global__ void __launch_bounds__(64) RIO_ZENT_ATTR k_zstd_ent(const uint8_t *__restrict__ span, DevBufs d,
                                                  const unsigned long long *nblocks, uint64_t dec_cap) {
   __shared__ ZLds L;
   const int l = lane_id();

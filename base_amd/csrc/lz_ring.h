@@ -10,7 +10,10 @@ constexpr uint32_t kL2Ring = 4096, kL2Mask = kL2Ring - 1;
 constexpr uint32_t kL2Span = 1536;                   // output bytes per batch at most
 constexpr uint32_t kL2Near = kL2Ring - kL2Span - 16;  // bytes before the batch kept in the ring (the
                                                        // batch's zeroing may round up one dword)
-constexpr int kL2Waves = 16;                          // per CU (launch sizing)
+#ifndef RIO_L2_WAVES
+#define RIO_L2_WAVES 20  // 5 per SIMD: k_flate_lz2 is register-allocated for that (RIO_LZ2_WPE)
+#endif
+constexpr int kL2Waves = RIO_L2_WAVES;                          // per CU (launch sizing)
 static_assert(kL2Near >= kL2Span + 16 + 258, "HBM sources must be flushed two batches back");
 
 __device__ __forceinline__ uint32_t tok_len(uint32_t t) {
