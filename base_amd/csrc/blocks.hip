@@ -115,7 +115,12 @@ __global__ void __launch_bounds__(256) k_parse(DevBufs d, ParseArgs a) {
 #endif
 constexpr int kLeanBatch = RIO_LEAN_BATCH;
 
-__global__ void __launch_bounds__(256) k_parse_lean(DevBufs d, ParseArgs a) {
+#ifdef RIO_LEAN_WPE  // (experiments: waves per SIMD k_parse_lean is register-allocated for)
+#define RIO_LEAN_ATTR __attribute__((amdgpu_waves_per_eu(RIO_LEAN_WPE)))
+#else
+#define RIO_LEAN_ATTR
+#endif
+__global__ void __launch_bounds__(256) RIO_LEAN_ATTR k_parse_lean(DevBufs d, ParseArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_win[4][1040];
   __shared__ __attribute__((aligned(16))) uint16_t s_tpos[4][264];
   uint8_t *lwin = s_win[threadIdx.x >> 6];

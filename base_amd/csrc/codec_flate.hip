@@ -1336,7 +1336,10 @@ constexpr uint32_t kSyncSeg = 1024;                       // bits per lane per r
 constexpr uint32_t kSyncBits = 64 * kSyncSeg;             // bits per round
 constexpr uint32_t kSyncWinDw = kSyncBits / 32 + 32;      // staged dwords (+ run-out margin)
 constexpr int kSyncIters = 8;
-constexpr int kSyncWaves = 12;                            // per CU (launch sizing)
+#ifndef RIO_SYNC_WAVES
+#define RIO_SYNC_WAVES 12
+#endif
+constexpr int kSyncWaves = RIO_SYNC_WAVES;                 // per CU (launch sizing)
 
 struct SyncLds {
   StreamLds T;  // the DEFLATE block's tables (ring / tbuf unused)
@@ -1424,7 +1427,12 @@ __device__ __forceinline__ uint32_t sync_decode(const StreamLds &T, const uint32
   return r;
 }
 
-__global__ void __launch_bounds__(64) k_flate_sync(const uint8_t *__restrict__ span, DevBufs d,
+#ifdef RIO_SYNC_WPE  // (experiments: waves per SIMD the Huffman pass is register-allocated for)
+#define RIO_SYNC_ATTR __attribute__((amdgpu_waves_per_eu(RIO_SYNC_WPE)))
+#else
+#define RIO_SYNC_ATTR
+#endif
+__global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *__restrict__ span, DevBufs d,
                                                    const unsigned long long *nblocks, uint64_t nchunks,
                                                    uint64_t dec_cap) {
   __shared__ SyncLds S;

@@ -57,7 +57,10 @@ constexpr uint64_t kZLitStride = kZBlockMax + 256;  // per-wave literal buffer
 #endif
 constexpr int kZWaves = RIO_ZWAVES;  // resident zstd waves per CU (LDS ~10 KiB each)
 constexpr int kZSeqWaves = 8;                        // k_zstd_seq waves per CU (64 jobs each; every job of a C4 span in flight)
-constexpr int kZFixWaves = 8;                        // k_zstd_fix waves per CU
+#ifndef RIO_ZFIX_WAVES
+#define RIO_ZFIX_WAVES 20  // 5 per SIMD (8: 162.0 ms for C4, 20: 156.1, 28: 159.8)
+#endif
+constexpr int kZFixWaves = RIO_ZFIX_WAVES;            // k_zstd_fix waves per CU
 #ifndef RIO_ZSTD_SEQ2
 #define RIO_ZSTD_SEQ2 1
 #endif
