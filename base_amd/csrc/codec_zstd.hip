@@ -1558,7 +1558,11 @@ __device__ __forceinline__ void zs2_settle(T &x) {
   asm volatile("" : "+v"(x));
 }
 
-constexpr int kZs2Jobs = 15;
+#ifndef RIO_ZS2_JOBS
+#define RIO_ZS2_JOBS 15
+#endif
+constexpr int kZs2Jobs = RIO_ZS2_JOBS;         // job slots per wave
+constexpr int kZs2Groups = 15 / kZs2Jobs;      // 4-wave workgroups per CU (60 slots' tables fill the LDS)
 constexpr int kZs2Cells = 512 + 512 + 256;  // ll (log <= 9), ml (<= 9), of (<= 8)
 
 __device__ __forceinline__ uint16_t zs2_cell(uint32_t c, int log) {
@@ -2512,8 +2516,8 @@ void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long
   uint64_t g = max_blocks < grid ? max_blocks : grid;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(k_zstd_ent, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
-  if (kZstdSeq2)  // one 4-wave workgroup per CU (its LDS is the CU's)
-    hipLaunchKernelGGL(k_zstd_seq2, dim3((unsigned)(grid / kZWaves)), dim3(256), 0, st, d);
+  if (kZstdSeq2)  // 4-wave workgroups sharing the CU's LDS (kZs2Groups per CU)
+    hipLaunchKernelGGL(k_zstd_seq2, dim3((unsigned)(grid / kZWaves * kZs2Groups)), dim3(256), 0, st, d);
   else
     hipLaunchKernelGGL(k_zstd_seq, dim3((unsigned)(grid / kZWaves * kZSeqWaves)), dim3(64), 0, st, d);
   uint64_t g3 = grid / kZWaves * kZFixWaves;
