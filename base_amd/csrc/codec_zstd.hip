@@ -1531,6 +1531,15 @@ struct ZBr64 {
   __device__ __forceinline__ uint32_t Dc(int32_t i) const { return w[max(qtop - i, 0)]; }
   // ring: this lane's kZs2Ring dwords (D_i at i mod kZs2Ring)
   __device__ __forceinline__ void reload(const uint32_t (&ring)[kZs2Ring]) {
+#if RIO_ZS2_BRANCHLESS
+    // (experiment) the ring dword read every time, the refill selected: no
+    // exec-mask branch per reload
+    const bool need = avail <= 32;
+    const uint32_t v = ring[cons & (kZs2Ring - 1)];
+    win = need ? ((win << 32) | v) : win;
+    cons += need ? 1 : 0;
+    avail += need ? 32 : 0;
+#else
     if (avail <= 32) {
       // in the ring once retired from the registers (else a direct load: rare)
       // the ring always holds it: >= 24 dwords at the start of every group of
@@ -1541,6 +1550,7 @@ struct ZBr64 {
       cons++;
       avail += 32;
     }
+#endif
   }
   __device__ __forceinline__ uint32_t read(int nb) {  // nb <= 31
     avail -= nb;
@@ -2024,7 +2034,11 @@ __device__ __forceinline__ uint32_t zr_slot(uint32_t x) {
   return x - __umulhi(x >> 12, 0xFFFFFFFFu / kZRingK + 1u) * kZRing;
 }
 __device__ __forceinline__ uint8_t zr_src(const uint8_t *ring, const uint8_t *out, uint32_t pos, uint32_t base) {
+#if RIO_ZEXEC_NOFAR  // (measurement only: far sources read from the ring -- wrong bytes, the cost of their loads)
+  return ring[zr_slot(pos)];
+#else
   return pos + kZHist >= base ? ring[zr_slot(pos)] : out[pos];
+#endif
 }
 // k mod d for k < 2^20, d >= 1
 __device__ __forceinline__ uint32_t z_umod(uint32_t k, uint32_t dv) {

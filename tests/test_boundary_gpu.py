@@ -255,3 +255,35 @@ def test_unmarshal_error_is_sticky(gpu_ctx):
     assert got == list(range(20))
     assert not sc.Scan()  # stays false
     assert str(sc.Finish()) == "bad record 20"
+
+
+@pytest.mark.parametrize("codec", ["flate", "zstd"])
+def test_async_device_path_after_host_result(gpu_ctx, oracle, codec):
+    """rio_scan_device_async + rio_sync on a ctx whose previous call was a host
+    result of a compressed codec (rio_scan_span compacts the decoded blocks):
+    the device batch's records are this call's decode regions, not the previous
+    call's compacted bytes (pipeline.cpp resets last_cmp per enqueue)."""
+    import struct
+    import torch
+    from base_amd.recordio import gpu
+    from base_amd.recordio.writer import write_file, WriterOpts
+    if codec == "zstd" and not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    rng = random.Random(91)
+    code = gpu.RIO_CODEC_FLATE if codec == "flate" else gpu.RIO_CODEC_ZSTD
+    files = []
+    for k in range(2):
+        recs = [bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, 600))) for _ in range(700)]
+        files.append((write_file(recs, WriterOpts(Transformers=[codec], MaxItems=64)), recs))
+    for data, recs in files:
+        h = struct.unpack_from("<I", data, 20)[0] * 32768
+        b = gpu_ctx.scan_span(data[h:], file_off=h, is_file_end=True, codec=code)  # host result: compacted
+        assert gpu.batch_items(b) == recs
+    data, recs = files[0]
+    h = struct.unpack_from("<I", data, 20)[0] * 32768
+    body = data[h:]
+    dev = torch.frombuffer(bytearray(body), dtype=torch.uint8).to("cuda:0")
+    gpu_ctx.scan_device_async(dev.data_ptr(), len(body), file_off=h, codec=code)
+    b = gpu_ctx.sync()
+    assert b.err.code == 0, b.err.msg
+    assert gpu.device_batch_items(b, body) == recs

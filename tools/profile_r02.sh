@@ -5,7 +5,7 @@
 # limits), over shorter runs of the same benches. Output: gpurun_out/r02/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-O=gpurun_out/r02
+O=${PROF_OUT:-gpurun_out/r02}
 mkdir -p $O
 timeout -k 10 200 python3 tools/bench_zstd.py --make-data --data /tmp/c4.rio > $O/c4data.log 2>&1 || exit $?
 C2="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-flate --no-zstd --no-c5"
