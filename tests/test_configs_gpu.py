@@ -215,3 +215,47 @@ def test_v2_random(gpu_ctx, oracle, codec, flush_p, nshard, maxrecords, datasize
         assert sc.Err() is None
         assert sc.Scan() and sc.Get() == v
     sc.Finish()
+
+
+def test_c5_shaped_file_set(gpu_ctx, oracle):
+    """C5 (configs[4]) in miniature: trailer-indexed flate files of FASTQ-like
+    records (tools/c5_data.py, 2 MiB of records each instead of 64 MiB). Each
+    file's trailer index (read through the GPU scanner's Trailer, ReadLastBlock
+    from EOF) equals the writer's block offsets; the file bodies placed back to
+    back on the device decode in one rio_scan_device launch to every file's
+    records in file-set order; and a two-rank index split of one file
+    (shard.split_blocks) covers its records exactly once."""
+    import torch
+    import c5_data
+    from base_amd.recordio import gpu, shard
+    rb = 2 << 20
+    files = [c5_data.make_base(k, record_bytes=rb, workers=4) for k in range(3)]
+    want, bodies = [], []
+    for k, (data, nrec, rec_bytes, offsets) in enumerate(files):
+        recs = c5_data.base_records(k, record_bytes=rb)
+        assert len(recs) == nrec
+        sc = gpu.NewScanner(data, ctx=gpu_ctx)
+        assert c5_data.parse_index(sc.Trailer()) == offsets
+        got = []
+        while sc.Scan():
+            got.append(sc.Get())
+        assert sc.Finish() is None and got == recs
+        want.extend(recs)
+        bodies.append(data[offsets[0]:shard.trailer_offset(data)])
+        if k == 0:  # the index split: rank r decodes blocks [lo, hi) of the body
+            body_end = shard.trailer_offset(data)
+            parts = []
+            for r in range(2):
+                lo, hi = shard.split_blocks(offsets, body_end, r, 2)
+                if hi > lo:
+                    b = gpu_ctx.scan_span(data[lo:hi], file_off=lo, is_file_end=True, codec=gpu.RIO_CODEC_FLATE)
+                    assert b.err.code == 0, b.err.msg
+                    parts.extend(gpu.batch_items(b))
+            assert parts == recs
+        ref = oracle.scan(data)
+        assert ref.err == "" and ref.items == recs
+    span = b"".join(bodies)
+    dev = torch.frombuffer(bytearray(span), dtype=torch.uint8).to("cuda:0")
+    b = gpu_ctx.scan_device(dev.data_ptr(), len(span), file_off=0, is_file_end=True, codec=gpu.RIO_CODEC_FLATE)
+    assert b.err.code == 0, b.err.msg
+    assert gpu.device_batch_items(b, span) == want
