@@ -2020,6 +2020,12 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
 #ifndef RIO_ZRING_K
 #define RIO_ZRING_K 5
 #endif
+#ifndef RIO_ZEXEC_NOLIT
+#define RIO_ZEXEC_NOLIT 0
+#endif
+#ifndef RIO_ZEXEC_NOREADY
+#define RIO_ZEXEC_NOREADY 0
+#endif
 constexpr uint32_t kZRingK = RIO_ZRING_K;  // ring = kZRingK x 4 KiB
 constexpr uint32_t kZRing = kZRingK * 4096;
 constexpr uint32_t kZPart = 2 * kZPiece;
@@ -2133,7 +2139,7 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
             wave_lds_sync();
             const uint8_t *lb = reinterpret_cast<const uint8_t *>(litbuf) + (litpos - a0);
             const uint32_t lp = lexcl - ls;
-            if (myll && myll <= 32) {
+            if (myll && myll <= 32 && !RIO_ZEXEC_NOLIT) {  // (RIO_ZEXEC_NOLIT: measurement only, wrong bytes)
               const uint32_t q0 = base + p;
               for (uint32_t k = 0; k < myll; k++) ring[zr_slot(q0 + k)] = lb[lp + k];
             }
@@ -2159,8 +2165,25 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
             const uint32_t R = zrl(dst, (uint32_t)(__ffsll((long long)mm) - 1));
             const uint32_t src_end = src + (myml < off ? myml : off);
             const bool ready = m && src_end <= R && myml <= 32;
-            if (ready) {
-              if (off >= 8 || myml <= off) {  // no byte of an 8-byte piece depends on another
+            if (ready && !RIO_ZEXEC_NOREADY) {  // (RIO_ZEXEC_NOREADY: measurement only, wrong bytes)
+              // the source wholly in the ring or wholly flushed (src + kZHist vs base is
+              // monotone in the byte), neither ring range wrapping: 12 aligned bytes per
+              // 8-byte piece, two funnel shifts, byte stores at immediate offsets
+              const bool all_ring = src + kZHist >= base, all_far = src + myml - 1 + kZHist < base;
+              const uint32_t ss = zr_slot(src), ds = zr_slot(dst);
+              if ((off >= 8 || myml <= off) && (all_far || (all_ring && ss + myml + 12 <= kZRing)) &&
+                  ds + myml <= kZRing) {
+                for (uint32_t k = 0; k < myml; k += 8) {
+                  const uint32_t *w = all_ring ? reinterpret_cast<const uint32_t *>(ring + ((ss + k) & ~3u))
+                                               : reinterpret_cast<const uint32_t *>(out + ((src + k) & ~3u));
+                  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = (src + k) & 3u;  // ss = src (mod 4)
+                  const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                  uint8_t *dp = ring + ds + k;
+#pragma unroll
+                  for (int jj = 0; jj < 8; jj++)
+                    if (k + jj < myml) dp[jj] = (uint8_t)((jj < 4 ? x0 : x1) >> (8 * (jj & 3)));
+                }
+              } else if (off >= 8 || myml <= off) {  // no byte of an 8-byte piece depends on another
                 for (uint32_t k = 0; k < myml; k += 8) {
                   uint8_t v[8];
 #pragma unroll
