@@ -2080,6 +2080,7 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
     const uint32_t *lit32 = reinterpret_cast<const uint32_t *>(region + lit0);    // 16-aligned
     uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
     uint32_t olen = 0, litpos = 0, flushed = 0, fstart = 0, zerr = 0;
+    uint32_t synced = 0;  // bytes below it: flushed and visible to this wave (the last vmcnt(0) drain)
     // one group ahead: its 64 entries and the first 256 bytes of its literals
     // (from dword-aligned pf_nx; ~0: not prefetched), so a group usually
     // starts without waiting for memory
@@ -2159,7 +2160,14 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
           const unsigned long long mm = __ballot(m);
           if (mm) {
             const uint32_t dst = base + p + myll, src = dst - off;
-            if (__ballot(m && src + kZHist < base)) zmem_sync();  // flushed sources: visible first
+            {  // bytes read from the decode region (pos + kZHist < base) visible first: drain
+               // the wave's stores only when one of them lies at or above the last drain's mark
+              const uint32_t hi = min(src + (myml < off ? myml : off), base - kZHist);
+              if (__ballot(m && src + kZHist < base && hi > synced)) {
+                zmem_sync();
+                synced = flushed;
+              }
+            }
             // one parallel round: short matches whose source ends before the
             // part's first match, each by its own lane ...
             const uint32_t R = zrl(dst, (uint32_t)(__ffsll((long long)mm) - 1));
