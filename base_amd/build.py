@@ -17,7 +17,7 @@ LIB = os.path.join(OUT_DIR, "librio_gpu.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RIO_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["kernels.hip", "blocks.hip", "crc.hip", "codec.hip", "codec_flate.hip", "codec_zstd.hip", "legacy.hip", "encode.hip", "deflate_enc.hip",
+SOURCES = ["kernels.hip", "blocks.hip", "crc.hip", "codec.hip", "codec_flate.hip", "codec_zstd.hip", "legacy.hip", "encode.hip", "deflate_enc.hip", "zstd_enc.hip",
            "pipeline.cpp", "messages.cpp", "scanner.cpp", "crc_tables.cpp"]
 FLAGS = (["-DRIO_CHECKED"] if os.environ.get("RIO_CHECKED") else []) + (["-DRIO_FLSTAT"] if os.environ.get("RIO_FLSTAT") else []) + (["-DRIO_ZPROF"] if os.environ.get("RIO_ZPROF") else []) + os.environ.get("RIO_EXTRA_FLAGS", "").split() + ([f"-DRIO_FOLD_COPIES={os.environ['RIO_FOLD_COPIES']}"] if os.environ.get("RIO_FOLD_COPIES") else []) + ([f"-DRIO_CRC_WAVES={os.environ['RIO_CRC_WAVES']}"] if os.environ.get("RIO_CRC_WAVES") else []) + ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
          "-I", CSRC, "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result"]

@@ -34,6 +34,12 @@ struct CrcTabs {
 void launch_enc_chunks(const EncArgs &a, uint64_t nchunks, const CrcTabs &t, int ncu, hipStream_t st);
 void launch_deflate_bound(const EncArgs &a, hipStream_t st);
 void launch_deflate(const EncArgs &a, hipStream_t st);
+// zstd (zstd_enc.hip): tables of the predefined sequence codes (ZeTabs,
+// zstd_enc.h), scratch of zstd_enc_scratch_words(ncu) u64
+struct ZeTabs;
+void launch_zstd_enc_bound(const EncArgs &a, hipStream_t st);
+uint64_t zstd_enc_scratch_words(int ncu);
+void launch_zstd_enc(const EncArgs &a, const ZeTabs *tabs, unsigned long long *scratch, int ncu, hipStream_t st);
 void launch_enc_boff(const unsigned long long *ck0, unsigned long long *boff, uint64_t nblocks, hipStream_t st);
 
 }  // namespace rio

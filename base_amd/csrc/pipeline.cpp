@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "encode.h"
+#include "zstd_enc.h"
 #include "legacy.h"
 #include "pipeline.h"
 #include "rio_internal.h"
@@ -137,6 +138,9 @@ struct rio_ctx {
   uint64_t e_blk_cap = 0;
   uint8_t *e_hdr = nullptr, *e_comp = nullptr, *e_data = nullptr, *e_out = nullptr;
   uint64_t e_hdr_cap = 0, e_comp_cap = 0, e_data_cap = 0, e_out_cap = 0;
+  unsigned long long *e_zscr = nullptr;  // zstd encode: the waves' sequence lists
+  uint64_t e_zscr_cap = 0;
+  ZeTabs *e_ztab = nullptr;              // zstd encode: predefined FSE tables (uploaded once)
   unsigned long long *e_ends = nullptr, *e_boff = nullptr;
   uint64_t e_ends_cap = 0, e_boff_cap = 0;
   uint8_t *d_v1 = nullptr;
@@ -198,7 +202,7 @@ static void free_all(rio_ctx *c) {
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.cmp, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len,
-                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff};
+                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab};
   for (void *p : ps)
     if (p) hipFree(p);
   if (c->h_ctl) hipHostFree(c->h_ctl);
@@ -1260,6 +1264,22 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
     if (egrow(&c->e_comp, &c->e_comp_cap, comp_total + 64)) return -1;
     ea.comp = c->e_comp;
     launch_deflate(ea, st);
+  } else if (ea.codec == RIO_CODEC_ZSTD) {  // one frame per payload (zstd_enc.hip)
+    launch_zstd_enc_bound(ea, st);
+    launch_chunk_scan(ea.nck, ea.comp_off, d.scan_tmp, nb, st);
+    unsigned long long comp_total = 0;
+    HIP_OK(hipMemcpyAsync(&comp_total, ea.comp_off + nb, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (egrow(&c->e_comp, &c->e_comp_cap, comp_total + 64)) return -1;
+    if (egrow(&c->e_zscr, &c->e_zscr_cap, zstd_enc_scratch_words(c->ncu))) return -1;
+    if (!c->e_ztab) {
+      ZeTabs t;
+      ze_build_tabs(t);
+      if (dalloc(&c->e_ztab, 1)) return -1;
+      HIP_OK(hipMemcpy(c->e_ztab, &t, sizeof(t), hipMemcpyHostToDevice));
+    }
+    ea.comp = c->e_comp;
+    launch_zstd_enc(ea, c->e_ztab, c->e_zscr, c->ncu, st);
   }
   launch_enc_nck(ea, st);
   launch_chunk_scan(ea.nck, ea.ck0, d.scan_tmp, nb, st);
@@ -1288,8 +1308,8 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
 
 static int encode_check(rio_ctx *ctx, const rio_encode_args *a, rio_error *err) {
   if (!ctx || !a) return -1;
-  if (a->codec != RIO_CODEC_NONE && a->codec != RIO_CODEC_FLATE) {
-    rio_set_error(err, RIO_ERR_ARG, 0, "encode: codec %d not supported (none, flate)", a->codec);
+  if (a->codec != RIO_CODEC_NONE && a->codec != RIO_CODEC_FLATE && a->codec != RIO_CODEC_ZSTD) {
+    rio_set_error(err, RIO_ERR_ARG, 0, "encode: codec %d not supported (none, flate, zstd)", a->codec);
     return RIO_ERR_ARG;
   }
   if (a->kind < RIO_BLOCK_BODY || a->kind > RIO_BLOCK_TRAILER) {

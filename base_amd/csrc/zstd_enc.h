@@ -1,0 +1,221 @@
+// zstd frame encoding for the writer's "zstd" transformer (SURVEY.md §8(f) 1:
+// the mirror of recordiozstd's zstdUncompress; the reference compresses with
+// DataDog/zstd v1.4.1 = libzstd's ZSTD_compress, recordiozstd.go:31-52). Any
+// valid zstd frame that libzstd decodes to the payload is a correct "zstd"
+// block; these are the pieces shared by the GPU encoder (zstd_enc.hip) and its
+// host checks:
+//   - FSE compression tables of the three predefined sequence distributions
+//     (RFC 8878 3.1.1.3.2.2; built as libzstd's FSE_buildCTable: the same
+//     symbol spread as the decoder's tables, next states sorted by symbol,
+//     per symbol deltaNbBits / deltaFindState);
+//   - the sequence codes and extra bits (RFC 8878 3.1.1.3.2.1.1, with
+//     libzstd's value-masking: every baseline is aligned to its bit range);
+//   - the sequences' backward bitstream: states initialised from the last
+//     sequence, then for sequences n-2 .. 0 the OF, ML, LL state transitions
+//     and the LL, ML, OF extra bits, the ML, OF, LL final states and the end
+//     mark -- so the decoder, reading from the end, meets the first sequence
+//     first.
+#pragma once
+#include <stdint.h>
+
+#ifndef __HIPCC__
+#define __host__
+#define __device__
+#define __forceinline__ inline
+#endif
+
+namespace rio {
+
+constexpr int kZeLLLog = 6, kZeMLLog = 6, kZeOFLog = 5;
+constexpr int kZeLLSyms = 36, kZeMLSyms = 53, kZeOFSyms = 29;
+// RFC 8878 3.1.1.3.2.2 default distributions
+constexpr int16_t kZeLLNorm[kZeLLSyms] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                          2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+constexpr int16_t kZeMLNorm[kZeMLSyms] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                          1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                          1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+constexpr int16_t kZeOFNorm[kZeOFSyms] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+                                          1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+// FSE compression table of one predefined distribution
+struct ZeFse {
+  uint16_t state[64];  // next state values (tableSize + position), sorted by symbol
+  int32_t dfind[53];   // deltaFindState
+  uint32_t dnb[53];    // deltaNbBits
+  int32_t log;
+};
+struct ZeTabs {
+  ZeFse ll, ml, of;
+};
+
+// FSE_buildCTable for a normalized distribution (host)
+inline void ze_build_fse(const int16_t *norm, int nsym, int log, ZeFse &t) {
+  const int ts = 1 << log;
+  int sym_at[64];
+  int cumul[54];
+  int high = ts - 1;
+  cumul[0] = 0;
+  for (int u = 1; u <= nsym; u++) {
+    if (norm[u - 1] == -1) {  // low-probability symbols take the table's end
+      cumul[u] = cumul[u - 1] + 1;
+      sym_at[high--] = u - 1;
+    } else {
+      cumul[u] = cumul[u - 1] + norm[u - 1];
+    }
+  }
+  const int step = (ts >> 1) + (ts >> 3) + 3, mask = ts - 1;
+  int pos = 0;
+  for (int s = 0; s < nsym; s++)
+    for (int k = 0; k < norm[s]; k++) {
+      sym_at[pos] = s;
+      pos = (pos + step) & mask;
+      while (pos > high) pos = (pos + step) & mask;
+    }
+  for (int u = 0; u < ts; u++) t.state[cumul[sym_at[u]]++] = (uint16_t)(ts + u);
+  int total = 0;
+  for (int s = 0; s < nsym; s++) {
+    const int n = norm[s];
+    if (n == 0) {
+      t.dnb[s] = (uint32_t)(((log + 1) << 16) - ts);
+      t.dfind[s] = 0;
+    } else if (n == -1 || n == 1) {
+      t.dnb[s] = (uint32_t)((log << 16) - ts);
+      t.dfind[s] = total - 1;
+      total++;
+    } else {
+      int hb = 31;
+      while (!((uint32_t)(n - 1) >> hb)) hb--;
+      const int max_out = log - hb;
+      const int min_plus = n << max_out;
+      t.dnb[s] = (uint32_t)((max_out << 16) - min_plus);
+      t.dfind[s] = total - n;
+      total += n;
+    }
+  }
+  for (int s = nsym; s < 53; s++) {
+    t.dnb[s] = 0;
+    t.dfind[s] = 0;
+  }
+  t.log = log;
+}
+
+inline void ze_build_tabs(ZeTabs &t) {
+  ze_build_fse(kZeLLNorm, kZeLLSyms, kZeLLLog, t.ll);
+  ze_build_fse(kZeMLNorm, kZeMLSyms, kZeMLLog, t.ml);
+  ze_build_fse(kZeOFNorm, kZeOFSyms, kZeOFLog, t.of);
+}
+
+__host__ __device__ __forceinline__ uint32_t ze_highbit(uint32_t v) {
+  uint32_t h = 0;
+  while (v >>= 1) h++;
+  return h;
+}
+// literal length -> code (libzstd ZSTD_LLcode)
+__host__ __device__ __forceinline__ uint32_t ze_ll_code(uint32_t ll) {
+  if (ll < 16) return ll;
+  if (ll < 24) return 16 + ((ll - 16) >> 1);
+  if (ll < 32) return 20 + ((ll - 24) >> 2);
+  if (ll < 48) return 22 + ((ll - 32) >> 3);
+  if (ll < 64) return 24;
+  return ze_highbit(ll) + 19;
+}
+// match length - 3 -> code (libzstd ZSTD_MLcode)
+__host__ __device__ __forceinline__ uint32_t ze_ml_code(uint32_t mb) {
+  if (mb < 32) return mb;
+  if (mb < 40) return 32 + ((mb - 32) >> 1);
+  if (mb < 48) return 36 + ((mb - 40) >> 2);
+  if (mb < 64) return 38 + ((mb - 48) >> 3);
+  if (mb < 96) return 40 + ((mb - 64) >> 4);
+  if (mb < 128) return 42;
+  return ze_highbit(mb) + 36;
+}
+// extra bits of a code (= the decoder's kZCodes ... >> 24)
+__host__ __device__ __forceinline__ uint32_t ze_ll_bits(uint32_t c) {
+  return c < 16 ? 0u : (c < 25 ? (uint32_t)(0x433221111ull >> (4 * (c - 16))) & 15u : c - 19);
+}
+__host__ __device__ __forceinline__ uint32_t ze_ml_bits(uint32_t c) {
+  return c < 32 ? 0u : (c < 43 ? (uint32_t)(0x54433221111ull >> (4 * (c - 32))) & 15u : c - 36);
+}
+
+// forward bit writer, bytes out as they complete
+struct ZeBits {
+  uint64_t acc;
+  uint32_t nb;
+  uint8_t *out;
+  uint64_t pos;
+  __host__ __device__ __forceinline__ void add(uint32_t v, uint32_t n) {
+    acc |= (uint64_t)(v & (uint32_t)((1ull << n) - 1)) << nb;
+    nb += n;
+    while (nb >= 8) {
+      out[pos++] = (uint8_t)acc;
+      acc >>= 8;
+      nb -= 8;
+    }
+  }
+  __host__ __device__ __forceinline__ void close() {  // end mark, then the last partial byte
+    add(1, 1);
+    if (nb) out[pos++] = (uint8_t)acc;
+    acc = 0;
+    nb = 0;
+  }
+};
+
+__host__ __device__ __forceinline__ uint32_t ze_init(const ZeFse &t, uint32_t sym) {
+  const uint32_t nbo = (t.dnb[sym] + (1u << 15)) >> 16;
+  const uint32_t v = (nbo << 16) - t.dnb[sym];
+  return t.state[(int32_t)(v >> nbo) + t.dfind[sym]];
+}
+__host__ __device__ __forceinline__ void ze_encode(ZeBits &w, const ZeFse &t, uint32_t &st, uint32_t sym) {
+  const uint32_t nbo = (st + t.dnb[sym]) >> 16;
+  w.add(st, nbo);
+  st = t.state[(int32_t)(st >> nbo) + t.dfind[sym]];
+}
+
+// One sequence: literal length, match length (>= 3), offset (>= 1)
+struct ZeSeq {
+  uint32_t ll, ml, off;
+};
+
+// The sequences section's bitstream of seqs[0..n) (n >= 1) at w.out + w.pos
+template <class GetSeq>
+__host__ __device__ void ze_sequences(ZeBits &w, const ZeTabs &T, uint32_t n, GetSeq get) {
+  ZeSeq q = get(n - 1);
+  uint32_t ofv = q.off + 3, mb = q.ml - 3;
+  uint32_t llc = ze_ll_code(q.ll), mlc = ze_ml_code(mb), ofc = ze_highbit(ofv);
+  uint32_t s_ml = ze_init(T.ml, mlc), s_of = ze_init(T.of, ofc), s_ll = ze_init(T.ll, llc);
+  w.add(q.ll, ze_ll_bits(llc));
+  w.add(mb, ze_ml_bits(mlc));
+  w.add(ofv, ofc);
+  for (uint32_t i = n - 1; i-- > 0;) {
+    q = get(i);
+    ofv = q.off + 3;
+    mb = q.ml - 3;
+    llc = ze_ll_code(q.ll);
+    mlc = ze_ml_code(mb);
+    ofc = ze_highbit(ofv);
+    ze_encode(w, T.of, s_of, ofc);
+    ze_encode(w, T.ml, s_ml, mlc);
+    ze_encode(w, T.ll, s_ll, llc);
+    w.add(q.ll, ze_ll_bits(llc));
+    w.add(mb, ze_ml_bits(mlc));
+    w.add(ofv, ofc);
+  }
+  w.add(s_ml, T.ml.log);
+  w.add(s_of, T.of.log);
+  w.add(s_ll, T.ll.log);
+  w.close();
+}
+
+// frame header: magic, single segment, 8-byte content size, no checksum
+constexpr uint32_t kZeFrameHdr = 13;
+__host__ __device__ __forceinline__ void ze_frame_header(uint8_t *o, uint64_t content) {
+  o[0] = 0x28;
+  o[1] = 0xB5;
+  o[2] = 0x2F;
+  o[3] = 0xFD;
+  o[4] = 0xE0;  // FCS field 8 bytes, Single_Segment_Flag
+  for (int k = 0; k < 8; k++) o[5 + k] = (uint8_t)(content >> (8 * k));
+}
+constexpr uint32_t kZeBlock = 16384;  // block content (more blocks, smaller per-block sequence lists)
+
+}  // namespace rio

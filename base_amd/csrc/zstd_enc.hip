@@ -1,0 +1,357 @@
+// zstd encoder of the writer's "zstd" transformer on the GPU (SURVEY.md §8(f)
+// 1; the reference compresses with DataDog/zstd = libzstd's ZSTD_compress,
+// recordiozstd.go:31-52, and any frame libzstd decodes to the payload is a
+// correct "zstd" block: tests/test_encode_gpu.py decodes these with libzstd,
+// the oracle and the GPU scanner).
+//
+// One wave per recordio block, its payload (varint header + items, the whole
+// of it transformed, writerv2.go:432-441) as one frame (single segment, 8-byte
+// content size, no checksum) of blocks of <= 16 KiB:
+//   - matches as in the DEFLATE encoder (deflate_enc.hip): rounds of 64
+//     positions, a 4,096-entry LDS hash of 4-byte prefixes (lookups, then
+//     inserts), lanes at or after the parse cursor extend their candidate 16
+//     bytes per step, a wave-uniform greedy walk picks the sequences -- here
+//     any distance back in the frame (the window is the frame), lengths up to
+//     the block's end; the walk appends (literal length, match length,
+//     offset) to the wave's scratch list;
+//   - the block: a raw literals section (the runs between matches, copied by
+//     a lane per sequence after wave prefix sums place them), the sequences
+//     section in predefined mode: the FSE bitstream (zstd_enc.h) written by
+//     the wave in step (wave-uniform state, the sequences read back 64 at a
+//     time and taken by readlane), lane 0 storing the bytes;
+//   - a block that does not shrink goes out raw (its compressed attempt's
+//     writes past the raw size are suppressed).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_common.h"
+#include "encode.h"
+#include "rio_internal.h"
+#include "zstd_enc.h"
+
+namespace rio {
+
+constexpr int kZeHashBits = 12;
+constexpr uint32_t kZeNone = 0xffffffffu;
+constexpr int kZeWaves = 4;                      // waves per workgroup (16 KiB of hash each)
+constexpr uint32_t kZeMaxSeq = kZeBlock / 4 + 1;  // sequences per block (matches are >= 4 bytes)
+
+// payload bytes: varint header scratch, then the block's items
+struct ZeSrc {
+  const uint8_t *hdr;
+  unsigned long long hlen;
+  const uint8_t *data;
+  unsigned long long len;
+  __device__ __forceinline__ uint32_t byte(unsigned long long p) const { return p < hlen ? hdr[p] : data[p - hlen]; }
+  // 16 bytes at p (bytes at or past len: 0, never loaded)
+  __device__ __forceinline__ void load16(unsigned long long p, uint32_t (&w)[4]) const {
+    const uint8_t *q = nullptr;
+    if (p + 16 <= len) {
+      if (p + 16 <= hlen) q = hdr + p;
+      else if (p >= hlen) q = data + (p - hlen);
+    }
+    if (q) {
+      const uintptr_t a = (uintptr_t)q;
+      const uint32_t *d = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(a & 3) * 8;
+      if (sh == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) w[k] = d[k];
+      } else {
+        uint32_t e[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) e[k] = d[k];  // the 5th dword holds byte 15: inside the payload
+#pragma unroll
+        for (int k = 0; k < 4; k++) w[k] = (e[k] >> sh) | (e[k + 1] << (32 - sh));
+      }
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t v = 0;
+      for (int j = 0; j < 4; j++)
+        if (p + 4 * k + j < len) v |= byte(p + 4 * k + j) << (8 * j);
+      w[k] = v;
+    }
+  }
+};
+
+__device__ __forceinline__ uint32_t ze_common16(const uint32_t (&a)[4], const uint32_t (&b)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t x = a[k] ^ b[k];
+    if (x) return 4 * k + ((__ffs(x) - 1) >> 3);
+  }
+  return 16;
+}
+
+// bit writer of the wave: every lane keeps the same state, lane 0 stores;
+// bytes at or past lim are not stored (a block that grows goes out raw)
+struct ZeWaveBits {
+  uint64_t acc;
+  uint32_t nb;
+  uint8_t *out;
+  uint64_t pos, lim;
+  bool st;
+  __device__ __forceinline__ void add(uint32_t v, uint32_t n) {
+    acc |= (uint64_t)(v & (uint32_t)((1ull << n) - 1)) << nb;
+    nb += n;
+    while (nb >= 8) {
+      if (st && pos < lim) out[pos] = (uint8_t)acc;
+      pos++;
+      acc >>= 8;
+      nb -= 8;
+    }
+  }
+  __device__ __forceinline__ void close() {
+    add(1, 1);
+    if (nb) {
+      if (st && pos < lim) out[pos] = (uint8_t)acc;
+      pos++;
+    }
+  }
+};
+
+__device__ __forceinline__ void ze_encode_w(ZeWaveBits &w, const ZeFse &t, uint32_t &s, uint32_t sym) {
+  const uint32_t nbo = (s + t.dnb[sym]) >> 16;
+  w.add(s, nbo);
+  s = t.state[(int32_t)(s >> nbo) + t.dfind[sym]];
+}
+
+// the wave's global stores complete (and visible to its other lanes' loads)
+__device__ __forceinline__ void ze_mem_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ ZeSeq ze_unpack(unsigned long long v) {
+  return ZeSeq{(uint32_t)(v & 0xffffu), (uint32_t)((v >> 16) & 0xffffu), (uint32_t)(v >> 32)};
+}
+
+__device__ __forceinline__ ZeSrc zsrc_of(const EncArgs &a, uint64_t b) {
+  ZeSrc s;
+  const uint64_t f0 = b * a.per_block;
+  const uint64_t f = f0 < a.n_items ? f0 : a.n_items;
+  s.hdr = a.hdr + a.hdr_off[b];
+  s.hlen = a.hdr_len[b];
+  s.data = a.data + (f == 0 ? 0ull : a.item_end[f - 1]);
+  s.len = a.pay_len[b];
+  return s;
+}
+
+__global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeTabs *__restrict__ T,
+                                                          unsigned long long *__restrict__ scratch) {
+  __shared__ uint32_t s_hash[kZeWaves][1 << kZeHashBits];
+  const int wv = threadIdx.x >> 6;
+  uint32_t *hash = s_hash[wv];
+  const int l = lane_id();
+  const uint64_t wave = (uint64_t)blockIdx.x * kZeWaves + wv;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kZeWaves;
+  unsigned long long *seq = scratch + wave * kZeMaxSeq;
+  for (uint64_t b = wave; b < a.nblocks; b += nwaves) {
+    const ZeSrc s = zsrc_of(a, b);
+    const unsigned long long L = s.len;
+    uint8_t *out = a.comp + a.comp_off[b];
+    for (int i = l; i < (1 << kZeHashBits); i += 64) hash[i] = kZeNone;
+    wave_lds_sync();
+    if (l == 0) ze_frame_header(out, L);
+    unsigned long long o = kZeFrameHdr;
+    if (L == 0 && l == 0) {  // one empty raw block
+      out[o] = 1;
+      out[o + 1] = 0;
+      out[o + 2] = 0;
+    }
+    if (L == 0) o += 3;
+    for (unsigned long long b0 = 0; b0 < L; b0 += kZeBlock) {
+      const unsigned long long b1 = L - b0 < kZeBlock ? L : b0 + kZeBlock;
+      const uint32_t bsz = (uint32_t)(b1 - b0);
+      // ---- matches: rounds of 64 positions, greedy walk from the cursor
+      uint32_t nseq = 0;
+      unsigned long long cur = b0, lit_start = b0;
+      uint32_t nx[4];
+      s.load16(b0 + l, nx);
+      for (unsigned long long base = b0; base < b1; base += 64) {
+        const unsigned long long p = base + l;
+        uint32_t cw[4] = {nx[0], nx[1], nx[2], nx[3]};
+        if (base + 64 < b1) s.load16(p + 64, nx);
+        const bool has4 = p + 4 <= b1;
+        const uint32_t h = (cw[0] * 0x9E3779B1u) >> (32 - kZeHashBits);
+        const uint32_t cand = has4 ? hash[h] : kZeNone;
+        wave_lds_sync();
+        if (has4) hash[h] = (uint32_t)p;  // (payloads < 4 GiB: checked by the host)
+        uint32_t m = 0;
+        if (has4 && p >= cur && cand != kZeNone) {
+          const uint32_t maxm = (uint32_t)(b1 - p);
+          uint32_t cc[4];
+          s.load16(cand, cc);
+          m = ze_common16(cc, cw);
+          while (m == 16 * ((m + 15) / 16) && m > 0 && m < maxm) {  // all equal so far
+            uint32_t a16[4], b16[4];
+            s.load16(cand + m, a16);
+            s.load16(p + m, b16);
+            const uint32_t k = ze_common16(a16, b16);
+            m += k;
+            if (k < 16) break;
+          }
+          if (m > maxm) m = maxm;
+          if (m < 4) m = 0;
+        }
+        unsigned long long pos = cur;
+        const unsigned long long rend = base + 64 < b1 ? base + 64 : b1;
+        while (pos < rend) {
+          const uint32_t lane = (uint32_t)(pos - base);
+          const uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)m, (int)lane);
+          if (ml >= 4) {
+            const uint32_t cd = (uint32_t)__builtin_amdgcn_readlane((int)cand, (int)lane);
+            if (l == 0)
+              seq[nseq] = (unsigned long long)(pos - lit_start) | ((unsigned long long)ml << 16) |
+                          ((unsigned long long)(uint32_t)(pos - cd) << 32);
+            nseq++;
+            pos += ml;
+            lit_start = pos;
+          } else {
+            pos++;
+          }
+        }
+        cur = pos;
+      }
+      // ---- the block: header placeholder, raw literals, sequences
+      const unsigned long long bh = o, lim = bh + 3 + bsz + 16;
+      unsigned long long q = bh + 3;
+      ze_mem_sync();  // the list's stores (lane 0) visible to every lane's loads
+      unsigned long long nlit = 0;
+      {  // literal count: the block minus its matches
+        unsigned long long msum = 0;
+        for (uint32_t g = 0; g < nseq; g += 64) {
+          const uint32_t i = g + (uint32_t)l;
+          const ZeSeq z = i < nseq ? ze_unpack(seq[i]) : ZeSeq{0, 0, 0};
+          msum += wave_sum<unsigned long long>(z.ml);
+        }
+        nlit = bsz - msum;
+      }
+      if (l == 0) {
+        out[q] = (uint8_t)(0 | (3 << 2) | ((nlit & 15) << 4));  // Raw_Literals_Block, 20-bit size
+        out[q + 1] = (uint8_t)(nlit >> 4);
+        out[q + 2] = (uint8_t)(nlit >> 12);
+      }
+      q += 3;
+      {  // the runs before every match (lane per sequence), then the tail
+        unsigned long long src0 = b0, dst0 = q;
+        for (uint32_t g = 0; g < nseq; g += 64) {
+          const uint32_t i = g + (uint32_t)l;
+          const ZeSeq z = i < nseq ? ze_unpack(seq[i]) : ZeSeq{0, 0, 0};
+          const uint32_t lin = wave_incl_sum_dpp(z.ll), tin = wave_incl_sum_dpp(z.ll + z.ml);
+          const unsigned long long sp = src0 + (tin - z.ll - z.ml), dp = dst0 + (lin - z.ll);
+          for (uint32_t k = 0; k < z.ll; k++) out[dp + k] = (uint8_t)s.byte(sp + k);
+          src0 += (uint32_t)__builtin_amdgcn_readlane((int)tin, 63);
+          dst0 += (uint32_t)__builtin_amdgcn_readlane((int)lin, 63);
+        }
+        for (unsigned long long k = l; src0 + k < b1; k += 64) out[dst0 + k] = (uint8_t)s.byte(src0 + k);
+      }
+      q += nlit;
+      if (l == 0) {  // Number_of_Sequences, then the compression modes (all predefined)
+        if (nseq < 128) {
+          out[q] = (uint8_t)nseq;
+        } else if (nseq < 0x7F00) {
+          out[q] = (uint8_t)((nseq >> 8) + 0x80);
+          out[q + 1] = (uint8_t)nseq;
+        } else {
+          out[q] = 0xFF;
+          out[q + 1] = (uint8_t)(nseq - 0x7F00);
+          out[q + 2] = (uint8_t)((nseq - 0x7F00) >> 8);
+        }
+        if (nseq) out[q + (nseq < 128 ? 1 : nseq < 0x7F00 ? 2 : 3)] = 0;
+      }
+      q += (nseq < 128 ? 1 : nseq < 0x7F00 ? 2 : 3) + (nseq ? 1 : 0);
+      if (nseq) {  // the FSE bitstream, the wave in step, sequences from the last
+        ZeWaveBits w{0, 0, out, q, lim, l == 0};
+        uint32_t chunk = ~0u;
+        unsigned long long v = 0;
+        auto get = [&](uint32_t i) -> ZeSeq {
+          if ((i >> 6) != chunk) {
+            chunk = i >> 6;
+            const uint32_t k = (chunk << 6) + (uint32_t)l;
+            v = k < nseq ? seq[k] : 0ull;
+          }
+          const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)(i & 63));
+          const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)(i & 63));
+          return ze_unpack(((unsigned long long)hi << 32) | lo);
+        };
+        ZeSeq z = get(nseq - 1);
+        uint32_t ofv = z.off + 3, mb = z.ml - 3;
+        uint32_t llc = ze_ll_code(z.ll), mlc = ze_ml_code(mb), ofc = ze_highbit(ofv);
+        uint32_t s_ml = ze_init(T->ml, mlc), s_of = ze_init(T->of, ofc), s_ll = ze_init(T->ll, llc);
+        w.add(z.ll, ze_ll_bits(llc));
+        w.add(mb, ze_ml_bits(mlc));
+        w.add(ofv, ofc);
+        for (uint32_t i = nseq - 1; i-- > 0;) {
+          z = get(i);
+          ofv = z.off + 3;
+          mb = z.ml - 3;
+          llc = ze_ll_code(z.ll);
+          mlc = ze_ml_code(mb);
+          ofc = ze_highbit(ofv);
+          ze_encode_w(w, T->of, s_of, ofc);
+          ze_encode_w(w, T->ml, s_ml, mlc);
+          ze_encode_w(w, T->ll, s_ll, llc);
+          w.add(z.ll, ze_ll_bits(llc));
+          w.add(mb, ze_ml_bits(mlc));
+          w.add(ofv, ofc);
+        }
+        w.add(s_ml, (uint32_t)T->ml.log);
+        w.add(s_of, (uint32_t)T->of.log);
+        w.add(s_ll, (uint32_t)T->ll.log);
+        w.close();
+        q = w.pos;
+      }
+      const bool last = b1 >= L;
+      const unsigned long long csz = q - (bh + 3);
+      uint32_t bhv;
+      if (csz >= bsz) {  // raw block
+        for (uint32_t k = l; k < bsz; k += 64) out[bh + 3 + k] = (uint8_t)s.byte(b0 + k);
+        bhv = (last ? 1u : 0u) | (0u << 1) | (bsz << 3);
+        o = bh + 3 + bsz;
+      } else {
+        bhv = (last ? 1u : 0u) | (2u << 1) | ((uint32_t)csz << 3);
+        o = q;
+      }
+      if (l == 0) {
+        out[bh] = (uint8_t)bhv;
+        out[bh + 1] = (uint8_t)(bhv >> 8);
+        out[bh + 2] = (uint8_t)(bhv >> 16);
+      }
+      wave_lds_sync();
+    }
+    if (l == 0) a.pay_len[b] = o;
+  }
+}
+
+// per block: the frame's bound (into nck, scanned into comp_off)
+__global__ void k_zstd_enc_bound(EncArgs a) {
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < a.nblocks;
+       b += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long L = a.pay_len[b];
+    const unsigned long long nblk = L / kZeBlock + 1;
+    a.nck[b] = (kZeFrameHdr + L + 19 * nblk + 64 + 15) & ~15ull;
+  }
+}
+
+void launch_zstd_enc_bound(const EncArgs &a, hipStream_t st) {
+  uint64_t g = (a.nblocks + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(k_zstd_enc_bound, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, a);
+}
+
+static uint64_t zstd_enc_grid(int ncu) { return (uint64_t)(ncu > 0 ? ncu : 256) * 2; }  // 2 workgroups per CU (LDS)
+
+uint64_t zstd_enc_scratch_words(int ncu) { return zstd_enc_grid(ncu) * kZeWaves * kZeMaxSeq; }
+
+void launch_zstd_enc(const EncArgs &a, const ZeTabs *tabs, unsigned long long *scratch, int ncu, hipStream_t st) {
+  uint64_t g = (a.nblocks + kZeWaves - 1) / kZeWaves;
+  const uint64_t cap = zstd_enc_grid(ncu);
+  if (g > cap) g = cap;
+  hipLaunchKernelGGL(k_zstd_enc, dim3((unsigned)(g ? g : 1)), dim3(64 * kZeWaves), 0, st, a, tabs, scratch);
+}
+
+}  // namespace rio

@@ -3,8 +3,9 @@ the block serialisation, chunk framing and CRC32 on the GPU (rio_encode,
 SURVEY.md §8(f) 1).
 
 Same state machine, header order and bytes as the reference for the none
-transformer; "flate" blocks are valid DEFLATE streams of the same payloads
-(GPU-encoded, deflate_enc.hip), so they decode to the same records. The reference serialises each block on a goroutine as it fills
+transformer; "flate" blocks are valid DEFLATE streams and "zstd" blocks valid
+zstd frames of the same payloads (GPU-encoded, deflate_enc.hip / zstd_enc.hip),
+so they decode to the same records. The reference serialises each block on a goroutine as it fills
 (MaxItems + 1 items, writerv2.go:315, 366-368) and writes blocks in sequence;
 here the items between two block-ending calls (Flush, SetTrailer, Finish) are
 kept and encoded by one rio_encode call -- once a run holds `batch_bytes`, its
@@ -32,13 +33,15 @@ class GpuWriter:
         if opts.MaxItems == 0:
             opts.MaxItems = F.DEFAULT_PACKED_ITEMS
         opts.MaxItems = min(opts.MaxItems, F.MAX_PACKED_ITEMS)
-        # transformers: none, or one "flate" / "flate N" (recordioflate.go:31-52)
+        # transformers: none, or one "flate" / "flate N" (recordioflate.go:31-52) or
+        # "zstd" / "zstd N" (recordiozstd.go:31-52)
         self.codec, self.level = gpu.RIO_CODEC_NONE, 0
         if opts.Transformers:
             name, _, arg = opts.Transformers[0].partition(" ")
-            if len(opts.Transformers) != 1 or name != "flate":
-                raise ValueError("GpuWriter encodes none or one flate transformer (got %r)" % (opts.Transformers,))
-            self.codec = gpu.RIO_CODEC_FLATE
+            if len(opts.Transformers) != 1 or name not in ("flate", "zstd"):
+                raise ValueError("GpuWriter encodes none or one flate / zstd transformer (got %r)"
+                                 % (opts.Transformers,))
+            self.codec = gpu.RIO_CODEC_FLATE if name == "flate" else gpu.RIO_CODEC_ZSTD
             self.level = int(arg) if arg.strip() else -1
         self.opts = opts
         self.out = out

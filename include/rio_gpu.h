@@ -233,7 +233,10 @@ typedef struct rio_encode_args {
     uint64_t items_per_block;  /* MaxItems + 1; 0 = 16385 */
     int32_t codec;             /* RIO_CODEC_NONE, or RIO_CODEC_FLATE: a raw DEFLATE stream per
                                   block ("flate N" transformer, recordioflate.go:31-52; any valid
-                                  stream decodes alike -- the bytes are not klauspost's) */
+                                  stream decodes alike -- the bytes are not klauspost's), or
+                                  RIO_CODEC_ZSTD: one zstd frame per block ("zstd N",
+                                  recordiozstd.go:31-52; raw literals, predefined sequence
+                                  codes, <= 16 KiB blocks -- decoded by libzstd alike) */
     int32_t kind;              /* enum rio_block_kind */
     int32_t level;             /* flate: 0 stored blocks (NoCompression), otherwise one
                                   fixed-Huffman block with greedy hash-chain matches */

@@ -168,3 +168,51 @@ def test_encode_flate_decodes(gpu_ctx, oracle):
         k += 1
     assert k == 5
     assert comp < 0.75 * plain, (comp, plain)  # fixed Huffman + greedy matches on FASTQ-like text
+
+
+@pytest.mark.gpu
+def test_encode_zstd_decodes(gpu_ctx, oracle):
+    """zstd blocks from the GPU encoder (one frame per block payload: raw
+    literals, predefined sequence codes, <= 16 KiB blocks, raw blocks where
+    they do not shrink) decode -- GPU scanner, the oracle's libzstd-semantics
+    decoder, libzstd itself (the library DataDog/zstd wraps) -- to the records
+    written; text compresses."""
+    from base_amd.recordio import gpu
+    from base_amd.recordio.codecs import have_zstd, zstd_decompress_ref
+    from conftest import oracle_has_zstd
+    if not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    rng = random.Random(6)
+    sets = [fastq_records(rng, 3000), records(rng, 300), [b""] * 50, [b"x" * 100000] * 3,
+            [bytes([i % 7]) * rng.randrange(0, 600) for i in range(2000)], [rng.randbytes(70000)]]
+    for tr in ("zstd", "zstd 5"):
+        for i, recs in enumerate(sets):
+            data = gpu_write(recs, WriterOpts(Transformers=[tr], MaxItems=rng.choice([1, 50, 1000])),
+                             trailer=b"trail" * 3, ctx=gpu_ctx, batch_bytes=1 << 18)
+            ref = oracle.scan(data)
+            assert ref.err == "" and ref.items == recs and ref.trailer == b"trail" * 3, (tr, i)
+            sc = gpu.NewScanner(data, ctx=gpu_ctx)
+            got = []
+            while sc.Scan():
+                got.append(sc.Get())
+            assert sc.Finish() is None and got == recs, (tr, i)
+    if not have_zstd():
+        return
+    # every block's payload is a zstd frame libzstd decodes to the packed payload
+    recs = fastq_records(rng, 800)
+    data = gpu_write(recs, WriterOpts(Transformers=["zstd"], MaxItems=199), ctx=gpu_ctx)
+    off, k, comp, plain = 32768, 0, 0, 0
+    while off < len(data):
+        total = int.from_bytes(data[off + 20:off + 24], "little")
+        pay = b"".join(data[off + c * 32768 + 28: off + c * 32768 + 28 +
+                            int.from_bytes(data[off + c * 32768 + 16:off + c * 32768 + 20], "little")]
+                       for c in range(total))
+        blk = recs[k * 200:(k + 1) * 200]
+        want = F.packed_block_payload(blk)
+        assert zstd_decompress_ref(pay, len(want) + 1) == want
+        comp += len(pay)
+        plain += len(want)
+        off += total * 32768
+        k += 1
+    assert k == 4
+    assert comp < 0.75 * plain, (comp, plain)

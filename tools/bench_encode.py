@@ -2,7 +2,8 @@
 (1e6 x 256 B, 253 per block) replicated R times device-resident, encoded by
 rio_encode_device into a chunk stream (packed headers, framing, padding,
 CRC32), then scanned back by rio_scan_device as the parity check (item count,
-and the first replica's views against the records). Prints one JSON line."""
+and the first replica's views against the records). --codec 1 / 2: the C3
+FASTQ-like records through the GPU flate / zstd encoders. Prints one JSON line."""
 import argparse
 import ctypes
 import json
@@ -18,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--replicas", type=int, default=32)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--codec", type=int, default=0)  # 0 none (C2 records), 1 flate (C3 records)
+    ap.add_argument("--codec", type=int, default=0)  # 0 none (C2 records), 1 flate / 2 zstd (C3 records)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -32,7 +33,7 @@ def main():
         data = torch.from_numpy(np.ascontiguousarray(recs).reshape(-1)).cuda().repeat(R)
         ends = (torch.arange(1, n + 1, dtype=torch.int64, device="cuda") * 256)
         per = 253
-    else:  # C3: FASTQ-like records (tools/c3_data.py), 1,024 per block, flate
+    else:  # C3: FASTQ-like records (tools/c3_data.py), 1,024 per block, flate or zstd
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import c3_data
         recs = c3_data.records(0, 1 << 17)
