@@ -105,11 +105,7 @@ inline void ze_build_tabs(ZeTabs &t) {
   ze_build_fse(kZeOFNorm, kZeOFSyms, kZeOFLog, t.of);
 }
 
-__host__ __device__ __forceinline__ uint32_t ze_highbit(uint32_t v) {
-  uint32_t h = 0;
-  while (v >>= 1) h++;
-  return h;
-}
+__host__ __device__ __forceinline__ uint32_t ze_highbit(uint32_t v) { return v ? 31u - (uint32_t)__builtin_clz(v) : 0u; }
 // literal length -> code (libzstd ZSTD_LLcode)
 __host__ __device__ __forceinline__ uint32_t ze_ll_code(uint32_t ll) {
   if (ll < 16) return ll;

@@ -17,8 +17,9 @@
 //   - the block: a raw literals section (the runs between matches, copied by
 //     a lane per sequence after wave prefix sums place them), the sequences
 //     section in predefined mode: the FSE bitstream (zstd_enc.h) written by
-//     the wave in step (wave-uniform state, the sequences read back 64 at a
-//     time and taken by readlane), lane 0 storing the bytes;
+//     the wave in step (wave-uniform state, the three tables spread over the
+//     lanes and the sequences read back 64 at a time, both taken by
+//     readlane), lane 0 storing the bytes;
 //   - a block that does not shrink goes out raw (its compressed attempt's
 //     writes past the raw size are suppressed).
 #include <hip/hip_runtime.h>
@@ -93,30 +94,61 @@ struct ZeWaveBits {
   uint8_t *out;
   uint64_t pos, lim;
   bool st;
-  __device__ __forceinline__ void add(uint32_t v, uint32_t n) {
+  __device__ __forceinline__ void put(uint32_t byte) {
+    if (st && pos < lim) out[pos] = (uint8_t)byte;
+    pos++;
+  }
+  __device__ __forceinline__ void add(uint32_t v, uint32_t n) {  // n <= 31
     acc |= (uint64_t)(v & (uint32_t)((1ull << n) - 1)) << nb;
     nb += n;
-    while (nb >= 8) {
-      if (st && pos < lim) out[pos] = (uint8_t)acc;
-      pos++;
-      acc >>= 8;
-      nb -= 8;
+    if (nb >= 32) {  // a whole dword out (nb < 63 before)
+      const uint32_t x = (uint32_t)acc;
+      put(x);
+      put(x >> 8);
+      put(x >> 16);
+      put(x >> 24);
+      acc >>= 32;
+      nb -= 32;
     }
   }
   __device__ __forceinline__ void close() {
     add(1, 1);
-    if (nb) {
-      if (st && pos < lim) out[pos] = (uint8_t)acc;
-      pos++;
+    while (nb > 0) {
+      put((uint32_t)acc);
+      acc >>= 8;
+      nb = nb > 8 ? nb - 8 : 0;
     }
   }
 };
 
-__device__ __forceinline__ void ze_encode_w(ZeWaveBits &w, const ZeFse &t, uint32_t &s, uint32_t sym) {
-  const uint32_t nbo = (s + t.dnb[sym]) >> 16;
-  w.add(s, nbo);
-  s = t.state[(int32_t)(s >> nbo) + t.dfind[sym]];
-}
+// One FSE table held across the wave's lanes (entry k in lane k): the encoder's
+// state is wave-uniform, so every lookup is a readlane -- no memory latency in
+// the serial chain
+struct ZeLaneFse {
+  uint32_t state, dnb;
+  int32_t dfind;
+  int32_t log;
+  __device__ __forceinline__ void load(const ZeFse &t, int l) {
+    state = l < (1 << t.log) ? t.state[l] : 0u;
+    dnb = l < 53 ? t.dnb[l] : 0u;
+    dfind = l < 53 ? t.dfind[l] : 0;
+    log = t.log;
+  }
+  __device__ __forceinline__ uint32_t rd(uint32_t v, uint32_t k) const {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k);
+  }
+  __device__ __forceinline__ uint32_t init(uint32_t sym) const {
+    const uint32_t d = rd(dnb, sym);
+    const uint32_t nbo = (d + (1u << 15)) >> 16;
+    const uint32_t v = (nbo << 16) - d;
+    return rd(state, (uint32_t)((int32_t)(v >> nbo) + (int32_t)rd((uint32_t)dfind, sym)));
+  }
+  __device__ __forceinline__ void encode(ZeWaveBits &w, uint32_t &s, uint32_t sym) const {
+    const uint32_t nbo = (s + rd(dnb, sym)) >> 16;
+    w.add(s, nbo);
+    s = rd(state, (uint32_t)((int32_t)(s >> nbo) + (int32_t)rd((uint32_t)dfind, sym)));
+  }
+};
 
 // the wave's global stores complete (and visible to its other lanes' loads)
 __device__ __forceinline__ void ze_mem_sync() {
@@ -149,6 +181,10 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
   const uint64_t wave = (uint64_t)blockIdx.x * kZeWaves + wv;
   const uint64_t nwaves = (uint64_t)gridDim.x * kZeWaves;
   unsigned long long *seq = scratch + wave * kZeMaxSeq;
+  ZeLaneFse f_ll, f_ml, f_of;
+  f_ll.load(T->ll, l);
+  f_ml.load(T->ml, l);
+  f_of.load(T->of, l);
   for (uint64_t b = wave; b < a.nblocks; b += nwaves) {
     const ZeSrc s = zsrc_of(a, b);
     const unsigned long long L = s.len;
@@ -243,7 +279,13 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
           const ZeSeq z = i < nseq ? ze_unpack(seq[i]) : ZeSeq{0, 0, 0};
           const uint32_t lin = wave_incl_sum_dpp(z.ll), tin = wave_incl_sum_dpp(z.ll + z.ml);
           const unsigned long long sp = src0 + (tin - z.ll - z.ml), dp = dst0 + (lin - z.ll);
-          for (uint32_t k = 0; k < z.ll; k++) out[dp + k] = (uint8_t)s.byte(sp + k);
+          for (uint32_t k = 0; k < z.ll; k += 16) {  // 16 source bytes per load round
+            uint32_t w16[4];
+            s.load16(sp + k, w16);
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+              if (k + j < z.ll) out[dp + k + j] = (uint8_t)(w16[j >> 2] >> (8 * (j & 3)));
+          }
           src0 += (uint32_t)__builtin_amdgcn_readlane((int)tin, 63);
           dst0 += (uint32_t)__builtin_amdgcn_readlane((int)lin, 63);
         }
@@ -281,7 +323,7 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
         ZeSeq z = get(nseq - 1);
         uint32_t ofv = z.off + 3, mb = z.ml - 3;
         uint32_t llc = ze_ll_code(z.ll), mlc = ze_ml_code(mb), ofc = ze_highbit(ofv);
-        uint32_t s_ml = ze_init(T->ml, mlc), s_of = ze_init(T->of, ofc), s_ll = ze_init(T->ll, llc);
+        uint32_t s_ml = f_ml.init(mlc), s_of = f_of.init(ofc), s_ll = f_ll.init(llc);
         w.add(z.ll, ze_ll_bits(llc));
         w.add(mb, ze_ml_bits(mlc));
         w.add(ofv, ofc);
@@ -292,16 +334,16 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
           llc = ze_ll_code(z.ll);
           mlc = ze_ml_code(mb);
           ofc = ze_highbit(ofv);
-          ze_encode_w(w, T->of, s_of, ofc);
-          ze_encode_w(w, T->ml, s_ml, mlc);
-          ze_encode_w(w, T->ll, s_ll, llc);
+          f_of.encode(w, s_of, ofc);
+          f_ml.encode(w, s_ml, mlc);
+          f_ll.encode(w, s_ll, llc);
           w.add(z.ll, ze_ll_bits(llc));
           w.add(mb, ze_ml_bits(mlc));
           w.add(ofv, ofc);
         }
-        w.add(s_ml, (uint32_t)T->ml.log);
-        w.add(s_of, (uint32_t)T->of.log);
-        w.add(s_ll, (uint32_t)T->ll.log);
+        w.add(s_ml, (uint32_t)f_ml.log);
+        w.add(s_of, (uint32_t)f_of.log);
+        w.add(s_ll, (uint32_t)f_ll.log);
         w.close();
         q = w.pos;
       }
