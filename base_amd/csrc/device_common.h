@@ -7,6 +7,10 @@
 
 #include "rio_internal.h"
 
+#ifndef RIO_VIEW_NT
+#define RIO_VIEW_NT 0
+#endif
+
 namespace rio {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -507,6 +511,16 @@ __device__ __forceinline__ void straddler_from_regs(const uint32_t (&bnd)[4], ui
   }
 }
 
+// item view stores of the fast path: written once, read by the caller (not
+// by this pass) -- RIO_VIEW_NT builds stream them past the caches
+__device__ __forceinline__ void view_store(unsigned long long *p, unsigned long long v) {
+#if RIO_VIEW_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 template <bool kBnd>
 __device__ __forceinline__ int small_header(const Payload &pl, const ParseOut &po, const uint8_t *lwin,
                                             const uint16_t *ltpos, uint32_t nitems, uint32_t hdr,
@@ -563,15 +577,15 @@ __device__ __forceinline__ int small_header(const Payload &pl, const ParseOut &p
     if (o <= nitems) {
       const uint64_t slot = po.item_base + (o - 1);
       if (slot < po.item_cap) {
-        po.item_len[slot] = vk;
+        view_store(po.item_len + slot, vk);
         if (pl.contig) {
-          po.item_off[slot] = po.view_base + sk;
+          view_store(po.item_off + slot, po.view_base + sk);
         } else {
           const uint32_t j = sk / (uint32_t)kMaxPayload;
           phys = (pl.c0 + j) * (unsigned long long)kChunk + kChunkHdr + (sk - j * (uint32_t)kMaxPayload);
           sd = chunks && vk > 0 && j != (sk + vk - 1) / (uint32_t)kMaxPayload;
           if (sd && sparse_side) {
-            po.item_off[slot] = kItemInRecords | phys;
+            view_store(po.item_off + slot, kItemInRecords | phys);
           } else if (sd) {
             StradDesc dsc;
             dsc.c0 = pl.c0;
@@ -581,7 +595,7 @@ __device__ __forceinline__ int small_header(const Payload &pl, const ParseOut &p
             po.strad[pl.c0 + j] = dsc;
             po.ssz[pl.c0 + j] = pad16(vk);
           } else {
-            po.item_off[slot] = (vk == 0 && sk >= plen) ? 0ull : phys;
+            view_store(po.item_off + slot, (vk == 0 && sk >= plen) ? 0ull : phys);
           }
         }
       } else {

@@ -202,6 +202,124 @@ __host__ __device__ void ze_sequences(ZeBits &w, const ZeTabs &T, uint32_t n, Ge
   w.close();
 }
 
+// ---- Huffman-coded literals (RFC 8878 3.1.1.3.1, 4.2.1; libzstd HUF_*)
+constexpr uint32_t kZeHufMax = 11;  // the format allows 11-bit codes
+
+// Code lengths (<= kZeHufMax) of a complete prefix code for the symbols with
+// cnt > 0 (>= 2 of them, all < 256): Huffman by repeated minimum pairs, then
+// lengths clamped to kZeHufMax and the Kraft sum brought back to exactly 1
+// (the decoder deduces the last symbol's weight from it). len[s] = 0 for
+// absent symbols. Serial (one lane); parent/work arrays of 512 entries.
+__host__ __device__ inline void ze_huf_lengths(const uint32_t *cnt, uint32_t nsym, uint8_t *len, uint32_t *w,
+                                               uint16_t *parent) {
+  // nodes 0..nsym-1 leaves, nsym.. internal; w = weight (~0: consumed)
+  uint32_t n = nsym;
+  for (uint32_t s = 0; s < nsym; s++) w[s] = cnt[s] ? cnt[s] : 0xffffffffu;
+  uint32_t live = 0;
+  for (uint32_t s = 0; s < nsym; s++) live += cnt[s] ? 1 : 0;
+  while (live > 1) {
+    uint32_t a = 0xffffffffu, b = 0xffffffffu;
+    for (uint32_t k = 0; k < n; k++) {
+      if (w[k] == 0xffffffffu) continue;
+      if (a == 0xffffffffu || w[k] < w[a]) {
+        b = a;
+        a = k;
+      } else if (b == 0xffffffffu || w[k] < w[b]) {
+        b = k;
+      }
+    }
+    w[n] = w[a] + w[b];
+    parent[a] = (uint16_t)n;
+    parent[b] = (uint16_t)n;
+    w[a] = w[b] = 0xffffffffu;
+    n++;
+    live--;
+  }
+  const uint32_t root = n - 1;
+  for (uint32_t s = 0; s < nsym; s++) {
+    uint32_t d = 0;
+    if (cnt[s]) {
+      for (uint32_t k = s; k != root; k = parent[k]) d++;
+    }
+    len[s] = (uint8_t)(d > kZeHufMax ? kZeHufMax : d);
+  }
+  // Kraft sum in units of 2^-kZeHufMax: make it exactly 2^kZeHufMax
+  uint32_t kraft = 0;
+  for (uint32_t s = 0; s < nsym; s++)
+    if (len[s]) kraft += 1u << (kZeHufMax - len[s]);
+  while (kraft > (1u << kZeHufMax)) {  // lengthen the longest code below the cap
+    uint32_t best = 0xffffffffu;
+    for (uint32_t s = 0; s < nsym; s++)
+      if (len[s] && len[s] < kZeHufMax && (best == 0xffffffffu || len[s] > len[best] ||
+                                          (len[s] == len[best] && cnt[s] < cnt[best])))
+        best = s;
+    kraft -= 1u << (kZeHufMax - len[best] - 1);
+    len[best]++;
+  }
+  while (kraft < (1u << kZeHufMax)) {  // shorten the longest code that still fits
+    uint32_t best = 0xffffffffu;
+    for (uint32_t s = 0; s < nsym; s++)
+      if (len[s] > 1 && kraft + (1u << (kZeHufMax - len[s])) <= (1u << kZeHufMax) &&
+          (best == 0xffffffffu || len[s] > len[best] || (len[s] == len[best] && cnt[s] > cnt[best])))
+        best = s;
+    kraft += 1u << (kZeHufMax - len[best]);
+    len[best]--;
+  }
+}
+
+// canonical code values of HUF_buildCTable: longest codes first from 0, each
+// shorter rank starting at (previous start + count) / 2, symbols ascending
+__host__ __device__ inline uint32_t ze_huf_codes(const uint8_t *len, uint32_t nsym, uint16_t *val) {
+  uint32_t maxb = 0;
+  uint16_t nper[kZeHufMax + 2] = {0}, vper[kZeHufMax + 2] = {0};
+  for (uint32_t s = 0; s < nsym; s++) {
+    nper[len[s]]++;
+    if (len[s] > maxb) maxb = len[s];
+  }
+  uint32_t mn = 0;
+  for (uint32_t b = maxb; b > 0; b--) {
+    vper[b] = (uint16_t)mn;
+    mn += nper[b];
+    mn >>= 1;
+  }
+  for (uint32_t s = 0; s < nsym; s++) val[s] = len[s] ? vper[len[s]]++ : 0;
+  return maxb;
+}
+
+// the tree description, direct representation (max symbol <= 128): header
+// byte 127 + N, then the 4-bit weights of symbols 0..N-1 (the last symbol's
+// is deduced); weight = maxb + 1 - len. Returns the bytes written.
+__host__ __device__ inline uint32_t ze_huf_weights(const uint8_t *len, uint32_t last, uint32_t maxb, uint8_t *o) {
+  o[0] = (uint8_t)(127 + last);
+  for (uint32_t s = 0; s < last; s += 2) {
+    const uint32_t w0 = len[s] ? maxb + 1 - len[s] : 0;
+    const uint32_t w1 = (s + 1 < last && len[s + 1]) ? maxb + 1 - len[s + 1] : 0;
+    o[1 + s / 2] = (uint8_t)((w0 << 4) | w1);
+  }
+  return 1 + (last + 1) / 2;
+}
+
+// Compressed_Literals_Block header (4 streams): the smallest size format that
+// holds both sizes; returns its bytes (3, 4 or 5)
+__host__ __device__ inline uint32_t ze_lit_header(uint8_t *o, uint32_t regen, uint32_t comp) {
+  uint64_t v;
+  uint32_t n;
+  if (regen <= 1023 && comp <= 1023) {
+    v = 2u | (1u << 2) | ((uint64_t)regen << 4) | ((uint64_t)comp << 14);
+    n = 3;
+  } else if (regen <= 16383 && comp <= 16383) {
+    v = 2u | (2u << 2) | ((uint64_t)regen << 4) | ((uint64_t)comp << 18);
+    n = 4;
+  } else {
+    v = 2u | (3u << 2) | ((uint64_t)regen << 4) | ((uint64_t)comp << 22);
+    n = 5;
+  }
+  for (uint32_t k = 0; k < n; k++) o[k] = (uint8_t)(v >> (8 * k));
+  return n;
+}
+// the 4 streams' symbol ranges: (n + 3) / 4 each, the last the rest
+__host__ __device__ __forceinline__ uint32_t ze_seg(uint32_t n) { return (n + 3) / 4; }
+
 // frame header: magic, single segment, 8-byte content size, no checksum
 constexpr uint32_t kZeFrameHdr = 13;
 __host__ __device__ __forceinline__ void ze_frame_header(uint8_t *o, uint64_t content) {

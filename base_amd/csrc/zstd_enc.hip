@@ -36,6 +36,8 @@ constexpr int kZeHashBits = 12;
 constexpr uint32_t kZeNone = 0xffffffffu;
 constexpr int kZeWaves = 4;                      // waves per workgroup (16 KiB of hash each)
 constexpr uint32_t kZeMaxSeq = kZeBlock / 4 + 1;  // sequences per block (matches are >= 4 bytes)
+constexpr uint32_t kZeWaveWords = kZeMaxSeq + kZeBlock / 8;  // per wave: the sequence list, then the literals
+constexpr int kZeRing = 128;                      // Huffman stream staging dwords per wave
 
 // payload bytes: varint header scratch, then the block's items
 struct ZeSrc {
@@ -175,12 +177,24 @@ __device__ __forceinline__ ZeSrc zsrc_of(const EncArgs &a, uint64_t b) {
 __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeTabs *__restrict__ T,
                                                           unsigned long long *__restrict__ scratch) {
   __shared__ uint32_t s_hash[kZeWaves][1 << kZeHashBits];
+  __shared__ uint32_t s_hist[kZeWaves][256];      // literal counts
+  __shared__ uint32_t s_w[kZeWaves][260];         // Huffman build: node weights
+  __shared__ uint16_t s_par[kZeWaves][260];       // ... parents
+  __shared__ uint16_t s_val[kZeWaves][132];       // code values of symbols 0..128
+  __shared__ uint8_t s_len[kZeWaves][132];        // code lengths
+  __shared__ uint32_t s_ring[kZeWaves][kZeRing];  // stream bits being assembled
   const int wv = threadIdx.x >> 6;
   uint32_t *hash = s_hash[wv];
+  uint32_t *hist = s_hist[wv];
+  uint16_t *hval = s_val[wv];
+  uint8_t *hlen = s_len[wv];
+  uint32_t *ring = s_ring[wv];
   const int l = lane_id();
   const uint64_t wave = (uint64_t)blockIdx.x * kZeWaves + wv;
   const uint64_t nwaves = (uint64_t)gridDim.x * kZeWaves;
-  unsigned long long *seq = scratch + wave * kZeMaxSeq;
+  unsigned long long *seq = scratch + wave * kZeWaveWords;
+  uint8_t *lit = reinterpret_cast<uint8_t *>(seq + kZeMaxSeq);
+  for (int i = l; i < kZeRing; i += 64) ring[i] = 0;
   ZeLaneFse f_ll, f_ml, f_of;
   f_ll.load(T->ll, l);
   f_ml.load(T->ml, l);
@@ -266,14 +280,12 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
         }
         nlit = bsz - msum;
       }
-      if (l == 0) {
-        out[q] = (uint8_t)(0 | (3 << 2) | ((nlit & 15) << 4));  // Raw_Literals_Block, 20-bit size
-        out[q + 1] = (uint8_t)(nlit >> 4);
-        out[q + 2] = (uint8_t)(nlit >> 12);
-      }
-      q += 3;
-      {  // the runs before every match (lane per sequence), then the tail
-        unsigned long long src0 = b0, dst0 = q;
+      // literals: the runs before every match (a lane per sequence, placed by
+      // prefix sums) and the tail, gathered into the wave's scratch and counted
+      for (int i = l; i < 256; i += 64) hist[i] = 0;
+      wave_lds_sync();
+      {
+        unsigned long long src0 = b0, dst0 = 0;
         for (uint32_t g = 0; g < nseq; g += 64) {
           const uint32_t i = g + (uint32_t)l;
           const ZeSeq z = i < nseq ? ze_unpack(seq[i]) : ZeSeq{0, 0, 0};
@@ -284,14 +296,124 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
             s.load16(sp + k, w16);
 #pragma unroll
             for (int j = 0; j < 16; j++)
-              if (k + j < z.ll) out[dp + k + j] = (uint8_t)(w16[j >> 2] >> (8 * (j & 3)));
+              if (k + j < z.ll) {
+                const uint32_t c = (w16[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                lit[dp + k + j] = (uint8_t)c;
+                atomicAdd(&hist[c], 1u);
+              }
           }
           src0 += (uint32_t)__builtin_amdgcn_readlane((int)tin, 63);
           dst0 += (uint32_t)__builtin_amdgcn_readlane((int)lin, 63);
         }
-        for (unsigned long long k = l; src0 + k < b1; k += 64) out[dst0 + k] = (uint8_t)s.byte(src0 + k);
+        for (unsigned long long k = l; src0 + k < b1; k += 64) {
+          const uint32_t c = s.byte(src0 + k);
+          lit[dst0 + k] = (uint8_t)c;
+          atomicAdd(&hist[c], 1u);
+        }
       }
-      q += nlit;
+      ze_mem_sync();  // the literals visible to every lane
+      wave_lds_sync();
+      // Huffman-coded literals (4 streams, direct weights) when they shrink
+      bool huf = false;
+      uint32_t hlast = 0, maxb = 0, seg = 0, sb[4] = {0, 0, 0, 0}, comp = 0, hn = 0;
+      if (nlit >= 64) {
+        uint32_t lmax = 0, ldist = 0;
+        for (int k = l; k < 256; k += 64)
+          if (hist[k]) {
+            lmax = (uint32_t)k;
+            ldist++;
+          }
+        uint32_t dist = ldist;
+        for (int o2 = 32; o2 > 0; o2 >>= 1) {
+          dist += (uint32_t)__shfl_xor((int)dist, o2, 64);
+          const uint32_t t = (uint32_t)__shfl_xor((int)lmax, o2, 64);
+          lmax = t > lmax ? t : lmax;
+        }
+        hlast = lmax;
+        if (dist >= 2 && hlast <= 128) {
+          if (l == 0) {
+            ze_huf_lengths(hist, hlast + 1, hlen, s_w[wv], s_par[wv]);
+            maxb = ze_huf_codes(hlen, hlast + 1, hval);
+          }
+          maxb = (uint32_t)__builtin_amdgcn_readfirstlane((int)maxb);
+          wave_lds_sync();
+          seg = ze_seg((uint32_t)nlit);
+          for (int k = 0; k < 4; k++) {  // each stream's bytes: its code bits + the end mark
+            const uint32_t a0 = min((uint32_t)k * seg, (uint32_t)nlit);
+            const uint32_t a1 = k < 3 ? min((uint32_t)(k + 1) * seg, (uint32_t)nlit) : (uint32_t)nlit;
+            uint32_t bits = 0;
+            for (uint32_t i = a0 + l; i < a1; i += 64) bits += hlen[lit[i]];
+            bits = wave_sum<uint32_t>(bits);
+            sb[k] = (bits + 1 + 7) / 8;
+          }
+          const uint32_t tree = 1 + (hlast + 1) / 2;
+          comp = tree + 6 + sb[0] + sb[1] + sb[2] + sb[3];
+          hn = (nlit <= 1023 && comp <= 1023) ? 3u : (nlit <= 16383 && comp <= 16383) ? 4u : 5u;
+          huf = hn + comp < 3 + nlit && sb[0] < 65536 && sb[1] < 65536 && sb[2] < 65536;
+        }
+      }
+      if (huf) {
+        const uint32_t tree = 1 + (hlast + 1) / 2;
+        if (l == 0) {
+          ze_lit_header(out + q, (uint32_t)nlit, comp);
+          ze_huf_weights(hlen, hlast, maxb, out + q + hn);
+          uint8_t *jt = out + q + hn + tree;
+          for (int k = 0; k < 3; k++) {
+            jt[2 * k] = (uint8_t)sb[k];
+            jt[2 * k + 1] = (uint8_t)(sb[k] >> 8);
+          }
+        }
+        unsigned long long sbase = q + hn + tree + 6;
+        for (int k = 0; k < 4; k++) {  // stream k: its symbols last to first, bits placed by a wave scan
+          const uint32_t a0 = min((uint32_t)k * seg, (uint32_t)nlit);
+          const uint32_t a1 = k < 3 ? min((uint32_t)(k + 1) * seg, (uint32_t)nlit) : (uint32_t)nlit;
+          const uint32_t ns = a1 - a0;
+          uint32_t bitpos = 0, flushed = 0;
+          for (uint32_t e0 = 0; e0 <= ns; e0 += 64) {  // (the last round also places the end mark)
+            const uint32_t e = e0 + (uint32_t)l;
+            uint32_t ln = 0, v = 0;
+            if (e < ns) {
+              const uint32_t c = lit[a1 - 1 - e];
+              ln = hlen[c];
+              v = hval[c];
+            } else if (e == ns) {
+              ln = 1;  // the end mark
+              v = 1;
+            }
+            const uint32_t incl = wave_incl_sum_dpp(ln);
+            if (ln) {
+              const uint32_t pos = bitpos + incl - ln, wd = pos >> 5, sh = pos & 31u;
+              atomicOr(&ring[wd & (kZeRing - 1)], v << sh);
+              if (sh + ln > 32) atomicOr(&ring[(wd + 1) & (kZeRing - 1)], v >> (32 - sh));
+            }
+            bitpos += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            wave_lds_sync();
+            const bool fin = e0 + 64 > ns;
+            const uint32_t nbytes = (bitpos + 7) >> 3;
+            const uint32_t done = fin ? (nbytes + 3) >> 2 : bitpos >> 5;  // dwords complete (all at the end)
+            if (flushed + (uint32_t)l < done) {
+              const uint32_t d = flushed + (uint32_t)l, slot = d & (kZeRing - 1);
+              const uint32_t x = ring[slot];
+              ring[slot] = 0;
+#pragma unroll
+              for (int j = 0; j < 4; j++)
+                if (4 * d + j < nbytes && sbase + 4 * d + j < lim) out[sbase + 4 * d + j] = (uint8_t)(x >> (8 * j));
+            }
+            flushed = done;
+            wave_lds_sync();
+          }
+          sbase += sb[k];
+        }
+        q = sbase;
+      } else {
+        if (l == 0) {
+          out[q] = (uint8_t)(0 | (3 << 2) | ((nlit & 15) << 4));  // Raw_Literals_Block, 20-bit size
+          out[q + 1] = (uint8_t)(nlit >> 4);
+          out[q + 2] = (uint8_t)(nlit >> 12);
+        }
+        for (unsigned long long k = l; k < nlit; k += 64) out[q + 3 + k] = lit[k];
+        q += 3 + nlit;
+      }
       if (l == 0) {  // Number_of_Sequences, then the compression modes (all predefined)
         if (nseq < 128) {
           out[q] = (uint8_t)nseq;
@@ -387,7 +509,7 @@ void launch_zstd_enc_bound(const EncArgs &a, hipStream_t st) {
 
 static uint64_t zstd_enc_grid(int ncu) { return (uint64_t)(ncu > 0 ? ncu : 256) * 2; }  // 2 workgroups per CU (LDS)
 
-uint64_t zstd_enc_scratch_words(int ncu) { return zstd_enc_grid(ncu) * kZeWaves * kZeMaxSeq; }
+uint64_t zstd_enc_scratch_words(int ncu) { return zstd_enc_grid(ncu) * kZeWaves * kZeWaveWords; }
 
 void launch_zstd_enc(const EncArgs &a, const ZeTabs *tabs, unsigned long long *scratch, int ncu, hipStream_t st) {
   uint64_t g = (a.nblocks + kZeWaves - 1) / kZeWaves;

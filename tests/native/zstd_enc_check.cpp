@@ -46,9 +46,41 @@ static std::vector<uint8_t> enc(const std::vector<uint8_t> &src, const ZeTabs &T
     size_t bh = o; o += 3;
     size_t c0 = o;
     const uint32_t nl = lits.size();
-    out[o++] = (uint8_t)(0 | (3 << 2) | ((nl & 15) << 4));
-    out[o++] = (uint8_t)(nl >> 4); out[o++] = (uint8_t)(nl >> 12);
-    memcpy(&out[o], lits.data(), nl); o += nl;
+    bool huf = false;
+    if (nl >= 64) {  // Huffman literals when they shrink (max symbol <= 128, >= 2 symbols)
+      uint32_t cnt[256] = {0}, w[512]; uint16_t par[512]; uint8_t len[256]; uint16_t val[256];
+      for (uint8_t c : lits) cnt[c]++;
+      uint32_t last = 0, distinct = 0;
+      for (int k = 0; k < 256; k++) if (cnt[k]) { last = k; distinct++; }
+      if (distinct >= 2 && last <= 128) {
+        ze_huf_lengths(cnt, last + 1, len, w, par);
+        const uint32_t maxb = ze_huf_codes(len, last + 1, val);
+        std::vector<uint8_t> sec(nl + 1024);
+        uint32_t t = ze_huf_weights(len, last, maxb, sec.data());
+        uint32_t jt = t; t += 6;
+        const uint32_t seg = ze_seg(nl);
+        uint32_t ssz[4];
+        for (int k = 0; k < 4; k++) {
+          const uint32_t a = k * seg < nl ? k * seg : nl, b = k < 3 ? ((k + 1) * seg < nl ? (k + 1) * seg : nl) : nl;
+          ZeBits bw{0, 0, sec.data(), t};
+          for (uint32_t i = b; i-- > a;) bw.add(val[lits[i]], len[lits[i]]);
+          bw.close();
+          ssz[k] = bw.pos - t; t = bw.pos;
+        }
+        for (int k = 0; k < 3; k++) { sec[jt + 2 * k] = ssz[k]; sec[jt + 2 * k + 1] = ssz[k] >> 8; }
+        uint8_t hdr[5];
+        const uint32_t hn = ze_lit_header(hdr, nl, t);
+        if (hn + t < 3 + nl) {
+          memcpy(&out[o], hdr, hn); o += hn; memcpy(&out[o], sec.data(), t); o += t;
+          huf = true;
+        }
+      }
+    }
+    if (!huf) {
+      out[o++] = (uint8_t)(0 | (3 << 2) | ((nl & 15) << 4));
+      out[o++] = (uint8_t)(nl >> 4); out[o++] = (uint8_t)(nl >> 12);
+      memcpy(&out[o], lits.data(), nl); o += nl;
+    }
     const uint32_t n = seqs.size();
     if (n < 128) out[o++] = n;
     else if (n < 0x7F00) { out[o++] = (n >> 8) + 0x80; out[o++] = n & 0xff; }
@@ -78,7 +110,7 @@ static std::vector<uint8_t> enc(const std::vector<uint8_t> &src, const ZeTabs &T
 int main() {
   ZeTabs T; ze_build_tabs(T);
   srand(1);
-  int fails = 0;
+  int fails = 0; size_t tin = 0, tout = 0;
   for (int t = 0; t < 40; t++) {
     size_t n = (t < 5) ? (size_t)(t * 7) : (size_t)(rand() % 300000);
     std::vector<uint8_t> s(n);
@@ -90,13 +122,13 @@ int main() {
       else if (kind == 2) s[i] = (i % 97 < 50) ? 'x' : alpha[rand() & 3];
       else s[i] = (i > 1000 && rand() % 5) ? s[i - 1 - rand() % 1000] : rand() & 255;
     }
-    auto c = enc(s, T);
+    auto c = enc(s, T); tin += n; tout += c.size();
     std::vector<uint8_t> d(n + 1);
     size_t r = ZSTD_decompress(d.data(), n + 1, c.data(), c.size());
     bool ok = !ZSTD_isError(r) && r == n && memcmp(d.data(), s.data(), n) == 0;
     if (!ok) { fails++; printf("FAIL t=%d n=%zu kind=%d err=%s\n", t, n, kind, ZSTD_isError(r) ? ZSTD_getErrorName(r) : "mismatch"); }
     
   }
-  printf("fails=%d\n", fails);
+  printf("fails=%d total_in=%zu total_out=%zu\n", fails, tin, tout);
   return fails != 0;
 }
