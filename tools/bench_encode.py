@@ -69,8 +69,12 @@ def main():
     # parity: scan the encoded stream back on the device
     b = ctx.scan_device(out.data_ptr(), out_len, 32768, True, a.codec)
     ok = b.stop == gpu.RIO_STOP_EOF and b.n_items == n
+    # transformed payload bytes: the chunk headers' size fields (offset 16 of every chunk)
+    sizes = out[:out_len].view(-1, 32768)[:, 16:20].contiguous().view(torch.int32)
+    pay = int(sizes.sum().item())
     detail = {"stop": int(b.stop), "n_items": int(b.n_items), "err": b.err.msg.decode(),
-              "ratio": round(int(data.numel()) / out_len, 3)}
+              "ratio": round(int(data.numel()) / out_len, 3), "payload_bytes": pay,
+              "payload_ratio": round(int(data.numel()) / pay, 3)}
     if a.codec == 0:  # the first 3,952 blocks (whole 253-record blocks) equal the bench's C2 file
         want = bench.make_c2_file()[0][32768:32768 + 3952 * 65536]
         detail["bytes_equal"] = out[:len(want)].cpu().numpy().tobytes() == want
