@@ -205,18 +205,23 @@ __host__ __device__ void ze_sequences(ZeBits &w, const ZeTabs &T, uint32_t n, Ge
 // ---- Huffman-coded literals (RFC 8878 3.1.1.3.1, 4.2.1; libzstd HUF_*)
 constexpr uint32_t kZeHufMax = 11;  // the format allows 11-bit codes
 
-// Code lengths (<= kZeHufMax) of a complete prefix code for the symbols with
-// cnt > 0 (>= 2 of them, all < 256): Huffman by repeated minimum pairs, then
-// lengths clamped to kZeHufMax and the Kraft sum brought back to exactly 1
-// (the decoder deduces the last symbol's weight from it). len[s] = 0 for
-// absent symbols. Serial (one lane); parent/work arrays of 512 entries.
-__host__ __device__ inline void ze_huf_lengths(const uint32_t *cnt, uint32_t nsym, uint8_t *len, uint32_t *w,
-                                               uint16_t *parent) {
+// Code lengths (<= maxlen) of a complete prefix code for the symbols with
+// cnt > 0 (>= 2 of them): Huffman by repeated minimum pairs, then lengths
+// clamped to maxlen and the Kraft sum brought back to exactly 1 (zstd's decoder
+// deduces the last symbol's weight from it; Go's inflater accepts only complete
+// codes). len[s] = 0 for absent symbols. Serial (one lane); w / parent hold
+// 2 * nsym nodes. Shared by the zstd (maxlen 11) and DEFLATE (15, 7) encoders.
+__host__ __device__ inline void huf_lengths(const uint32_t *cnt, uint32_t nsym, uint32_t maxlen, uint8_t *len,
+                                            uint32_t *w, uint16_t *parent) {
   // nodes 0..nsym-1 leaves, nsym.. internal; w = weight (~0: consumed)
   uint32_t n = nsym;
   for (uint32_t s = 0; s < nsym; s++) w[s] = cnt[s] ? cnt[s] : 0xffffffffu;
   uint32_t live = 0;
   for (uint32_t s = 0; s < nsym; s++) live += cnt[s] ? 1 : 0;
+  if (live < 2) {  // (callers pass two symbols or more; a lone one gets 1 bit)
+    for (uint32_t s = 0; s < nsym; s++) len[s] = cnt[s] ? 1 : 0;
+    return;
+  }
   while (live > 1) {
     uint32_t a = 0xffffffffu, b = 0xffffffffu;
     for (uint32_t k = 0; k < n; k++) {
@@ -241,30 +246,35 @@ __host__ __device__ inline void ze_huf_lengths(const uint32_t *cnt, uint32_t nsy
     if (cnt[s]) {
       for (uint32_t k = s; k != root; k = parent[k]) d++;
     }
-    len[s] = (uint8_t)(d > kZeHufMax ? kZeHufMax : d);
+    len[s] = (uint8_t)(d > maxlen ? maxlen : d);
   }
-  // Kraft sum in units of 2^-kZeHufMax: make it exactly 2^kZeHufMax
+  // Kraft sum in units of 2^-maxlen: make it exactly 2^maxlen
+  const uint32_t one = 1u << maxlen;
   uint32_t kraft = 0;
   for (uint32_t s = 0; s < nsym; s++)
-    if (len[s]) kraft += 1u << (kZeHufMax - len[s]);
-  while (kraft > (1u << kZeHufMax)) {  // lengthen the longest code below the cap
+    if (len[s]) kraft += 1u << (maxlen - len[s]);
+  while (kraft > one) {  // lengthen the longest code below the cap
     uint32_t best = 0xffffffffu;
     for (uint32_t s = 0; s < nsym; s++)
-      if (len[s] && len[s] < kZeHufMax && (best == 0xffffffffu || len[s] > len[best] ||
-                                          (len[s] == len[best] && cnt[s] < cnt[best])))
+      if (len[s] && len[s] < maxlen &&
+          (best == 0xffffffffu || len[s] > len[best] || (len[s] == len[best] && cnt[s] < cnt[best])))
         best = s;
-    kraft -= 1u << (kZeHufMax - len[best] - 1);
+    kraft -= 1u << (maxlen - len[best] - 1);
     len[best]++;
   }
-  while (kraft < (1u << kZeHufMax)) {  // shorten the longest code that still fits
+  while (kraft < one) {  // shorten the longest code that still fits
     uint32_t best = 0xffffffffu;
     for (uint32_t s = 0; s < nsym; s++)
-      if (len[s] > 1 && kraft + (1u << (kZeHufMax - len[s])) <= (1u << kZeHufMax) &&
+      if (len[s] > 1 && kraft + (1u << (maxlen - len[s])) <= one &&
           (best == 0xffffffffu || len[s] > len[best] || (len[s] == len[best] && cnt[s] > cnt[best])))
         best = s;
-    kraft += 1u << (kZeHufMax - len[best]);
+    kraft += 1u << (maxlen - len[best]);
     len[best]--;
   }
+}
+__host__ __device__ inline void ze_huf_lengths(const uint32_t *cnt, uint32_t nsym, uint8_t *len, uint32_t *w,
+                                               uint16_t *parent) {
+  huf_lengths(cnt, nsym, kZeHufMax, len, w, parent);
 }
 
 // canonical code values of HUF_buildCTable: longest codes first from 0, each
