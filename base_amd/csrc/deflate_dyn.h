@@ -9,7 +9,12 @@
 #pragma once
 #include <stdint.h>
 
-#include "zstd_enc.h"  // huf_lengths
+#ifndef __HIPCC__  // the host check compiles this with g++
+#define __host__
+#define __device__
+#define __forceinline__ inline
+#endif
+
 
 namespace rio {
 
@@ -72,32 +77,104 @@ struct DzTrees {
   uint8_t ll_len[kDzLit], d_len[kDzDist], cl_len[kDzCl];
   uint16_t ll_code[kDzLit], d_code[kDzDist], cl_code[kDzCl];
   uint16_t rle[kDzLit + kDzDist];  // code-length symbol | extra value << 5
+  uint16_t ord[kDzLit];            // live symbols by ascending (count, symbol)
   uint32_t nrle, hlit, hdist, hclen, hdr_bits;
 };
 
-// the trees of a block from its counts (ll_cnt includes end-of-block);
-// cnt arrays are modified (absent fillers for degenerate alphabets); w /
-// parent: 2 * kDzLit node scratch
-__host__ __device__ inline void dz_build(uint32_t *ll_cnt, uint32_t *d_cnt, DzTrees &t, uint32_t *w, uint16_t *par) {
-  uint32_t used = 0, lastll = 0, lastd = 0;
-  for (uint32_t s = 0; s < kDzLit; s++)
-    if (ll_cnt[s]) {
-      used++;
-      lastll = s;
+// Huffman code lengths (<= maxlen, a complete code) of the nlive >= 2 live
+// symbols in ord (ascending count, then symbol): the two-queue construction
+// (leaves in order, internal nodes in creation order are both sorted), node
+// depths from the root down, counts per length clamped to maxlen and the
+// Kraft sum brought back to exactly 1, then the lengths handed out longest
+// first to the rarest symbols. O(nlive); w: nlive, par: 2 * nlive entries.
+__host__ __device__ inline void huf_lengths_q(const uint32_t *cnt, uint32_t nsym, const uint16_t *ord, uint32_t nlive,
+                                              uint32_t maxlen, uint8_t *len, uint32_t *w, uint16_t *par) {
+  for (uint32_t s = 0; s < nsym; s++) len[s] = 0;
+  uint32_t i = 0, j = 0;
+  for (uint32_t k = 0; k + 1 < nlive; k++) {
+    uint32_t nd[2], wt[2];
+    for (int q = 0; q < 2; q++) {
+      if (i < nlive && (j >= k || cnt[ord[i]] <= w[j])) {
+        wt[q] = cnt[ord[i]];
+        nd[q] = i++;
+      } else {
+        wt[q] = w[j];
+        nd[q] = nlive + j++;
+      }
     }
-  if (used < 2) ll_cnt[ll_cnt[0] ? 1 : 0] = 1;  // a complete code needs two symbols
+    w[k] = wt[0] + wt[1];
+    par[nd[0]] = par[nd[1]] = (uint16_t)(nlive + k);
+  }
+  // depths of the internal nodes (into w), root = nlive - 2
+  const uint32_t root = nlive - 2;
+  w[root] = 0;
+  for (uint32_t k = root; k-- > 0;) w[k] = w[par[nlive + k] - nlive] + 1;
+  uint32_t bl[16];
+  for (uint32_t b = 0; b < 16; b++) bl[b] = 0;
+  for (uint32_t q = 0; q < nlive; q++) {
+    const uint32_t d = w[par[q] - nlive] + 1;
+    bl[d > maxlen ? maxlen : d]++;
+  }
+  const uint32_t one = 1u << maxlen;
+  uint32_t kraft = 0;
+  for (uint32_t b = 1; b <= maxlen; b++) kraft += bl[b] << (maxlen - b);
+  while (kraft > one) {  // one code of the longest length below the cap gets a bit longer
+    uint32_t b = maxlen - 1;
+    while (!bl[b]) b--;
+    bl[b]--;
+    bl[b + 1]++;
+    kraft -= 1u << (maxlen - b - 1);
+  }
+  while (kraft < one) {  // one code of the longest length that still fits gets a bit shorter
+    uint32_t b = maxlen;
+    while (b > 1 && (!bl[b] || kraft + (1u << (maxlen - b)) > one)) b--;
+    bl[b]--;
+    bl[b - 1]++;
+    kraft += 1u << (maxlen - b);
+  }
+  uint32_t q = 0;
+  for (uint32_t b = maxlen; b >= 1; b--)
+    for (uint32_t c = 0; c < bl[b]; c++) len[ord[q++]] = (uint8_t)b;
+}
+
+// live symbols by ascending (count, symbol) into ord (insertion: small alphabets)
+__host__ __device__ inline uint32_t dz_sort(const uint32_t *cnt, uint32_t nsym, uint16_t *ord) {
+  uint32_t n = 0;
+  for (uint32_t s = 0; s < nsym; s++) {
+    if (!cnt[s]) continue;
+    uint32_t p = n++;
+    while (p > 0 && cnt[ord[p - 1]] > cnt[s]) {
+      ord[p] = ord[p - 1];
+      p--;
+    }
+    ord[p] = (uint16_t)s;
+  }
+  return n;
+}
+
+// degenerate alphabets: a complete code needs two symbols (absent ones get
+// count 1); before the literal/length order is taken
+__host__ __device__ inline void dz_fill(uint32_t *ll_cnt, uint32_t *d_cnt) {
+  uint32_t used = 0;
+  for (uint32_t s = 0; s < kDzLit; s++) used += ll_cnt[s] ? 1 : 0;
+  if (used < 2) ll_cnt[ll_cnt[0] ? 1 : 0] = 1;
   used = 0;
-  for (uint32_t s = 0; s < kDzDist; s++)
-    if (d_cnt[s]) {
-      used++;
-      lastd = s;
-    }
+  for (uint32_t s = 0; s < kDzDist; s++) used += d_cnt[s] ? 1 : 0;
   if (used < 2) {  // no or one distance code: two of them present (a complete 1-bit code)
     if (!d_cnt[0]) d_cnt[0] = 1;
     if (used == 0 || !d_cnt[1]) d_cnt[d_cnt[1] ? 2 : 1] = 1;
   }
-  huf_lengths(ll_cnt, kDzLit, 15, t.ll_len, w, par);
-  huf_lengths(d_cnt, kDzDist, 15, t.d_len, w, par);
+}
+
+// the trees of a block from its counts (ll_cnt includes end-of-block, dz_fill
+// applied) and t.ord = the ll_n live literal/length symbols in order; w /
+// par: 2 * kDzLit node scratch
+__host__ __device__ inline void dz_build(const uint32_t *ll_cnt, const uint32_t *d_cnt, uint32_t ll_n, DzTrees &t,
+                                         uint32_t *w, uint16_t *par) {
+  uint32_t lastll = 0, lastd = 0;
+  huf_lengths_q(ll_cnt, kDzLit, t.ord, ll_n, 15, t.ll_len, w, par);
+  const uint32_t dn = dz_sort(d_cnt, kDzDist, t.ord);
+  huf_lengths_q(d_cnt, kDzDist, t.ord, dn, 15, t.d_len, w, par);
   lastll = 0;
   for (uint32_t s = 0; s < kDzLit; s++)
     if (t.ll_len[s]) lastll = s;
@@ -145,10 +222,11 @@ __host__ __device__ inline void dz_build(uint32_t *ll_cnt, uint32_t *d_cnt, DzTr
     }
     i += run;
   }
-  used = 0;
+  uint32_t used = 0;
   for (uint32_t k = 0; k < kDzCl; k++) used += cl_cnt[k] ? 1 : 0;
   if (used < 2) cl_cnt[cl_cnt[0] ? 1 : 0] = 1;
-  huf_lengths(cl_cnt, kDzCl, 7, t.cl_len, w, par);
+  const uint32_t cn = dz_sort(cl_cnt, kDzCl, t.ord);
+  huf_lengths_q(cl_cnt, kDzCl, t.ord, cn, 7, t.cl_len, w, par);
   t.hclen = 19;
   while (t.hclen > 4 && t.cl_len[kDzClOrder[t.hclen - 1]] == 0) t.hclen--;
   dz_codes(t.ll_len, kDzLit, t.ll_code);

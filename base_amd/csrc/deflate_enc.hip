@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "deflate_dyn.h"
 #include "device_common.h"
 #include "encode.h"
 #include "rio_internal.h"
@@ -288,13 +289,287 @@ __global__ void __launch_bounds__(256) k_deflate_stored(EncArgs a) {
   }
 }
 
+// ---- dynamic Huffman (levels >= 2, the default) ----------------------------
+// The same hash/greedy parse, in sub-blocks of kDySub payload bytes, each its
+// own DEFLATE block: the round's chosen tokens go to the wave's token list in
+// HBM (u32: a literal byte, or 1 << 31 | length << 16 | distance - 1) and
+// their symbols into LDS histograms; then the literal/length order (a wave
+// rank sort), the trees (lane 0, deflate_dyn.h: O(symbols)), the cost of the
+// dynamic block against the fixed one from the histograms, the header (lane 0
+// into the ring) and the tokens re-read 64 at a time, coded with the chosen
+// trees (<= 48 bits each) and placed by a wave prefix sum like k_deflate's.
+constexpr int kDySub = 32768;  // payload bytes per DEFLATE block
+constexpr int kDyWaves = 2;    // waves per workgroup (~23 KB LDS each)
+constexpr int kDyRing = 256;   // staging dwords: a dynamic header is <= 4,500 bits
+
+struct alignas(16) DyWave {  // (16: the rank sort reads ll_cnt as uint4)
+  uint32_t hash[1 << kDHashBits];
+  uint32_t ll_cnt[288], d_cnt[32];
+  uint32_t w[kDzLit];
+  uint16_t par[2 * kDzLit];
+  uint32_t ring[kDyRing];
+  DzTrees t;
+};
+
+struct DyRingSink {  // lane 0: header bits into the ring
+  uint32_t *ring;
+  unsigned long long pos;
+  __device__ void add(uint32_t v, uint32_t n) {
+    if (!n) return;
+    const uint32_t k = (uint32_t)(pos >> 5), sh = (uint32_t)(pos & 31);
+    ring[k & (kDyRing - 1)] |= v << sh;
+    if (sh + n > 32) ring[(k + 1) & (kDyRing - 1)] |= v >> (32 - sh);
+    pos += n;
+  }
+};
+
+__device__ __forceinline__ uint32_t dy_fixlen(uint32_t s) { return s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8; }
+
+__device__ __forceinline__ uint32_t dy_wave_sum(uint32_t v) {
+  return __shfl(wave_incl_sum<uint32_t>(v), 63, 64);
+}
+
+__device__ __forceinline__ void dy_mem_sync() {  // this wave's global stores visible to its lanes' loads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__global__ void __launch_bounds__(64 * kDyWaves) k_deflate_dyn(EncArgs a, uint32_t *scratch) {
+  __shared__ DyWave s_w[kDyWaves];
+  const int wv = threadIdx.x >> 6;
+  DyWave &W = s_w[wv];
+  uint32_t *hash = W.hash;
+  uint32_t *ring = W.ring;
+  DzTrees &t = W.t;
+  const int l = lane_id();
+  const uint64_t nwaves = (uint64_t)gridDim.x * kDyWaves;
+  uint32_t *tok = scratch + ((uint64_t)blockIdx.x * kDyWaves + wv) * kDySub;
+  for (uint64_t b = (uint64_t)blockIdx.x * kDyWaves + wv; b < a.nblocks; b += nwaves) {
+    const DSrc s = dsrc_of(a, b);
+    const unsigned long long L = s.len;
+    uint32_t *out = reinterpret_cast<uint32_t *>(a.comp + a.comp_off[b]);
+    for (int i = l; i < (1 << kDHashBits); i += 64) hash[i] = kDNone;
+    for (int i = l; i < kDyRing; i += 64) ring[i] = 0;
+    unsigned long long bitpos = 0, flushed = 0, cur = 0;
+    auto flush = [&]() {
+      wave_lds_sync();
+      const unsigned long long done = bitpos >> 5;
+      for (unsigned long long k = flushed + l; k < done; k += 64) {
+        const uint32_t slot = (uint32_t)(k & (kDyRing - 1));
+        out[k] = ring[slot];
+        ring[slot] = 0;
+      }
+      flushed = done;
+      wave_lds_sync();
+    };
+    uint32_t nx[4];
+    s.load16(l, nx);
+    for (unsigned long long b0 = 0;; b0 += kDySub) {
+      const unsigned long long b1 = b0 + kDySub < L ? b0 + kDySub : L;
+      const bool final = b1 >= L;
+      for (int i = l; i < 288; i += 64) W.ll_cnt[i] = 0;
+      if (l < 32) W.d_cnt[l] = 0;
+      wave_lds_sync();
+      uint32_t ntok = 0;
+      for (unsigned long long base = b0; base < b1; base += 64) {
+        const unsigned long long p = base + l;
+        uint32_t cw[4] = {nx[0], nx[1], nx[2], nx[3]};
+        if (base + 64 < L) s.load16(p + 64, nx);
+        const bool has4 = p + 4 <= L;
+        const uint32_t h = (cw[0] * 0x9E3779B1u) >> (32 - kDHashBits);
+        const uint32_t cand = has4 ? hash[h] : kDNone;
+        wave_lds_sync();
+        if (has4) hash[h] = (uint32_t)p;
+        uint32_t m = 0;
+        if (has4 && p >= cur && p < b1 && cand != kDNone && p - cand <= 32768) {
+          const unsigned long long room = b1 - p;
+          const uint32_t maxm = room < 258 ? (uint32_t)room : 258u;
+          uint32_t cc[4];
+          s.load16(cand, cc);
+          m = common16(cc, cw);
+          while (m == 16 * ((m + 15) / 16) && m > 0 && m < maxm) {
+            uint32_t a16[4], b16[4];
+            s.load16(cand + m, a16);
+            s.load16(p + m, b16);
+            const uint32_t k = common16(a16, b16);
+            m += k;
+            if (k < 16) break;
+          }
+          if (m > maxm) m = maxm;
+          if (m < 4) m = 0;
+        }
+        unsigned long long chosen = 0, pos = cur;
+        const unsigned long long rend = base + 64 < b1 ? base + 64 : b1;
+        while (pos < rend) {
+          const uint32_t lane = (uint32_t)(pos - base);
+          const uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)m, (int)lane);
+          chosen |= 1ull << lane;
+          pos += ml >= 4 ? ml : 1;
+        }
+        cur = pos;
+        if ((chosen >> l) & 1) {
+          const uint32_t idx = ntok + (uint32_t)__popcll(chosen & ((1ull << l) - 1));
+          uint32_t tk;
+          if (m >= 4) {
+            const uint32_t d = (uint32_t)(p - cand);
+            uint32_t sym, e, v;
+            dz_len_sym(m, sym, e, v);
+            atomicAdd(&W.ll_cnt[sym], 1u);
+            dz_dist_sym(d, sym, e, v);
+            atomicAdd(&W.d_cnt[sym], 1u);
+            tk = 0x80000000u | (m << 16) | (d - 1);
+          } else {
+            tk = cw[0] & 0xff;
+            atomicAdd(&W.ll_cnt[tk], 1u);
+          }
+          tok[idx] = tk;
+        }
+        ntok += (uint32_t)__popcll(chosen);
+      }
+      wave_lds_sync();
+      if (l == 0) {
+        W.ll_cnt[256]++;  // end of block
+        dz_fill(W.ll_cnt, W.d_cnt);
+      }
+      wave_lds_sync();
+      {  // literal/length symbols by ascending (count, symbol): rank of each
+        uint32_t c[5], r[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 5; k++) c[k] = l + 64 * k < (int)kDzLit ? W.ll_cnt[l + 64 * k] : 0u;
+        const uint4 *cv = reinterpret_cast<const uint4 *>(W.ll_cnt);
+        for (int q = 0; q < 72; q++) {
+          const uint4 v = cv[q];
+          const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const uint32_t ts = 4 * q + j;
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+              r[k] += (e[j] != 0) & ((e[j] < c[k]) | ((e[j] == c[k]) & (ts < (uint32_t)(l + 64 * k))));
+          }
+        }
+        uint32_t live = 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+          if (c[k]) {
+            t.ord[r[k]] = (uint16_t)(l + 64 * k);
+            live++;
+          }
+        live = dy_wave_sum(live);
+        wave_lds_sync();
+        if (l == 0) dz_build(W.ll_cnt, W.d_cnt, live, t, W.w, W.par);
+        wave_lds_sync();
+      }
+      uint32_t dyn = 0, fix = 0;
+      for (int i = l; i < (int)kDzLit; i += 64) {
+        dyn += W.ll_cnt[i] * t.ll_len[i];
+        fix += W.ll_cnt[i] * dy_fixlen(i);
+      }
+      if (l < (int)kDzDist) {
+        dyn += W.d_cnt[l] * t.d_len[l];
+        fix += W.d_cnt[l] * 5;
+      }
+      dyn = dy_wave_sum(dyn) + t.hdr_bits;
+      fix = dy_wave_sum(fix) + 3;
+      const bool use_dyn = dyn < fix;
+      if (!use_dyn) {  // the fixed code (RFC 1951 3.2.6; 288 literal/length symbols)
+        for (int i = l; i < (int)kDzLit; i += 64) {
+          const uint32_t n = dy_fixlen(i);
+          const uint32_t c = i < 144 ? 0x30 + i : i < 256 ? 0x190 + (i - 144) : i < 280 ? i - 256 : 0xC0 + (i - 280);
+          t.ll_len[i] = (uint8_t)n;
+          t.ll_code[i] = (uint16_t)rev_bits(c, n);
+        }
+        if (l < (int)kDzDist) {
+          t.d_len[l] = 5;
+          t.d_code[l] = (uint16_t)rev_bits(l, 5);
+        }
+      }
+      wave_lds_sync();
+      if (l == 0) {
+        DyRingSink o{ring, bitpos};
+        if (use_dyn) {
+          dz_header(o, t, final);
+        } else {
+          o.add(final ? 1u : 0u, 1);
+          o.add(1, 2);
+        }
+        W.w[0] = (uint32_t)(o.pos - bitpos);
+      }
+      wave_lds_sync();
+      bitpos += W.w[0];
+      flush();
+      dy_mem_sync();  // the token list's stores visible to every lane
+      uint32_t tn = l < (int)ntok ? tok[l] : 0;
+      for (uint32_t g = 0; g < ntok; g += 64) {
+        const uint32_t tk = tn;
+        const bool have = g + l < ntok;
+        if (g + 64 + l < ntok) tn = tok[g + 64 + l];
+        unsigned long long v = 0;
+        uint32_t nb = 0;
+        if (have) {
+          if (tk >> 31) {
+            const uint32_t m = (tk >> 16) & 0x1ff, d = (tk & 0xffff) + 1;
+            uint32_t sym, e, x;
+            dz_len_sym(m, sym, e, x);
+            v = t.ll_code[sym];
+            nb = t.ll_len[sym];
+            v |= (unsigned long long)x << nb;
+            nb += e;
+            dz_dist_sym(d, sym, e, x);
+            v |= (unsigned long long)t.d_code[sym] << nb;
+            nb += t.d_len[sym];
+            v |= (unsigned long long)x << nb;
+            nb += e;
+          } else {
+            v = t.ll_code[tk];
+            nb = t.ll_len[tk];
+          }
+        }
+        const uint32_t incl = wave_incl_sum<uint32_t>(nb);
+        const uint32_t tot = __shfl(incl, 63, 64);
+        if (nb) {
+          const unsigned long long o = bitpos + (incl - nb);
+          const uint32_t k = (uint32_t)(o >> 5), sh = (uint32_t)(o & 31);
+          const unsigned long long lo = v << sh;
+          atomicOr(&ring[k & (kDyRing - 1)], (uint32_t)lo);
+          if (sh + nb > 32) atomicOr(&ring[(k + 1) & (kDyRing - 1)], (uint32_t)(lo >> 32));
+          if (sh + nb > 64) atomicOr(&ring[(k + 2) & (kDyRing - 1)], (uint32_t)(v >> (64 - sh)));
+        }
+        bitpos += tot;
+        flush();
+      }
+      if (l == 0) {
+        DyRingSink o{ring, bitpos};
+        o.add(t.ll_code[256], t.ll_len[256]);
+      }
+      bitpos += t.ll_len[256];
+      if (final) break;
+      flush();
+    }
+    wave_lds_sync();
+    const unsigned long long nd = (bitpos + 31) >> 5;
+    for (unsigned long long k = flushed + l; k < nd; k += 64) {
+      const uint32_t slot = (uint32_t)(k & (kDyRing - 1));
+      out[k] = ring[slot];
+      ring[slot] = 0;
+    }
+    wave_lds_sync();
+    if (l == 0) a.pay_len[b] = (bitpos + 7) >> 3;
+  }
+}
+
+static uint64_t deflate_dyn_grid(int ncu) { return (uint64_t)(ncu > 0 ? ncu : 256) * 3; }  // 3 workgroups per CU (LDS)
+
+uint64_t deflate_scratch_words(int ncu) { return deflate_dyn_grid(ncu) * kDyWaves * kDySub / 2; }
+
 // per block: the compressed region's bound (into nck, scanned into comp_off)
 __global__ void k_deflate_bound(EncArgs a) {
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < a.nblocks;
        b += (uint64_t)gridDim.x * blockDim.x) {
     const unsigned long long L = a.pay_len[b];
     const unsigned long long stored = L + 5 * (L / 65535 + 1);
-    const unsigned long long fixed = L + L / 8 + 16;
+    const unsigned long long fixed = L + L / 8 + 16 + 2 * (L / kDySub + 1);  // (a fixed block per kDySub)
     a.nck[b] = ((stored > fixed ? stored : fixed) + 64 + 15) & ~15ull;
   }
 }
@@ -305,13 +580,20 @@ void launch_deflate_bound(const EncArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(k_deflate_bound, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, a);
 }
 
-void launch_deflate(const EncArgs &a, hipStream_t st) {
+void launch_deflate(const EncArgs &a, unsigned long long *scratch, int ncu, hipStream_t st) {
   uint64_t g = (a.nblocks + kDWaves - 1) / kDWaves;
   if (g > 8192) g = 8192;
-  if (a.level == 0)
+  if (a.level == 0) {
     hipLaunchKernelGGL(k_deflate_stored, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, a);
-  else
+  } else if (a.level == 1) {
     hipLaunchKernelGGL(k_deflate, dim3((unsigned)(g ? g : 1)), dim3(64 * kDWaves), 0, st, a);
+  } else {
+    uint64_t gd = (a.nblocks + kDyWaves - 1) / kDyWaves;
+    const uint64_t cap = deflate_dyn_grid(ncu);
+    if (gd > cap) gd = cap;
+    hipLaunchKernelGGL(k_deflate_dyn, dim3((unsigned)(gd ? gd : 1)), dim3(64 * kDyWaves), 0, st, a,
+                       reinterpret_cast<uint32_t *>(scratch));
+  }
 }
 
 }  // namespace rio

@@ -33,7 +33,10 @@ struct CrcTabs {
 };
 void launch_enc_chunks(const EncArgs &a, uint64_t nchunks, const CrcTabs &t, int ncu, hipStream_t st);
 void launch_deflate_bound(const EncArgs &a, hipStream_t st);
-void launch_deflate(const EncArgs &a, hipStream_t st);
+// level 0 stored, 1 fixed Huffman, others (the default -1 included) dynamic
+// Huffman, which needs scratch of deflate_scratch_words(ncu) u64
+uint64_t deflate_scratch_words(int ncu);
+void launch_deflate(const EncArgs &a, unsigned long long *scratch, int ncu, hipStream_t st);
 // zstd (zstd_enc.hip): tables of the predefined sequence codes (ZeTabs,
 // zstd_enc.h), scratch of zstd_enc_scratch_words(ncu) u64
 struct ZeTabs;

@@ -138,7 +138,7 @@ struct rio_ctx {
   uint64_t e_blk_cap = 0;
   uint8_t *e_hdr = nullptr, *e_comp = nullptr, *e_data = nullptr, *e_out = nullptr;
   uint64_t e_hdr_cap = 0, e_comp_cap = 0, e_data_cap = 0, e_out_cap = 0;
-  unsigned long long *e_zscr = nullptr;  // zstd encode: the waves' sequence lists
+  unsigned long long *e_zscr = nullptr;  // zstd / dynamic flate encode: the waves' sequence / token lists
   uint64_t e_zscr_cap = 0;
   ZeTabs *e_ztab = nullptr;              // zstd encode: predefined FSE tables (uploaded once)
   unsigned long long *e_ends = nullptr, *e_boff = nullptr;
@@ -1262,8 +1262,9 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
     HIP_OK(hipMemcpyAsync(&comp_total, ea.comp_off + nb, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (egrow(&c->e_comp, &c->e_comp_cap, comp_total + 64)) return -1;
+    if (ea.level != 0 && ea.level != 1 && egrow(&c->e_zscr, &c->e_zscr_cap, deflate_scratch_words(c->ncu))) return -1;
     ea.comp = c->e_comp;
-    launch_deflate(ea, st);
+    launch_deflate(ea, c->e_zscr, c->ncu, st);
   } else if (ea.codec == RIO_CODEC_ZSTD) {  // one frame per payload (zstd_enc.hip)
     launch_zstd_enc_bound(ea, st);
     launch_chunk_scan(ea.nck, ea.comp_off, d.scan_tmp, nb, st);

@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 #include <zlib.h>
+#include "zstd_enc.h"  // ZeBits
 #include "deflate_dyn.h"
 using namespace rio;
 
@@ -53,7 +54,9 @@ static std::vector<uint8_t> enc(const std::vector<uint8_t> &s) {
     DzTrees t; uint32_t wk[2 * kDzLit]; uint16_t par[2 * kDzLit];
     uint32_t lc2[kDzLit], dc2[kDzDist];
     memcpy(lc2, llc, sizeof lc2); memcpy(dc2, dc, sizeof dc2);
-    dz_build(lc2, dc2, t, wk, par);
+    dz_fill(lc2, dc2);
+    const uint32_t ln = dz_sort(lc2, kDzLit, t.ord);
+    dz_build(lc2, dc2, ln, t, wk, par);
     uint64_t dyn = t.hdr_bits, fix = 3;
     for (auto &k : toks) {
       uint32_t c, n, sym, e, v;

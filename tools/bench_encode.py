@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--replicas", type=int, default=32)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--codec", type=int, default=0)  # 0 none (C2 records), 1 flate / 2 zstd (C3 records)
+    ap.add_argument("--level", type=int, default=6)  # flate: 0 stored, 1 fixed Huffman, else dynamic
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -50,7 +51,7 @@ def main():
     out = torch.empty(cap, dtype=torch.uint8, device="cuda")
     boff = torch.empty(nb, dtype=torch.int64, device="cuda")
     ctx = gpu.Context(0, max_span_bytes=cap)
-    args = gpu.RioEncodeArgs(data.data_ptr(), ends.data_ptr(), n, per, a.codec, gpu.RIO_BLOCK_BODY, 6, 0)
+    args = gpu.RioEncodeArgs(data.data_ptr(), ends.data_ptr(), n, per, a.codec, gpu.RIO_BLOCK_BODY, a.level, 0)
     err = gpu.RioError()
     olen = ctypes.c_uint64()
     times = []
@@ -81,8 +82,8 @@ def main():
         ok = ok and detail["bytes_equal"]
     rec_bytes = int(data.numel())
     GiB = float(1 << 30)
-    res = {"workload": "encode %s records x %d (%d records, %d per block), codec %d" %
-           ("C2" if a.codec == 0 else "C3", R, n, per, a.codec),
+    res = {"workload": "encode %s records x %d (%d records, %d per block), codec %d level %d" %
+           ("C2" if a.codec == 0 else "C3", R, n, per, a.codec, a.level),
            "record_bytes": rec_bytes, "out_bytes": out_len, "ms": round(dt * 1e3, 3),
            "records_GiBps": round(rec_bytes / dt / GiB, 1),
            "hbm_alg_GBps": round((rec_bytes + out_len) / dt / 1e9, 1),  # records read + stream written
