@@ -301,9 +301,10 @@ __global__ void __launch_bounds__(256) k_deflate_stored(EncArgs a) {
 constexpr int kDySub = 32768;  // payload bytes per DEFLATE block
 constexpr int kDyWaves = 2;    // waves per workgroup (~23 KB LDS each)
 constexpr int kDyRing = 256;   // staging dwords: a dynamic header is <= 4,500 bits
+constexpr uint16_t kDyNone = 0xffff;
 
 struct alignas(16) DyWave {  // (16: the rank sort reads ll_cnt as uint4)
-  uint32_t hash[1 << kDHashBits];
+  uint16_t hash[1 << kDHashBits];  // low 16 bits of the last position (kDyNone: none)
   uint32_t ll_cnt[288], d_cnt[32];
   uint32_t w[kDzLit];
   uint16_t par[2 * kDzLit];
@@ -335,11 +336,14 @@ __device__ __forceinline__ void dy_mem_sync() {  // this wave's global stores vi
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__global__ void __launch_bounds__(64 * kDyWaves) k_deflate_dyn(EncArgs a, uint32_t *scratch) {
+#ifndef RIO_DY_ATTR
+#define RIO_DY_ATTR
+#endif
+__global__ void __launch_bounds__(64 * kDyWaves) RIO_DY_ATTR k_deflate_dyn(EncArgs a, uint32_t *scratch) {
   __shared__ DyWave s_w[kDyWaves];
   const int wv = threadIdx.x >> 6;
   DyWave &W = s_w[wv];
-  uint32_t *hash = W.hash;
+  uint16_t *hash = W.hash;
   uint32_t *ring = W.ring;
   DzTrees &t = W.t;
   const int l = lane_id();
@@ -349,7 +353,7 @@ __global__ void __launch_bounds__(64 * kDyWaves) k_deflate_dyn(EncArgs a, uint32
     const DSrc s = dsrc_of(a, b);
     const unsigned long long L = s.len;
     uint32_t *out = reinterpret_cast<uint32_t *>(a.comp + a.comp_off[b]);
-    for (int i = l; i < (1 << kDHashBits); i += 64) hash[i] = kDNone;
+    for (int i = l; i < (1 << kDHashBits); i += 64) hash[i] = kDyNone;
     for (int i = l; i < kDyRing; i += 64) ring[i] = 0;
     unsigned long long bitpos = 0, flushed = 0, cur = 0;
     auto flush = [&]() {
@@ -378,11 +382,15 @@ __global__ void __launch_bounds__(64 * kDyWaves) k_deflate_dyn(EncArgs a, uint32
         if (base + 64 < L) s.load16(p + 64, nx);
         const bool has4 = p + 4 <= L;
         const uint32_t h = (cw[0] * 0x9E3779B1u) >> (32 - kDHashBits);
-        const uint32_t cand = has4 ? hash[h] : kDNone;
+        // the candidate: the latest position with these low 16 bits (any
+        // earlier position of this block; the byte compare below decides)
+        const uint32_t e = has4 ? hash[h] : kDyNone;
+        const uint32_t delta = (uint32_t)(uint16_t)((uint32_t)p - e);
+        const unsigned long long cand = p - delta;
         wave_lds_sync();
-        if (has4) hash[h] = (uint32_t)p;
+        if (has4) hash[h] = (uint16_t)p;
         uint32_t m = 0;
-        if (has4 && p >= cur && p < b1 && cand != kDNone && p - cand <= 32768) {
+        if (has4 && p >= cur && p < b1 && e != kDyNone && delta != 0 && delta <= 32768) {
           const unsigned long long room = b1 - p;
           const uint32_t maxm = room < 258 ? (uint32_t)room : 258u;
           uint32_t cc[4];
@@ -559,7 +567,11 @@ __global__ void __launch_bounds__(64 * kDyWaves) k_deflate_dyn(EncArgs a, uint32
   }
 }
 
-static uint64_t deflate_dyn_grid(int ncu) { return (uint64_t)(ncu > 0 ? ncu : 256) * 3; }  // 3 workgroups per CU (LDS)
+#ifndef RIO_DY_WG
+#define RIO_DY_WG 4
+#endif
+// workgroups per CU: 4 (VGPRs: 2 waves per SIMD)
+static uint64_t deflate_dyn_grid(int ncu) { return (uint64_t)(ncu > 0 ? ncu : 256) * RIO_DY_WG; }
 
 uint64_t deflate_scratch_words(int ncu) { return deflate_dyn_grid(ncu) * kDyWaves * kDySub / 2; }
 
