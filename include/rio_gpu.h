@@ -235,11 +235,13 @@ typedef struct rio_encode_args {
                                   block ("flate N" transformer, recordioflate.go:31-52; any valid
                                   stream decodes alike -- the bytes are not klauspost's), or
                                   RIO_CODEC_ZSTD: one zstd frame per block ("zstd N",
-                                  recordiozstd.go:31-52; raw literals, predefined sequence
-                                  codes, <= 16 KiB blocks -- decoded by libzstd alike) */
+                                  recordiozstd.go:31-52; Huffman-coded literals where
+                                  they shrink, predefined sequence codes, <= 16 KiB blocks -- decoded by libzstd alike) */
     int32_t kind;              /* enum rio_block_kind */
-    int32_t level;             /* flate: 0 stored blocks (NoCompression), otherwise one
-                                  fixed-Huffman block with greedy hash-chain matches */
+    int32_t level;             /* flate: 0 stored blocks (NoCompression), 1 fixed-Huffman
+                                  blocks, otherwise (the default -1 included) a dynamic- or
+                                  fixed-Huffman block per 32 KiB, whichever is smaller; both
+                                  with greedy hash matches */
     int32_t reserved;
 } rio_encode_args;
 /* Host memory in and out: writes the chunk stream to out (out_cap bytes) and
