@@ -54,19 +54,18 @@ struct ZeSrc {
       else if (p >= hlen) q = data + (p - hlen);
     }
     if (q) {
+      // 5 aligned dwords funnel-shifted (v_alignbyte), branch-free across
+      // lanes; an aligned q reloads dword 3 as the 5th (the next may lie past
+      // the payload)
       const uintptr_t a = (uintptr_t)q;
       const uint32_t *d = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-      const uint32_t sh = (uint32_t)(a & 3) * 8;
-      if (sh == 0) {
+      const uint32_t nb = (uint32_t)(a & 3);
+      uint32_t e[5];
 #pragma unroll
-        for (int k = 0; k < 4; k++) w[k] = d[k];
-      } else {
-        uint32_t e[5];
+      for (int k = 0; k < 4; k++) e[k] = d[k];
+      e[4] = d[nb ? 4 : 3];
 #pragma unroll
-        for (int k = 0; k < 5; k++) e[k] = d[k];  // the 5th dword holds byte 15: inside the payload
-#pragma unroll
-        for (int k = 0; k < 4; k++) w[k] = (e[k] >> sh) | (e[k + 1] << (32 - sh));
-      }
+      for (int k = 0; k < 4; k++) w[k] = __builtin_amdgcn_alignbyte(e[k + 1], e[k], nb);
       return;
     }
 #pragma unroll
