@@ -33,8 +33,9 @@ class GpuWriter:
         if opts.MaxItems == 0:
             opts.MaxItems = F.DEFAULT_PACKED_ITEMS
         opts.MaxItems = min(opts.MaxItems, F.MAX_PACKED_ITEMS)
-        # transformers: none, or one "flate" / "flate N" (recordioflate.go:31-52) or
-        # "zstd" / "zstd N" (recordiozstd.go:31-52)
+        # transformers: none, or one "flate" / "flate N" (recordioflate.go:31-52: N = 0
+        # stored blocks, 1 fixed Huffman, otherwise dynamic Huffman per 32 KiB, the
+        # smaller of dynamic / fixed) or "zstd" / "zstd N" (recordiozstd.go:31-52)
         self.codec, self.level = gpu.RIO_CODEC_NONE, 0
         if opts.Transformers:
             name, _, arg = opts.Transformers[0].partition(" ")
