@@ -143,6 +143,10 @@ struct rio_ctx {
   ZeTabs *e_ztab = nullptr;              // zstd encode: predefined FSE tables (uploaded once)
   unsigned long long *e_ends = nullptr, *e_boff = nullptr;
   uint64_t e_ends_cap = 0, e_boff_cap = 0;
+  uint32_t *e_ckmap = nullptr;            // chunk -> block of the encoded stream
+  uint64_t e_ckmap_cap = 0;
+  unsigned long long *e_scan = nullptr;   // scan scratch of the per-block arrays
+  uint64_t e_scan_cap = 0;
   uint8_t *d_v1 = nullptr;
   uint64_t d_v1_cap = 0;
   V1Job *d_v1_jobs = nullptr;
@@ -202,7 +206,7 @@ static void free_all(rio_ctx *c) {
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.cmp, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len,
-                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab};
+                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan};
   for (void *p : ps)
     if (p) hipFree(p);
   if (c->h_ctl) hipHostFree(c->h_ctl);
@@ -257,6 +261,24 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   HIP_OK(hipMemcpy(d.crc_fix_b, fb.data(), fb.size() * 4, hipMemcpyHostToDevice));
   HIP_OK(hipHostMalloc((void **)&c->h_ctl, sizeof(Ctl), hipHostMallocDefault));
   return 0;
+}
+
+int rio_ctx_reserve_span(rio_ctx *c, uint64_t bytes) {
+  bytes = (bytes + kChunk - 1) / kChunk * kChunk;
+  if (bytes <= c->max_span) return 0;
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipStreamSynchronize(c->st));
+  if (c->st2 != c->st) HIP_OK(hipStreamSynchronize(c->st2));
+  c->max_span = bytes;
+  c->max_chunks = bytes / kChunk;
+  c->max_blocks = c->max_chunks;
+  if (c->side_cap < bytes / 8 + (1 << 20)) c->side_cap = bytes / 8 + (1 << 20);
+  if (c->item_cap < bytes / 64 + 1024) c->item_cap = bytes / 64 + 1024;
+  if (c->d_span) {  // host-span staging: reallocated at the new size on next use
+    hipFree(c->d_span);
+    c->d_span = nullptr;
+  }
+  return alloc_bufs(c);
 }
 
 rio_ctx *rio_open(const rio_config *cfg) {
@@ -1217,20 +1239,21 @@ int egrow(T **p, uint64_t *cap, uint64_t n) {
 
 }  // namespace
 
+// out == nullptr: sizing only (*out_len); out == kOwnOut: into the ctx's own
+// device buffer e_out (grown to the stream), block offsets into e_boff. The
+// per-block arrays, chunk map and scan scratch grow with the stream, so any
+// number of blocks / chunks encodes (no ctx span capacity applies).
+static uint8_t *const kOwnOut = reinterpret_cast<uint8_t *>(1);
+
 static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data, const unsigned long long *ends,
                       uint8_t *out, uint64_t out_cap, uint64_t *out_len, unsigned long long *boff, rio_error *err) {
-  DevBufs &d = c->d;
   hipStream_t st = c->st;
   const uint64_t per = a->items_per_block ? a->items_per_block : 16385;  // DefaultPackedItems + 1
   const uint64_t nb = a->n_items ? (a->n_items + per - 1) / per : 0;
   *out_len = 0;
   if (nb == 0) return 0;
-  if (nb > c->max_chunks) {
-    rio_set_error(err, RIO_ERR_CAPACITY, 0, "%" PRIu64 " blocks exceed the ctx's %" PRIu64 " chunks", nb,
-                  c->max_chunks);
-    return RIO_ERR_CAPACITY;
-  }
   if (egrow(&c->e_blk, &c->e_blk_cap, 6 * (nb + 1))) return -1;
+  if (egrow(&c->e_scan, &c->e_scan_cap, (nb + 2047) / 2048 + 16)) return -1;
   EncArgs ea{};
   ea.data = data;
   ea.item_end = ends;
@@ -1248,7 +1271,7 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
   ea.comp_off = c->e_blk + 5 * (nb + 1);
   HIP_OK(hipEventRecord(c->ev[kEvStart], st));
   launch_enc_count(ea, st);
-  launch_chunk_scan(ea.hdr_len, ea.hdr_off, d.scan_tmp, nb, st);
+  launch_chunk_scan(ea.hdr_len, ea.hdr_off, c->e_scan, nb, st);
   unsigned long long hdr_total = 0;
   HIP_OK(hipMemcpyAsync(&hdr_total, ea.hdr_off + nb, 8, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
@@ -1257,7 +1280,7 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
   launch_enc_header(ea, st);
   if (ea.codec == RIO_CODEC_FLATE) {  // the payloads compressed into comp (deflate_enc.hip)
     launch_deflate_bound(ea, st);
-    launch_chunk_scan(ea.nck, ea.comp_off, d.scan_tmp, nb, st);
+    launch_chunk_scan(ea.nck, ea.comp_off, c->e_scan, nb, st);
     unsigned long long comp_total = 0;
     HIP_OK(hipMemcpyAsync(&comp_total, ea.comp_off + nb, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -1267,7 +1290,7 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
     launch_deflate(ea, c->e_zscr, c->ncu, st);
   } else if (ea.codec == RIO_CODEC_ZSTD) {  // one frame per payload (zstd_enc.hip)
     launch_zstd_enc_bound(ea, st);
-    launch_chunk_scan(ea.nck, ea.comp_off, d.scan_tmp, nb, st);
+    launch_chunk_scan(ea.nck, ea.comp_off, c->e_scan, nb, st);
     unsigned long long comp_total = 0;
     HIP_OK(hipMemcpyAsync(&comp_total, ea.comp_off + nb, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -1283,24 +1306,25 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
     launch_zstd_enc(ea, c->e_ztab, c->e_zscr, c->ncu, st);
   }
   launch_enc_nck(ea, st);
-  launch_chunk_scan(ea.nck, ea.ck0, d.scan_tmp, nb, st);
+  launch_chunk_scan(ea.nck, ea.ck0, c->e_scan, nb, st);
   unsigned long long nchunks = 0;
   HIP_OK(hipMemcpyAsync(&nchunks, ea.ck0 + nb, 8, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   *out_len = nchunks * kChunk;
-  if (nchunks > c->max_chunks) {
-    rio_set_error(err, RIO_ERR_CAPACITY, 0, "%llu chunks exceed the ctx's %" PRIu64, nchunks, c->max_chunks);
-    return RIO_ERR_CAPACITY;
-  }
-  if (out && *out_len > out_cap) {
+  if (!out) return 0;  // sizing only
+  if (out == kOwnOut) {
+    if (egrow(&c->e_out, &c->e_out_cap, *out_len) || egrow(&c->e_boff, &c->e_boff_cap, nb + 1)) return -1;
+    out = c->e_out;
+    boff = c->e_boff;
+  } else if (*out_len > out_cap) {
     rio_set_error(err, RIO_ERR_CAPACITY, 0, "output too small: need %" PRIu64 " bytes", *out_len);
     return RIO_ERR_CAPACITY;
   }
-  if (!out) return 0;  // sizing only
-  ea.ck_block = d.ck_block;
+  if (egrow(&c->e_ckmap, &c->e_ckmap_cap, nchunks + 1)) return -1;
+  ea.ck_block = c->e_ckmap;
   ea.out = out;
   launch_enc_ckmap(ea, st);
-  launch_enc_chunks(ea, nchunks, CrcTabs{d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b}, c->ncu, st);
+  launch_enc_chunks(ea, nchunks, CrcTabs{c->d.crc_fold, c->d.crc_mul, c->d.crc_fix_a, c->d.crc_fix_b}, c->ncu, st);
   if (boff) launch_enc_boff(ea.ck0, boff, nb, st);
   HIP_OK(hipEventRecord(c->ev[kEvEnd], st));
   HIP_OK(hipStreamSynchronize(st));
@@ -1347,17 +1371,15 @@ extern "C" int rio_encode(rio_ctx *ctx, const rio_encode_args *a, uint8_t *out, 
   if (n) HIP_OK(hipMemcpyAsync(c->e_ends, a->item_end, n * 8, hipMemcpyHostToDevice, c->st));
   const uint64_t per = a->items_per_block ? a->items_per_block : 16385;
   const uint64_t nb = n ? (n + per - 1) / per : 0;
-  // size first, then encode into the ctx's device output and copy back
-  int rc = encode_dev(c, a, c->e_data, c->e_ends, nullptr, 0, out_len, nullptr, err);
+  // one pass: encoded into the ctx's device output (sized from the chunk
+  // counts), then copied back if the caller's buffer holds it
+  int rc = encode_dev(c, a, c->e_data, c->e_ends, kOwnOut, 0, out_len, nullptr, err);
   if (rc) return rc;
   if (*out_len > out_cap) {
     rio_set_error(err, RIO_ERR_CAPACITY, 0, "output too small: need %" PRIu64 " bytes", *out_len);
     return RIO_ERR_CAPACITY;
   }
   if (*out_len == 0) return 0;
-  if (egrow(&c->e_out, &c->e_out_cap, *out_len) || egrow(&c->e_boff, &c->e_boff_cap, nb + 1)) return -1;
-  rc = encode_dev(c, a, c->e_data, c->e_ends, c->e_out, c->e_out_cap, out_len, c->e_boff, err);
-  if (rc) return rc;
   HIP_OK(hipMemcpyAsync(out, c->e_out, *out_len, hipMemcpyDeviceToHost, c->st));
   if (block_off) HIP_OK(hipMemcpyAsync(block_off, c->e_boff, nb * 8, hipMemcpyDeviceToHost, c->st));
   HIP_OK(hipStreamSynchronize(c->st));

@@ -20,6 +20,9 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
 int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
                           rio_results *res, rio_batch *out);
 uint64_t rio_ctx_max_span(rio_ctx *c);
+// grow the ctx's span capacity (and the buffers sized by it) to at least
+// `bytes`; 0 on success (a no-op when it is already that large)
+int rio_ctx_reserve_span(rio_ctx *c, uint64_t bytes);
 // the ctx's pools of pinned buffers and result sets (scanners borrow and return them)
 int rio_ctx_take_buf(rio_ctx *c, uint64_t need, uint8_t **p, uint64_t *cap);
 void rio_ctx_give_buf(rio_ctx *c, uint8_t *p, uint64_t cap);

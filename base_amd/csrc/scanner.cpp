@@ -308,6 +308,8 @@ struct rio_scanner {
     }
     const int is_end = (at + got >= file_size);
     if (v1 && mode == 0) return rio_scan_v1_span_mode(ctx, *buf, got, at, is_end, rs, out);
+    // a header / trailer block longer than the ctx's span: the span grows to it
+    if (mode != 0 && rio_ctx_reserve_span(ctx, got) != 0) return -1;
     return rio_scan_span_mode(ctx, *buf, got, at, is_end, lim, cdc, mode, rs, out);
   }
   int decode(uint64_t at, uint64_t n, int32_t cdc, int32_t mode, uint64_t lim, rio_batch *out) {
@@ -365,7 +367,10 @@ void read_header(rio_scanner *s) {
     s->read_serial(hdr, sizeof(hdr), 0, &st);
     uint32_t total;
     memcpy(&total, hdr + 20, 4);
-    if (st == 0 && total > 0 && (uint64_t)total * kCk < n) n = (uint64_t)total * kCk;
+    if (st == 0 && total > 0) {  // the whole header block, however long (the span grows to it)
+      n = (uint64_t)total * kCk;
+      if (n > s->file_size) n = s->file_size;
+    }
   }
   rio_batch b;
   if (s->decode(0, n, RIO_CODEC_NONE, 1, UINT64_MAX, &b) != 0) {
@@ -378,7 +383,7 @@ void read_header(rio_scanner *s) {
     return;
   }
   if (b.n_blocks == 0) {
-    if (b.stop == RIO_STOP_MORE) {
+    if (b.stop == RIO_STOP_MORE) {  // (n is the header block's own extent: not reached)
       s->set_errf(RIO_ERR_CAPACITY, 0, "header block larger than the GPU span (%" PRIu64 " bytes)", maxspan);
       return;
     }
@@ -519,10 +524,28 @@ bool next_batch(rio_scanner *s) {
           s->done = true;
         }
       }
-      if (b.stop == RIO_STOP_MORE && b.consumed == 0) {
-        s->set_errf(RIO_ERR_CAPACITY, s->off, "block at offset %" PRIu64 " larger than the GPU span",
+      if (b.stop == RIO_STOP_MORE && b.consumed == 0 && s->v1) {
+        s->set_errf(RIO_ERR_CAPACITY, s->off, "record at offset %" PRIu64 " larger than the GPU span",
                     s->off);
         return false;
+      }
+      if (b.stop == RIO_STOP_MORE && b.consumed == 0) {
+        // a block longer than the ctx's span (the reference reads any block):
+        // the span grows to the block's extent (its first chunk's total) and
+        // the block decodes alone
+        uint8_t hdr[RIO_CHUNK_HEADER_SIZE];
+        int st;
+        s->read_full(hdr, sizeof(hdr), s->off, &st);
+        uint32_t total = 0;
+        if (st == 0) memcpy(&total, hdr + 20, 4);
+        uint64_t need = (uint64_t)total * kCk;
+        if (need > s->file_size - s->off) need = s->file_size - s->off;
+        if (need <= n || rio_ctx_reserve_span(s->ctx, need) != 0) {
+          s->set_errf(RIO_ERR_CAPACITY, s->off, "block at offset %" PRIu64 " larger than the GPU span",
+                      s->off);
+          return false;
+        }
+        continue;  // again, at the grown span
       }
       s->off += b.consumed;
       // the bytes after this span, read while the batch is consumed
@@ -862,7 +885,9 @@ int64_t rio_scanner_gather(rio_scanner *s, const uint64_t *blocks, const int64_t
     bl[i].off = uniq[i];
     uint8_t hdr[RIO_CHUNK_HEADER_SIZE];
     int st;
-    if (s->v1 || uniq[i] % kCk != 0 || uniq[i] >= s->file_size) continue;  // the exact path reports it
+    // the exact path reports these; a block at or past the shard's limit is EOF
+    // there (ChunkScanner.Scan, chunk.go:259-262), not an item
+    if (s->v1 || uniq[i] % kCk != 0 || uniq[i] >= s->file_size || uniq[i] >= s->limit) continue;
     s->read_full(hdr, sizeof(hdr), uniq[i], &st);
     if (st != 0) continue;
     uint32_t total, index;

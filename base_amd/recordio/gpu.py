@@ -26,6 +26,7 @@ LIB_PATH = os.environ.get("RIO_GPU_LIB") or os.path.join(_ROOT, "lib", "librio_g
 RIO_CODEC_NONE, RIO_CODEC_FLATE, RIO_CODEC_ZSTD = 0, 1, 2
 RIO_STOP_MORE, RIO_STOP_EOF, RIO_STOP_ERROR = 0, 1, 2
 RIO_ERR_CAPACITY = 98
+RIO_ERR_LOCATION = 22  # "Invalid location ..." / no item at a location (scannerv2.go:348-361)
 RIO_ERR_LEGACY = 20    # (no longer returned: v1 files decode natively)
 RIO_ERR_V1_RECORD = 24  # v1 record header / read errors (deprecated/recordio.go:258-300)
 RIO_ERR_V1_PACKED = 25  # v1 packed-record errors (deprecated/packer.go:214-272)
@@ -84,7 +85,7 @@ EXPORTS = [
     "rio_scanner_new", "rio_scanner_scan", "rio_scanner_get", "rio_scanner_next_batch", "rio_scanner_err",
     "rio_scanner_header_len", "rio_scanner_header_kv", "rio_scanner_trailer", "rio_scanner_seek",
     "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish", "rio_scanner_gather",
-    "rio_memory_reader", "rio_scan_v1_span", "rio_encode", "rio_encode_device",
+    "rio_memory_reader", "rio_scan_v1_span", "rio_encode", "rio_encode_device", "rio_build_id",
 ]
 
 _lib = None
@@ -99,7 +100,10 @@ def load(path: str = LIB_PATH):
             return _lib
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: run __graft_entry__.build() (there is no CPU fallback)")
+        from .. import build as B
+        B.check_lib(path)  # refuses a library not built from this tree's sources
         L = ctypes.CDLL(path)
+        L.rio_build_id.restype = ctypes.c_char_p
         P, U64, I64, I32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32
         L.rio_open.restype = P
         L.rio_open.argtypes = [ctypes.POINTER(RioConfig)]
@@ -339,6 +343,11 @@ def batch_items(b: RioBatch) -> List[bytes]:
     return items
 
 
+def build_id() -> str:
+    """rio_build_id() of the loaded library (the tree hash it was built from)."""
+    return load().rio_build_id().decode()
+
+
 def _hip():
     """The process's HIP runtime (the one librio_gpu.so bound: torch's, when imported first)."""
     return ctypes.CDLL("libamdhip64.so.7")
@@ -423,19 +432,28 @@ class MemorySource:
 
 
 class _FileReader:
-    """io.ReaderAt over a file object: os.pread when it has a descriptor,
-    else seek + read under a lock (the scanner's read-ahead thread and the
-    caller's thread -- Trailer, Gather -- may read at once)."""
+    """io.ReaderAt over a file object: os.pread for a plain OS file (raw or
+    buffered io.FileIO), else seek + read under a lock (the scanner's
+    read-ahead thread and the caller's thread -- Trailer, Gather -- may read at
+    once). Wrappers such as gzip.GzipFile or bz2.BZ2File expose the descriptor
+    of the compressed file underneath, so they are read through their own
+    seek + read, never pread."""
 
     def __init__(self, f):
+        import io
         self.f = f
         f.seek(0, os.SEEK_END)
         self.size = f.tell()
         self._lock = threading.Lock()
-        try:
-            self._fd = f.fileno()
-        except (AttributeError, OSError, ValueError):
-            self._fd = None
+        raw = f
+        if isinstance(f, (io.BufferedReader, io.BufferedRandom)):
+            raw = f.raw
+        self._fd = None
+        if isinstance(raw, io.FileIO):
+            try:
+                self._fd = raw.fileno()
+            except (OSError, ValueError):
+                self._fd = None
 
         def read_at(user, buf, n, off):
             try:

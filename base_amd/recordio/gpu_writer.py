@@ -8,13 +8,18 @@ zstd frames of the same payloads (GPU-encoded, deflate_enc.hip / zstd_enc.hip),
 so they decode to the same records. The reference serialises each block on a goroutine as it fills
 (MaxItems + 1 items, writerv2.go:315, 366-368) and writes blocks in sequence;
 here the items between two block-ending calls (Flush, SetTrailer, Finish) are
-kept and encoded by one rio_encode call -- once a run holds `batch_bytes`, its
-whole blocks are encoded early -- so thousands of blocks go through one launch.
+kept and encoded by rio_encode calls of up to `batch_bytes` of whole blocks
+each -- once a run holds `batch_bytes`, its whole blocks are encoded early -- so
+thousands of blocks go through one launch. Errors stick as the reference's
+errors.Once does: a transformer config that does not parse (NewWriter), or a
+flate level outside [-2, 9] (the first transformed block), stops every later
+write and is reported by Err() / Finish().
 The Index callback runs after a block's location is known, as in the
 reference (writerv2.go:458-470: after serialisation, before the write)."""
 from __future__ import annotations
 
 import dataclasses
+import re
 from typing import Optional
 
 from . import format as F
@@ -22,6 +27,19 @@ from . import gpu
 from .writer import ItemLocation, WriterOpts, _has_trailer
 
 _INITIAL, _BODY, _TRAILER, _FINISHED = range(4)
+_ATOI = re.compile(r"[+-]?[0-9]+\Z")
+
+
+def _atoi(config: str) -> int:
+    """Go's strconv.Atoi (decimal, optional sign), as recordioflate.Init and
+    recordiozstd.parseConfig parse a transformer's config
+    (recordioflate.go:76-81, recordiozstd.go:19-25)."""
+    if not _ATOI.match(config):
+        raise RuntimeError('strconv.Atoi: parsing "%s": invalid syntax' % config)
+    v = int(config)
+    if not -(1 << 63) <= v < (1 << 63):
+        raise RuntimeError('strconv.Atoi: parsing "%s": value out of range' % config)
+    return v
 
 
 class GpuWriter:
@@ -33,6 +51,12 @@ class GpuWriter:
         if opts.MaxItems == 0:
             opts.MaxItems = F.DEFAULT_PACKED_ITEMS
         opts.MaxItems = min(opts.MaxItems, F.MAX_PACKED_ITEMS)
+        self.opts = opts
+        self.out = out
+        self.ctx = ctx or gpu.default_context()
+        self.batch_bytes = batch_bytes
+        self.n_written = 0
+        self.err: Optional[Exception] = None
         # transformers: none, or one "flate" / "flate N" (recordioflate.go:31-52: N = 0
         # stored blocks, 1 fixed Huffman, otherwise dynamic Huffman per 32 KiB, the
         # smaller of dynamic / fixed) or "zstd" / "zstd N" (recordiozstd.go:31-52)
@@ -43,13 +67,12 @@ class GpuWriter:
                 raise ValueError("GpuWriter encodes none or one flate / zstd transformer (got %r)"
                                  % (opts.Transformers,))
             self.codec = gpu.RIO_CODEC_FLATE if name == "flate" else gpu.RIO_CODEC_ZSTD
-            self.level = int(arg) if arg.strip() else -1
-        self.opts = opts
-        self.out = out
-        self.ctx = ctx or gpu.default_context()
-        self.batch_bytes = batch_bytes
-        self.n_written = 0
-        self.err: Optional[Exception] = None
+            self.level = -1
+            if arg:
+                try:  # a config error is NewWriter's: w.err.Set (writerv2.go:318-320)
+                    self.level = _atoi(arg)
+                except RuntimeError as e:
+                    self._set_err(e)
         self.header = []
         self.state = _BODY if opts.SkipHeader else _INITIAL
         if not opts.SkipHeader:
@@ -61,28 +84,72 @@ class GpuWriter:
         self.run_items = []  # ... and their marshalled bytes
         self.run_bytes = 0
 
+    def _set_err(self, e):
+        if self.err is None:  # errors.Once: the first error sticks
+            self.err = e
+
+    def _transform_err(self):
+        """The error klauspost's flate.NewWriter returns on the first block a
+        transform runs on (recordioflate.go:31-34: levels outside
+        [HuffmanOnly, BestCompression] = [-2, 9])."""
+        if self.codec == gpu.RIO_CODEC_FLATE and not -2 <= self.level <= 9:
+            return RuntimeError("flate: invalid compression level %d: want value in range [-2, 9]" % self.level)
+        return None
+
     def _write(self, data: bytes):
-        self.out.write(data)
-        self.n_written += len(data)
+        if self.err is None:  # flushBlock writes only while no error is set (writerv2.go:491-495)
+            self.out.write(data)
+            self.n_written += len(data)
+
+    def _encode_blocks(self, items, per: int, kind: int):
+        """rio_encode of whole blocks; the error sticks (serializeBlock's fq.err.Set)."""
+        if self.err is None and kind != gpu.RIO_BLOCK_HEADER:
+            e = self._transform_err()
+            if e is not None:
+                self._set_err(e)
+        if self.err is not None:
+            return None, None
+        try:
+            return self.ctx.encode(items, per, kind, self.codec if kind != gpu.RIO_BLOCK_HEADER else
+                                   gpu.RIO_CODEC_NONE, self.level)
+        except gpu.RecordioError as e:
+            self._set_err(e)
+            return None, None
 
     def _encode_run(self, n: int):
-        """Encode the first n items of the run (whole blocks unless the run ends)."""
-        if n == 0:
-            return
-        objs, items = self.run_objs[:n], self.run_items[:n]
-        del self.run_objs[:n], self.run_items[:n]
-        self.run_bytes -= sum(len(x) for x in items)
+        """Encode the first n items of the run (whole blocks unless the run ends),
+        one rio_encode call per group of whole blocks of at most batch_bytes (a
+        single larger block alone). The run keeps its items until they are
+        encoded (or the writer's error is set)."""
         per = self.opts.MaxItems + 1
-        data, boff = self.ctx.encode(items, per, gpu.RIO_BLOCK_BODY, self.codec, self.level)
-        base = self.n_written
-        if self.opts.Index is not None:
-            for i, v in enumerate(objs):
-                self.opts.Index(ItemLocation(base + boff[i // per], i % per), v)
-        self._write(data)
+        done = 0
+        while done < n:
+            # whole blocks while the group stays within batch_bytes (at least one)
+            end, nbytes = done, 0
+            while end < n:
+                blk = self.run_items[end:min(end + per, n)]
+                b = sum(len(x) for x in blk)
+                if end > done and nbytes + b > self.batch_bytes:
+                    break
+                nbytes += b
+                end = min(end + per, n)
+            objs, items = self.run_objs[done:end], self.run_items[done:end]
+            data, boff = self._encode_blocks(items, per, gpu.RIO_BLOCK_BODY)
+            base = self.n_written
+            if self.opts.Index is not None:  # called even after an error, as flushBlock does
+                for i, v in enumerate(objs):
+                    off = base + boff[i // per] if boff is not None else base
+                    self.opts.Index(ItemLocation(off, i % per), v)
+            if data is not None:
+                self._write(data)
+            done = end
+        del self.run_objs[:n], self.run_items[:n]
+        self.run_bytes = sum(len(x) for x in self.run_items)
 
     def _flush_header(self):
-        data, _ = self.ctx.encode([F.marshal_header(self.header)], 1, gpu.RIO_BLOCK_HEADER)
-        self._write(data)
+        data, _ = self._encode_blocks([F.marshal_header(self.header)], 1, gpu.RIO_BLOCK_HEADER)
+        if data is not None:
+            self._write(data)
 
     def AddHeader(self, key: str, value):
         if self.state != _INITIAL:
@@ -120,8 +187,9 @@ class GpuWriter:
         else:
             raise RuntimeError(f"SetTrailer: wrong state: {self.state}")
         self.state = _TRAILER
-        enc, _ = self.ctx.encode([bytes(data)], 1, gpu.RIO_BLOCK_TRAILER, self.codec, self.level)
-        self._write(enc)
+        enc, _ = self._encode_blocks([bytes(data)], 1, gpu.RIO_BLOCK_TRAILER)
+        if enc is not None:
+            self._write(enc)
 
     def Err(self):
         return self.err

@@ -332,10 +332,8 @@ def main():
     else:
         torch.cuda.set_device(local)
 
-    from base_amd import build as B
-    if not os.path.exists(B.LIB):
-        B.build()
     from base_amd.recordio import gpu
+    gpu.load()  # refuses a library whose build id is not this tree's (base_amd/build.py)
 
     data, nrec = make_c2_file()
     body = data[CHUNK:]
@@ -413,7 +411,8 @@ def main():
                       "records_per_gpu": int(n_items), "record_bytes": RECORD_SIZE,
                       "parallelism": f"{world} GPU(s), independent replica sets",
                       "bytes_in_per_gpu": span_len},
-           "roofline": roof}
+           "roofline": roof,
+           "build_id": gpu.build_id(), "lib": os.path.relpath(gpu.LIB_PATH, ROOT)}
     ctx.close()
     del dev
     torch.cuda.empty_cache()

@@ -153,6 +153,9 @@ void rio_close(rio_ctx *ctx);
 /* thread-local text of the last rio_open / ABI failure */
 const char *rio_last_error(void);
 int rio_abi_version(void);
+/* build provenance: a hash of the library's sources, this header and its
+ * compile flags (16 hex digits; base_amd/build.py tree_build_id) */
+const char *rio_build_id(void);
 /* the HIP stream the ctx launches on (hipStream_t as void*) */
 void *rio_stream(rio_ctx *ctx);
 
@@ -248,8 +251,8 @@ typedef struct rio_encode_args {
  * each block's offset in it (ItemLocation.Block minus the stream's file
  * offset) to block_off (ceil(n_items / items_per_block) entries, may be NULL).
  * Returns 0 with *out_len; RIO_ERR_CAPACITY with the needed *out_len when out
- * is too small, or when the stream exceeds the ctx's span capacity; < 0 on a
- * runtime failure. */
+ * is too small; < 0 on a runtime failure. The stream is encoded once (into
+ * device memory the ctx grows to fit; the ctx's span capacity does not apply). */
 int rio_encode(rio_ctx *ctx, const rio_encode_args *a, uint8_t *out, uint64_t out_cap, uint64_t *out_len,
                uint64_t *block_off, rio_error *err);
 /* The same with data, item_end, out and block_off in device memory (the

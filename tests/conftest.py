@@ -42,10 +42,8 @@ def golden_bytes(case):
 
 @pytest.fixture(scope="session")
 def gpu_lib():
-    """librio_gpu.so, built in-tree; a GPU test fails loudly when it is missing."""
-    from base_amd import build as B
-    if not os.path.exists(B.LIB):
-        B.build()
+    """librio_gpu.so, built in-tree; a GPU test fails loudly when it is missing or
+    was not built from this tree's sources (its build id, base_amd/build.py)."""
     from base_amd.recordio import gpu
     return gpu.load()
 

@@ -287,3 +287,29 @@ def test_async_device_path_after_host_result(gpu_ctx, oracle, codec):
     b = gpu_ctx.sync()
     assert b.err.code == 0, b.err.msg
     assert gpu.device_batch_items(b, body) == recs
+
+
+def test_file_objects(gpu_ctx, oracle, tmp_path):
+    """NewScanner over file objects (the reference takes an io.ReadSeeker): a
+    raw and a buffered OS file are read with pread; a gzip.GzipFile (whose
+    fileno() is the compressed file's descriptor) through its own seek + read,
+    so the decompressed bytes are scanned."""
+    import gzip
+    from base_amd.recordio import gpu
+    from base_amd.recordio.writer import WriterOpts, write_file
+    rng = random.Random(9)
+    recs = [rng.randbytes(rng.randrange(0, 3000)) for _ in range(800)]
+    data = write_file(recs, WriterOpts(MaxItems=31), trailer=b"tr")
+    plain = tmp_path / "f.rio"
+    plain.write_bytes(data)
+    gz = tmp_path / "f.rio.gz"
+    with gzip.open(gz, "wb") as f:
+        f.write(data)
+    for opener in (lambda: open(plain, "rb"), lambda: open(plain, "rb", buffering=0), lambda: gzip.open(gz, "rb")):
+        with opener() as f:
+            sc = gpu.NewScanner(f, ctx=gpu_ctx)
+            assert sc.Trailer() == b"tr"
+            got = []
+            while sc.Scan():
+                got.append(sc.Get())
+            assert sc.Finish() is None and got == recs

@@ -105,18 +105,94 @@ def test_encode_c2_round_trip(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_encode_capacity(gpu_ctx):
-    """A stream larger than the ctx's span reports RIO_ERR_CAPACITY."""
+def test_encode_past_ctx_span(gpu_ctx):
+    """rio_encode grows its own buffers: a stream longer than the ctx's span
+    encodes (no RIO_ERR_CAPACITY), and a scanner on that small ctx reads a block
+    longer than its span (the span grows to the block, as the reference reads
+    any block)."""
     from base_amd.recordio import gpu
-    ctx = gpu.Context(0, max_span_bytes=1 << 20)
+    ctx = gpu.Context(0, max_span_bytes=1 << 20)  # 32 chunks
     try:
-        with pytest.raises(gpu.RecordioError) as e:
-            ctx.encode([b"x" * 200000] * 10, 1)
-        assert e.value.code == gpu.RIO_ERR_CAPACITY
-        data, boff = ctx.encode([b"x" * 200000] * 3, 1)  # 3 blocks x 7 chunks fit
-        assert len(data) == 21 * 32768 and boff == [0, 7 * 32768, 14 * 32768]
+        data, boff = ctx.encode([b"x" * 200000] * 10, 1)  # 10 blocks x 7 chunks
+        assert len(data) == 70 * 32768 and boff == [7 * 32768 * i for i in range(10)]
+        recs = [bytes([i]) * 150000 for i in range(20)]  # one block of 3 MB
+        got = gpu_write(recs, WriterOpts(), ctx=ctx)
+        assert got == write_file(recs, WriterOpts())
+        sc = gpu.NewScanner(got, ctx=ctx)
+        items = []
+        while sc.Scan():
+            items.append(sc.Get())
+        assert sc.Finish() is None and items == recs
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_writer_block_larger_than_default_span(gpu_ctx):
+    """16,385 items of 20 KiB at the default MaxItems: one block of 336 MB, more
+    than the default ctx's 256 MiB span. The writer encodes it, and
+    it scans back through a 64 MiB-span ctx."""
+    import hashlib
+    import os
+    from base_amd.recordio import gpu
+    blob = os.urandom(16385 * 20480)
+    recs = [blob[i * 20480:(i + 1) * 20480] for i in range(16385)]
+    buf = io.BytesIO()
+    from base_amd.recordio.gpu_writer import GpuWriter
+    w = GpuWriter(buf, WriterOpts(KeyTrailer=True))
+    for r in recs:
+        w.Append(r)
+    w.SetTrailer(b"end")
+    assert w.Finish() is None
+    data = buf.getvalue()
+    sc = gpu.NewScanner(data, ctx=gpu_ctx)
+    assert sc.Trailer() == b"end"
+    h, n = hashlib.sha256(), 0
+    while True:
+        got = sc.ScanBatch(1 << 14)
+        if not got:
+            break
+        for r in got:
+            assert len(r) == 20480
+            h.update(r)
+        n += len(got)
+    assert sc.Finish() is None and n == 16385
+    assert h.digest() == hashlib.sha256(blob).digest()
+
+
+@pytest.mark.gpu
+def test_writer_config_errors(gpu_ctx):
+    """Transformer configs as the reference's factories parse them: a config
+    that is not a decimal int fails NewWriter (strconv.Atoi's error, nothing
+    written); a flate level outside [-2, 9] fails the first transformed block
+    (klauspost flate.NewWriter's error: the header is written, the block is not),
+    and the error sticks (Err, Finish)."""
+    from base_amd.recordio.gpu_writer import GpuWriter
+    for cfg in ("flate x", "zstd 1.5", "flate  3"):
+        buf = io.BytesIO()
+        w = GpuWriter(buf, WriterOpts(Transformers=[cfg]), ctx=gpu_ctx)
+        w.Append(b"abc")
+        arg = cfg.split(" ", 1)[1]
+        assert str(w.Err()) == 'strconv.Atoi: parsing "%s": invalid syntax' % arg
+        assert str(w.Finish()) == str(w.Err()) and buf.getvalue() == b""
+    for lvl in (10, -3, 42):
+        buf = io.BytesIO()
+        w = GpuWriter(buf, WriterOpts(Transformers=["flate %d" % lvl], MaxItems=2), ctx=gpu_ctx)
+        assert w.Err() is None
+        for i in range(7):
+            w.Append(b"item %d" % i)
+        msg = "flate: invalid compression level %d: want value in range [-2, 9]" % lvl
+        assert str(w.Finish()) == msg
+        assert len(buf.getvalue()) == 32768  # the header block alone
+    for cfg in ("flate -2", "flate +9", "flate 0", "zstd -7", "zstd 30"):
+        recs = [b"r%d" % i * 40 for i in range(100)]
+        got = gpu_write(recs, WriterOpts(Transformers=[cfg], MaxItems=13), ctx=gpu_ctx)
+        from base_amd.recordio import gpu
+        sc = gpu.NewScanner(got, ctx=gpu_ctx)
+        items = []
+        while sc.Scan():
+            items.append(sc.Get())
+        assert sc.Finish() is None and items == recs, cfg
 
 
 def fastq_records(rng, n):

@@ -114,3 +114,35 @@ def test_memory_reader_and_readahead(oracle, transformers):
         t.join()
     for items, err in out:
         assert err is None and items == ref.items
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transformers", CODECS)
+def test_gather_respects_shard_limit(gpu_ctx, oracle, transformers):
+    """Gather on a NewShardScanner: a location in a block at or past the shard's
+    limit is what Seek + Scan gives there -- ChunkScanner.Scan stops at the limit
+    (chunk.go:259-262), so there is no item -- on the fast path as on the exact
+    one; locations inside the shard return their items."""
+    from base_amd.recordio import gpu
+    from base_amd.recordio.writer import ItemLocation
+    _skip(transformers, oracle)
+    recs, data = _file(transformers, 51, n=900, max_items=29)
+    ref = oracle.scan(data)
+    sc = gpu.NewShardScanner(data, gpu.ScannerOpts(), 0, 1, 2, ctx=gpu_ctx)
+    mine = []
+    while sc.Scan():
+        mine.append(sc.Get())
+    assert sc.Err() is None and 0 < len(mine) < len(recs)
+    inside = [ItemLocation(*ref.locations[i]) for i in range(0, len(mine), 7)]
+    assert sc.Gather(inside) == [recs[i] for i in range(0, len(mine), 7)]
+    outside = ItemLocation(*ref.locations[len(mine) + 5])
+    # the exact path: Seek + Scan on a scanner of the same shard finds no item
+    ex = gpu.NewShardScanner(data, gpu.ScannerOpts(), 0, 1, 2, ctx=gpu_ctx)
+    ex.Seek(outside)
+    assert ex.Err() is None and not ex.Scan()
+    ex.Finish()
+    with pytest.raises(gpu.RecordioError) as ei:
+        sc.Gather(inside[:2] + [outside])
+    assert ei.value.index == 2 and ei.value.items == [recs[0], recs[7]]
+    assert ei.value.code == gpu.RIO_ERR_LOCATION
+    sc.Finish()
