@@ -205,6 +205,8 @@ __global__ void __launch_bounds__(256) RIO_LEAN_ATTR k_parse_lean(DevBufs d, Par
             ParseOut po;
             po.item_off = d.item_off;
             po.item_len = d.item_len;
+            po.item_end = a.end_mode ? d.item_off : nullptr;
+            po.whole = false;
             po.item_base = bases[j];
             po.item_cap = a.item_cap;
             po.view_base = 0;
@@ -223,6 +225,7 @@ __global__ void __launch_bounds__(256) RIO_LEAN_ATTR k_parse_lean(DevBufs d, Par
           d.blk_a[b] = 0;
           d.blk_b[b] = 0;
           d.blk_hdr[b] = hdr;
+          if (a.end_mode) d.blk_data[b] = c0s[j] * (uint64_t)kChunk;
         } else {
           d.blk_coff[atomicAdd(&d.ctl->n_retry, 1ull)] = b;
         }
@@ -259,9 +262,15 @@ __global__ void __launch_bounds__(256) k_parse_slow(DevBufs d, ParseArgs a) {
       const unsigned long long len = (a.codec == RIO_CODEC_NONE) ? d.blk_len[b] : d.blk_out_len[b];
       const Payload pl = (a.codec != RIO_CODEC_NONE) ? make_contig_payload(d.dec + d.blk_dec_off[b], len)
                                                      : desc_payload(a.span, d, c0, meta, len, d.ck_pay[c0]);
+      // item-end mode, none codec, chunks other than the last short (not what
+      // the writer makes, but valid): the payload is gathered whole into the
+      // span-shaped side buffer at the block's own offset, where it fits
+      const bool whole = a.end_mode && a.codec == RIO_CODEC_NONE && !pl.regular && total > 1;
       ParseOut po;
       po.item_off = d.item_off;
       po.item_len = d.item_len;
+      po.item_end = a.end_mode ? d.item_off : nullptr;
+      po.whole = whole;
       po.item_base = d.blk_item_base[b];
       po.item_cap = a.item_cap;
       po.view_base = (a.codec != RIO_CODEC_NONE) ? (kItemInRecords | d.blk_dec_off[b]) : 0;
@@ -276,6 +285,14 @@ __global__ void __launch_bounds__(256) k_parse_slow(DevBufs d, ParseArgs a) {
           if (l == 0) atomicOr(&d.ctl->out_overflow, 16ull);
         } else {
           parse_header<kParseWrite>(pl, r, po);
+          if (whole) {  // chunk by chunk, back to back
+            uint64_t o = 0;
+            for (uint64_t c = c0; c < c0 + total; c++) {
+              const uint64_t n = d.ck_size[c];
+              for (uint64_t k = l; k < n; k += 64) d.side[c0 * kChunk + o + k] = a.span[c * kChunk + kChunkHdr + k];
+              o += n;
+            }
+          }
         }
       }
       if (l == 0) {
@@ -283,6 +300,10 @@ __global__ void __launch_bounds__(256) k_parse_slow(DevBufs d, ParseArgs a) {
         d.blk_a[b] = r.a;
         d.blk_b[b] = r.b;
         d.blk_hdr[b] = r.hdr_len;
+        if (a.end_mode && r.status == kBlkOk)
+          d.blk_data[b] = (a.codec != RIO_CODEC_NONE) ? (kItemInRecords | d.blk_dec_off[b])
+                          : whole                     ? (kItemInRecords | c0 * (uint64_t)kChunk)
+                                                      : c0 * (uint64_t)kChunk;
         if (r.status != kBlkOk && a.mode == kModeBody) atomicMin(&d.ctl->first_block_event, 2 * (c0 + total - 1) + 1);
       }
     }
@@ -322,7 +343,7 @@ __global__ void __launch_bounds__(256) k_dec_nitems(DevBufs d, const unsigned lo
 // whole wave across the chunk header(s) into the side buffer -- at its own span
 // offset (sparse) or at ck_sbase[slot] (compact) -- and the item's view set.
 __global__ void __launch_bounds__(256) k_strad(const uint8_t *__restrict__ span, DevBufs d, uint64_t nslots,
-                                               uint64_t side_cap, int32_t sparse) {
+                                               uint64_t side_cap, int32_t sparse, int32_t end_mode) {
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const int l = lane_id();
@@ -341,7 +362,7 @@ __global__ void __launch_bounds__(256) k_strad(const uint8_t *__restrict__ span,
         if (l == 0) atomicOr(&d.ctl->out_overflow, 4ull);
         continue;
       }
-      if (l == 0) d.item_off[s.item] = kItemInRecords | dst;
+      if (l == 0 && !end_mode) d.item_off[s.item] = kItemInRecords | dst;  // (item-end mode: implied)
       // piecewise: each piece is contiguous in one chunk payload
       unsigned long long p = s.src, o = 0;
       while (o < s.len) {
@@ -556,13 +577,38 @@ void launch_dec_nitems(const DevBufs &d, const unsigned long long *nblocks, uint
   hipLaunchKernelGGL(k_dec_nitems, dim3(grid_of(max_blocks, 256, 1024)), dim3(256), 0, st, d, nblocks);
 }
 
-void launch_strad(const uint8_t *span, const DevBufs &d, uint64_t nslots, uint64_t side_cap, int32_t sparse,
+void launch_strad(const uint8_t *span, const DevBufs &d, uint64_t nslots, uint64_t side_cap, int32_t sparse, int32_t end_mode,
                   hipStream_t st) {
-  hipLaunchKernelGGL(k_strad, dim3(grid_of(nslots, 256, 1024)), dim3(256), 0, st, span, d, nslots, side_cap, sparse);
+  hipLaunchKernelGGL(k_strad, dim3(grid_of(nslots, 256, 1024)), dim3(256), 0, st, span, d, nslots, side_cap, sparse, end_mode);
 }
 
 void launch_resolve(const DevBufs &d, const ResolveArgs &a, hipStream_t st) {
   hipLaunchKernelGGL(k_resolve, dim3(1), dim3(64), 0, st, d, a);
+}
+
+// Segment scans (rio_scan_device_segments_async): each valid block's file
+// (the segment holding its first chunk) and its offset in that file.
+__global__ void __launch_bounds__(256) k_block_files(DevBufs d, const unsigned long long *seg_end,
+                                                     const unsigned long long *seg_file_off, uint64_t nseg) {
+  const uint64_t nb = d.ctl->n_valid_blocks;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long off = d.blk_c0[b] * (unsigned long long)kChunk;
+    uint64_t lo = 0, hi = nseg;  // first segment whose end is past off
+    while (lo < hi) {
+      const uint64_t m = (lo + hi) >> 1;
+      if (seg_end[m] <= off) lo = m + 1;
+      else hi = m;
+    }
+    const unsigned long long s0 = lo ? seg_end[lo - 1] : 0;
+    d.blk_seg[b] = lo;
+    d.blk_file_off[b] = (lo < nseg ? seg_file_off[lo] : 0) + (off - s0);
+  }
+}
+
+void launch_block_files(const DevBufs &d, const unsigned long long *seg_end, const unsigned long long *seg_file_off,
+                        uint64_t nseg, uint64_t max_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_block_files, dim3(grid_of(max_blocks, 256, 2048)), dim3(256), 0, st, d, seg_end, seg_file_off,
+                     nseg);
 }
 
 }  // namespace rio

@@ -210,6 +210,8 @@ struct HdrResult {
 // where kParseWrite puts item views and straddler descriptors
 struct ParseOut {
   unsigned long long *item_off, *item_len;
+  unsigned long long *item_end;  // item-end mode: cumSize per item here (item_off / item_len unused)
+  bool whole;                    // item-end mode: the block's payload is gathered whole (no straddlers)
   uint64_t item_base, item_cap;
   unsigned long long view_base;  // compressed: kItemInRecords | offset of the decoded block
   StradDesc *strad;              // per chunk slot
@@ -234,10 +236,24 @@ __device__ __forceinline__ unsigned long long pad16(unsigned long long n) { retu
 // item crossing a chunk payload boundary, a straddler descriptor in the slot of
 // the chunk it starts in (k_strad fills item_off)
 __device__ __forceinline__ void emit_item(const Payload &pl, const ParseOut &po, uint64_t o, unsigned long long st,
-                                          unsigned long long v) {
+                                          unsigned long long v, unsigned long long cum) {
   const uint64_t slot = po.item_base + (o - 1);
   if (slot >= po.item_cap) {
     atomicOr(po.overflow, 1ull);
+    return;
+  }
+  if (po.item_end) {  // cumSize (scannerv2.go:83-91); a straddler still needs its bytes gathered
+    po.item_end[slot] = cum;
+    if (po.whole || !(v > 0 && pl.straddles(st, v))) return;
+    uint64_t c, lo;
+    pl.chunk_of(st, c, lo);
+    StradDesc dsc;
+    dsc.c0 = pl.c0;
+    dsc.src = st;
+    dsc.len = v;
+    dsc.item = slot;
+    po.strad[c] = dsc;
+    po.ssz[c] = pad16(v);
     return;
   }
   po.item_len[slot] = v;
@@ -352,7 +368,7 @@ __device__ HdrResult parse_header(const Payload &pl, const HdrResult &known, con
           if (pass == 0) {
             if (v > plen) lrange = true;
           } else {
-            emit_item(pl, po, o, hdr + run + lsum, v);
+            emit_item(pl, po, o, hdr + run + lsum, v, run + lsum + v);
           }
           lsum += v;
         }
@@ -576,7 +592,23 @@ __device__ __forceinline__ int small_header(const Payload &pl, const ParseOut &p
     unsigned long long phys = 0;
     if (o <= nitems) {
       const uint64_t slot = po.item_base + (o - 1);
-      if (slot < po.item_cap) {
+      if (slot < po.item_cap && po.item_end) {  // cumSize: the item's end past the header
+        view_store(po.item_end + slot, (unsigned long long)(sk + vk - hdr));
+        if (chunks) {
+          const uint32_t j = sk / (uint32_t)kMaxPayload;
+          sd = vk > 0 && j != (sk + vk - 1) / (uint32_t)kMaxPayload;
+          phys = (pl.c0 + j) * (unsigned long long)kChunk + kChunkHdr + (sk - j * (uint32_t)kMaxPayload);
+          if (sd && !sparse_side) {
+            StradDesc dsc;
+            dsc.c0 = pl.c0;
+            dsc.src = sk;
+            dsc.len = vk;
+            dsc.item = slot;
+            po.strad[pl.c0 + j] = dsc;
+            po.ssz[pl.c0 + j] = pad16(vk);
+          }
+        }
+      } else if (slot < po.item_cap) {
         view_store(po.item_len + slot, vk);
         if (pl.contig) {
           view_store(po.item_off + slot, po.view_base + sk);
@@ -695,7 +727,23 @@ __device__ bool fast_header(const Payload &pl, const uint32_t (&w)[4], HdrResult
     unsigned long long phys = 0;
     if (have) {
       const uint64_t slot = po.item_base + (o - 1);
-      if (slot < po.item_cap) {
+      if (slot < po.item_cap && po.item_end) {  // cumSize
+        po.item_end[slot] = st + v - hdr;
+        if (chunks) {
+          const uint32_t j = st / (uint32_t)kMaxPayload;
+          sd = v > 0 && j != (st + (uint32_t)v - 1) / (uint32_t)kMaxPayload;
+          phys = (pl.c0 + j) * (unsigned long long)kChunk + kChunkHdr + (st - j * (uint32_t)kMaxPayload);
+          if (sd && !sparse_side) {
+            StradDesc dsc;
+            dsc.c0 = pl.c0;
+            dsc.src = st;
+            dsc.len = v;
+            dsc.item = slot;
+            po.strad[pl.c0 + j] = dsc;
+            po.ssz[pl.c0 + j] = pad16(v);
+          }
+        }
+      } else if (slot < po.item_cap) {
         po.item_len[slot] = v;
         if (pl.contig) {
           po.item_off[slot] = po.view_base + st;

@@ -70,6 +70,8 @@ __device__ __forceinline__ void parse_block(const DevBufs &d, const ParseArgs &a
       ParseOut po;
       po.item_off = d.item_off;
       po.item_len = d.item_len;
+      po.item_end = a.end_mode ? d.item_off : nullptr;
+      po.whole = false;
       po.item_base = base;
       po.item_cap = a.item_cap;
       po.view_base = (a.codec != RIO_CODEC_NONE) ? (kItemInRecords | d.blk_dec_off[b]) : 0;
@@ -92,6 +94,8 @@ __device__ __forceinline__ void parse_block(const DevBufs &d, const ParseArgs &a
     d.blk_a[b] = ea;
     d.blk_b[b] = eb;
     d.blk_hdr[b] = hdr;
+    if (a.end_mode && status == kBlkOk)
+      d.blk_data[b] = (a.codec != RIO_CODEC_NONE) ? (kItemInRecords | d.blk_dec_off[b]) : c0 * (uint64_t)kChunk;
     if (event != kNone) atomicMin(&d.ctl->first_block_event, event);
   }
 }

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -40,9 +41,11 @@ void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hip
 void launch_parse_lean(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
 void launch_parse_slow(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
 void launch_dec_nitems(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st);
-void launch_strad(const uint8_t *span, const DevBufs &d, uint64_t nslots, uint64_t side_cap, int32_t sparse,
+void launch_strad(const uint8_t *span, const DevBufs &d, uint64_t nslots, uint64_t side_cap, int32_t sparse, int32_t end_mode,
                   hipStream_t st);
 void launch_resolve(const DevBufs &d, const ResolveArgs &a, hipStream_t st);
+void launch_block_files(const DevBufs &d, const unsigned long long *seg_end, const unsigned long long *seg_file_off,
+                        uint64_t nseg, uint64_t max_blocks, hipStream_t st);
 // crc.hip
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
                 hipStream_t st, const ParseArgs *fused);
@@ -112,6 +115,7 @@ struct rio_ctx {
   hipEvent_t ev[kNumEv] = {};
   hipEvent_t evA = nullptr, evB = nullptr;  // stream hand-offs (no timing)
   bool last_had_dec = false;
+  bool item_end_mode = false;  // RIO_CFG_ITEM_END: device results carry item_end (cumSize)
   bool last_cmp = false;  // the last host result's records are the compacted blocks (d.cmp)
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
   uint64_t side_cap = 0, item_cap = 0, dec_cap = 0;
@@ -161,8 +165,12 @@ struct rio_ctx {
   std::mutex pool_mu;
   std::vector<std::pair<uint8_t *, uint64_t>> buf_pool;
   std::vector<rio_results *> res_pool;
+  // segment scans: the segment table on the device (seg_end | seg_file_off) and its host copy
+  unsigned long long *d_seg = nullptr;
+  uint64_t d_seg_cap = 0;
+  std::vector<uint64_t> seg_end_h, seg_file_h;
   // last async call
-  uint64_t last_nchunks = 0, last_file_off = 0, last_in_bytes = 0;
+  uint64_t last_nchunks = 0, last_file_off = 0, last_in_bytes = 0, last_nseg = 0;
   int32_t last_codec = 0, last_mode = 0;
   const uint8_t *last_span = nullptr;
 };
@@ -192,7 +200,8 @@ static int alloc_bufs(rio_ctx *c) {
   if (dalloc(&d.blk_c0, nb) || dalloc(&d.blk_meta, nb) || dalloc(&d.blk_len, nb) || dalloc(&d.blk_nitems, nb) ||
       dalloc(&d.blk_hdr, nb) || dalloc(&d.blk_item_base, nb + 1) || dalloc(&d.blk_status, nb) ||
       dalloc(&d.blk_a, nb) || dalloc(&d.blk_b, nb) || dalloc(&d.blk_out_len, nb) || dalloc(&d.blk_dec_off, nb + 1) ||
-      dalloc(&d.blk_need, nb) || dalloc(&d.fl, nb) || dalloc(&d.blk_coff, 2 * (nb + 1)))
+      dalloc(&d.blk_need, nb) || dalloc(&d.fl, nb) || dalloc(&d.blk_coff, 2 * (nb + 1)) || dalloc(&d.blk_data, nb) ||
+      dalloc(&d.blk_file_off, nb) || dalloc(&d.blk_seg, nb))
     return -1;
   if (dalloc(&d.scan_tmp, (n + 2047) / 2048 + 16) || dalloc(&d.strad, n)) return -1;
   if (dalloc(&d.item_off, c->item_cap) || dalloc(&d.item_len, c->item_cap) || dalloc(&d.side, c->side_cap))
@@ -203,10 +212,10 @@ static int alloc_bufs(rio_ctx *c) {
 static void free_all(rio_ctx *c) {
   DevBufs &d = c->d;
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
-                d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.cmp, d.item_off, d.item_len, d.side,
+                d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.blk_data, d.blk_file_off, d.blk_seg, d.cmp, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len,
-                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan};
+                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan, c->d_seg};
   for (void *p : ps)
     if (p) hipFree(p);
   if (c->h_ctl) hipHostFree(c->h_ctl);
@@ -227,11 +236,12 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, c->device));
   c->ncu = prop.multiProcessorCount;
-  // test hook: a small flate token region per block and round forces the
-  // yield / resume path across rounds (and the host retry with more rounds)
-  if (const char *f = getenv("RIO_FL_TOKCAP")) c->d.tok_limit = strtoull(f, nullptr, 10);
-  // test hook: few Huffman-pass waves, so every stream decodes many blocks
-  if (const char *f = getenv("RIO_FL_GRID")) c->d.fl_grid = strtoull(f, nullptr, 10);
+  // flate tuning / test parameters: a small token region per block and round
+  // forces the yield / resume path across rounds (and the host retry with more
+  // rounds); few Huffman-pass waves make every stream decode many blocks
+  c->d.tok_limit = cfg ? cfg->flate_tok_limit : 0;
+  c->d.fl_grid = cfg ? cfg->flate_grid : 0;
+  c->item_end_mode = cfg && (cfg->flags & RIO_CFG_ITEM_END);
   uint64_t span = (cfg && cfg->max_span_bytes) ? cfg->max_span_bytes : (256ull << 20);
   span = (span + kChunk - 1) / kChunk * kChunk;
   c->max_span = span;
@@ -457,7 +467,8 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   const bool fused = RIO_FUSED_PARSE && codec == RIO_CODEC_NONE && run_parse && run_crc && nchunks > 0;
   const CrcArgs ca{RIO_ABLATE, 0};
   if (nchunks > 0 && run_parse) {
-    ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap, sparse, 0};
+    ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap, sparse,
+                 (c->item_end_mode && sparse) ? 1 : 0};
     if (codec != RIO_CODEC_NONE) launch_dec_nitems(d, c->nblocks_dev, max_blocks, st2);
     launch_block_scan(d.blk_nitems, d.blk_item_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
     if (fused) {
@@ -477,7 +488,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     launch_parse_slow(d, pa, max_blocks, st2);
     if (codec == RIO_CODEC_NONE) {
       if (!sparse) launch_chunk_scan(d.ck_ssz, d.ck_sbase, d.scan_tmp, nchunks, st2);
-      launch_strad(span, d, nchunks, c->side_cap, sparse, st2);
+      launch_strad(span, d, nchunks, c->side_cap, sparse, pa.end_mode, st2);
     }
   } else if (nchunks == 0) {
     HIP_OK(hipMemsetAsync(d.blk_item_base, 0, 8, st2));
@@ -503,6 +514,7 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
                    uint64_t in_bytes, rio_batch *out, rio_results *res) {
   const Ctl &k = *c->h_ctl;
   memset(out, 0, sizeof(*out));
+  out->err_segment = -1;
   out->in_bytes = in_bytes;
   out->n_blocks = k.n_valid_blocks;
   out->n_items = k.n_items;
@@ -515,10 +527,16 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
   const uint64_t nb = k.n_valid_blocks;
   if (!res) {  // device results
     out->records = d_records;
-    out->item_off = reinterpret_cast<const uint64_t *>(c->d.item_off);
-    out->item_len = reinterpret_cast<const uint64_t *>(c->d.item_len);
     out->block_first_item = reinterpret_cast<const uint64_t *>(c->d.blk_item_base);
     out->block_file_off = nullptr;
+    if (c->item_end_mode) {  // the cumSize-shaped output (rio_gpu.h)
+      out->item_end = reinterpret_cast<const uint64_t *>(c->d.item_off);
+      out->block_data = reinterpret_cast<const uint64_t *>(c->d.blk_data);
+      out->block_first_off = reinterpret_cast<const uint64_t *>(c->d.blk_hdr);
+    } else {
+      out->item_off = reinterpret_cast<const uint64_t *>(c->d.item_off);
+      out->item_len = reinterpret_cast<const uint64_t *>(c->d.item_len);
+    }
     return 0;
   }
   // host copies of the valid prefix: item views, block table, straddlers / decoded bytes
@@ -576,8 +594,8 @@ static int grow_for_overflow(rio_ctx *c, int32_t codec) {
   return 0;
 }
 
-// RIO_DEBUG=1: per-block state of the last run on stderr (development aid)
-static void debug_dump(rio_ctx *c) {
+// -DRIO_DEBUG_DUMP builds: per-block state of every run on stderr (development aid)
+[[maybe_unused]] static void debug_dump(rio_ctx *c) {
   unsigned long long nb = 0;
   hipMemcpy(&nb, c->nblocks_dev, 8, hipMemcpyDeviceToHost);
   std::vector<unsigned long long> a(nb), st(nb), ol(nb), bl(nb), me(nb), doff(nb), ni(nb), ib(nb), ea(nb), eb(nb),
@@ -641,7 +659,9 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
     // a flate block needed more Huffman/copy rounds than were launched
     if ((c->h_ctl->out_overflow & 0x1000) && c->fl_rounds < 64) c->fl_rounds = c->fl_rounds * 2 > 64 ? 64 : c->fl_rounds * 2;
   }
-  if (getenv("RIO_DEBUG")) debug_dump(c);
+#ifdef RIO_DEBUG_DUMP
+  debug_dump(c);
+#endif
   float ms = 0;
   hipEventElapsedTime(&ms, c->ev[kEvStart], c->ev[kEvEnd]);
   // host results of a compressed codec: only the decoded record bytes cross PCIe
@@ -729,8 +749,43 @@ extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_
   ctx->last_codec = codec;
   ctx->last_mode = kModeBody;
   ctx->last_span = (const uint8_t *)dev_span;
+  ctx->last_nseg = 0;
   return enqueue(ctx, (const uint8_t *)dev_span, nchunks, UINT64_MAX, 1, (nbytes % kChunk) != 0, codec, kModeBody,
                  true, 0);
+}
+
+extern "C" int rio_scan_device_segments_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes,
+                                              const uint64_t *seg_end, const uint64_t *seg_file_off, uint64_t nseg,
+                                              int32_t codec) {
+  if (!ctx || (nseg && (!seg_end || !seg_file_off))) return -1;
+  for (uint64_t s = 0; s < nseg; s++) {
+    const uint64_t lo = s ? seg_end[s - 1] : 0;
+    if (seg_end[s] < lo || seg_end[s] % kChunk != 0 || seg_file_off[s] % kChunk != 0) {
+      set_last_error("segment %" PRIu64 ": ends must ascend, ends and file offsets be multiples of 32768", s);
+      return -1;
+    }
+  }
+  if (nseg && seg_end[nseg - 1] != (nbytes + kChunk - 1) / kChunk * kChunk) {
+    set_last_error("the segments must cover the span");
+    return -1;
+  }
+  HIP_OK(hipSetDevice(ctx->device));
+  if (ctx->d_seg_cap < 2 * nseg + 2) {
+    if (dalloc(&ctx->d_seg, 2 * nseg + 2)) return -1;
+    ctx->d_seg_cap = 2 * nseg + 2;
+  }
+  ctx->seg_end_h.assign(seg_end, seg_end + nseg);
+  ctx->seg_file_h.assign(seg_file_off, seg_file_off + nseg);
+  if (nseg) {  // (the host copies outlive the async copies)
+    HIP_OK(hipMemcpyAsync(ctx->d_seg, ctx->seg_end_h.data(), nseg * 8, hipMemcpyHostToDevice, ctx->st));
+    HIP_OK(hipMemcpyAsync(ctx->d_seg + nseg, ctx->seg_file_h.data(), nseg * 8, hipMemcpyHostToDevice, ctx->st));
+  }
+  if (rio_scan_device_async(ctx, dev_span, nbytes, 0, codec)) return -1;
+  ctx->last_nseg = nseg;
+  if (nseg)
+    launch_block_files(ctx->d, ctx->d_seg, ctx->d_seg + nseg, nseg, ctx->last_nchunks ? ctx->last_nchunks : 1,
+                       ctx->st);
+  return 0;
 }
 
 extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
@@ -738,10 +793,12 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
   HIP_OK(hipSetDevice(ctx->device));
   HIP_OK(hipMemcpyAsync(ctx->h_ctl, ctx->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->st));
   HIP_OK(hipStreamSynchronize(ctx->st));
-  if (ctx->last_codec == RIO_CODEC_ZSTD && getenv("RIO_ZSTAT"))
+#ifdef RIO_ZPROF  // profiling builds: where the zstd entropy pass spends its cycles
+  if (ctx->last_codec == RIO_CODEC_ZSTD)
     fprintf(stderr, "rio: zstd blocks on the serial path: %llu; entropy-pass cycles lit %llu tables %llu seq %llu block %llu\n",
             (unsigned long long)ctx->h_ctl->pad[1], ctx->h_ctl->zprof[0], ctx->h_ctl->zprof[1], ctx->h_ctl->zprof[2],
             ctx->h_ctl->zprof[3]);
+#endif
   float ms = 0;
   hipEventElapsedTime(&ms, ctx->ev[kEvStart], ctx->ev[kEvEnd]);
   if (collect(ctx, ctx->last_span, ctx->last_file_off, ctx->last_codec, ctx->last_mode, ctx->last_in_bytes, out,
@@ -751,6 +808,19 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
   if (ctx->h_ctl->out_overflow) {
     rio_set_error(&out->err, RIO_ERR_CAPACITY, 0, "output capacity exceeded");
     out->stop = RIO_STOP_ERROR;
+  }
+  if (ctx->last_nseg) {  // segment scan: per-block files, and the error's file
+    out->block_file_off = reinterpret_cast<const uint64_t *>(ctx->d.blk_file_off);
+    out->block_segment = reinterpret_cast<const uint64_t *>(ctx->d.blk_seg);
+    if (out->stop == RIO_STOP_ERROR) {
+      const std::vector<uint64_t> &e = ctx->seg_end_h;
+      const uint64_t so = out->err.file_off;  // a span offset (the span starts at 0)
+      const uint64_t s = (uint64_t)(std::upper_bound(e.begin(), e.end(), so) - e.begin());
+      if (s < e.size()) {
+        out->err_segment = (int64_t)s;
+        out->err.file_off = ctx->seg_file_h[s] + so - (s ? e[s - 1] : 0);
+      }
+    }
   }
   return 0;
 }

@@ -166,7 +166,11 @@ struct DevBufs {
   unsigned long long *blk_dec_off;    // offset of the block's decoded bytes in dec (n + 1)
   unsigned long long *blk_need;       // decoded size found by the exact pass after a region overflow
   unsigned long long *blk_coff;       // host results: compact offsets of the decoded blocks (n + 1), then a scratch (n + 1)
-  // outputs: item views into the span or the records buffer (side / dec)
+  unsigned long long *blk_data;       // item-end output: where the block's payload lies (rio_batch.block_data)
+  unsigned long long *blk_file_off;   // segment scans: the block's offset in its file
+  unsigned long long *blk_seg;        // segment scans: the block's file (segment index)
+  // outputs: item views into the span or the records buffer (side / dec); in
+  // item-end mode (ParseArgs::end_mode) item_off holds item_end (cumSize) instead
   unsigned long long *item_off, *item_len;
   uint8_t *side;        // straddling items (none codec)
   StradDesc *strad;     // straddler per chunk slot
@@ -179,8 +183,8 @@ struct DevBufs {
   FlState *fl;                   // per block (flate)
   uint32_t *tok;                 // flate tokens: block b's region starts at blk_c0[b] * kTokPerChunk
   uint64_t tok_cap;              // u32 entries at tok
-  uint64_t tok_limit;            // tokens per block and round (0: the whole region; RIO_FL_TOKCAP, tests)
-  uint64_t fl_grid;              // Huffman-pass workgroups (0: all resident; RIO_FL_GRID, tests)
+  uint64_t tok_limit;            // tokens per block and round (0: the whole region; rio_config.flate_tok_limit)
+  uint64_t fl_grid;              // Huffman-pass workgroups (0: all resident; rio_config.flate_grid)
   unsigned long long *fl_more;   // per round: blocks whose token region filled (kFlRounds)
   uint8_t *zlit;                 // zstd: one literal buffer per decoder wave (codec_zstd.hip)
   unsigned long long *zjob;      // zstd: job header offsets (bytes from tok)
@@ -207,8 +211,8 @@ struct ParseArgs {
   int32_t codec;
   const unsigned long long *nblocks;  // device count
   uint64_t item_cap, side_cap;
-  int32_t sparse;  // straddlers go to a span-shaped side buffer at their own span offset
-  int32_t pad;
+  int32_t sparse;    // straddlers go to a span-shaped side buffer at their own span offset
+  int32_t end_mode;  // RIO_CFG_ITEM_END (sparse results only): item_end[i] = cumSize into item_off
   // k_parse over a list of blocks (the ones k_parse_lean declined) instead of all
   const unsigned long long *list;
   const unsigned long long *list_n;

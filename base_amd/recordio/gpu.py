@@ -41,9 +41,13 @@ class RioError(ctypes.Structure):
                 ("msg", ctypes.c_char * 512)]
 
 
+RIO_CFG_ITEM_END = 1  # device results carry item_end (cumSize) + block_data / block_first_off
+
+
 class RioConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_int32), ("max_span_bytes", ctypes.c_uint64),
-                ("max_out_bytes", ctypes.c_uint64), ("max_items", ctypes.c_uint64)]
+                ("max_out_bytes", ctypes.c_uint64), ("max_items", ctypes.c_uint64),
+                ("flate_tok_limit", ctypes.c_uint64), ("flate_grid", ctypes.c_uint64)]
 
 
 class RioBatch(ctypes.Structure):
@@ -54,7 +58,10 @@ class RioBatch(ctypes.Structure):
                 ("block_file_off", ctypes.POINTER(ctypes.c_uint64)), ("n_blocks", ctypes.c_uint64),
                 ("consumed", ctypes.c_uint64), ("stop", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("in_bytes", ctypes.c_uint64), ("kernel_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
-                ("err", RioError)]
+                ("err", RioError),
+                ("item_end", ctypes.POINTER(ctypes.c_uint64)), ("block_data", ctypes.POINTER(ctypes.c_uint64)),
+                ("block_first_off", ctypes.POINTER(ctypes.c_uint64)),
+                ("block_segment", ctypes.POINTER(ctypes.c_uint64)), ("err_segment", ctypes.c_int64)]
 
 
 READ_AT = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
@@ -86,6 +93,7 @@ EXPORTS = [
     "rio_scanner_header_len", "rio_scanner_header_kv", "rio_scanner_trailer", "rio_scanner_seek",
     "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish", "rio_scanner_gather",
     "rio_memory_reader", "rio_scan_v1_span", "rio_encode", "rio_encode_device", "rio_build_id",
+    "rio_scan_device_segments_async",
 ]
 
 _lib = None
@@ -104,6 +112,10 @@ def load(path: str = LIB_PATH):
         B.check_lib(path)  # refuses a library not built from this tree's sources
         L = ctypes.CDLL(path)
         L.rio_build_id.restype = ctypes.c_char_p
+        L.rio_scan_device_segments_async.restype = ctypes.c_int
+        L.rio_scan_device_segments_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                     ctypes.c_int32]
         P, U64, I64, I32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32
         L.rio_open.restype = P
         L.rio_open.argtypes = [ctypes.POINTER(RioConfig)]
@@ -185,9 +197,12 @@ def _err(e: RioError) -> RecordioError:
 class Context:
     """One rio_ctx: a device, a HIP stream and fixed-capacity buffers."""
 
-    def __init__(self, device: int = 0, max_span_bytes: int = 0, max_out_bytes: int = 0, max_items: int = 0):
+    def __init__(self, device: int = 0, max_span_bytes: int = 0, max_out_bytes: int = 0, max_items: int = 0,
+                 item_end: bool = False, flate_tok_limit: int = 0, flate_grid: int = 0):
         self.L = load()
-        cfg = RioConfig(device, 0, max_span_bytes, max_out_bytes, max_items)
+        cfg = RioConfig(device, RIO_CFG_ITEM_END if item_end else 0, max_span_bytes, max_out_bytes, max_items,
+                        flate_tok_limit, flate_grid)
+        self.item_end = item_end
         self.h = self.L.rio_open(ctypes.byref(cfg))
         if not self.h:
             raise RuntimeError("rio_open failed: " + self.L.rio_last_error().decode())
@@ -281,6 +296,19 @@ class Context:
         if rc != 0:
             raise RuntimeError("rio_scan_device_async: " + self.L.rio_last_error().decode())
 
+    def scan_device_segments_async(self, dev_ptr: int, nbytes: int, seg_end, seg_file_off,
+                                   codec: int = RIO_CODEC_NONE):
+        """rio_scan_device_segments_async: nseg file bodies back to back at
+        dev_ptr (segment s = bytes [seg_end[s-1], seg_end[s]), starting at byte
+        seg_file_off[s] of its file); rio_sync's results carry block_segment and
+        block_file_off per block."""
+        n = len(seg_end)
+        e = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in seg_end])
+        f = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in seg_file_off])
+        rc = self.L.rio_scan_device_segments_async(self.h, dev_ptr, nbytes, e, f, n, codec)
+        if rc != 0:
+            raise RuntimeError("rio_scan_device_segments_async: " + self.L.rio_last_error().decode())
+
     def sync(self) -> RioBatch:
         out = RioBatch()
         if self.L.rio_sync(self.h, ctypes.byref(out)) != 0:
@@ -366,12 +394,55 @@ def dev_to_host(ptr: int, nbytes: int) -> bytes:
     return buf.raw
 
 
+def _dev_u64(ptr, n: int):
+    import numpy as np
+    return np.frombuffer(dev_to_host(ctypes.cast(ptr, ctypes.c_void_p).value, 8 * n), dtype=np.uint64)
+
+
+def item_end_views(b: RioBatch):
+    """(off, len) item views of an item-end batch (RIO_CFG_ITEM_END), in the
+    item_off convention (bit 63: in records), from item_end, block_data,
+    block_first_off and block_first_item -- the consumer rule of rio_gpu.h."""
+    import numpy as np
+    n, nb = int(b.n_items), int(b.n_blocks)
+    end = _dev_u64(b.item_end, n).astype(np.int64)
+    first = _dev_u64(b.block_first_item, nb + 1).astype(np.int64)
+    data = _dev_u64(b.block_data, nb)
+    foff = _dev_u64(b.block_first_off, nb).astype(np.int64)
+    blk = np.repeat(np.arange(nb), np.diff(first))
+    start_in_blk = np.concatenate([[True], np.diff(blk) != 0]) if n else np.zeros(0, bool)
+    prev = np.concatenate([[0], end[:-1]]) if n else end
+    prev = np.where(start_in_blk, 0, prev)
+    s = foff[blk] + prev
+    e = foff[blk] + end
+    ln = (e - s).astype(np.uint64)
+    in_rec = (data[blk] >> np.uint64(63)).astype(bool)
+    D = (data[blk] & np.uint64((1 << 63) - 1)).astype(np.int64)
+    k = s // 32740
+    chunked = D + k * 32768 + 28 + s % 32740
+    cross = (~in_rec) & (e - s > 0) & ((e - 1) // 32740 != k)
+    off = np.where(in_rec, D + s, chunked).astype(np.uint64)
+    off[cross | in_rec] |= np.uint64(ITEM_IN_RECORDS)
+    return off, ln
+
+
 def device_batch_items(b: RioBatch, span_host: bytes) -> List[bytes]:
     """Items of a device batch (rio_scan_device) as bytes; span_host is the span's host copy."""
     import numpy as np
     n = int(b.n_items)
     if n == 0:
         return []
+    if b.item_end:
+        off, ln = item_end_views(b)
+        rec = dev_to_host(b.records, int(b.records_len)) if b.records_len else b""
+        out = []
+        for o, k in zip(off.tolist(), ln.tolist()):
+            if o & ITEM_IN_RECORDS:
+                o &= ~ITEM_IN_RECORDS
+                out.append(rec[o:o + k])
+            else:
+                out.append(span_host[o:o + k])
+        return out
     off = np.frombuffer(dev_to_host(ctypes.cast(b.item_off, ctypes.c_void_p).value, 8 * n), dtype=np.uint64)
     ln = np.frombuffer(dev_to_host(ctypes.cast(b.item_len, ctypes.c_void_p).value, 8 * n), dtype=np.uint64)
     rec = dev_to_host(b.records, int(b.records_len)) if b.records_len else b""

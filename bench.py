@@ -20,7 +20,7 @@ Prints ONE JSON line (rank 0).
 from __future__ import annotations
 
 import argparse
-import hashlib
+import ctypes
 import json
 import os
 import sys
@@ -166,10 +166,20 @@ def c5_flate(args, local, rank, world, dist):
     """BASELINE.json configs[4]: 1024 trailer-indexed flate files (64 MiB of C3
     records each, tools/c5_data.py) over the ranks -- files assigned by
     size-balanced greedy assignment (shard.assign_files), every rank's files
-    device-resident, decoded as batches of whole file bodies back to back (block
-    ranges from each file's trailer index). Strong scaling: the 1024 files are
-    fixed as N grows; value = all files' bytes / max time over ranks. No record
-    byte crosses xGMI; the one collective is the ordered-output prefix (RCCL)."""
+    device-resident, decoded as batches of whole file bodies back to back, one
+    rio_scan_device_segments_async launch per batch (each body a segment: its
+    blocks' ItemLocation.Block offsets are their own file's). The 1024 files are
+    copies of c5_data.N_BASE distinct base files (generating 1024 distinct 64 MiB
+    files would take ~10 minutes per run); every file is decoded and checked on
+    its own. Strong scaling: the 1024 files are fixed as N grows; value = all
+    files' bytes / max time over ranks. No record byte crosses xGMI; the one
+    collective is the ordered-output prefix (RCCL).
+
+    Parity (untimed pass, every file of the rank): each file's records -- its
+    blocks' item bytes by the item_end output -- equal its base's records, and
+    its blocks' file offsets equal its trailer index. Timed pass: the batches
+    alternate between two contexts (two streams), each batch's result checked
+    (no error, its record count) when its context is next used or at the end."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import c5_data
@@ -196,13 +206,14 @@ def c5_flate(args, local, rank, world, dist):
         with open(path + ".json") as f:
             metas.append(json.load(f))
     gen_s = time.perf_counter() - t0
-    # each file's block index (its trailer item; parsed on the host at open time)
-    spans = []
+    # each base's block index (its trailer item, read through the GPU scanner)
+    spans, index = [], []
     for k, data in enumerate(bases):
         sc = gpu.NewScanner(data, ctx=gpu.default_context(local))
         offs = c5_data.parse_index(sc.Trailer())
         assert sc.Finish() is None and len(offs) == -(-metas[k]["nrec"] // c5_data.PER_BLOCK)
         spans.append((offs[0], shard.trailer_offset(data)))
+        index.append(offs)
     sizes = [len(bases[f % c5_data.N_BASE]) for f in range(c5_data.N_FILES)]
     mine = shard.assign_files(sizes, world)[rank]
     body_len = [spans[k][1] - spans[k][0] for k in range(c5_data.N_BASE)]
@@ -222,39 +233,83 @@ def c5_flate(args, local, rank, world, dist):
     dev = torch.empty(max(total, 1), dtype=torch.uint8, device=f"cuda:{local}")
     dbase = [torch.frombuffer(bytearray(bases[k][spans[k][0]:spans[k][1]]), dtype=torch.uint8).to(dev.device)
              for k in range(c5_data.N_BASE)]
-    layout, pos = [], 0
+    layout, pos = [], 0  # per batch: (span offset, bytes, records, segment ends, segment file offsets)
     for bt in batches:
         lo = pos
+        ends, foffs = [], []
         for f in bt:
-            n = body_len[f % c5_data.N_BASE]
-            dev[pos:pos + n].copy_(dbase[f % c5_data.N_BASE])
+            k = f % c5_data.N_BASE
+            n = body_len[k]
+            dev[pos:pos + n].copy_(dbase[k])
             pos += n
-        layout.append((lo, pos - lo, sum(metas[f % c5_data.N_BASE]["nrec"] for f in bt)))
+            ends.append(pos - lo)
+            foffs.append(spans[k][0])
+        layout.append((lo, pos - lo, sum(metas[f % c5_data.N_BASE]["nrec"] for f in bt), ends, foffs))
     del dbase
     torch.cuda.synchronize()
-    biggest = max((n for _, n, _ in layout), default=0)
-    max_items = max((k for _, _, k in layout), default=0)
-    ctx = gpu.Context(local, max_span_bytes=max(biggest, 32768), max_items=max_items + 1024)
-    parity = None
-    if mine:  # the first file of this rank's first batch against the generator
-        f0 = batches[0][0] % c5_data.N_BASE
-        b = ctx.scan_device(dev.data_ptr(), body_len[f0], file_off=spans[f0][0], is_file_end=True,
-                            codec=gpu.RIO_CODEC_FLATE)
-        items = gpu.device_batch_items(b, bases[f0][spans[f0][0]:spans[f0][1]])
-        want = c5_data.base_records(f0)
-        parity = (b.err.code == 0 and len(items) == len(want)
-                  and hashlib.sha256(b"".join(items)).digest() == hashlib.sha256(b"".join(want)).digest())
+    biggest = max((n for _, n, _, _, _ in layout), default=0)
+    max_items = max((k for _, _, k, _, _ in layout), default=0)
+    ctxs = [gpu.Context(local, max_span_bytes=max(biggest, 32768), max_items=max_items + 1024, item_end=True)
+            for _ in range(2)]
 
-    def step():
-        n = 0
-        for lo, nbytes, nrec in layout:
-            ctx.scan_device_async(dev.data_ptr() + lo, nbytes, spans[0][0], gpu.RIO_CODEC_FLATE)
-            r = ctx.sync()
-            assert r.err.code == 0 and r.n_items == nrec, (r.err.msg, r.n_items, nrec)
-            n += r.n_items
-        return n
+    def launch(ctx, i):
+        lo, nbytes, _, ends, foffs = layout[i]
+        ctx.scan_device_segments_async(dev.data_ptr() + lo, nbytes, ends, foffs, gpu.RIO_CODEC_FLATE)
+
+    def done(r, i):
+        assert r.err.code == 0 and r.stop == gpu.RIO_STOP_EOF and r.n_items == layout[i][2], \
+            (r.err.msg, r.n_items, layout[i][2])
+        return int(r.n_items)
+
+    # parity pass: every file of the rank against its base's records and index
+    files_ok = 0
+    if mine:
+        want = {}
+        for k in range(c5_data.N_BASE):
+            w = b"".join(c5_data.base_records(k))
+            want[k] = torch.frombuffer(bytearray(w), dtype=torch.uint8).to(dev.device)
+        for i, bt in enumerate(batches):
+            launch(ctxs[0], i)
+            r = ctxs[0].sync()
+            done(r, i)
+            nb = int(r.n_blocks)
+            u64 = lambda p, n: np.frombuffer(gpu.dev_to_host(ctypes.cast(p, ctypes.c_void_p).value, 8 * n),
+                                             dtype=np.uint64).astype(np.int64)
+            first = u64(r.block_first_item, nb + 1)
+            end = u64(r.item_end, int(r.n_items))
+            data_ = u64(r.block_data, nb) & ((1 << 63) - 1)  # (bit 63: in records)
+            foff = u64(r.block_first_off, nb)
+            seg = u64(r.block_segment, nb)
+            boff = u64(r.block_file_off, nb)
+            rec = devcheck_copy(r.records, int(r.records_len), dev.device)
+            nbytes = np.where(first[1:] > first[:-1], end[np.maximum(first[1:] - 1, 0)], 0)
+            bounds = np.searchsorted(seg, np.arange(len(bt) + 1))
+            for j, f in enumerate(bt):
+                k = f % c5_data.N_BASE
+                b0, b1 = bounds[j], bounds[j + 1]
+                got = torch.cat([rec[int(data_[b] + foff[b]):int(data_[b] + foff[b] + nbytes[b])]
+                                 for b in range(b0, b1)])
+                if torch.equal(got, want[k]) and boff[b0:b1].tolist() == index[k]:
+                    files_ok += 1
+            del rec
+        del want
+    parity = files_ok == len(mine)
 
     steps = max(1, min(args.steps, 3))
+
+    def step():
+        n, pending = 0, [None, None]
+        for i in range(len(layout)):
+            c = i % 2
+            if pending[c] is not None:
+                n += done(ctxs[c].sync(), pending[c])
+            launch(ctxs[c], i)
+            pending[c] = i
+        for c in range(2):
+            if pending[c] is not None:
+                n += done(ctxs[c].sync(), pending[c])
+        return n
+
     step()
     if dist is not None:
         dist.barrier()
@@ -267,23 +322,33 @@ def c5_flate(args, local, rank, world, dist):
         dist.barrier()
     dt = (time.perf_counter() - t0) / steps
     all_bytes = sum(sizes)
-    ok = bool(parity) if mine else True
+    ok = parity
     if dist is not None:
         t = torch.tensor([dt, 0.0 if ok else 1.0], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, ok = float(t[0].item()), t[1].item() == 0.0
         # the ordered-output prefix: where this rank's records land in the file-set order
         shard.ordered_prefix(n_items, sum(metas[f % c5_data.N_BASE]["rec_bytes"] for f in mine))
-    ctx.close()
+    for c in ctxs:
+        c.close()
     del dev
     torch.cuda.empty_cache()
     return {"metric": "recordio scan GiB/s device-resident (compressed in), C5 1024 trailer-indexed flate files",
             "value": round(all_bytes / dt / 2 ** 30, 2), "unit": "GiB/s", "n_gpus": world,
             "scaling": "strong", "ms_per_step": round(dt * 1e3, 3), "steps": steps, "parity": ok,
+            "parity_files_checked": len(mine), "parity_files_ok": files_ok,
             "config": {"files": c5_data.N_FILES, "file_record_bytes": c5_data.FILE_RECORD_BYTES,
                        "records_per_block": c5_data.PER_BLOCK, "distinct_base_files": c5_data.N_BASE,
+                       "note": "file f is a copy of base f % %d (each decoded and checked on its own)"
+                               % c5_data.N_BASE,
                        "files_bytes_total": all_bytes, "files_this_rank": len(mine),
-                       "batches_this_rank": len(batches), "gen_s": round(gen_s, 1)}}
+                       "batches_this_rank": len(batches), "launch": "rio_scan_device_segments_async, "
+                       "one per batch, batches alternating over 2 contexts (streams)", "gen_s": round(gen_s, 1)}}
+
+
+def devcheck_copy(ptr, nbytes, device):
+    import devcheck
+    return devcheck.dev_copy(ptr, nbytes, device)
 
 
 def main():
@@ -347,8 +412,9 @@ def main():
         dev[CHUNK + r * nbody:CHUNK + (r + 1) * nbody].copy_(body_dev)
     torch.cuda.synchronize()
     n_items = nrec * args.replicas
-    # items are views into the span; only chunk-straddling items are gathered (side buffer)
-    ctx = gpu.Context(local, max_span_bytes=total, max_items=n_items + 1024)
+    # items are views into the span (RIO_CFG_ITEM_END: the cumSize-shaped output,
+    # 8 B per item); only chunk-straddling items are gathered (side buffer)
+    ctx = gpu.Context(local, max_span_bytes=total, max_items=n_items + 1024, item_end=True)
     span_ptr = dev.data_ptr() + CHUNK
     span_len = total - CHUNK
 
@@ -359,6 +425,7 @@ def main():
     b = step()
     assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
     assert b.n_items == n_items, (b.n_items, n_items)
+    bb = b
     for _ in range(args.warmup):
         step()
 
@@ -378,10 +445,18 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
+    # parity of the timed path: the last step's output, every record of every
+    # replica gathered on the GPU against the generator's records (tools/devcheck.py)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import devcheck
+    want, want_len = devcheck.records_tensors(c2_records(), dev.device)
+    chk = devcheck.check_replicated(bb, dev[CHUNK:], want, want_len, args.replicas)
+    del want, want_len
+    ok = bool(chk["ok"])
     if dist is not None:
-        t = torch.tensor([dt], device=coll_dev(local), dtype=torch.float64)
+        t = torch.tensor([dt, 0.0 if ok else 1.0], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt, ok = float(t[0].item()), t[1].item() == 0.0
     ms_per_step = dt / args.steps * 1e3
     in_bytes = span_len * world
     value = in_bytes * args.steps / dt / 2 ** 30
@@ -391,9 +466,10 @@ def main():
     crc_avg = float(np.mean(crc_ms))
     alg = span_len
     achieved = alg / (crc_avg * 1e-3) / 1e9
-    # whole pipeline: chunk bytes in + item views (16 B) + block table out (straddlers,
-    # ~1 per block here, are ~0.4 % of the bytes and not counted)
-    pipe_alg = span_len + 16 * n_items + 8 * int(b.n_blocks)
+    # whole pipeline (SURVEY.md §8(d) B_alg): chunk bytes in + item_end (8 B per
+    # item) + block metadata (block_first_item, block_data, block_first_off: 24 B
+    # per block) + the straddlers gathered (one ~256 B record per 2-chunk block)
+    pipe_alg = span_len + 8 * n_items + 24 * int(b.n_blocks) + 256 * int(b.n_blocks)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_crc", args.replicas),
             "kernel": "k_crc", "kernel_ms": round(crc_avg, 3),
@@ -412,6 +488,9 @@ def main():
                       "parallelism": f"{world} GPU(s), independent replica sets",
                       "bytes_in_per_gpu": span_len},
            "roofline": roof,
+           "parity": {"ok": ok, "checked": "every record of every replica of the last timed step vs the "
+                                           "generator (on the GPU)", "items_checked": chk["items_checked"],
+                      "bytes_checked": chk["bytes_checked"], "output": "item_end (RIO_CFG_ITEM_END)"},
            "build_id": gpu.build_id(), "lib": os.path.relpath(gpu.LIB_PATH, ROOT)}
     ctx.close()
     del dev

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RIO_ABI_VERSION 1
+#define RIO_ABI_VERSION 2
 #define RIO_CHUNK_SIZE 32768        /* internal.ChunkSize, chunk.go:25 */
 #define RIO_CHUNK_HEADER_SIZE 28    /* internal.ChunkHeaderSize, chunk.go:22 */
 #define RIO_MAX_CHUNK_PAYLOAD 32740 /* internal.MaxChunkPayloadSize, chunk.go:28 */
@@ -97,12 +97,24 @@ typedef struct rio_error {
     char msg[512];      /* the reference's error text, byte for byte where defined */
 } rio_error;
 
+/* rio_config.flags */
+#define RIO_CFG_ITEM_END 1u  /* device results (rio_scan_device / _async) carry the
+                                cumSize-shaped item output: rio_batch.item_end,
+                                block_data, block_first_off instead of item_off /
+                                item_len (8 B per item instead of 16) */
+
 typedef struct rio_config {
     int32_t device;             /* HIP device ordinal */
-    int32_t flags;              /* reserved, 0 */
+    int32_t flags;              /* RIO_CFG_* bits */
     uint64_t max_span_bytes;    /* largest span per call (multiple of 32768); 0 = 256 MiB */
     uint64_t max_out_bytes;     /* straddler-bytes capacity per call (grown on demand); 0 = span/8 + 1 MiB */
     uint64_t max_items;         /* item-view capacity per call (grown on demand); 0 = span/64 + 1024 */
+    /* tuning / test parameters of the flate decoder (0 = the defaults): tokens
+     * per block and round (a small value forces the yield / resume path across
+     * rounds), and Huffman-pass workgroups (a small value makes every wave
+     * decode many blocks) */
+    uint64_t flate_tok_limit;
+    uint64_t flate_grid;
 } rio_config;
 
 typedef struct rio_ctx rio_ctx;
@@ -139,6 +151,31 @@ typedef struct rio_batch {
     float kernel_ms;     /* device time of the decode pipeline (HIP events) */
     float total_ms;      /* including H2D / D2H for rio_scan_span */
     rio_error err;
+    /* RIO_CFG_ITEM_END device results (item_off / item_len are then NULL): the
+     * reference's rawItemList shape (scannerv2.go:24-49, 83-91). Block b's items
+     * [F, E) = [block_first_item[b], block_first_item[b+1]) are
+     *   item i = payload bytes [s, e) of block b,
+     *   s = block_first_off[b] + (i > F ? item_end[i-1] : 0), e = block_first_off[b] + item_end[i]
+     * (item_end = cumSize: block-relative inclusive prefix of the sizes;
+     * block_first_off = firstOff: the packed header's length). With
+     * D = block_data[b] & ~RIO_ITEM_IN_RECORDS:
+     *   block_data[b] & RIO_ITEM_IN_RECORDS: the payload is contiguous at
+     *     records + D (decoded flate / zstd blocks; none blocks with short
+     *     middle chunks, gathered) -> records[D + s, D + e);
+     *   else (none codec): the payload is the block's chunk payloads in the span,
+     *     its first chunk at span + D: with k = s / 32740 and
+     *     o = D + k * 32768 + 28 + s % 32740, an item within one chunk payload
+     *     ((e - 1) / 32740 == k) is span[o, o + e - s), an item crossing into the
+     *     next chunk is records[o, o + e - s) (gathered at its own span offset). */
+    const uint64_t *item_end;         /* n_items entries */
+    const uint64_t *block_data;       /* n_blocks entries */
+    const uint64_t *block_first_off;  /* n_blocks entries */
+    /* rio_scan_device_segments_async results: block b belongs to file
+     * block_segment[b] (device array, n_blocks entries; block_file_off is then
+     * the device array of the blocks' own file offsets), and an error's
+     * err.file_off is an offset in file err_segment's bytes (else -1) */
+    const uint64_t *block_segment;
+    int64_t err_segment;
 } rio_batch;
 
 enum rio_stop {
@@ -196,6 +233,20 @@ int rio_scan_v1_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_
 int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, uint64_t file_off,
                           int32_t codec);
 int rio_sync(rio_ctx *ctx, rio_batch *out);
+
+/* Many files in one launch (a rank's trailer-indexed
+ * files decoded together). The span holds nseg file bodies back to back:
+ * segment s is span bytes [seg_end[s-1], seg_end[s]) (seg_end[-1] = 0), every
+ * boundary a multiple of 32768 and a block boundary of its file, and begins
+ * at byte seg_file_off[s] of its file. As rio_scan_device_async (the span ends
+ * at the last file's end), plus, in the rio_sync results, each block's file
+ * (block_segment) and its offset in that file (block_file_off: the
+ * ItemLocation.Block a Seek in that file takes). The scan stops at the first
+ * error in span order, reported with its file (err_segment) -- the files after
+ * a failing one are not decoded in that launch: scan them again without it.
+ * seg_end / seg_file_off are host arrays, not retained. */
+int rio_scan_device_segments_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, const uint64_t *seg_end,
+                                   const uint64_t *seg_file_off, uint64_t nseg, int32_t codec);
 
 /* Device time (HIP events) of the last completed run, per stage:
  * [0] block parse + item views + straddler gather (second stream, overlaps [2]),

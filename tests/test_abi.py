@@ -24,7 +24,18 @@ def test_header_lists_exports():
 def test_library_exports_all_symbols(gpu_lib):
     missing = [n for n in declared_functions() if not hasattr(gpu_lib, n)]
     assert missing == []
-    assert gpu_lib.rio_abi_version() == 1
+    assert gpu_lib.rio_abi_version() == 2
+
+
+def test_build_id_matches_tree(gpu_lib):
+    """The loaded library was built from this tree's sources and flags: its
+    rio_build_id() is the tree hash (base_amd/build.py), and a library with
+    another id is refused."""
+    from base_amd import build as B
+    from base_amd.recordio import gpu
+    assert gpu.build_id() == B.tree_build_id() == B.lib_build_id(B.LIB)
+    assert len(gpu.build_id()) == 16
+    assert B.tree_build_id(B.FLAGS + ["-DX"]) != B.tree_build_id()
 
 
 def test_codec_registry_lookup(gpu_lib):

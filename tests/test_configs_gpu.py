@@ -259,3 +259,59 @@ def test_c5_shaped_file_set(gpu_ctx, oracle):
     b = gpu_ctx.scan_device(dev.data_ptr(), len(span), file_off=0, is_file_end=True, codec=gpu.RIO_CODEC_FLATE)
     assert b.err.code == 0, b.err.msg
     assert gpu.device_batch_items(b, span) == want
+
+
+def test_c5_segments_scan(gpu_ctx, oracle):
+    """rio_scan_device_segments_async over C5-shaped file bodies back to back:
+    every block's file (block_segment) and its offset in that file
+    (block_file_off == the file's trailer index, ItemLocation.Block), the
+    records of each file through the item_end output; a corrupt chunk in the
+    second file stops the batch there, reported in that file's coordinates
+    (err_segment, err.file_off) with the first file's records delivered."""
+    import torch
+    import c5_data
+    from base_amd.recordio import gpu, shard
+    rb = 1 << 20
+    files = [c5_data.make_base(k, record_bytes=rb, workers=4) for k in range(3)]
+    recs = [c5_data.base_records(k, record_bytes=rb) for k in range(3)]
+    bodies, ends, foffs = [], [], []
+    for data, nrec, rec_bytes, offsets in files:
+        bodies.append(data[offsets[0]:shard.trailer_offset(data)])
+        ends.append(sum(map(len, bodies)))
+        foffs.append(offsets[0])
+    span = b"".join(bodies)
+    dev = torch.frombuffer(bytearray(span), dtype=torch.uint8).to("cuda:0")
+    ctx = gpu.Context(0, max_span_bytes=len(span) + 32768, item_end=True)
+    try:
+        ctx.scan_device_segments_async(dev.data_ptr(), len(span), ends, foffs, gpu.RIO_CODEC_FLATE)
+        b = ctx.sync()
+        assert b.err.code == 0 and b.stop == gpu.RIO_STOP_EOF and b.err_segment == -1, b.err.msg
+        nb = int(b.n_blocks)
+        seg = np.frombuffer(gpu.dev_to_host(ctypes.cast(b.block_segment, ctypes.c_void_p).value, 8 * nb),
+                            dtype=np.uint64)
+        boff = np.frombuffer(gpu.dev_to_host(ctypes.cast(b.block_file_off, ctypes.c_void_p).value, 8 * nb),
+                             dtype=np.uint64)
+        first = np.frombuffer(gpu.dev_to_host(ctypes.cast(b.block_first_item, ctypes.c_void_p).value, 8 * (nb + 1)),
+                              dtype=np.uint64)
+        items = gpu.device_batch_items(b, span)
+        for k, (data, nrec, rec_bytes, offsets) in enumerate(files):
+            sel = np.nonzero(seg == k)[0]
+            assert boff[sel].tolist() == offsets  # ItemLocation.Block of every block of file k
+            got = items[int(first[sel[0]]):int(first[sel[-1] + 1])]
+            assert got == recs[k]
+        # a corrupt chunk in file 1: the error in file 1's coordinates
+        bad = bytearray(span)
+        at = ends[0] + 5 * 32768 + 1000
+        bad[at] ^= 0x40
+        dev.copy_(torch.frombuffer(bad, dtype=torch.uint8))
+        ctx.scan_device_segments_async(dev.data_ptr(), len(span), ends, foffs, gpu.RIO_CODEC_FLATE)
+        b = ctx.sync()
+        assert b.stop == gpu.RIO_STOP_ERROR and b.err_segment == 1
+        assert b.err.file_off == foffs[1] + 5 * 32768
+        data1 = files[1][0]
+        ref = oracle.scan(bytes(data1[:foffs[1]]) + bytes(bad[ends[0]:ends[1]]), read_trailer=False)
+        assert b.err.msg.decode() == ref.err
+        items = gpu.device_batch_items(b, bytes(bad))
+        assert items == recs[0] + ref.items
+    finally:
+        ctx.close()

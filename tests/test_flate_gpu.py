@@ -13,19 +13,12 @@ pytestmark = pytest.mark.gpu
 
 
 def make_ctx(env=None, span=64 << 20):
+    """A ctx with the flate decoder's test parameters (rio_config.flate_tok_limit,
+    flate_grid) from `env` = {"tok_limit": n, "grid": n}."""
     from base_amd.recordio import gpu
-    old = {}
-    for k, v in (env or {}).items():
-        old[k] = os.environ.get(k)
-        os.environ[k] = str(v)
-    try:
-        return gpu.Context(0, max_span_bytes=span)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    env = env or {}
+    return gpu.Context(0, max_span_bytes=span, flate_tok_limit=env.get("tok_limit", 0),
+                       flate_grid=env.get("grid", 0))
 
 
 def scan_all(data, ctx):
@@ -103,7 +96,7 @@ def test_many_blocks_per_stream(gpu_lib):
     # dozens of blocks (state carried from block to block must be reset)
     recs = mixed_records(11, 700)
     data = write(recs, 6, "go", max_items=1)
-    c = make_ctx({"RIO_FL_GRID": 2})
+    c = make_ctx({"grid": 2})
     try:
         items, err = scan_all(data, c)
     finally:
@@ -118,7 +111,7 @@ def test_token_region_yield_and_resume(gpu_lib, cap):
     # retries with more
     recs = mixed_records(cap, 300)
     data = write(recs, 6, "go", max_items=49)  # 50 records per block
-    c = make_ctx({"RIO_FL_TOKCAP": cap})
+    c = make_ctx({"tok_limit": cap})
     try:
         items, err = scan_all(data, c)
     finally:
@@ -144,7 +137,7 @@ def test_rounds_exhausted_is_a_capacity_error(gpu_lib):
     rng = random.Random(3)
     recs = [bytes(rng.getrandbits(8) for _ in range(30000))]  # stored: ~10k tokens
     data = write(recs, 6, "go")
-    c = make_ctx({"RIO_FL_TOKCAP": 64})
+    c = make_ctx({"tok_limit": 64})
     try:
         items, err = scan_all(data, c)
     finally:

@@ -59,21 +59,26 @@ def test_c2_generator_is_oracle(c2, oracle):
     assert b"".join(ref.items) == recs.tobytes()
 
 
+@pytest.mark.parametrize("item_end", [True, False])
 @pytest.mark.parametrize("replicas", [1, 4])
-def test_c2_device_async_every_record(c2, replicas):
+def test_c2_device_async_every_record(c2, replicas, item_end):
+    """bench.py's timed call pair, in both output shapes: item_end (cumSize,
+    RIO_CFG_ITEM_END, what the bench times) and item_off / item_len."""
     import devcheck
     import torch
     from base_amd.recordio import gpu
     data, nrec, recs = c2
     dev = _replicated(data, replicas)
-    ctx = gpu.Context(0, max_span_bytes=dev.numel(), max_items=nrec * replicas + 1024)
+    ctx = gpu.Context(0, max_span_bytes=dev.numel(), max_items=nrec * replicas + 1024, item_end=item_end)
     for _ in range(2):  # a second run over the same ctx (the bench's steps reuse it)
         b = _async_scan(ctx, dev, gpu.RIO_CODEC_NONE)
         assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
         assert b.n_items == nrec * replicas and b.n_blocks == 3953 * replicas
+        assert bool(b.item_end) == item_end and bool(b.item_off) != item_end
         first = np.frombuffer(gpu.dev_to_host(ctypes.cast(b.block_first_item, ctypes.c_void_p).value,
                                               8 * (int(b.n_blocks) + 1)), dtype=np.uint64)
-        assert first[0] == 0 and np.all(np.diff(first.astype(np.int64))[:-1] == 253)
+        per = np.diff(first.astype(np.int64)).reshape(replicas, 3953)  # 3,952 blocks of 253, one of 144
+        assert first[0] == 0 and np.all(per[:, :-1] == 253) and np.all(per[:, -1] == 1000000 - 3952 * 253)
         want, want_len = devcheck.records_tensors(recs, dev.device)
         res = devcheck.check_replicated(b, dev[CH:], want, want_len, replicas)
         assert res["ok"], res
@@ -93,15 +98,15 @@ def c3():
     return data, nrec, rec_bytes, recs
 
 
-@pytest.mark.parametrize("replicas", [1, 2])
-def test_c3_base_file_device_async(c3, replicas):
+@pytest.mark.parametrize("replicas,item_end", [(1, False), (2, True)])
+def test_c3_base_file_device_async(c3, replicas, item_end):
     import devcheck
     import torch
     from base_amd.recordio import gpu
     data, nrec, rec_bytes, recs = c3
     assert len(recs) == nrec and sum(map(len, recs)) == rec_bytes
     dev = _replicated(data, replicas)
-    ctx = gpu.Context(0, max_span_bytes=dev.numel(), max_items=nrec * replicas + 1024)
+    ctx = gpu.Context(0, max_span_bytes=dev.numel(), max_items=nrec * replicas + 1024, item_end=item_end)
     b = _async_scan(ctx, dev, gpu.RIO_CODEC_FLATE)
     assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
     want, want_len = devcheck.records_tensors(recs, dev.device)

@@ -46,14 +46,14 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
         b = ctx1.scan_device(dev.data_ptr() + CH, len(body), file_off=CH, is_file_end=True, codec=codec)
         assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, b.err.msg
         items = gpu.device_batch_items(b, body)
-        want = want_fn()
+        want = want_fn()  # (kept for the timed-output check)
         h_got = hashlib.sha256(b"".join(items)).hexdigest()
         h_want = hashlib.sha256(b"".join(want)).hexdigest()
         parity = (len(items) == nrec and h_got == h_want and [len(x) for x in items] == [len(x) for x in want])
         ctx1.close()
 
     span_len = total - CH
-    ctx = gpu.Context(device, max_span_bytes=total, max_items=nrec * replicas + 1024)
+    ctx = gpu.Context(device, max_span_bytes=total, max_items=nrec * replicas + 1024, item_end=True)
     ptr = dev.data_ptr() + CH
 
     def step():
@@ -69,11 +69,19 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        bb = step()
         stages.append(ctx.stage_times())
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     st = np.mean(np.array(stages), axis=0)
+    timed_parity = None
+    if check:  # the last timed step's output: every record of every replica, on the GPU
+        import devcheck
+        w, wl = devcheck.records_tensors(want, dev.device)
+        chk = devcheck.check_replicated(bb, dev[CH:], w, wl, replicas)
+        del w, wl
+        timed_parity = {"ok": bool(chk["ok"]), "items_checked": chk["items_checked"],
+                        "bytes_checked": chk["bytes_checked"]}
     out_bytes = rec_bytes * replicas
     ctx.close()
     del dev
@@ -88,7 +96,8 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
         "config": {"workload": workload, "base_file_bytes": len(data), "base_records": nrec,
                    "base_record_bytes": rec_bytes, "replicas": replicas, "span_bytes": span_len,
                    "records_bytes": out_bytes},
-        "parity": parity}
+        "parity": parity and bool(timed_parity and timed_parity["ok"]),
+        "parity_timed_output": timed_parity}
 
 
 TARGET_RECORD_BYTES = 10 << 30  # configs[2]: 10 GiB of uncompressed records

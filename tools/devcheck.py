@@ -30,13 +30,44 @@ def dev_copy(ptr: int, nbytes: int, device, dtype=torch.uint8) -> torch.Tensor:
     return t[:nbytes // el]
 
 
+def _ptr(p):
+    return ctypes.cast(p, ctypes.c_void_p).value
+
+
+def item_end_tensors(b, device):
+    """(off, length, in_records) of an item-end batch (RIO_CFG_ITEM_END), by the
+    consumer rule of include/rio_gpu.h, computed on the device."""
+    n, nb = int(b.n_items), int(b.n_blocks)
+    end = dev_copy(_ptr(b.item_end), 8 * n, device, torch.int64)
+    first = dev_copy(_ptr(b.block_first_item), 8 * (nb + 1), device, torch.int64)
+    data = dev_copy(_ptr(b.block_data), 8 * nb, device, torch.int64)
+    foff = dev_copy(_ptr(b.block_first_off), 8 * nb, device, torch.int64)
+    counts = first[1:] - first[:-1]
+    blk = torch.repeat_interleave(torch.arange(nb, device=device), counts, output_size=n)
+    prev = torch.zeros_like(end)
+    prev[1:] = end[:-1]
+    prev[first[:-1][counts > 0]] = 0  # each block's first item starts at the header's end
+    s = foff[blk] + prev
+    e = foff[blk] + end
+    rec_blk = data[blk] < 0  # bit 63
+    D = data[blk] & ((1 << 63) - 1)
+    k = torch.div(s, 32740, rounding_mode="floor")
+    chunked = D + k * 32768 + 28 + (s - k * 32740)
+    cross = (~rec_blk) & (e > s) & (torch.div(e - 1, 32740, rounding_mode="floor") != k)
+    off = torch.where(rec_blk, D + s, chunked)
+    return off, e - s, rec_blk | cross
+
+
 def batch_tensors(b, device):
     """(off int64, length int64, in_records bool, records uint8) of a device batch."""
     n = int(b.n_items)
-    raw = dev_copy(ctypes.cast(b.item_off, ctypes.c_void_p).value, 8 * n, device, torch.int64)
-    ln = dev_copy(ctypes.cast(b.item_len, ctypes.c_void_p).value, 8 * n, device, torch.int64)
-    in_rec = raw < 0  # bit 63
-    off = raw & ((1 << 63) - 1)
+    if b.item_end:
+        off, ln, in_rec = item_end_tensors(b, device)
+    else:
+        raw = dev_copy(_ptr(b.item_off), 8 * n, device, torch.int64)
+        ln = dev_copy(_ptr(b.item_len), 8 * n, device, torch.int64)
+        in_rec = raw < 0  # bit 63
+        off = raw & ((1 << 63) - 1)
     rec = dev_copy(b.records, int(b.records_len), device) if b.records_len else torch.zeros(1, dtype=torch.uint8,
                                                                                              device=device)
     return off, ln, in_rec, rec
