@@ -234,6 +234,157 @@ __global__ void __launch_bounds__(256) RIO_LEAN_ATTR k_parse_lean(DevBufs d, Par
   }
 }
 
+// The lean path in item-end mode (RIO_CFG_ITEM_END device results, the
+// none codec): the same block shape as k_parse_lean, one block per wave
+// iteration with the next block's descriptor loaded while this one is parsed,
+// cumSize per item (8 B) written coalesced, and nothing but the arrays this
+// path touches passed in (the full DevBufs costs ~90 scalar registers, whose
+// spills dominated the previous kernel's instruction stream). Declined blocks
+// go to the list for k_parse, untouched.
+struct LeanArgs {
+  const uint8_t *span;
+  const unsigned long long *blk_c0, *blk_meta, *blk_len, *blk_item_base;
+  unsigned long long *blk_status, *blk_hdr, *blk_data, *blk_coff;
+  unsigned long long *item_end;
+  uint8_t *side;
+  Ctl *ctl;
+  const unsigned long long *nblocks;
+  uint64_t limit_chunk, item_cap;
+};
+
+__global__ void __launch_bounds__(256) k_lean_end(LeanArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[4][1040];
+  __shared__ __attribute__((aligned(16))) uint16_t s_tpos[4][264];
+  uint8_t *lwin = s_win[threadIdx.x >> 6];
+  uint16_t *ltpos = s_tpos[threadIdx.x >> 6];
+  const uint64_t nb = *a.nblocks;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const int l = lane_id();
+  // lane j < 4 holds descriptor field j of the wave's next block
+  const unsigned long long *dsrc = l == 0 ? a.blk_c0 : l == 1 ? a.blk_meta : l == 2 ? a.blk_len : a.blk_item_base;
+  unsigned long long desc = (l < 4 && wave < nb) ? dsrc[wave] : 0;
+  for (uint64_t b = wave; b < nb; b += nwaves) {
+    const uint64_t c0 = readlane_u64(desc, 0);
+    const unsigned long long meta = readlane_u64(desc, 1), len = readlane_u64(desc, 2);
+    const uint64_t base = readlane_u64(desc, 3);
+    const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
+    const uint64_t nck = meta & kMetaTotalMask;
+    const bool ok = (meta & kMetaComplete) && (meta & kMetaRegular) && cls == kMagicPacked && c0 < a.limit_chunk &&
+                    len < (1ull << 32);
+    uint32_t w[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u}, bnd[4] = {0, 0, 0, 0};
+    const uint8_t *ck = a.span + c0 * kChunk;
+    if (ok) {
+      const uint32_t size0 = len < (uint64_t)kMaxPayload ? (uint32_t)len : (uint32_t)kMaxPayload;
+      if (16u * l + 16 <= size0) {  // 4-byte aligned: 28 + 16 l
+        const uint4 v = *reinterpret_cast<const uint4 *>(ck + kChunkHdr + 16 * l);
+        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+      }
+      if (nck >= 2) {  // payload kBndW0 + 16 l: chunk c0's tail, then c0 + 1's head
+        const uint8_t *src = (l < 32) ? ck + kChunkHdr + kBndW0 + 16 * l : ck + kChunk + kChunkHdr + 16 * (l - 32);
+        const uint4 v = *reinterpret_cast<const uint4 *>(src);
+        bnd[0] = v.x, bnd[1] = v.y, bnd[2] = v.z, bnd[3] = v.w;
+      }
+    }
+    const uint64_t bn = b + nwaves;  // the next block's descriptor, in flight while this one is parsed
+    desc = (l < 4 && bn < nb) ? dsrc[bn] : 0;
+    bool done = false;
+    uint32_t hdr = 0;
+    if (ok) {
+      const uint32_t tmask = term4(w[0]) | (term4(w[1]) << 4) | (term4(w[2]) << 8) | (term4(w[3]) << 12);
+      const uint32_t cnt = __popc(tmask);
+      const uint32_t incl = wave_incl_sum_dpp(cnt);
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      *reinterpret_cast<uint4 *>(lwin + 16 * l) = make_uint4(w[0], w[1], w[2], w[3]);
+      {  // terminator positions of ordinals 0..263 (a header of <= 256 sizes ends by then)
+        uint32_t m = (incl - cnt < 264u) ? tmask : 0u, o = incl - cnt;
+        while (m && o < 264u) {
+          const uint32_t i = __ffs(m) - 1;
+          m &= m - 1;
+          ltpos[o++] = (uint16_t)(16 * l + i);
+        }
+      }
+      wave_lds_sync();
+      const uint32_t p0 = ltpos[0];
+      const uint32_t nitems = (total > 0 && p0 < 2) ? uvarint4(lds_bytes4(lwin, 0), p0 + 1) : ~0u;
+      if (nitems <= 256 && nitems < total) {
+        hdr = (uint32_t)ltpos[nitems] + 1;
+        const uint32_t plen = (uint32_t)len;
+        uint32_t v[4], st[4];
+        bool lng = false, bad = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          v[k] = 0;
+          const uint32_t o = 64u * k + (uint32_t)l + 1;
+          if (o <= nitems) {
+            const uint32_t e = ltpos[o], n = e - ltpos[o - 1];  // varint o: bytes e-n+1 .. e
+            if (n > 4) lng = true;
+            else v[k] = uvarint4(lds_bytes4(lwin, e + 1 - n), n);
+            bad |= v[k] > plen;
+          }
+        }
+        // item starts: u32 scans (steps below 2^28: a scan's first wrap leaves incl < v)
+        uint32_t carry = hdr;
+        bool wrap = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t inc = wave_incl_sum_dpp(v[k]);
+          wrap |= inc < v[k];
+          st[k] = carry + inc - v[k];
+          const uint32_t add = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+          wrap |= carry + add < carry;
+          carry += add;
+        }
+        // straddlers: only across the first chunk boundary, inside the boundary
+        // window (written from the registers); any other crossing is declined
+        bool far = false, sd[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t s_ = st[k], e_ = st[k] + v[k];
+          sd[k] = v[k] > 0 && s_ < (uint32_t)kMaxPayload && e_ > (uint32_t)kMaxPayload;
+          far |= v[k] > 0 && s_ / (uint32_t)kMaxPayload != (e_ - 1) / (uint32_t)kMaxPayload &&
+                 !(sd[k] && s_ >= kBndW0 && e_ <= kBndW0 + 1024);
+        }
+        if (!__ballot(lng || bad || wrap || far) && carry == plen) {
+          done = true;
+          const uint64_t cap = a.item_cap;
+#pragma unroll
+          for (int k = 0; k < 4; k++) {  // cumSize (scannerv2.go:83-91): the item's end past the header
+            const uint32_t o = 64u * k + (uint32_t)l + 1;
+            const uint64_t slot = base + (o - 1);
+            if (o <= nitems && slot < cap) view_store(a.item_end + slot, (unsigned long long)(st[k] + v[k] - hdr));
+          }
+          if (base + nitems > cap && l == 0) atomicOr(&a.ctl->out_overflow, 1ull);
+          unsigned long long sm = __ballot(sd[0]) | __ballot(sd[1]) | __ballot(sd[2]) | __ballot(sd[3]);
+          if (sm) {  // the straddler at the boundary, from the registers
+            const int L = __ffsll((long long)sm) - 1;
+            uint32_t S = 0, V = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const bool has = (__ballot(sd[k]) >> L) & 1ull;
+              if (has) {
+                S = (uint32_t)__builtin_amdgcn_readlane((int)st[k], L);
+                V = (uint32_t)__builtin_amdgcn_readlane((int)v[k], L);
+              }
+            }
+            straddler_from_regs(bnd, a.side, S, V, c0 * (unsigned long long)kChunk + kChunkHdr + S);
+          }
+        }
+      }
+      wave_lds_sync();  // the next block's window reuses lwin / ltpos
+    }
+    if (l == 0) {
+      if (done) {
+        a.blk_status[b] = kBlkOk;
+        a.blk_hdr[b] = hdr;
+        a.blk_data[b] = c0 * (uint64_t)kChunk;
+      } else {
+        a.blk_coff[atomicAdd(&a.ctl->n_retry, 1ull)] = b;
+      }
+    }
+  }
+}
+
 // The blocks k_parse left to the general parser (headers past the first 1 KiB,
 // irregular chunk layouts, and every malformed header: parse_header computes
 // the reference's error values).
@@ -547,6 +698,21 @@ static inline unsigned grid_of(uint64_t n, unsigned per, unsigned cap) {
 
 void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
   hipLaunchKernelGGL(k_parse, dim3(grid_of(max_blocks, 4 * kBatch, RIO_PARSE_GRID)), dim3(256), 0, st, d, a);
+}
+
+void launch_lean_end(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
+  static unsigned cap = 0;
+  if (!cap) {  // one resident round: workgroups per CU at this build's occupancy x CUs
+    int per_cu = 0, dev = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lean_end, 256, 0) != hipSuccess || per_cu < 1)
+      per_cu = 4;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+      ncu = 256;
+    cap = (unsigned)(per_cu * ncu);
+  }
+  LeanArgs la{a.span, d.blk_c0, d.blk_meta, d.blk_len, d.blk_item_base, d.blk_status, d.blk_hdr, d.blk_data,
+              d.blk_coff, d.item_off, d.side, d.ctl, a.nblocks, a.limit_chunk, a.item_cap};
+  hipLaunchKernelGGL(k_lean_end, dim3(grid_of(max_blocks, 4, cap)), dim3(256), 0, st, la);
 }
 
 void launch_parse_lean(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {

@@ -141,4 +141,40 @@ void codec_error_text(uint64_t code, uint64_t off, uint64_t file_off, rio_error 
   }
 }
 
+// ---------------------------------------------------------------- chains
+// Transformer chains (registry.go:121-146): the blocks one untransform stage
+// decoded, framed again as a chunk stream (chunk.go:31-53 layout: magic, crc 0,
+// flag 0, size, total, index; payloads of 32,740 bytes) so the next stage's
+// codec reads them like file chunks. Wave per block; block b's chunks start at
+// chunk soff[b] of out.
+__global__ void __launch_bounds__(256) k_reframe(const uint8_t *__restrict__ dec, const unsigned long long *dec_off,
+                                                 const unsigned long long *out_len, const unsigned long long *soff,
+                                                 uint64_t nv, uint32_t mlo, uint32_t mhi, uint8_t *__restrict__ out) {
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const int l = threadIdx.x & 63;
+  for (uint64_t b = wave; b < nv; b += nwaves) {
+    const uint64_t len = out_len[b], c0 = soff[b], total = soff[b + 1] - c0;
+    const uint8_t *src = dec + dec_off[b];
+    for (uint64_t j = 0; j < total; j++) {
+      uint8_t *ck = out + (c0 + j) * (uint64_t)kChunk;
+      const uint64_t lo = j * (uint64_t)kMaxPayload;
+      const uint32_t sz = (uint32_t)((len - lo) < (uint64_t)kMaxPayload ? (len - lo) : (uint64_t)kMaxPayload);
+      if (l < 7) {
+        const uint32_t h[7] = {mlo, mhi, 0u, 0u, sz, (uint32_t)total, (uint32_t)j};
+        reinterpret_cast<uint32_t *>(ck)[l] = h[l];
+      }
+      for (uint32_t k = l; k < sz; k += 64) ck[kChunkHdr + k] = src[lo + k];
+    }
+  }
+}
+
+void launch_reframe(const uint8_t *dec, const unsigned long long *dec_off, const unsigned long long *out_len,
+                    const unsigned long long *soff, uint64_t nv, uint64_t magic, uint8_t *out, hipStream_t st) {
+  uint64_t g = (nv + 3) / 4;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(k_reframe, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, dec, dec_off, out_len, soff, nv,
+                     (uint32_t)magic, (uint32_t)(magic >> 32), out);
+}
+
 }  // namespace rio

@@ -64,7 +64,9 @@ __device__ __forceinline__ void parse_block(const DevBufs &d, const ParseArgs &a
       ea = d.blk_a[b];
       eb = d.blk_b[b];
     }
-    if (parse) {
+    if (parse && a.no_items) {
+      parse = false;  // a chain's earlier stage: decoded, not parsed (status ok)
+    } else if (parse) {
       Payload pl = (a.codec != RIO_CODEC_NONE) ? make_contig_payload(d.dec + d.blk_dec_off[b], len)
                                                : desc_payload(a.span, d, c0, meta, len, pay0);
       ParseOut po;

@@ -39,6 +39,7 @@ void launch_block_scan(const unsigned long long *in, unsigned long long *out, un
 // blocks.hip
 void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
 void launch_parse_lean(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
+void launch_lean_end(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
 void launch_parse_slow(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st);
 void launch_dec_nitems(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st);
 void launch_strad(const uint8_t *span, const DevBufs &d, uint64_t nslots, uint64_t side_cap, int32_t sparse, int32_t end_mode,
@@ -169,6 +170,11 @@ struct rio_ctx {
   unsigned long long *d_seg = nullptr;
   uint64_t d_seg_cap = 0;
   std::vector<uint64_t> seg_end_h, seg_file_h;
+  // transformer chains: the reframed stage outputs (two, alternating) and their chunk offsets
+  uint8_t *d_chain[2] = {nullptr, nullptr};
+  uint64_t d_chain_cap[2] = {0, 0};
+  unsigned long long *d_chain_meta = nullptr;
+  uint64_t d_chain_meta_cap = 0;
   // last async call
   uint64_t last_nchunks = 0, last_file_off = 0, last_in_bytes = 0, last_nseg = 0;
   int32_t last_codec = 0, last_mode = 0;
@@ -215,7 +221,7 @@ static void free_all(rio_ctx *c) {
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.blk_data, d.blk_file_off, d.blk_seg, d.cmp, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len,
-                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan, c->d_seg};
+                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan, c->d_seg, c->d_chain[0], c->d_chain[1], c->d_chain_meta};
   for (void *p : ps)
     if (p) hipFree(p);
   if (c->h_ctl) hipHostFree(c->h_ctl);
@@ -417,8 +423,13 @@ static int ensure_side(rio_ctx *c, uint64_t need) {
 
 // sparse: straddlers land at their own span offset in a span-sized side buffer
 // (device-resident results, no straddler scan); else compacted (host results).
+// stage_flags (transformer chains): kStageNoItems -- decode, no packed parse
+// (a chain's earlier stage); kStageNoCrc -- the span is a reframed stage
+// output, not file chunks (no CRC stored)
+enum { kStageNoItems = 1, kStageNoCrc = 2 };
+
 static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t limit_chunk, int is_file_end,
-                   int tail_partial, int32_t codec, int32_t mode, bool sparse, int attempt) {
+                   int tail_partial, int32_t codec, int32_t mode, bool sparse, int attempt, int stage_flags = 0) {
   if (sparse && codec == RIO_CODEC_NONE && ensure_side(c, nchunks * (uint64_t)kChunk)) return -1;
   DevBufs &d = c->d;
   hipStream_t st = c->st, st2 = c->st2;
@@ -461,7 +472,9 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   HIP_OK(hipEventRecord(c->ev[kEvParse0], st2));
   // the shipped library always runs every stage; RIO_ABLATE (a -D of ablation
   // builds, tools/ablate.py) drops stages for measurement only
-  const bool run_parse = !(RIO_ABLATE & 2) && mode != kModeRaw, run_crc = !(RIO_ABLATE & 4) && mode != kModeRaw;
+  const bool run_parse = !(RIO_ABLATE & 2) && mode != kModeRaw,
+             run_crc = !(RIO_ABLATE & 4) && mode != kModeRaw && !(stage_flags & kStageNoCrc);
+  const bool no_items = (stage_flags & kStageNoItems) != 0;
   // ablation builds (-DRIO_FUSED_PARSE=1): none codec in one pass -- the wave
   // that checksums a block's first chunk parses the block
   const bool fused = RIO_FUSED_PARSE && codec == RIO_CODEC_NONE && run_parse && run_crc && nchunks > 0;
@@ -469,15 +482,18 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   if (nchunks > 0 && run_parse) {
     ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap, sparse,
                  (c->item_end_mode && sparse) ? 1 : 0};
-    if (codec != RIO_CODEC_NONE) launch_dec_nitems(d, c->nblocks_dev, max_blocks, st2);
+    pa.no_items = no_items ? 1 : 0;
+    if (no_items) HIP_OK(hipMemsetAsync(d.blk_nitems, 0, max_blocks * sizeof(unsigned long long), st2));
+    else if (codec != RIO_CODEC_NONE) launch_dec_nitems(d, c->nblocks_dev, max_blocks, st2);
     launch_block_scan(d.blk_nitems, d.blk_item_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
     if (fused) {
       HIP_OK(hipEventRecord(c->ev[kEvCrc0], st2));
       launch_crc(span, nchunks, d, ca, c->ncu, st2, &pa);
       HIP_OK(hipEventRecord(c->ev[kEvCrc1], st2));
-    } else if (codec == RIO_CODEC_NONE && mode == kModeBody) {
+    } else if (codec == RIO_CODEC_NONE && mode == kModeBody && !no_items) {
       // the common block shape in a lean kernel, the rest listed for k_parse
-      launch_parse_lean(d, pa, max_blocks, st2);
+      if (pa.end_mode) launch_lean_end(d, pa, max_blocks, st2);  // (item-end device results)
+      else launch_parse_lean(d, pa, max_blocks, st2);
       ParseArgs pl = pa;
       pl.list = d.blk_coff;
       pl.list_n = &d.ctl->n_retry;
@@ -632,9 +648,15 @@ static int grow_for_overflow(rio_ctx *c, int32_t codec) {
   }
 }
 
+static int run_chain(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span, uint64_t nbytes,
+                     uint64_t file_off, int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode,
+                     rio_results *res, rio_batch *out);
+
 static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span, uint64_t nbytes,
                     uint64_t file_off, int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode,
-                    rio_results *res, rio_batch *out) {
+                    rio_results *res, rio_batch *out, int stage_flags = 0) {
+  if (codec & RIO_CODEC_CHAIN_FLAG)
+    return run_chain(c, dspan, report_span, nbytes, file_off, is_file_end, limit_off, codec, mode, res, out);
   const bool to_host = res != nullptr;
   HIP_OK(hipSetDevice(c->device));
   const uint64_t nchunks = nbytes / kChunk;
@@ -648,7 +670,9 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
   uint64_t limit_chunk = UINT64_MAX;
   if (limit_off != UINT64_MAX) limit_chunk = limit_off <= file_off ? 0 : (limit_off - file_off + kChunk - 1) / kChunk;
   for (int attempt = 0; attempt < 4; attempt++) {
-    if (enqueue(c, dspan, nchunks, limit_chunk, is_file_end, tail_partial, codec, mode, !to_host, attempt)) return -1;
+    if (enqueue(c, dspan, nchunks, limit_chunk, is_file_end, tail_partial, codec, mode, !to_host, attempt,
+                stage_flags))
+      return -1;
     HIP_OK(hipMemcpyAsync(c->h_ctl, c->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipStreamSynchronize(c->st));
     if (c->h_ctl->out_overflow == 0) break;
@@ -666,8 +690,8 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
   hipEventElapsedTime(&ms, c->ev[kEvStart], c->ev[kEvEnd]);
   // host results of a compressed codec: only the decoded record bytes cross PCIe
   c->last_cmp = false;
-  if (to_host && codec != RIO_CODEC_NONE && c->h_ctl->out_overflow == 0 && c->h_ctl->n_valid_blocks > 0 &&
-      c->h_ctl->rec_bytes > 0) {
+  if (to_host && codec != RIO_CODEC_NONE && !(stage_flags & kStageNoItems) && c->h_ctl->out_overflow == 0 &&
+      c->h_ctl->n_valid_blocks > 0 && c->h_ctl->rec_bytes > 0) {
     if (c->d.cmp_cap < c->h_ctl->rec_bytes + 64) {
       if (dalloc(&c->d.cmp, c->h_ctl->rec_bytes + 64)) return -1;
       c->d.cmp_cap = c->h_ctl->rec_bytes + 64;
@@ -685,6 +709,99 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
     rio_set_error(&out->err, RIO_ERR_CAPACITY, file_off, "output capacity exceeded");
     out->stop = RIO_STOP_ERROR;
   }
+  return 0;
+}
+
+// ------------------------------------------------------------ transformer chains
+// registry.GetUntransformer's combined function (registry.go:121-146): the
+// chain t0..tn-1 is untransformed tn-1 first. Stage 1 runs the file's chunks
+// through everything but the packed parse -- chunk checks, CRC, block
+// structure, tn-1's decode -- so its stop (EOF, trailer, shard limit, the first
+// chunk or codec error) is the file's. The blocks it decoded are framed again as
+// chunks (k_reframe: 32,740-byte payloads, the block's magic) and decoded by
+// the next codec, and so on; the last stage also parses the packed headers.
+// A later stage's error lies in a block before stage 1's stop, so it comes
+// first in file order; it is reported at its block's file offset. (The
+// reference hands each stage the same scratch buffer, so a stage whose output
+// fits it can overwrite its own input; this implements the composition the
+// chain describes.)
+namespace rio {
+void launch_reframe(const uint8_t *dec, const unsigned long long *dec_off, const unsigned long long *out_len,
+                    const unsigned long long *soff, uint64_t nv, uint64_t magic, uint8_t *out, hipStream_t st);
+}
+
+static int ensure_dbuf(uint8_t **p, uint64_t *cap, uint64_t n) {
+  if (*cap >= n) return 0;
+  if (dalloc(p, n)) return -1;
+  *cap = n;
+  return 0;
+}
+
+static int run_chain(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span, uint64_t nbytes,
+                     uint64_t file_off, int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode,
+                     rio_results *res, rio_batch *out) {
+  const int n = (codec >> 8) & 0xff;
+  auto at = [&](int i) { return (codec >> (2 * i)) & 3; };
+  // stage 1: the file's chunks, the last transformer's untransform
+  if (run_span(c, dspan, report_span, nbytes, file_off, is_file_end, limit_off, at(n - 1), mode, res, out,
+               kStageNoItems))
+    return -1;
+  const Ctl s1 = *c->h_ctl;
+  const rio_batch b1 = *out;
+  const uint64_t magic = mode == kModeHeader ? 0xf70416c25cd9e1d9ull
+                         : mode == kModeTrailer ? 0x3a75dfcbd71abafeull : 0x2e3c0734eb47762eull;  // magic.go
+  uint64_t nv = s1.n_valid_blocks;
+  std::vector<unsigned long long> c0(nv), olen(nv), doff(nv);
+  if (nv) {
+    HIP_OK(hipMemcpy(c0.data(), c->d.blk_c0, nv * 8, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(olen.data(), c->d.blk_out_len, nv * 8, hipMemcpyDeviceToHost));
+  }
+  Ctl last = s1;      // the latest stage's control block
+  bool later_err = false;
+  for (int k = n - 2; k >= 0 && nv > 0; k--) {
+    // reframe the nv blocks decoded by the previous stage
+    std::vector<unsigned long long> soff(nv + 1, 0);
+    for (uint64_t b = 0; b < nv; b++) soff[b + 1] = soff[b] + (olen[b] ? (olen[b] - 1) / kMaxPayload + 1 : 1);
+    const uint64_t sbytes = soff[nv] * kChunk;
+    uint8_t *buf = c->d_chain[k & 1];
+    if (ensure_dbuf(&c->d_chain[k & 1], &c->d_chain_cap[k & 1], sbytes) ||
+        ensure_dbuf(reinterpret_cast<uint8_t **>(&c->d_chain_meta), &c->d_chain_meta_cap, 8 * (nv + 1)))
+      return -1;
+    buf = c->d_chain[k & 1];
+    HIP_OK(hipMemcpy(c->d_chain_meta, soff.data(), 8 * (nv + 1), hipMemcpyHostToDevice));
+    launch_reframe(c->d.dec, c->d.blk_dec_off, c->d.blk_out_len, c->d_chain_meta, nv, magic, buf, c->st);
+    HIP_OK(hipStreamSynchronize(c->st));
+    // the stage's chunks may outnumber the file's (decoded bytes): the span grows
+    if (rio_ctx_reserve_span(c, sbytes)) return -1;
+    if (run_span(c, buf, report_span, sbytes, file_off, 1, UINT64_MAX, at(k), mode, res, out,
+                 kStageNoCrc | (k > 0 ? kStageNoItems : 0)))
+      return -1;
+    last = *c->h_ctl;
+    if (c->h_ctl->stop_kind == 2) later_err = true;
+    nv = c->h_ctl->n_valid_blocks;  // a stage stops at its first error
+    if (k > 0 && nv) HIP_OK(hipMemcpy(olen.data(), c->d.blk_out_len, nv * 8, hipMemcpyDeviceToHost));
+    if (later_err) break;
+  }
+  // the chain's result: the last stage's items; the stop is the first stage's
+  // unless a later stage failed on a block before it
+  if (n < 2 || s1.n_valid_blocks == 0) return 0;  // (no block reached a later stage: stage 1's batch stands)
+  out->consumed = b1.consumed;
+  out->in_bytes = b1.in_bytes;
+  out->span = b1.span;
+  if (later_err) {
+    Ctl e = last;
+    if (e.stop_block != kNone && e.stop_block < c0.size()) e.blk_c0 = c0[e.stop_block];
+    rio_fill_error(e, file_off, mode, &out->err);
+    out->stop = RIO_STOP_ERROR;
+  } else if (out->err.code != RIO_ERR_CAPACITY) {
+    out->stop = b1.stop;
+    out->err = b1.err;
+  }
+  // host results: every block's offset in the file (the stages' own chunk
+  // indexes are of the reframed spans)
+  if (res && out->block_file_off)
+    for (uint64_t b = 0; b < out->n_blocks && b < c0.size(); b++)
+      const_cast<uint64_t *>(out->block_file_off)[b] = file_off + c0[b] * kChunk;
   return 0;
 }
 
@@ -737,6 +854,10 @@ extern "C" int rio_scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes,
 extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, uint64_t file_off,
                                      int32_t codec) {
   if (!ctx) return -1;
+  if (codec & RIO_CODEC_CHAIN_FLAG) {  // each stage needs the previous one's block sizes on the host
+    set_last_error("a transformer chain decodes through rio_scan_device / rio_scan_span, not the async entry");
+    return -1;
+  }
   HIP_OK(hipSetDevice(ctx->device));
   const uint64_t nchunks = nbytes / kChunk;
   if (nchunks > ctx->max_chunks) {
@@ -856,10 +977,7 @@ static int decode_raw(rio_ctx *c, const uint8_t *const *payloads, const uint32_t
   for (int i = 0; i < n; i++) total += lens[i];
   const uint64_t nch = total ? (total + kMaxPayload - 1) / kMaxPayload : 1;
   const uint64_t nbytes = nch * kChunk;
-  if (nch > c->max_chunks) {
-    rio_set_error(err, RIO_ERR_CAPACITY, 0, "block of %" PRIu64 " bytes exceeds ctx capacity", total);
-    return RIO_ERR_CAPACITY;
-  }
+  if (rio_ctx_reserve_span(c, nbytes)) return -1;  // a block longer than the span: the span grows to it
   if (c->h_stage_cap < nbytes) {
     if (c->h_stage) hipHostFree(c->h_stage);
     c->h_stage = nullptr;
@@ -946,11 +1064,60 @@ extern "C" int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, co
     }
     return 0;
   }
+  if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+  if (codec & RIO_CODEC_CHAIN_FLAG) {  // registry.go:121-146: the last transformer's untransform first
+    const int m = (codec >> 8) & 0xff;
+    if (m < 2 || m > 4) {
+      rio_set_error(err, RIO_ERR_ARG, 0, "bad chain codec %d", codec);
+      return RIO_ERR_ARG;
+    }
+    std::vector<uint8_t> cur;
+    const uint8_t *const *ps = payloads;
+    const uint32_t *ls = lens;
+    int np = n;
+    const uint8_t *one[1];
+    uint32_t one_len[1];
+    for (int k = m - 1; k >= 0; k--) {
+      const int32_t ck = (codec >> (2 * k)) & 3;
+      uint64_t need = 0;
+      int rc;
+      std::vector<uint8_t> nxt(k ? (size_t)(64 << 10) : 0);
+      for (;;) {  // the stage's output: scratch for the last stage, a host buffer before it
+        uint8_t *dst = k ? nxt.data() : scratch;
+        const uint64_t dcap = k ? nxt.size() : cap;
+        rc = decode_raw(ctx, ps, ls, np, ck, dst, dcap, &need, err);
+        if (k && rc == RIO_ERR_CAPACITY && need > nxt.size()) {
+          nxt.resize((size_t)need);
+          continue;
+        }
+        break;
+      }
+      if (rc) {
+        *out_len = need;
+        return rc;
+      }
+      if (k == 0) {
+        *out_len = need;
+        return 0;
+      }
+      if (need > UINT32_MAX) {
+        rio_set_error(err, RIO_ERR_CAPACITY, 0, "chain stage output of %" PRIu64 " bytes", need);
+        return RIO_ERR_CAPACITY;
+      }
+      nxt.resize((size_t)need);
+      cur.swap(nxt);
+      one[0] = cur.data();
+      one_len[0] = (uint32_t)cur.size();
+      ps = one;
+      ls = one_len;
+      np = 1;
+    }
+    return 0;
+  }
   if (codec != RIO_CODEC_FLATE && codec != RIO_CODEC_ZSTD) {
     rio_set_error(err, RIO_ERR_ARG, 0, "unknown codec %d", codec);
     return RIO_ERR_ARG;
   }
-  if (hipSetDevice(ctx->device) != hipSuccess) return -1;
   return decode_raw(ctx, payloads, lens, n, codec, scratch, cap, out_len, err);
 }
 

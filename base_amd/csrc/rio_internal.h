@@ -216,6 +216,10 @@ struct ParseArgs {
   // k_parse over a list of blocks (the ones k_parse_lean declined) instead of all
   const unsigned long long *list;
   const unsigned long long *list_n;
+  // a transformer chain's earlier stage: block structure and codec only, no
+  // packed-header parse (the decoded bytes are the next stage's input)
+  int32_t no_items;
+  int32_t pad2;
 };
 struct CrcArgs {
   int32_t flags;  // RIO_ABLATE of ablation builds (1 no CRC fold); 0 in the shipped library

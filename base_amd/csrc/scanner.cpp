@@ -600,9 +600,18 @@ int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec,
     }
     found++;
   }
-  if (found > 1) {  // a chain, untransformed in reverse order (registry.go:121-146)
+  if (found > 4) {  // longer chains than RIO_CODEC_CHAIN encodes
     rio_set_error(err, RIO_ERR_FALLBACK, 0, "transformer chain of %d: decode with recordio.NewScanner", found);
     return RIO_ERR_FALLBACK;
+  }
+  if (found > 1) {  // a chain, untransformed in reverse order (registry.go:121-146)
+    int32_t codes = 0;
+    for (int i = 0; i < n; i++) {
+      const int32_t ci = strncmp(values[i], "flate", 5) == 0 ? RIO_CODEC_FLATE : RIO_CODEC_ZSTD;
+      codes |= ci << (2 * i);
+    }
+    *codec = RIO_CODEC_CHAIN(found, codes);
+    return 0;
   }
   *codec = c;
   return 0;

@@ -24,6 +24,16 @@ _ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("RIO_GPU_LIB") or os.path.join(_ROOT, "lib", "librio_gpu.so")  # (override: experiments)
 
 RIO_CODEC_NONE, RIO_CODEC_FLATE, RIO_CODEC_ZSTD = 0, 1, 2
+RIO_CODEC_CHAIN_FLAG = 0x10000
+
+
+def codec_chain(*codecs: int) -> int:
+    """RIO_CODEC_CHAIN of the header's transformer values t0, t1, ... (each
+    RIO_CODEC_FLATE or RIO_CODEC_ZSTD; untransformed last to first)."""
+    codes = 0
+    for i, c in enumerate(codecs):
+        codes |= c << (2 * i)
+    return RIO_CODEC_CHAIN_FLAG | (len(codecs) << 8) | codes
 RIO_STOP_MORE, RIO_STOP_EOF, RIO_STOP_ERROR = 0, 1, 2
 RIO_ERR_CAPACITY = 98
 RIO_ERR_LOCATION = 22  # "Invalid location ..." / no item at a location (scannerv2.go:348-361)

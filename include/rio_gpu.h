@@ -43,6 +43,14 @@ enum rio_codec {
     RIO_CODEC_FLATE = 1, /* recordioflate.FlateUncompress, recordioflate.go:54-65 */
     RIO_CODEC_ZSTD = 2,  /* recordiozstd.zstdUncompress, recordiozstd.go:67-78 */
 };
+/* A chain of transformers (the header's "transformer" values t0 .. tn-1, 2 <=
+ * n <= 4, each flate or zstd): blocks were transformed by t0 first, so they
+ * are untransformed tn-1 first, t0 last (registry.go:121-146). As a codec
+ * argument: RIO_CODEC_CHAIN(n, t0 | t1 << 2 | t2 << 4 | t3 << 6). Host-
+ * synchronous calls only (rio_scan_span, rio_scan_device, rio_decode_block,
+ * the scanner layer): each stage is a launch over the previous stage's output. */
+#define RIO_CODEC_CHAIN_FLAG 0x10000
+#define RIO_CODEC_CHAIN(n, codes) (RIO_CODEC_CHAIN_FLAG | ((n) << 8) | (codes))
 
 /* Error codes carried in rio_error.code (the reference's error conditions). */
 enum rio_err_code {
@@ -69,8 +77,8 @@ enum rio_err_code {
     RIO_ERR_LEGACY = 20,        /* (unused since v1 files decode natively; kept for ABI stability) */
     RIO_ERR_IO = 21,            /* reader callback failed                      */
     RIO_ERR_LOCATION = 22,      /* "Invalid location %+v, block has only %d items" scannerv2.go:358 */
-    RIO_ERR_FALLBACK = 23,      /* transformers this library does not decode: a chain of several, or a
-                                   name other than flate/zstd (registry.go:113-148). Decode the file with
+    RIO_ERR_FALLBACK = 23,      /* transformers this library does not decode: a name other than
+                                   flate/zstd, or a chain of more than 4 (registry.go:113-148). Decode the file with
                                    recordio.NewShardScanner; msg is the reference's text for the case the
                                    name is not registered there either ("Transformer %s not found") */
     RIO_ERR_V1_RECORD = 24,     /* v1 record header / read errors (InternalScan): "recordio: crc check
@@ -197,10 +205,11 @@ const char *rio_build_id(void);
 void *rio_stream(rio_ctx *ctx);
 
 /* Transformer registry lookup (registry.go:113-148 + recordioflate/zstd Init):
- * resolves the header's "transformer" values to a codec. Returns 0 and sets
- * *codec, or RIO_ERR_FALLBACK for a chain of several transformers or a name
- * other than flate / zstd: the caller decodes such a file with the reference
- * scanner, whose registry may hold user transformers (registry.go:166). */
+ * resolves the header's "transformer" values to a codec -- none, flate, zstd,
+ * or a RIO_CODEC_CHAIN of 2-4 of flate / zstd. Returns 0 and sets *codec, or
+ * RIO_ERR_FALLBACK for a name other than flate / zstd (or a chain of more than
+ * 4): the caller decodes such a file with the reference scanner, whose
+ * registry may hold user transformers (registry.go:166). */
 int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec, rio_error *err);
 
 /* ---- batch layer ----

@@ -377,6 +377,29 @@ def main():
     add("err_unknown_transformer", d, [], header=[("transformer", "nonexistent")],
         err="Transformer nonexistent not found")
 
+    # transformer chains (registry.go:121-146: t0 applied first by the writer,
+    # untransformed last): two and three stages, a trailer (transformed too),
+    # and a corrupt inner stream whose chunk CRCs are valid
+    if have_zstd():
+        crecs = [rnd_bytes(rng, rng.choice([0, 1, 5, 300, 4000])) * rng.choice([1, 1, 30]) for _ in range(500)]
+        for name, trs, tr in (("chain_zstd_flate", ["zstd", "flate"], b"chain trailer"),
+                              ("chain_flate_zstd", ["flate 1", "zstd 3"], None),
+                              ("chain3_flate_zstd_flate", ["flate", "zstd", "flate 9"], b"T3")):
+            opts = WriterOpts(Transformers=list(trs), MaxItems=36, KeyTrailer=tr is not None)
+            d = write_file(crecs, opts, trailer=tr)
+            hdr = [("transformer", t) for t in trs] + ([("trailer", True)] if tr is not None else [])
+            add(name, d, crecs, header=hdr, trailer=tr)
+        # block 3 of chain_zstd_flate: one bit of its raw-DEFLATE stream flipped
+        d = bytearray(write_file(crecs, WriterOpts(Transformers=["zstd", "flate"], MaxItems=36)))
+        bl = blocks_of(bytes(d))
+        c0, _ = bl[3]
+        d[c0 * F.CHUNK_SIZE + 28 + 40] ^= 0x10
+        d = fix_crc(bytes(d), c0)
+        r = O.scan(d, read_trailer=False)
+        assert r.err and r.items == crecs[:len(r.items)], r.err
+        add("err_chain_inner", d, r.items, header=[("transformer", "zstd"), ("transformer", "flate")], err=r.err,
+            read_trailer=False, note="error text from the oracle (the chain's flate stage)")
+
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "cases": CASES}, f, indent=1)
     total = sum(c["size"] for c in CASES)

@@ -59,8 +59,11 @@ def test_codec_registry_lookup(gpu_lib):
     assert rc == 23 and msg == "Transformer nonexistent 3 not found"
     rc, _, msg = look(["flatex"])
     assert rc == 23 and msg == "Transformer flatex not found"
-    rc, _, _ = look(["flate", "zstd"])  # a chain: reverse-order untransform (registry.go:121-146)
-    assert rc == 23
+    # a chain: reverse-order untransform (registry.go:121-146), up to 4 stages
+    assert look(["flate", "zstd"])[:2] == (0, 0x10000 | (2 << 8) | 1 | (2 << 2))
+    assert look(["zstd 3", "flate", "flate 9"])[:2] == (0, 0x10000 | (3 << 8) | 2 | (1 << 2) | (1 << 4))
+    assert look(["flate"] * 5)[0] == 23  # longer: the reference scanner
+    assert look(["flate", "snappy"])[0] == 23
 
 
 def test_struct_layouts_match_header(tmp_path):

@@ -1,0 +1,166 @@
+"""Transformer chains on the GPU (registry.go:121-146): a file written with
+Transformers [t0, t1, ...] is untransformed tn-1 first. The golden chain cases
+run in test_gpu_parity.test_golden_cases; here the other entry points: the
+batch layer (host and device results, both output shapes), rio_decode_block,
+Seek / Gather, sharded scans, corrupt streams against the oracle, and the async
+entry's refusal (each stage needs the previous one's sizes on the host)."""
+import os
+import random
+import struct
+import sys
+
+import pytest
+
+from conftest import ROOT, golden_bytes, oracle_has_zstd
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+@pytest.fixture(scope="module")
+def chain_files(oracle):
+    from base_amd.recordio.writer import WriterOpts, write_file
+    if not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    rng = random.Random(17)
+    recs = [rng.randbytes(rng.choice([0, 3, 200, 3000])) * rng.choice([1, 1, 20]) for _ in range(900)]
+    out = {}
+    for trs in (["zstd", "flate"], ["flate 1", "zstd"], ["flate", "flate 9"], ["zstd", "flate", "zstd 1", "flate"]):
+        out[tuple(trs)] = write_file(recs, WriterOpts(Transformers=list(trs), MaxItems=41), trailer=b"TT")
+    return recs, out
+
+
+def _codec(trs):
+    from base_amd.recordio import gpu
+    return gpu.codec_chain(*[gpu.RIO_CODEC_FLATE if t.startswith("flate") else gpu.RIO_CODEC_ZSTD for t in trs])
+
+
+def _body(data):
+    hdr_chunks = struct.unpack_from("<I", data, 20)[0]
+    return hdr_chunks * 32768
+
+
+def test_chain_scanner_and_seek(gpu_ctx, oracle, chain_files):
+    from base_amd.recordio import gpu
+    from base_amd.recordio.writer import ItemLocation
+    recs, files = chain_files
+    for trs, data in files.items():
+        ref = oracle.scan(data)
+        assert ref.err == "" and ref.items == recs and ref.trailer == b"TT", trs
+        sc = gpu.NewScanner(data, ctx=gpu_ctx)
+        assert sc.Trailer() == b"TT"
+        got = []
+        while sc.Scan():
+            got.append(sc.Get())
+        assert sc.Finish() is None and got == recs, trs
+        sc = gpu.NewScanner(data, ctx=gpu_ctx)
+        pick = list(range(0, len(recs), 37))
+        assert sc.Gather([ItemLocation(*ref.locations[i]) for i in pick]) == [recs[i] for i in pick]
+        for i in pick[:5]:
+            sc.Seek(ItemLocation(*ref.locations[i]))
+            assert sc.Scan() and sc.Get() == recs[i]
+        sc.Finish()
+        # shards concatenate to the file
+        parts = []
+        for s in range(3):
+            sc = gpu.NewShardScanner(data, gpu.ScannerOpts(), s, s + 1, 3, ctx=gpu_ctx)
+            while sc.Scan():
+                parts.append(sc.Get())
+            assert sc.Finish() is None
+        assert parts == recs
+
+
+@pytest.mark.parametrize("item_end", [False, True])
+def test_chain_batch_layer(oracle, chain_files, item_end):
+    """rio_scan_span (host results, block offsets in the file) and
+    rio_scan_device (device results) over a chain file's body."""
+    import torch
+    from base_amd.recordio import gpu
+    recs, files = chain_files
+    ctx = gpu.Context(0, max_span_bytes=8 << 20, item_end=item_end)
+    try:
+        for trs, data in files.items():
+            body = data[_body(data):]
+            b = ctx.scan_span(body, file_off=_body(data), is_file_end=True, codec=_codec(trs))
+            assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, (trs, b.err.msg)
+            assert gpu.batch_items(b) == recs
+            ref = oracle.scan(data)
+            blocks = sorted({loc[0] for loc in ref.locations})
+            assert [b.block_file_off[i] for i in range(b.n_blocks)] == blocks
+            dev = torch.frombuffer(bytearray(body), dtype=torch.uint8).to("cuda:0")
+            bd = ctx.scan_device(dev.data_ptr(), len(body), file_off=_body(data), is_file_end=True,
+                                 codec=_codec(trs))
+            assert bd.stop == gpu.RIO_STOP_EOF and bd.err.code == 0, (trs, bd.err.msg)
+            assert gpu.device_batch_items(bd, body) == recs
+            with pytest.raises(RuntimeError):
+                ctx.scan_device_async(dev.data_ptr(), len(body), _body(data), _codec(trs))
+    finally:
+        ctx.close()
+
+
+def test_chain_decode_block(gpu_ctx, oracle, chain_files):
+    """rio_decode_block with a chain codec: the combined untransform of one block."""
+    from base_amd.recordio import format as F
+    from base_amd.recordio.codecs import make_compressor
+    recs, files = chain_files
+    for trs in files:
+        payload = F.packed_block_payload(recs[:60])
+        comp = payload
+        for t in trs:
+            comp = make_compressor(t)(comp)
+        pays = [comp[i:i + 1000] for i in range(0, len(comp), 1000)]
+        assert gpu_ctx.decode_block(pays, _codec(trs)) == payload
+
+
+def test_chain_corruption_matches_oracle(gpu_ctx, oracle, chain_files):
+    """Bit flips inside the compressed streams (chunk CRCs fixed, so only the
+    codecs and the packed parse can notice): the same items and error text as
+    the oracle's chain."""
+    import zlib
+    recs, files = chain_files
+    rng = random.Random(5)
+    for trs, data in files.items():
+        for trial in range(8):
+            b = bytearray(data)
+            c = rng.randrange(_body(data) // 32768, len(data) // 32768 - 1)  # not the trailer
+            o = c * 32768
+            size = struct.unpack_from("<I", b, o + 16)[0]
+            if size == 0:
+                continue
+            b[o + 28 + rng.randrange(size)] ^= 1 << rng.randrange(8)
+            struct.pack_into("<I", b, o + 8, zlib.crc32(bytes(b[o + 12:o + 28 + size])))
+            d = bytes(b)
+            ref = oracle.scan(d, read_trailer=False)
+            from base_amd.recordio import gpu
+            sc = gpu.NewScanner(d, ctx=gpu_ctx)
+            got = []
+            while sc.Scan():
+                got.append(sc.Get())
+            e = sc.Finish()
+            assert ("" if e is None else str(e)) == ref.err and got == ref.items, (trs, trial)
+
+
+def test_golden_chain_cases_decode(gpu_ctx, manifest):
+    """The committed chain fixtures (tests/golden/make_golden.py) through the
+    device batch path, against the manifest."""
+    import hashlib
+    import torch
+    from base_amd.recordio import gpu
+    for case in manifest:
+        if not case["name"].startswith("chain"):
+            continue
+        data = golden_bytes(case)
+        trs = [v for k, t, v in case["header"] if k == "transformer"]
+        body = data[_body(data):]
+        if case["trailer"] is not None:  # the body ends where the trailer block starts
+            body = body[:-32768 * (struct.unpack_from("<I", data, len(data) - 32768 + 24)[0] + 1)]
+        dev = torch.frombuffer(bytearray(body), dtype=torch.uint8).to("cuda:0")
+        b = gpu_ctx.scan_device(dev.data_ptr(), len(body), file_off=_body(data), is_file_end=True,
+                                codec=_codec(trs))
+        assert b.err.code == 0, b.err.msg
+        items = gpu.device_batch_items(b, body)
+        h = hashlib.sha256()
+        for it in items:
+            h.update(struct.pack("<Q", len(it)))
+            h.update(it)
+        assert len(items) == case["n_items"] and h.hexdigest() == case["items_sha256"]

@@ -243,21 +243,56 @@ def test_full_size_c2_property(oracle):
     ctx.close()
 
 
-def test_device_path_views(oracle):
-    """rio_scan_device (device-resident span): item views into the span plus
-    straddlers at their own span offset in the records buffer."""
+@pytest.mark.parametrize("codec", ["", "flate", "zstd"])
+@pytest.mark.parametrize("item_end", [False, True])
+def test_device_path_views(oracle, codec, item_end):
+    """rio_scan_device (device-resident span), in both output shapes: item views
+    into the span plus straddlers at their own span offset in the records
+    buffer, or item_end (cumSize) + block_data / block_first_off
+    (RIO_CFG_ITEM_END) -- the headline's output."""
     import torch
     from base_amd.recordio import gpu
-    ctx = gpu.Context(0, max_span_bytes=64 << 20)
+    if codec == "zstd" and not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    cid = {"": gpu.RIO_CODEC_NONE, "flate": gpu.RIO_CODEC_FLATE, "zstd": gpu.RIO_CODEC_ZSTD}[codec]
+    ctx = gpu.Context(0, max_span_bytes=64 << 20, item_end=item_end)
     rng = random.Random(11)
     for trial in range(10):
-        data, recs = _random_file(rng, "", rng.randrange(1, 2500), rng.choice([10, 300, 5000, 70000]))
+        data, recs = _random_file(rng, codec, rng.randrange(1, 2500), rng.choice([10, 300, 5000, 70000]))
         hdr_chunks = struct.unpack_from("<I", data, 20)[0]
         body = data[hdr_chunks * 32768:]
         dev = torch.frombuffer(bytearray(body), dtype=torch.uint8).to("cuda:0")
-        b = ctx.scan_device(dev.data_ptr(), len(body), file_off=hdr_chunks * 32768, is_file_end=True)
-        assert b.stop == gpu.RIO_STOP_EOF and b.err.code == 0, (trial, b.err.msg)
+        b = ctx.scan_device(dev.data_ptr(), len(body), file_off=hdr_chunks * 32768, is_file_end=True, codec=cid)
+        assert b.err.code == 0, (trial, b.err.msg)
+        assert bool(b.item_end) == item_end
         assert gpu.device_batch_items(b, body) == recs, trial
+    ctx.close()
+
+
+@pytest.mark.parametrize("item_end", [False, True])
+def test_device_path_corruption(oracle, item_end):
+    """The corruption sweep through rio_scan_device: the items before the first
+    error (both output shapes) and the oracle's error text."""
+    import torch
+    from base_amd.recordio import gpu
+    rng = random.Random(78)
+    data, recs = _random_file(rng, "", 800, 3000, trailer=False)
+    hdr_chunks = struct.unpack_from("<I", data, 20)[0]
+    h = hdr_chunks * 32768
+    ctx = gpu.Context(0, max_span_bytes=64 << 20, item_end=item_end)
+    n = len(data)
+    for trial in range(40):
+        b = bytearray(data)
+        o = rng.randrange(h, n) if rng.random() < 0.5 else rng.randrange(h // 32768, n // 32768) * 32768 + rng.randrange(28)
+        b[o] ^= 1 << rng.randrange(8)
+        d = bytes(b)
+        ref = oracle.scan(d, read_trailer=False)
+        body = d[h:]
+        dev = torch.frombuffer(bytearray(body), dtype=torch.uint8).to("cuda:0")
+        r = ctx.scan_device(dev.data_ptr(), len(body), file_off=h, is_file_end=True)
+        got_err = r.err.msg.decode() if r.stop == gpu.RIO_STOP_ERROR else ""
+        assert got_err == ref.err, (trial, o)
+        assert gpu.device_batch_items(r, body) == ref.items, (trial, o)
     ctx.close()
 
 
