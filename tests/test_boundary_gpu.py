@@ -71,21 +71,28 @@ def oracle_untransform(oracle, codec, comp):
 
 
 def test_decode_block_golden(gpu_ctx, manifest, oracle):
+    """Every flate / zstd body block of the golden fixtures (chains: the
+    combined untransform, the last transformer first -- registry.go:121-146)."""
     from base_amd.recordio import gpu
     from base_amd.recordio.format import MAGIC_PACKED
     rng = random.Random(5)
     checked = 0
     for case in manifest:
-        codec = codec_of(case)
-        if codec not in ("flate", "zstd") or case["err"]:
+        trs = [v.split()[0] for k, t, v in case["header"] if k == "transformer"]
+        if not trs or any(t not in ("flate", "zstd") for t in trs) or case["err"]:
             continue
-        if codec == "zstd" and not oracle_has_zstd(oracle):
+        if "zstd" in trs and not oracle_has_zstd(oracle):
             continue
-        cid = gpu.RIO_CODEC_FLATE if codec == "flate" else gpu.RIO_CODEC_ZSTD
+        ids = [gpu.RIO_CODEC_FLATE if t == "flate" else gpu.RIO_CODEC_ZSTD for t in trs]
+        cid = ids[0] if len(ids) == 1 else gpu.codec_chain(*ids)
         for magic, pays in body_blocks(golden_bytes(case)):
             if magic != MAGIC_PACKED:
                 continue
-            want, err = oracle_untransform(oracle, codec, b"".join(pays))
+            want, err = b"".join(pays), ""
+            for t in reversed(trs):
+                want, err = oracle_untransform(oracle, t, want)
+                if want is None:
+                    break
             assert want is not None, (case["name"], err)
             assert gpu_ctx.decode_block(pays, cid) == want, case["name"]
             assert gpu_ctx.decode_block(resplit(pays, rng), cid, cap=16) == want, case["name"]
