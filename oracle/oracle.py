@@ -216,3 +216,39 @@ def scan_count(data: bytes, start: int = 0, limit: int = 1, nshard: int = 1):
     b = ctypes.c_int64()
     n = lib().orc_scan_count(data, len(data), ctypes.byref(b), start, limit, nshard)
     return n, b.value
+
+
+# ---- the reference's vendored libdeflate (oracle/_ref, built by `make ref`) ----
+_REF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "libdeflate_ref.so")
+_ref_lib = None
+
+
+def build_ref() -> bool:
+    """Compile oracle/_ref/libdeflate_ref.so from /root/reference (build container
+    only). Returns whether it exists."""
+    if os.path.isdir("/root/reference/compress/libdeflate"):
+        subprocess.run(["make", "-C", os.path.dirname(os.path.abspath(__file__)), "ref"], check=True,
+                       capture_output=True)
+    return os.path.exists(_REF)
+
+
+def ref_inflate(data: bytes, cap: int = 1 << 26):
+    """libdeflate_deflate_decompress_ex of the reference's libdeflate v1.0:
+    (result, output, input bytes consumed); result 0 = LIBDEFLATE_SUCCESS."""
+    global _ref_lib
+    if _ref_lib is None:
+        L = ctypes.CDLL(_REF)
+        L.libdeflate_alloc_decompressor.restype = ctypes.c_void_p
+        L.libdeflate_deflate_decompress_ex.restype = ctypes.c_int
+        L.libdeflate_deflate_decompress_ex.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t,
+                                                      ctypes.c_void_p, ctypes.c_size_t,
+                                                      ctypes.POINTER(ctypes.c_size_t),
+                                                      ctypes.POINTER(ctypes.c_size_t)]
+        L._d = L.libdeflate_alloc_decompressor()
+        _ref_lib = L
+    L = _ref_lib
+    buf = ctypes.create_string_buffer(max(cap, 1))
+    nin, nout = ctypes.c_size_t(), ctypes.c_size_t()
+    rc = L.libdeflate_deflate_decompress_ex(L._d, data, len(data), buf, cap, ctypes.byref(nin), ctypes.byref(nout))
+    return rc, buf.raw[:nout.value] if rc == 0 else b"", nin.value
+
