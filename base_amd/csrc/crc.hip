@@ -105,7 +105,12 @@ struct CrcParseIn {
 };
 constexpr int kStageBytes = 1088;  // payload window staging: row 0 + 32 B of row 1 (then reused as the window)
 
-template <bool kParse>
+// kMeta: the chunk header checks of k_chunk_meta (chunk_meta, device_common.h)
+// on the way: the chunk's and its predecessor's 32-byte headers come in by
+// scalar loads (issued a chunk ahead, like the size), lane 0 stores the fields
+// the block scans read. The span's chunk sizes then come from the headers
+// themselves, so this pass runs first.
+template <bool kParse, bool kMeta>
 __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restrict__ span, uint64_t nchunks,
                                                        const uint32_t *__restrict__ ck_size,
                                                        const uint32_t *__restrict__ fix_a,
@@ -133,14 +138,33 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
   uint4 buf[kBufs][kRows];
   uint8_t *stage = kParse ? s_stage[threadIdx.x >> 6] : nullptr;
   uint16_t *tpos = kParse ? s_tpos[threadIdx.x >> 6] : nullptr;
-  uint32_t size = ck_size[c];
+  // kMeta: the headers of chunk c and of c - 1 (scalar loads; the first chunk of the span has none before it)
+  const uint32_t *hdr_c = reinterpret_cast<const uint32_t *>(span + c * kChunk);
+  uint32_t h[8], hp[8];
+  if (kMeta) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) h[i] = hdr_c[i];
+    const uint32_t *hdr_p = reinterpret_cast<const uint32_t *>(span + (c ? c - 1 : 0) * kChunk);
+#pragma unroll
+    for (int i = 0; i < 8; i++) hp[i] = hdr_p[i];
+  }
+  uint32_t size = kMeta ? h[4] : ck_size[c];
 #pragma unroll
   for (int q = 0; q < kBufs - 1; q++) load_stage(buf[q], span + c * kChunk, q, l);
   for (;;) {
     const uint8_t *ck = span + c * kChunk;
     const uint64_t cn = c + nwaves;
     const bool more = cn < nchunks;
-    const uint32_t size_n = ck_size[more ? cn : c];
+    uint32_t hn[8], hpn[8];
+    if (kMeta) {  // the next chunk's headers, in flight during this chunk
+      const uint32_t *a = reinterpret_cast<const uint32_t *>(span + (more ? cn : c) * kChunk);
+      const uint32_t *p = reinterpret_cast<const uint32_t *>(span + ((more ? cn : c) - 1) * kChunk);
+#pragma unroll
+      for (int i = 0; i < 8; i++) hn[i] = a[i];
+#pragma unroll
+      for (int i = 0; i < 8; i++) hpn[i] = p[i];  // (cn > c >= 0: cn - 1 exists)
+    }
+    const uint32_t size_n = kMeta ? hn[4] : ck_size[more ? cn : c];
     const uint32_t sz = size > (uint32_t)kMaxPayload ? (uint32_t)kMaxPayload : size;
     const int end = kChunkHdr + (int)sz;
     const bool full = (sz == (uint32_t)kMaxPayload);
@@ -179,6 +203,22 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
       // (flags & 2: the encode path computes CRCs of chunks it is writing -- no compare)
       if (crc != stored && fold && !(ca.flags & 2)) atomicMin(&d.ctl->first_crc_err, (unsigned long long)c);
     }
+    if (kMeta) {
+      const ChunkMeta m = chunk_meta(h[0], h[1], h[4], h[5], h[6], c > 0, hp[0], hp[1], hp[5], hp[6]);
+      if (l == 0) {
+        d.ck_size[c] = h[4];
+        d.ck_total[c] = h[5];
+        d.ck_index[c] = h[6];
+        d.ck_info[c] = m.info;
+        d.ck_ssz[c] = 0;  // straddler slots, filled by the parse
+        if (m.err) atomicMin(&d.ctl->first_chunk_err, (unsigned long long)c);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        h[i] = hn[i];
+        hp[i] = hpn[i];
+      }
+    }
     if (kParse && starts) {
       const uint32_t b = pin.ck_block[c];
       const unsigned long long meta = pin.blk_meta[b], len = pin.blk_len[b];
@@ -202,7 +242,7 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
 }
 
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
-                hipStream_t st, const ParseArgs *fused) {
+                hipStream_t st, const ParseArgs *fused, bool meta) {
   uint64_t g = (nchunks + kCrcWaves - 1) / kCrcWaves;
   const uint64_t cap = (uint64_t)(ncu > 0 ? ncu : 256);
   if (g > cap) g = cap;
@@ -210,12 +250,16 @@ void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const C
   const CrcParseIn pin{d.ck_index, d.ck_block, d.blk_meta, d.blk_len, d.blk_item_base, d.ck_pay};
 #if RIO_FUSED_PARSE
   if (fused)
-    hipLaunchKernelGGL(k_crc<true>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
-                       d.crc_fix_a, d.crc_fix_b, d, ca, pin, *fused);
+    hipLaunchKernelGGL((k_crc<true, false>), dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks,
+                       d.ck_size, d.crc_fix_a, d.crc_fix_b, d, ca, pin, *fused);
   else
 #endif
-    hipLaunchKernelGGL(k_crc<false>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
-                       d.crc_fix_a, d.crc_fix_b, d, ca, pin, ParseArgs{});
+  if (meta)
+    hipLaunchKernelGGL((k_crc<false, true>), dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks,
+                       d.ck_size, d.crc_fix_a, d.crc_fix_b, d, ca, pin, ParseArgs{});
+  else
+    hipLaunchKernelGGL((k_crc<false, false>), dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks,
+                       d.ck_size, d.crc_fix_a, d.crc_fix_b, d, ca, pin, ParseArgs{});
 }
 
 }  // namespace rio

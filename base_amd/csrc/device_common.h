@@ -31,6 +31,48 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
   return ((unsigned long long)hi << 32) | lo;
 }
 
+// ---------------------------------------------------------------- chunk headers
+// little-endian u32 words of the magics (magic.go:15-36)
+constexpr uint32_t kHdrLo = 0x5cd9e1d9u, kHdrHi = 0xf70416c2u;
+constexpr uint32_t kPkdLo = 0xeb47762eu, kPkdHi = 0x2e3c0734u;
+constexpr uint32_t kTrlLo = 0xd71abafeu, kTrlHi = 0x3a75dfcbu;
+
+__device__ __forceinline__ uint32_t magic_class(uint32_t lo, uint32_t hi) {
+  if (lo == kPkdLo && hi == kPkdHi) return kMagicPacked;
+  if (lo == kHdrLo && hi == kHdrHi) return kMagicHeader;
+  if (lo == kTrlLo && hi == kTrlHi) return kMagicTrailer;
+  return kMagicOther;
+}
+
+// A chunk header's checks, in the order readChunk / ChunkScanner.Scan make
+// them (chunk.go:273-287, 333-336): the size limit, then -- against the previous
+// chunk of the span (none: the span starts on a block boundary) -- the index of
+// a block's first chunk, the magic, the index and the total inside a block.
+struct ChunkMeta {
+  uint32_t info;  // magic class | error << 8
+  uint32_t err;
+};
+__device__ __forceinline__ ChunkMeta chunk_meta(uint32_t mlo, uint32_t mhi, uint32_t size, uint32_t total,
+                                                uint32_t index, bool has_prev, uint32_t plo, uint32_t phi,
+                                                uint32_t ptotal, uint32_t pindex) {
+  uint32_t err = kCkOk;
+  if (size > (uint32_t)kMaxPayload) {
+    err = kCkSize;
+  } else {
+    const bool prev_end = !has_prev || (int64_t)pindex == (int64_t)ptotal - 1;
+    if (prev_end) {
+      if (index != 0) err = kCkIndex;
+    } else if (mlo != plo || mhi != phi) {
+      err = kCkMagicChanged;
+    } else if ((uint64_t)index != (uint64_t)pindex + 1) {
+      err = kCkIndex;
+    } else if (total != ptotal) {
+      err = kCkTotal;
+    }
+  }
+  return ChunkMeta{magic_class(mlo, mhi) | (err << 8), err};
+}
+
 // ---------------------------------------------------------------- wave scans
 template <class T>
 __device__ __forceinline__ T wave_incl_sum(T v) {

@@ -21,18 +21,6 @@
 
 namespace rio {
 
-// little-endian u32 words of the magics (magic.go:15-36)
-constexpr uint32_t kHdrLo = 0x5cd9e1d9u, kHdrHi = 0xf70416c2u;
-constexpr uint32_t kPkdLo = 0xeb47762eu, kPkdHi = 0x2e3c0734u;
-constexpr uint32_t kTrlLo = 0xd71abafeu, kTrlHi = 0x3a75dfcbu;
-
-__device__ __forceinline__ uint32_t magic_class(uint32_t lo, uint32_t hi) {
-  if (lo == kPkdLo && hi == kPkdHi) return kMagicPacked;
-  if (lo == kHdrLo && hi == kHdrHi) return kMagicHeader;
-  if (lo == kTrlLo && hi == kTrlHi) return kMagicTrailer;
-  return kMagicOther;
-}
-
 constexpr uint32_t kNoBlock = 0xffffffffu;
 
 // ---------------------------------------------------------------- k_chunk_meta
@@ -43,40 +31,19 @@ __global__ void __launch_bounds__(256) k_chunk_meta(const uint8_t *__restrict__ 
     const uint32_t *h = reinterpret_cast<const uint32_t *>(span + c * kChunk);
     const uint4 a = *reinterpret_cast<const uint4 *>(h);      // magic lo, hi, crc, flag
     const uint4 b = *reinterpret_cast<const uint4 *>(h + 4);  // size, total, index, data
-    const uint32_t size = b.x, total = b.y, index = b.z;
-    const uint32_t cls = magic_class(a.x, a.y);
-    uint32_t err = kCkOk;
-    if (size > (uint32_t)kMaxPayload) {
-      err = kCkSize;
-    } else {
-      bool prev_end = true;  // the span starts on a block boundary
-      uint32_t plo = 0, phi = 0, ptotal = 0, pindex = 0;
-      if (c > 0) {
-        const uint32_t *p = reinterpret_cast<const uint32_t *>(span + (c - 1) * kChunk);
-        const uint4 pa = *reinterpret_cast<const uint4 *>(p);
-        const uint4 pb = *reinterpret_cast<const uint4 *>(p + 4);
-        plo = pa.x;
-        phi = pa.y;
-        ptotal = pb.y;
-        pindex = pb.z;
-        prev_end = (int64_t)pindex == (int64_t)ptotal - 1;
-      }
-      if (prev_end) {
-        if (index != 0) err = kCkIndex;
-      } else if (a.x != plo || a.y != phi) {
-        err = kCkMagicChanged;
-      } else if ((uint64_t)index != (uint64_t)pindex + 1) {
-        err = kCkIndex;
-      } else if (total != ptotal) {
-        err = kCkTotal;
-      }
+    uint4 pa = make_uint4(0, 0, 0, 0), pb = make_uint4(0, 0, 0, 0);
+    if (c > 0) {
+      const uint32_t *p = reinterpret_cast<const uint32_t *>(span + (c - 1) * kChunk);
+      pa = *reinterpret_cast<const uint4 *>(p);
+      pb = *reinterpret_cast<const uint4 *>(p + 4);
     }
-    d.ck_size[c] = size;
-    d.ck_total[c] = total;
-    d.ck_index[c] = index;
-    d.ck_info[c] = cls | (err << 8);
+    const ChunkMeta m = chunk_meta(a.x, a.y, b.x, b.y, b.z, c > 0, pa.x, pa.y, pb.y, pb.z);
+    d.ck_size[c] = b.x;
+    d.ck_total[c] = b.y;
+    d.ck_index[c] = b.z;
+    d.ck_info[c] = m.info;
     d.ck_ssz[c] = 0;  // straddler slots, filled by k_parse
-    if (err != kCkOk) atomicMin(&d.ctl->first_chunk_err, (unsigned long long)c);
+    if (m.err) atomicMin(&d.ctl->first_chunk_err, (unsigned long long)c);
   }
 }
 

@@ -49,7 +49,7 @@ void launch_block_files(const DevBufs &d, const unsigned long long *seg_end, con
                         uint64_t nseg, uint64_t max_blocks, hipStream_t st);
 // crc.hip
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
-                hipStream_t st, const ParseArgs *fused);
+                hipStream_t st, const ParseArgs *fused, bool meta);
 // codec.hip
 void launch_compact(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
@@ -116,6 +116,7 @@ struct rio_ctx {
   hipEvent_t ev[kNumEv] = {};
   hipEvent_t evA = nullptr, evB = nullptr;  // stream hand-offs (no timing)
   bool last_had_dec = false;
+  bool last_crc_first = false;  // the last run's k_crc also checked the chunk headers (ran before the scans)
   bool item_end_mode = false;  // RIO_CFG_ITEM_END: device results carry item_end (cumSize)
   bool last_cmp = false;  // the last host result's records are the compacted blocks (d.cmp)
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
@@ -447,8 +448,25 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     HIP_OK(hipMemsetAsync(d.blk_need, 0, nchunks * sizeof(unsigned long long), st));
   HIP_OK(hipMemsetAsync(c->nblocks_dev, 0, 2 * sizeof(unsigned long long), st));
   const uint64_t max_blocks = nchunks ? nchunks : 1;
+  // the shipped library always runs every stage; RIO_ABLATE (a -D of ablation
+  // builds, tools/ablate.py) drops stages for measurement only
+  const bool run_parse = !(RIO_ABLATE & 2) && mode != kModeRaw,
+             run_crc = !(RIO_ABLATE & 4) && mode != kModeRaw && !(stage_flags & kStageNoCrc);
+  const bool no_items = (stage_flags & kStageNoItems) != 0;
+  // ablation builds (-DRIO_FUSED_PARSE=1): none codec in one pass -- the wave
+  // that checksums a block's first chunk parses the block
+  const bool fused = RIO_FUSED_PARSE && codec == RIO_CODEC_NONE && run_parse && run_crc && nchunks > 0;
+  const CrcArgs ca{RIO_ABLATE, 0};
+  // k_crc reads every chunk: it also checks the chunk headers (k_chunk_meta's
+  // work, from scalar loads of the header it streams), so it runs first and
+  // the chunk scans follow it; spans without a CRC pass take k_chunk_meta
+  const bool meta_in_crc = run_crc && !fused && nchunks > 0;
+  c->last_crc_first = meta_in_crc;
+  HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
+  if (meta_in_crc) launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr, true);
+  HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
   if (nchunks > 0) {
-    launch_chunk_meta(span, nchunks, d, st);
+    if (!meta_in_crc) launch_chunk_meta(span, nchunks, d, st);
     launch_chunk_scans(span, nchunks, d, c->nblocks_dev, codec, st);
   }
   HIP_OK(hipEventRecord(c->ev[kEvScans], st));
@@ -470,15 +488,6 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   // parse path on st2 (the ctx's one stream unless an ablation build splits it)
   HIP_OK(hipStreamWaitEvent(st2, c->evA, 0));
   HIP_OK(hipEventRecord(c->ev[kEvParse0], st2));
-  // the shipped library always runs every stage; RIO_ABLATE (a -D of ablation
-  // builds, tools/ablate.py) drops stages for measurement only
-  const bool run_parse = !(RIO_ABLATE & 2) && mode != kModeRaw,
-             run_crc = !(RIO_ABLATE & 4) && mode != kModeRaw && !(stage_flags & kStageNoCrc);
-  const bool no_items = (stage_flags & kStageNoItems) != 0;
-  // ablation builds (-DRIO_FUSED_PARSE=1): none codec in one pass -- the wave
-  // that checksums a block's first chunk parses the block
-  const bool fused = RIO_FUSED_PARSE && codec == RIO_CODEC_NONE && run_parse && run_crc && nchunks > 0;
-  const CrcArgs ca{RIO_ABLATE, 0};
   if (nchunks > 0 && run_parse) {
     ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap, sparse,
                  (c->item_end_mode && sparse) ? 1 : 0};
@@ -488,7 +497,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     launch_block_scan(d.blk_nitems, d.blk_item_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
     if (fused) {
       HIP_OK(hipEventRecord(c->ev[kEvCrc0], st2));
-      launch_crc(span, nchunks, d, ca, c->ncu, st2, &pa);
+      launch_crc(span, nchunks, d, ca, c->ncu, st2, &pa, false);
       HIP_OK(hipEventRecord(c->ev[kEvCrc1], st2));
     } else if (codec == RIO_CODEC_NONE && mode == kModeBody && !no_items) {
       // the common block shape in a lean kernel, the rest listed for k_parse
@@ -512,11 +521,6 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   }
   HIP_OK(hipEventRecord(c->ev[kEvParse1], st2));
   HIP_OK(hipEventRecord(c->evB, st2));
-  if (!fused) {
-    HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
-    if (nchunks > 0 && run_crc) launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr);
-    HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
-  }
   HIP_OK(hipStreamWaitEvent(st, c->evB, 0));
   if (mode != kModeRaw) {
     ResolveArgs ra{span, nchunks, is_file_end, tail_partial, mode, codec, c->nblocks_dev, limit_chunk, sparse, 0};
@@ -953,6 +957,7 @@ extern "C" int rio_stage_times(rio_ctx *ctx, float *ms, int n) {
   if (ctx->last_had_dec) hipEventElapsedTime(&t[1], ctx->ev[kEvScans], ctx->ev[kEvDec]);
   hipEventElapsedTime(&t[2], ctx->ev[kEvCrc0], ctx->ev[kEvCrc1]);
   hipEventElapsedTime(&t[3], ctx->ev[kEvStart], ctx->ev[kEvScans]);
+  if (ctx->last_crc_first) t[3] -= t[2];  // (the headers were checked inside k_crc)
   hipEventElapsedTime(&t[4], ctx->ev[kEvStart], ctx->ev[kEvEnd]);
   const int k = n < 5 ? n : 5;
   for (int i = 0; i < k; i++) ms[i] = t[i];

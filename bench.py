@@ -339,7 +339,7 @@ def c5_flate(args, local, rank, world, dist):
             "parity_files_checked": len(mine), "parity_files_ok": files_ok,
             "config": {"files": c5_data.N_FILES, "file_record_bytes": c5_data.FILE_RECORD_BYTES,
                        "records_per_block": c5_data.PER_BLOCK, "distinct_base_files": c5_data.N_BASE,
-                       "note": "file f is a copy of base f % %d (each decoded and checked on its own)"
+                       "note": "file f is a copy of base f mod %d (each decoded and checked on its own)"
                                % c5_data.N_BASE,
                        "files_bytes_total": all_bytes, "files_this_rank": len(mine),
                        "batches_this_rank": len(batches), "launch": "rio_scan_device_segments_async, "
