@@ -106,10 +106,12 @@ struct CrcParseIn {
 constexpr int kStageBytes = 1088;  // payload window staging: row 0 + 32 B of row 1 (then reused as the window)
 
 // kMeta: the chunk header checks of k_chunk_meta (chunk_meta, device_common.h)
-// on the way: the chunk's and its predecessor's 32-byte headers come in by
-// scalar loads (issued a chunk ahead, like the size), lane 0 stores the fields
-// the block scans read. The span's chunk sizes then come from the headers
-// themselves, so this pass runs first.
+// on the way: the chunk's header is the first 28 bytes of its stage-0 row
+// (lanes 0 and 1, taken by readlane), its predecessor's comes in by one
+// vector load of lanes 0-1 issued before the fold and used after it; lane 0
+// stores the fields the block scans read. The span's chunk sizes come from the
+// headers themselves, so this pass runs first. (Scalar loads of the two
+// headers cost 6 %: they share lgkmcnt with the fold's LDS lookups.)
 template <bool kParse, bool kMeta>
 __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restrict__ span, uint64_t nchunks,
                                                        const uint32_t *__restrict__ ck_size,
@@ -138,46 +140,52 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
   uint4 buf[kBufs][kRows];
   uint8_t *stage = kParse ? s_stage[threadIdx.x >> 6] : nullptr;
   uint16_t *tpos = kParse ? s_tpos[threadIdx.x >> 6] : nullptr;
-  // kMeta: the headers of chunk c and of c - 1 (scalar loads; the first chunk of the span has none before it)
-  const uint32_t *hdr_c = reinterpret_cast<const uint32_t *>(span + c * kChunk);
-  uint32_t h[8], hp[8];
-  if (kMeta) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) h[i] = hdr_c[i];
-    const uint32_t *hdr_p = reinterpret_cast<const uint32_t *>(span + (c ? c - 1 : 0) * kChunk);
-#pragma unroll
-    for (int i = 0; i < 8; i++) hp[i] = hdr_p[i];
-  }
-  uint32_t size = kMeta ? h[4] : ck_size[c];
+  // kMeta: the size is not known ahead -- it is the chunk's own header, read
+  // out of the first row of stage 0 (lane 1's dwords are size / total / index)
+  uint32_t size = kMeta ? 0u : ck_size[c];
 #pragma unroll
   for (int q = 0; q < kBufs - 1; q++) load_stage(buf[q], span + c * kChunk, q, l);
   for (;;) {
     const uint8_t *ck = span + c * kChunk;
     const uint64_t cn = c + nwaves;
     const bool more = cn < nchunks;
-    uint32_t hn[8], hpn[8];
-    if (kMeta) {  // the next chunk's headers, in flight during this chunk
-      const uint32_t *a = reinterpret_cast<const uint32_t *>(span + (more ? cn : c) * kChunk);
-      const uint32_t *p = reinterpret_cast<const uint32_t *>(span + ((more ? cn : c) - 1) * kChunk);
-#pragma unroll
-      for (int i = 0; i < 8; i++) hn[i] = a[i];
-#pragma unroll
-      for (int i = 0; i < 8; i++) hpn[i] = p[i];  // (cn > c >= 0: cn - 1 exists)
-    }
-    const uint32_t size_n = kMeta ? hn[4] : ck_size[more ? cn : c];
-    const uint32_t sz = size > (uint32_t)kMaxPayload ? (uint32_t)kMaxPayload : size;
-    const int end = kChunkHdr + (int)sz;
-    const bool full = (sz == (uint32_t)kMaxPayload);
+    // kMeta: the predecessor's header (lanes 0, 1), in flight during the fold
+    uint4 ph = make_uint4(0, 0, 0, 0);
+    if (kMeta && c > 0 && l < 2) ph = *reinterpret_cast<const uint4 *>(ck - kChunk + 16 * l);
+    const uint32_t size_n = kMeta ? 0u : ck_size[more ? cn : c];
+    uint32_t mlo = 0, mhi = 0, total = 0, index = 0;
+    // (kMeta: set at stage 0, once its first row is in -- after the prefetch
+    // of stage 3 is issued, so the wait does not hold the pipeline back)
+    uint32_t sz = size > (uint32_t)kMaxPayload ? (uint32_t)kMaxPayload : size;
+    int end = kChunkHdr + (int)sz;
+    bool full = (sz == (uint32_t)kMaxPayload);
     // a block starts here: this wave parses it after the checksum (scalar load)
     const bool starts = kParse && pin.ck_index[c] == 0;
     uint32_t s[4] = {0, 0, 0, 0};
     uint32_t stored = 0;
-    const uint32_t fa = fix_a[sz], fb = fix_b[sz];
+    uint32_t fa = 0, fb = 0;
+    if (!kMeta) {
+      fa = fix_a[sz];
+      fb = fix_b[sz];
+    }
 #pragma unroll
     for (int q = 0; q < kStages; q++) {
       const int nq = q + kBufs - 1;  // stage to prefetch (this chunk or the next)
       if (nq < kStages) load_stage(buf[nq % kBufs], ck, nq, l);
       else if (more) load_stage(buf[nq % kBufs], span + cn * kChunk, nq - kStages, l);
+      if (kMeta && q == 0) {  // the header: lane 0 magic / crc / flag, lane 1 size / total / index
+        const uint4 r0 = buf[0][0];
+        size = (uint32_t)__builtin_amdgcn_readlane((int)r0.x, 1);
+        total = (uint32_t)__builtin_amdgcn_readlane((int)r0.y, 1);
+        index = (uint32_t)__builtin_amdgcn_readlane((int)r0.z, 1);
+        mlo = (uint32_t)__builtin_amdgcn_readlane((int)r0.x, 0);
+        mhi = (uint32_t)__builtin_amdgcn_readlane((int)r0.y, 0);
+        sz = size > (uint32_t)kMaxPayload ? (uint32_t)kMaxPayload : size;
+        end = kChunkHdr + (int)sz;
+        full = (sz == (uint32_t)kMaxPayload);
+        fa = fix_a[sz];
+        fb = fix_b[sz];
+      }
       if (kParse && q == 0 && starts) {  // rows 0..1 raw, before the fold masks them
         *reinterpret_cast<uint4 *>(stage + 16 * l) = buf[0][0];
         if (l < 2) *reinterpret_cast<uint4 *>(stage + 1024 + 16 * l) = buf[0][1];
@@ -204,19 +212,18 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
       if (crc != stored && fold && !(ca.flags & 2)) atomicMin(&d.ctl->first_crc_err, (unsigned long long)c);
     }
     if (kMeta) {
-      const ChunkMeta m = chunk_meta(h[0], h[1], h[4], h[5], h[6], c > 0, hp[0], hp[1], hp[5], hp[6]);
+      const ChunkMeta m = chunk_meta(mlo, mhi, size, total, index, c > 0,
+                                     (uint32_t)__builtin_amdgcn_readlane((int)ph.x, 0),
+                                     (uint32_t)__builtin_amdgcn_readlane((int)ph.y, 0),
+                                     (uint32_t)__builtin_amdgcn_readlane((int)ph.y, 1),
+                                     (uint32_t)__builtin_amdgcn_readlane((int)ph.z, 1));
       if (l == 0) {
-        d.ck_size[c] = h[4];
-        d.ck_total[c] = h[5];
-        d.ck_index[c] = h[6];
+        d.ck_size[c] = size;
+        d.ck_total[c] = total;
+        d.ck_index[c] = index;
         d.ck_info[c] = m.info;
         d.ck_ssz[c] = 0;  // straddler slots, filled by the parse
         if (m.err) atomicMin(&d.ctl->first_chunk_err, (unsigned long long)c);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        h[i] = hn[i];
-        hp[i] = hpn[i];
       }
     }
     if (kParse && starts) {

@@ -216,6 +216,22 @@ static inline unsigned grid_for(uint64_t n, unsigned per, unsigned cap) {
   return (unsigned)(g > cap ? cap : g);
 }
 
+// the control words a pipeline run reduces into, and the block counters, reset
+// in one launch (min-reduced words to ~0, counters to 0)
+__global__ void k_reset(Ctl *ctl, unsigned long long *nblocks) {
+  const int t = threadIdx.x;
+  if (t < 4) (&ctl->first_chunk_err)[t] = kNone;   // first_chunk_err .. first_incomplete
+  else if (t < 8) (&ctl->out_overflow)[t - 4] = 0;  // out_overflow, dec_need, pad[2]
+  else if (t < 10) (&ctl->flstat_esc)[t - 8] = 0;   // flstat_esc, n_retry
+  else if (t < 14) ctl->zprof[t - 10] = 0;
+  else if (t == 14) ctl->zjob_n = 0;
+  else if (t < 17) nblocks[t - 15] = 0;
+}
+
+void launch_reset(const DevBufs &d, unsigned long long *nblocks_dev, hipStream_t st) {
+  hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, d.ctl, nblocks_dev);
+}
+
 void launch_chunk_meta(const uint8_t *span, uint64_t nchunks, const DevBufs &d, hipStream_t st) {
   hipLaunchKernelGGL(k_chunk_meta, dim3(grid_for(nchunks, 256, 4096)), dim3(256), 0, st, span, nchunks, d);
 }

@@ -30,6 +30,7 @@
 namespace rio {
 // kernels.hip
 void launch_chunk_meta(const uint8_t *span, uint64_t nchunks, const DevBufs &d, hipStream_t st);
+void launch_reset(const DevBufs &d, unsigned long long *nblocks_dev, hipStream_t st);
 void launch_chunk_scans(const uint8_t *span, uint64_t nchunks, const DevBufs &d, unsigned long long *nblocks_dev,
                         int32_t codec, hipStream_t st);
 void launch_chunk_scan(const unsigned long long *in, unsigned long long *out, unsigned long long *tmp, uint64_t n,
@@ -117,6 +118,7 @@ struct rio_ctx {
   hipEvent_t evA = nullptr, evB = nullptr;  // stream hand-offs (no timing)
   bool last_had_dec = false;
   bool last_crc_first = false;  // the last run's k_crc also checked the chunk headers (ran before the scans)
+  int ev_parse0 = kEvParse0, ev_crc0 = kEvCrc0;  // the events the last run's parse / CRC stages start at
   bool item_end_mode = false;  // RIO_CFG_ITEM_END: device results carry item_end (cumSize)
   bool last_cmp = false;  // the last host result's records are the compacted blocks (d.cmp)
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
@@ -437,16 +439,10 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   c->last_nchunks = nchunks;
   c->last_cmp = false;  // records are d.dec / d.side until a host result compacts them
   HIP_OK(hipEventRecord(c->ev[kEvStart], st));
-  // control words are min-reduced: reset to ~0 (out_overflow to 0)
-  HIP_OK(hipMemsetAsync(d.ctl, 0xff, 4 * sizeof(unsigned long long), st));
-  HIP_OK(hipMemsetAsync(&d.ctl->out_overflow, 0, 4 * sizeof(unsigned long long), st));  // + dec_need, pad
-#ifdef RIO_ZPROF
-  HIP_OK(hipMemsetAsync(d.ctl->zprof, 0, sizeof(d.ctl->zprof), st));
-#endif
-  HIP_OK(hipMemsetAsync(&d.ctl->flstat_esc, 0, 2 * sizeof(unsigned long long), st));  // + n_retry
+  // control words (min-reduced: ~0; counters: 0) and the block counters, one launch
+  launch_reset(d, c->nblocks_dev, st);
   if (attempt == 0 && codec != RIO_CODEC_NONE && nchunks > 0)
     HIP_OK(hipMemsetAsync(d.blk_need, 0, nchunks * sizeof(unsigned long long), st));
-  HIP_OK(hipMemsetAsync(c->nblocks_dev, 0, 2 * sizeof(unsigned long long), st));
   const uint64_t max_blocks = nchunks ? nchunks : 1;
   // the shipped library always runs every stage; RIO_ABLATE (a -D of ablation
   // builds, tools/ablate.py) drops stages for measurement only
@@ -457,14 +453,17 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   // that checksums a block's first chunk parses the block
   const bool fused = RIO_FUSED_PARSE && codec == RIO_CODEC_NONE && run_parse && run_crc && nchunks > 0;
   const CrcArgs ca{RIO_ABLATE, 0};
-  // k_crc reads every chunk: it also checks the chunk headers (k_chunk_meta's
-  // work, from scalar loads of the header it streams), so it runs first and
-  // the chunk scans follow it; spans without a CRC pass take k_chunk_meta
-  const bool meta_in_crc = run_crc && !fused && nchunks > 0;
+  // order: k_chunk_meta, scans, (decode), parse, k_crc, resolve. Ablation
+  // builds with -DRIO_CRC_META=1 check the chunk headers inside k_crc, which
+  // then runs first (spans without a CRC pass still take k_chunk_meta)
+  const bool meta_in_crc = RIO_CRC_META && run_crc && !fused && nchunks > 0;
   c->last_crc_first = meta_in_crc;
-  HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
-  if (meta_in_crc) launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr, true);
-  HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
+  c->ev_crc0 = kEvCrc0;
+  if (meta_in_crc || !run_crc || fused || nchunks == 0) {  // (no CRC pass later: a zero-length interval here)
+    HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
+    if (meta_in_crc) launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr, true);
+    HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
+  }
   if (nchunks > 0) {
     if (!meta_in_crc) launch_chunk_meta(span, nchunks, d, st);
     launch_chunk_scans(span, nchunks, d, c->nblocks_dev, codec, st);
@@ -478,16 +477,22 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     if (codec == RIO_CODEC_FLATE && ensure_tok(c, nchunks, kTokPerChunk)) return -1;
     if (codec == RIO_CODEC_ZSTD && ensure_tok(c, nchunks, kZTokPerChunk)) return -1;
     if (codec == RIO_CODEC_ZSTD && (ensure_zlit(c) || ensure_zjob(c, nchunks))) return -1;
-    if (codec == RIO_CODEC_ZSTD) HIP_OK(hipMemsetAsync(&d.ctl->zjob_n, 0, sizeof(d.ctl->zjob_n), st));
     launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
     launch_codec_decode(span, d, c->nblocks_dev, max_blocks, nchunks, codec, c->dec_cap, c->fl_rounds, c->ncu, st);
     c->last_had_dec = true;
   }
-  HIP_OK(hipEventRecord(c->ev[kEvDec], st));
-  HIP_OK(hipEventRecord(c->evA, st));
-  // parse path on st2 (the ctx's one stream unless an ablation build splits it)
-  HIP_OK(hipStreamWaitEvent(st2, c->evA, 0));
-  HIP_OK(hipEventRecord(c->ev[kEvParse0], st2));
+  // (an event record costs ~5 us of GPU time between kernels: the stage
+  // boundaries share events where they coincide -- parse starts at kEvDec or
+  // kEvScans, the CRC at kEvParse1 -- and the hand-offs run only when an
+  // ablation build splits the parse onto a second stream)
+  if (c->last_had_dec) HIP_OK(hipEventRecord(c->ev[kEvDec], st));
+  c->ev_parse0 = c->last_had_dec ? kEvDec : kEvScans;
+  if (st2 != st) {
+    HIP_OK(hipEventRecord(c->evA, st));
+    HIP_OK(hipStreamWaitEvent(st2, c->evA, 0));
+    HIP_OK(hipEventRecord(c->ev[kEvParse0], st2));
+    c->ev_parse0 = kEvParse0;
+  }
   if (nchunks > 0 && run_parse) {
     ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap, sparse,
                  (c->item_end_mode && sparse) ? 1 : 0};
@@ -520,8 +525,17 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     HIP_OK(hipMemsetAsync(d.ck_sbase, 0, 8, st2));
   }
   HIP_OK(hipEventRecord(c->ev[kEvParse1], st2));
-  HIP_OK(hipEventRecord(c->evB, st2));
-  HIP_OK(hipStreamWaitEvent(st, c->evB, 0));
+  if (st2 != st) HIP_OK(hipEventRecord(c->evB, st2));
+  if (!meta_in_crc && !fused && run_crc && nchunks > 0) {
+    c->ev_crc0 = kEvParse1;
+    if (st2 != st) {
+      HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
+      c->ev_crc0 = kEvCrc0;
+    }
+    launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr, false);
+    HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
+  }
+  if (st2 != st) HIP_OK(hipStreamWaitEvent(st, c->evB, 0));
   if (mode != kModeRaw) {
     ResolveArgs ra{span, nchunks, is_file_end, tail_partial, mode, codec, c->nblocks_dev, limit_chunk, sparse, 0};
     launch_resolve(d, ra, st);
@@ -953,9 +967,9 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
 extern "C" int rio_stage_times(rio_ctx *ctx, float *ms, int n) {
   if (!ctx || !ms || n <= 0) return 0;
   float t[5] = {0, 0, 0, 0, 0};
-  hipEventElapsedTime(&t[0], ctx->ev[kEvParse0], ctx->ev[kEvParse1]);
+  hipEventElapsedTime(&t[0], ctx->ev[ctx->ev_parse0], ctx->ev[kEvParse1]);
   if (ctx->last_had_dec) hipEventElapsedTime(&t[1], ctx->ev[kEvScans], ctx->ev[kEvDec]);
-  hipEventElapsedTime(&t[2], ctx->ev[kEvCrc0], ctx->ev[kEvCrc1]);
+  hipEventElapsedTime(&t[2], ctx->ev[ctx->ev_crc0], ctx->ev[kEvCrc1]);
   hipEventElapsedTime(&t[3], ctx->ev[kEvStart], ctx->ev[kEvScans]);
   if (ctx->last_crc_first) t[3] -= t[2];  // (the headers were checked inside k_crc)
   hipEventElapsedTime(&t[4], ctx->ev[kEvStart], ctx->ev[kEvEnd]);

@@ -32,9 +32,8 @@
 
 namespace rio {
 
-constexpr int kZeHashBits = 12;
-constexpr uint32_t kZeNone = 0xffffffffu;
-constexpr int kZeWaves = 4;                      // waves per workgroup (16 KiB of hash each)
+constexpr int kZeHashBits = 12;                   // buckets of two 16-bit positions (16 KiB per wave)
+constexpr int kZeWaves = 4;                      // waves per workgroup
 constexpr uint32_t kZeMaxSeq = kZeBlock / 4 + 1;  // sequences per block (matches are >= 4 bytes)
 constexpr uint32_t kZeWaveWords = kZeMaxSeq + kZeBlock / 8;  // per wave: the sequence list, then the literals
 constexpr int kZeRing = 128;                      // Huffman stream staging dwords per wave
@@ -122,15 +121,18 @@ struct ZeWaveBits {
   }
 };
 
-// One FSE table held across the wave's lanes (entry k in lane k): the encoder's
-// state is wave-uniform, so every lookup is a readlane -- no memory latency in
-// the serial chain
+// One FSE table held across the wave's lanes (state entries 2l, 2l+1 and
+// 128+2l, 129+2l in lane l, symbol k's deltas in lane k): the encoder's state
+// is wave-uniform, so every lookup is a readlane -- no memory latency in the
+// serial chain
 struct ZeLaneFse {
-  uint32_t state, dnb;
+  uint32_t st0, st1, dnb;
   int32_t dfind;
   int32_t log;
   __device__ __forceinline__ void load(const ZeFse &t, int l) {
-    state = l < (1 << t.log) ? t.state[l] : 0u;
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(t.state);
+    st0 = sw[l];
+    st1 = sw[64 + l];
     dnb = l < 53 ? t.dnb[l] : 0u;
     dfind = l < 53 ? t.dfind[l] : 0;
     log = t.log;
@@ -138,18 +140,42 @@ struct ZeLaneFse {
   __device__ __forceinline__ uint32_t rd(uint32_t v, uint32_t k) const {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k);
   }
+  __device__ __forceinline__ uint32_t state_at(uint32_t k) const {
+    const uint32_t lane = (k >> 1) & 63u;
+    const uint32_t a = rd(st0, lane), b = rd(st1, lane);
+    const uint32_t v = (k & 128u) ? b : a;
+    return (k & 1u) ? (v >> 16) : (v & 0xffffu);
+  }
   __device__ __forceinline__ uint32_t init(uint32_t sym) const {
     const uint32_t d = rd(dnb, sym);
     const uint32_t nbo = (d + (1u << 15)) >> 16;
     const uint32_t v = (nbo << 16) - d;
-    return rd(state, (uint32_t)((int32_t)(v >> nbo) + (int32_t)rd((uint32_t)dfind, sym)));
+    return state_at((uint32_t)((int32_t)(v >> nbo) + (int32_t)rd((uint32_t)dfind, sym)));
   }
   __device__ __forceinline__ void encode(ZeWaveBits &w, uint32_t &s, uint32_t sym) const {
     const uint32_t nbo = (s + rd(dnb, sym)) >> 16;
     w.add(s, nbo);
-    s = rd(state, (uint32_t)((int32_t)(s >> nbo) + (int32_t)rd((uint32_t)dfind, sym)));
+    s = state_at((uint32_t)((int32_t)(s >> nbo) + (int32_t)rd((uint32_t)dfind, sym)));
   }
 };
+
+// the per-wave LDS a block's two coding phases share: literals (Huffman build,
+// stream staging), then sequences (code counts, one table slot)
+struct ZeHufLds {
+  uint32_t hist[256];  // literal counts
+  uint32_t w[260];     // Huffman build: node weights
+  uint16_t par[260];   // ... parents
+  uint16_t val[132];   // code values of symbols 0..128
+  uint8_t len[132];    // code lengths
+  uint32_t ring[kZeRing];  // stream bits being assembled
+};
+struct ZeFseLds {
+  uint32_t cnt[3][56];  // LL, OF, ML code counts
+  ZeFse t;              // the table being fitted
+  ZeFseWork w;
+  uint8_t desc[kZeDescMax];
+};
+constexpr int kZePhaseWords = ((sizeof(ZeHufLds) > sizeof(ZeFseLds) ? sizeof(ZeHufLds) : sizeof(ZeFseLds)) + 15) / 16 * 4;
 
 // the wave's global stores complete (and visible to its other lanes' loads)
 __device__ __forceinline__ void ze_mem_sync() {
@@ -176,33 +202,26 @@ __device__ __forceinline__ ZeSrc zsrc_of(const EncArgs &a, uint64_t b) {
 __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeTabs *__restrict__ T,
                                                           unsigned long long *__restrict__ scratch) {
   __shared__ uint32_t s_hash[kZeWaves][1 << kZeHashBits];
-  __shared__ uint32_t s_hist[kZeWaves][256];      // literal counts
-  __shared__ uint32_t s_w[kZeWaves][260];         // Huffman build: node weights
-  __shared__ uint16_t s_par[kZeWaves][260];       // ... parents
-  __shared__ uint16_t s_val[kZeWaves][132];       // code values of symbols 0..128
-  __shared__ uint8_t s_len[kZeWaves][132];        // code lengths
-  __shared__ uint32_t s_ring[kZeWaves][kZeRing];  // stream bits being assembled
+  __shared__ __attribute__((aligned(16))) uint32_t s_phase[kZeWaves][kZePhaseWords];
   const int wv = threadIdx.x >> 6;
   uint32_t *hash = s_hash[wv];
-  uint32_t *hist = s_hist[wv];
-  uint16_t *hval = s_val[wv];
-  uint8_t *hlen = s_len[wv];
-  uint32_t *ring = s_ring[wv];
+  ZeHufLds &H = *reinterpret_cast<ZeHufLds *>(s_phase[wv]);
+  ZeFseLds &F = *reinterpret_cast<ZeFseLds *>(s_phase[wv]);
+  uint32_t *hist = H.hist;
+  uint16_t *hval = H.val;
+  uint8_t *hlen = H.len;
+  uint32_t *ring = H.ring;
   const int l = lane_id();
   const uint64_t wave = (uint64_t)blockIdx.x * kZeWaves + wv;
   const uint64_t nwaves = (uint64_t)gridDim.x * kZeWaves;
   unsigned long long *seq = scratch + wave * kZeWaveWords;
   uint8_t *lit = reinterpret_cast<uint8_t *>(seq + kZeMaxSeq);
-  for (int i = l; i < kZeRing; i += 64) ring[i] = 0;
   ZeLaneFse f_ll, f_ml, f_of;
-  f_ll.load(T->ll, l);
-  f_ml.load(T->ml, l);
-  f_of.load(T->of, l);
   for (uint64_t b = wave; b < a.nblocks; b += nwaves) {
     const ZeSrc s = zsrc_of(a, b);
     const unsigned long long L = s.len;
     uint8_t *out = a.comp + a.comp_off[b];
-    for (int i = l; i < (1 << kZeHashBits); i += 64) hash[i] = kZeNone;
+    for (int i = l; i < (1 << kZeHashBits); i += 64) hash[i] = 0;  // (stale / empty entries: verified like any)
     wave_lds_sync();
     if (l == 0) ze_frame_header(out, L);
     unsigned long long o = kZeFrameHdr;
@@ -226,24 +245,36 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
         if (base + 64 < b1) s.load16(p + 64, nx);
         const bool has4 = p + 4 <= b1;
         const uint32_t h = (cw[0] * 0x9E3779B1u) >> (32 - kZeHashBits);
-        const uint32_t cand = has4 ? hash[h] : kZeNone;
+        const uint32_t e = has4 ? hash[h] : 0u;
         wave_lds_sync();
-        if (has4) hash[h] = (uint32_t)p;  // (payloads < 4 GiB: checked by the host)
-        uint32_t m = 0;
-        if (has4 && p >= cur && cand != kZeNone) {
+        if (has4) hash[h] = (e << 16) | (uint32_t)(p & 0xffffu);  // the newer position in way 0
+        // the two candidates: 16-bit positions, up to 64 KiB back (a stale
+        // or empty entry is a candidate like any other: bytes decide)
+        uint32_t m = 0, cand = 0;
+        if (has4 && p >= cur) {
           const uint32_t maxm = (uint32_t)(b1 - p);
-          uint32_t cc[4];
-          s.load16(cand, cc);
-          m = ze_common16(cc, cw);
-          while (m == 16 * ((m + 15) / 16) && m > 0 && m < maxm) {  // all equal so far
-            uint32_t a16[4], b16[4];
-            s.load16(cand + m, a16);
-            s.load16(p + m, b16);
-            const uint32_t k = ze_common16(a16, b16);
-            m += k;
-            if (k < 16) break;
+#pragma unroll
+          for (int way = 0; way < 2; way++) {
+            const uint32_t dd = (uint32_t)(p - (e >> (16 * way))) & 0xffffu;
+            if (dd == 0 || dd > p) continue;
+            const unsigned long long cd = p - dd;
+            uint32_t cc[4];
+            s.load16(cd, cc);
+            uint32_t mk = ze_common16(cc, cw);
+            while (mk == 16 * ((mk + 15) / 16) && mk > 0 && mk < maxm) {  // all equal so far
+              uint32_t a16[4], b16[4];
+              s.load16(cd + mk, a16);
+              s.load16(p + mk, b16);
+              const uint32_t k = ze_common16(a16, b16);
+              mk += k;
+              if (k < 16) break;
+            }
+            if (mk > maxm) mk = maxm;
+            if (mk > m) {  // (ties: way 0, the nearer)
+              m = mk;
+              cand = (uint32_t)cd;
+            }
           }
-          if (m > maxm) m = maxm;
           if (m < 4) m = 0;
         }
         unsigned long long pos = cur;
@@ -331,7 +362,7 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
         hlast = lmax;
         if (dist >= 2 && hlast <= 128) {
           if (l == 0) {
-            ze_huf_lengths(hist, hlast + 1, hlen, s_w[wv], s_par[wv]);
+            ze_huf_lengths(hist, hlast + 1, hlen, H.w, H.par);
             maxb = ze_huf_codes(hlen, hlast + 1, hval);
           }
           maxb = (uint32_t)__builtin_amdgcn_readfirstlane((int)maxb);
@@ -362,6 +393,8 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
             jt[2 * k + 1] = (uint8_t)(sb[k] >> 8);
           }
         }
+        for (int i = l; i < kZeRing; i += 64) ring[i] = 0;  // (the sequence phase shares this LDS)
+        wave_lds_sync();
         unsigned long long sbase = q + hn + tree + 6;
         for (int k = 0; k < 4; k++) {  // stream k: its symbols last to first, bits placed by a wave scan
           const uint32_t a0 = min((uint32_t)k * seg, (uint32_t)nlit);
@@ -413,7 +446,11 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
         for (unsigned long long k = l; k < nlit; k += 64) out[q + 3 + k] = lit[k];
         q += 3 + nlit;
       }
-      if (l == 0) {  // Number_of_Sequences, then the compression modes (all predefined)
+      // Number_of_Sequences, the modes byte, then per table (LL, OF, ML) a
+      // fitted distribution's description where it codes the block's
+      // sequences cheaper than the predefined one (zstd_enc.h ze_fit_table)
+      const uint32_t nsb = nseq < 128 ? 1u : nseq < 0x7F00 ? 2u : 3u;
+      if (l == 0) {
         if (nseq < 128) {
           out[q] = (uint8_t)nseq;
         } else if (nseq < 0x7F00) {
@@ -424,9 +461,45 @@ __global__ void __launch_bounds__(64 * kZeWaves) k_zstd_enc(EncArgs a, const ZeT
           out[q + 1] = (uint8_t)(nseq - 0x7F00);
           out[q + 2] = (uint8_t)((nseq - 0x7F00) >> 8);
         }
-        if (nseq) out[q + (nseq < 128 ? 1 : nseq < 0x7F00 ? 2 : 3)] = 0;
       }
-      q += (nseq < 128 ? 1 : nseq < 0x7F00 ? 2 : 3) + (nseq ? 1 : 0);
+      q += nsb;
+      if (nseq) {
+        wave_lds_sync();  // the literal phase's LDS is free
+        for (int i = l; i < 3 * 56; i += 64) (&F.cnt[0][0])[i] = 0u;
+        wave_lds_sync();
+        for (uint32_t g = 0; g < nseq; g += 64) {
+          const uint32_t i = g + (uint32_t)l;
+          if (i < nseq) {
+            const ZeSeq z = ze_unpack(seq[i]);
+            atomicAdd(&F.cnt[0][ze_ll_code(z.ll)], 1u);
+            atomicAdd(&F.cnt[1][ze_highbit(z.off + 3)], 1u);
+            atomicAdd(&F.cnt[2][ze_ml_code(z.ml - 3)], 1u);
+          }
+        }
+        wave_lds_sync();
+        const unsigned long long mq = q;
+        q += 1;
+        uint32_t modes = 0;
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+          const ZeFse &pre = t == 0 ? T->ll : t == 1 ? T->of : T->ml;
+          uint32_t dl = 0;
+          if (l == 0)
+            dl = t == 0   ? ze_fit_table(F.cnt[0], 36, kZeLLNorm, kZeLLSyms, kZeLLLog, F.t, F.w, F.desc)
+                 : t == 1 ? ze_fit_table(F.cnt[1], 32, kZeOFNorm, kZeOFSyms, kZeOFLog, F.t, F.w, F.desc)
+                          : ze_fit_table(F.cnt[2], 53, kZeMLNorm, kZeMLSyms, kZeMLLog, F.t, F.w, F.desc);
+          dl = (uint32_t)__builtin_amdgcn_readfirstlane((int)dl);
+          wave_lds_sync();  // lane 0's table and description visible
+          for (uint32_t k = (uint32_t)l; k < dl; k += 64)
+            if (q + k < lim) out[q + k] = F.desc[k];
+          q += dl;
+          ZeLaneFse &f = t == 0 ? f_ll : t == 1 ? f_of : f_ml;
+          f.load(dl ? F.t : pre, l);
+          modes |= (dl ? 2u : 0u) << (6 - 2 * t);
+          wave_lds_sync();  // the slot is free for the next table
+        }
+        if (l == 0 && mq < lim) out[mq] = (uint8_t)modes;
+      }
       if (nseq) {  // the FSE bitstream, the wave in step, sequences from the last
         ZeWaveBits w{0, 0, out, q, lim, l == 0};
         uint32_t chunk = ~0u;

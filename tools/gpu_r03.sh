@@ -10,6 +10,8 @@
 #   prof_c2    rocprofv3 kernel trace of the C2 bench
 #   prof_all   rocprofv3 kernel trace of C2 + C3 + C5 (no CPU baseline)
 #   pmc_c2     FETCH_SIZE / WRITE_SIZE passes over the C2 bench
+#   ab_meta    C2 bench alternating the product library and exp_lib/nometa
+#   enc_zstd / enc_flate   tools/bench_encode.py on the C3 records
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
@@ -35,10 +37,10 @@ while [ $# -gt 0 ]; do
   case "$1" in
     tests)
       step smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
-      step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
+      step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread ;;
     testsk)
       shift
-      step pytest_k 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$1" ;;
+      step pytest_k 600 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread -k "$1" ;;
     c2) step c2 300 $C2 ;;
     bench) step bench 600 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     full) step full 900 python3 bench.py ;;
@@ -53,6 +55,13 @@ while [ $# -gt 0 ]; do
         python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-flate --no-zstd --no-c5
       step pmc_c2_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_c2_write -o run -- \
         python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-flate --no-zstd --no-c5 ;;
+    ab_meta)  # k_crc with the header checks (product) vs -DRIO_CRC_META=0 (exp_lib/nometa), alternating
+      for i in 1 2; do
+        step c2_meta_$i 300 $C2
+        RIO_GPU_LIB=exp_lib/nometa/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_CRC_META=0" step c2_nometa_$i 300 $C2
+      done ;;
+    enc_zstd) step enc_zstd 300 python3 tools/bench_encode.py --codec 2 ;;
+    enc_flate) step enc_flate 300 python3 tools/bench_encode.py --codec 1 ;;
     *) echo "unknown step $1"; exit 2 ;;
   esac
   shift
