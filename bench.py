@@ -75,18 +75,18 @@ def make_c1_file():
     return make_c2_file(16385)
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r02b_c2_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03_c2_pmc.json")
 
 
 def pmc_traffic(kernel: str, replicas: int):
-    """HBM bytes per launch of `kernel` from the committed PMC pass (tools/profile_r02.sh:
+    """HBM bytes per launch of `kernel` from the committed PMC pass (tools/gpu_r03.sh pmc_c2:
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over this same bench command, FETCH_SIZE
     doubled per MI355X_MICROARCH.md). Only valid for the default replica count."""
     if replicas != REPLICAS or not os.path.exists(PMC_FILE):
         return None
     with open(PMC_FILE) as f:
         pm = json.load(f)
-    e = pm.get("rio::" + kernel) or pm.get("rio::%s<false>" % kernel)  # k_crc is a template
+    e = pm.get("rio::" + kernel) or pm.get("rio::%s<false, false>" % kernel)  # k_crc is a template
     if not e:
         return None
     return int(e.get("fetch_bytes", 0) + e.get("write_bytes", 0))
