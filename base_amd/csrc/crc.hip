@@ -105,14 +105,7 @@ struct CrcParseIn {
 };
 constexpr int kStageBytes = 1088;  // payload window staging: row 0 + 32 B of row 1 (then reused as the window)
 
-// kMeta: the chunk header checks of k_chunk_meta (chunk_meta, device_common.h)
-// on the way: the chunk's header is the first 28 bytes of its stage-0 row
-// (lanes 0 and 1, taken by readlane), its predecessor's comes in by one
-// vector load of lanes 0-1 issued before the fold and used after it; lane 0
-// stores the fields the block scans read. The span's chunk sizes come from the
-// headers themselves, so this pass runs first. (Scalar loads of the two
-// headers cost 6 %: they share lgkmcnt with the fold's LDS lookups.)
-template <bool kParse, bool kMeta>
+template <bool kParse>
 __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restrict__ span, uint64_t nchunks,
                                                        const uint32_t *__restrict__ ck_size,
                                                        const uint32_t *__restrict__ fix_a,
@@ -140,52 +133,27 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
   uint4 buf[kBufs][kRows];
   uint8_t *stage = kParse ? s_stage[threadIdx.x >> 6] : nullptr;
   uint16_t *tpos = kParse ? s_tpos[threadIdx.x >> 6] : nullptr;
-  // kMeta: the size is not known ahead -- it is the chunk's own header, read
-  // out of the first row of stage 0 (lane 1's dwords are size / total / index)
-  uint32_t size = kMeta ? 0u : ck_size[c];
+  uint32_t size = ck_size[c];
 #pragma unroll
   for (int q = 0; q < kBufs - 1; q++) load_stage(buf[q], span + c * kChunk, q, l);
   for (;;) {
     const uint8_t *ck = span + c * kChunk;
     const uint64_t cn = c + nwaves;
     const bool more = cn < nchunks;
-    // kMeta: the predecessor's header (lanes 0, 1), in flight during the fold
-    uint4 ph = make_uint4(0, 0, 0, 0);
-    if (kMeta && c > 0 && l < 2) ph = *reinterpret_cast<const uint4 *>(ck - kChunk + 16 * l);
-    const uint32_t size_n = kMeta ? 0u : ck_size[more ? cn : c];
-    uint32_t mlo = 0, mhi = 0, total = 0, index = 0;
-    // (kMeta: set at stage 0, once its first row is in -- after the prefetch
-    // of stage 3 is issued, so the wait does not hold the pipeline back)
-    uint32_t sz = size > (uint32_t)kMaxPayload ? (uint32_t)kMaxPayload : size;
-    int end = kChunkHdr + (int)sz;
-    bool full = (sz == (uint32_t)kMaxPayload);
+    const uint32_t size_n = ck_size[more ? cn : c];
+    const uint32_t sz = size > (uint32_t)kMaxPayload ? (uint32_t)kMaxPayload : size;
+    const int end = kChunkHdr + (int)sz;
+    const bool full = (sz == (uint32_t)kMaxPayload);
     // a block starts here: this wave parses it after the checksum (scalar load)
     const bool starts = kParse && pin.ck_index[c] == 0;
     uint32_t s[4] = {0, 0, 0, 0};
     uint32_t stored = 0;
-    uint32_t fa = 0, fb = 0;
-    if (!kMeta) {
-      fa = fix_a[sz];
-      fb = fix_b[sz];
-    }
+    const uint32_t fa = fix_a[sz], fb = fix_b[sz];
 #pragma unroll
     for (int q = 0; q < kStages; q++) {
       const int nq = q + kBufs - 1;  // stage to prefetch (this chunk or the next)
       if (nq < kStages) load_stage(buf[nq % kBufs], ck, nq, l);
       else if (more) load_stage(buf[nq % kBufs], span + cn * kChunk, nq - kStages, l);
-      if (kMeta && q == 0) {  // the header: lane 0 magic / crc / flag, lane 1 size / total / index
-        const uint4 r0 = buf[0][0];
-        size = (uint32_t)__builtin_amdgcn_readlane((int)r0.x, 1);
-        total = (uint32_t)__builtin_amdgcn_readlane((int)r0.y, 1);
-        index = (uint32_t)__builtin_amdgcn_readlane((int)r0.z, 1);
-        mlo = (uint32_t)__builtin_amdgcn_readlane((int)r0.x, 0);
-        mhi = (uint32_t)__builtin_amdgcn_readlane((int)r0.y, 0);
-        sz = size > (uint32_t)kMaxPayload ? (uint32_t)kMaxPayload : size;
-        end = kChunkHdr + (int)sz;
-        full = (sz == (uint32_t)kMaxPayload);
-        fa = fix_a[sz];
-        fb = fix_b[sz];
-      }
       if (kParse && q == 0 && starts) {  // rows 0..1 raw, before the fold masks them
         *reinterpret_cast<uint4 *>(stage + 16 * l) = buf[0][0];
         if (l < 2) *reinterpret_cast<uint4 *>(stage + 1024 + 16 * l) = buf[0][1];
@@ -211,21 +179,6 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
       // (flags & 2: the encode path computes CRCs of chunks it is writing -- no compare)
       if (crc != stored && fold && !(ca.flags & 2)) atomicMin(&d.ctl->first_crc_err, (unsigned long long)c);
     }
-    if (kMeta) {
-      const ChunkMeta m = chunk_meta(mlo, mhi, size, total, index, c > 0,
-                                     (uint32_t)__builtin_amdgcn_readlane((int)ph.x, 0),
-                                     (uint32_t)__builtin_amdgcn_readlane((int)ph.y, 0),
-                                     (uint32_t)__builtin_amdgcn_readlane((int)ph.y, 1),
-                                     (uint32_t)__builtin_amdgcn_readlane((int)ph.z, 1));
-      if (l == 0) {
-        d.ck_size[c] = size;
-        d.ck_total[c] = total;
-        d.ck_index[c] = index;
-        d.ck_info[c] = m.info;
-        d.ck_ssz[c] = 0;  // straddler slots, filled by the parse
-        if (m.err) atomicMin(&d.ctl->first_chunk_err, (unsigned long long)c);
-      }
-    }
     if (kParse && starts) {
       const uint32_t b = pin.ck_block[c];
       const unsigned long long meta = pin.blk_meta[b], len = pin.blk_len[b];
@@ -249,7 +202,7 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
 }
 
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
-                hipStream_t st, const ParseArgs *fused, bool meta) {
+                hipStream_t st, const ParseArgs *fused) {
   uint64_t g = (nchunks + kCrcWaves - 1) / kCrcWaves;
   const uint64_t cap = (uint64_t)(ncu > 0 ? ncu : 256);
   if (g > cap) g = cap;
@@ -257,16 +210,12 @@ void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const C
   const CrcParseIn pin{d.ck_index, d.ck_block, d.blk_meta, d.blk_len, d.blk_item_base, d.ck_pay};
 #if RIO_FUSED_PARSE
   if (fused)
-    hipLaunchKernelGGL((k_crc<true, false>), dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks,
-                       d.ck_size, d.crc_fix_a, d.crc_fix_b, d, ca, pin, *fused);
+    hipLaunchKernelGGL(k_crc<true>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
+                       d.crc_fix_a, d.crc_fix_b, d, ca, pin, *fused);
   else
 #endif
-  if (meta)
-    hipLaunchKernelGGL((k_crc<false, true>), dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks,
-                       d.ck_size, d.crc_fix_a, d.crc_fix_b, d, ca, pin, ParseArgs{});
-  else
-    hipLaunchKernelGGL((k_crc<false, false>), dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks,
-                       d.ck_size, d.crc_fix_a, d.crc_fix_b, d, ca, pin, ParseArgs{});
+    hipLaunchKernelGGL(k_crc<false>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
+                       d.crc_fix_a, d.crc_fix_b, d, ca, pin, ParseArgs{});
 }
 
 }  // namespace rio

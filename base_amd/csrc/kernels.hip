@@ -2,11 +2,11 @@
 // and the scans that enumerate blocks. Host orchestration in pipeline.cpp.
 //
 // Pipeline for one span of whole chunks (none codec):
-//   k_chunk_meta   per chunk: header fields, size check, the structural checks of
+//   chunk pass     per chunk: header fields, size check, the structural checks of
 //                  ChunkScanner.Scan against the previous chunk (chunk.go:253-294,
-//                  333-336).
-//   scans          payload prefix ck_pay; block enumeration (index == 0) with a
-//                  descriptor per block and its item count (first header varint).
+//                  333-336); payload prefix ck_pay; block enumeration (index == 0)
+//                  with a descriptor per block and its item count (first header
+//                  varint). Three launches (k_chunk_tiles / _partials / _apply).
 //   block scan     item slots per block.
 //   k_parse        (blocks.hip) wave per block: magic handling, header parse,
 //                  item views (parseChunksToItems, scannerv2.go:53-97, 363-388).
@@ -22,30 +22,6 @@
 namespace rio {
 
 constexpr uint32_t kNoBlock = 0xffffffffu;
-
-// ---------------------------------------------------------------- k_chunk_meta
-__global__ void __launch_bounds__(256) k_chunk_meta(const uint8_t *__restrict__ span, uint64_t nchunks,
-                                                    DevBufs d) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += stride) {
-    const uint32_t *h = reinterpret_cast<const uint32_t *>(span + c * kChunk);
-    const uint4 a = *reinterpret_cast<const uint4 *>(h);      // magic lo, hi, crc, flag
-    const uint4 b = *reinterpret_cast<const uint4 *>(h + 4);  // size, total, index, data
-    uint4 pa = make_uint4(0, 0, 0, 0), pb = make_uint4(0, 0, 0, 0);
-    if (c > 0) {
-      const uint32_t *p = reinterpret_cast<const uint32_t *>(span + (c - 1) * kChunk);
-      pa = *reinterpret_cast<const uint4 *>(p);
-      pb = *reinterpret_cast<const uint4 *>(p + 4);
-    }
-    const ChunkMeta m = chunk_meta(a.x, a.y, b.x, b.y, b.z, c > 0, pa.x, pa.y, pb.y, pb.z);
-    d.ck_size[c] = b.x;
-    d.ck_total[c] = b.y;
-    d.ck_index[c] = b.z;
-    d.ck_info[c] = m.info;
-    d.ck_ssz[c] = 0;  // straddler slots, filled by k_parse
-    if (m.err) atomicMin(&d.ctl->first_chunk_err, (unsigned long long)c);
-  }
-}
 
 // ---------------------------------------------------------------- scans
 // Exclusive scan over n values (n read from *n_dev when non-null, else n_host),
@@ -138,10 +114,6 @@ __global__ void __launch_bounds__(kScanThreads) k_scan_apply(F f, O o, const uns
   }
 }
 
-struct FlagLoad {  // block starts: index == 0
-  const uint32_t *ck_index;
-  __device__ unsigned long long operator()(uint64_t i) const { return ck_index[i] == 0 ? 1ull : 0ull; }
-};
 // Go 1.13 binary.Uvarint of the block's first payload bytes: the item count
 // (parseChunksToItems, scannerv2.go:65), used to reserve item slots before the
 // headers are parsed. 0 when it does not decode or cannot fit the block.
@@ -168,38 +140,6 @@ __device__ unsigned long long first_uvarint(const uint8_t *span, const DevBufs &
   return 0;
 }
 
-struct FlagOut {  // block starts -> block list + per-block descriptors
-  DevBufs d;
-  const uint8_t *span;
-  uint64_t nchunks;
-  int32_t codec;
-  __device__ void operator()(uint64_t i, unsigned long long ex, unsigned long long v) const {
-    d.ck_block[i] = (ex + v == 0) ? kNoBlock : (uint32_t)(ex + v - 1);  // chunks before any start: none
-    if (!v) return;
-    d.blk_c0[ex] = i;
-    const uint32_t total = d.ck_total[i];
-    const uint32_t cls = d.ck_info[i] & 0xffu;
-    unsigned long long meta = (unsigned long long)total | ((unsigned long long)cls << kMetaClsShift);
-    unsigned long long len = 0, nres = 0;
-    if (total != 0 && i + total <= nchunks) {
-      meta |= kMetaComplete;
-      const unsigned long long pay0 = d.ck_pay[i];
-      len = d.ck_pay[i + total] - pay0;
-      if (d.ck_pay[i + total - 1] - pay0 == (unsigned long long)(total - 1) * kMaxPayload) meta |= kMetaRegular;
-      if (codec == RIO_CODEC_NONE) nres = first_uvarint(span, d, i, total, len);
-    }
-    d.blk_meta[ex] = meta;
-    d.blk_len[ex] = len;
-    d.blk_nitems[ex] = nres;
-  }
-};
-struct SizeLoad {
-  const uint32_t *ck_size;
-  __device__ unsigned long long operator()(uint64_t i) const {
-    const uint32_t s = ck_size[i];
-    return s > (uint32_t)kMaxPayload ? 0ull : (unsigned long long)s;
-  }
-};
 struct U64Out {
   unsigned long long *out;
   __device__ void operator()(uint64_t i, unsigned long long ex, unsigned long long) const { out[i] = ex; }
@@ -208,6 +148,138 @@ struct U64Load {
   const unsigned long long *in;
   __device__ unsigned long long operator()(uint64_t i) const { return in[i]; }
 };
+
+// ---------------------------------------------------------------- chunk pass
+// The chunk headers and both per-chunk scans (payload prefix, block starts) in
+// three launches. Thread t of a tile owns chunks base + 8t .. base + 8t + 7.
+//   k_chunk_tiles    the headers (each thread's 8 and the one before them:
+//                    chunk_meta checks against the predecessor), the per-chunk
+//                    fields, the tile's sums of payload sizes and block starts;
+//   k_chunk_partials the two columns of tile sums scanned (one workgroup);
+//   k_chunk_apply    ck_pay, ck_block and the block descriptors (FlagOut).
+__global__ void __launch_bounds__(kScanThreads) k_chunk_tiles(const uint8_t *__restrict__ span, uint64_t nchunks,
+                                                              DevBufs d, unsigned long long *psize,
+                                                              unsigned long long *pflag) {
+  __shared__ unsigned long long lds[17];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  uint4 a[kScanItems], b[kScanItems], pa = make_uint4(0, 0, 0, 0), pb = make_uint4(0, 0, 0, 0);
+  if (i0 > 0 && i0 < nchunks) {
+    const uint4 *h = reinterpret_cast<const uint4 *>(span + (i0 - 1) * kChunk);
+    pa = h[0];
+    pb = h[1];
+  }
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++)
+    if (i0 + k < nchunks) {
+      const uint4 *h = reinterpret_cast<const uint4 *>(span + (i0 + k) * kChunk);
+      a[k] = h[0];  // magic lo, hi, crc, flag
+      b[k] = h[1];  // size, total, index, data
+    }
+  unsigned long long ss = 0, sf = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++) {
+    const uint64_t i = i0 + k;
+    if (i >= nchunks) break;
+    const ChunkMeta m = chunk_meta(a[k].x, a[k].y, b[k].x, b[k].y, b[k].z, i > 0, pa.x, pa.y, pb.y, pb.z);
+    d.ck_size[i] = b[k].x;
+    d.ck_total[i] = b[k].y;
+    d.ck_index[i] = b[k].z;
+    d.ck_info[i] = m.info;
+    d.ck_ssz[i] = 0;  // straddler slots, filled by the parse
+    if (m.err) atomicMin(&d.ctl->first_chunk_err, (unsigned long long)i);
+    ss += b[k].x > (uint32_t)kMaxPayload ? 0ull : (unsigned long long)b[k].x;
+    sf += b[k].z == 0 ? 1ull : 0ull;
+    pa = a[k];
+    pb = b[k];
+  }
+  unsigned long long ts, tf;
+  block_excl_scan(ss, &ts, lds);
+  block_excl_scan(sf, &tf, lds);
+  if (threadIdx.x == 0) {
+    psize[blockIdx.x] = ts;
+    pflag[blockIdx.x] = tf;
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_chunk_partials(uint64_t nchunks, unsigned long long *psize,
+                                                         unsigned long long *pflag, unsigned long long *pay_total,
+                                                         unsigned long long *nblocks) {
+  __shared__ unsigned long long lds[17];
+  const uint64_t ntiles = (nchunks + kScanTile - 1) / kScanTile;
+  unsigned long long cs = 0, cf = 0;
+  for (uint64_t base = 0; base < ntiles; base += blockDim.x) {
+    const uint64_t i = base + threadIdx.x;
+    const bool in = i < ntiles;
+    unsigned long long ts, tf;
+    const unsigned long long es = block_excl_scan(in ? psize[i] : 0ull, &ts, lds);
+    const unsigned long long ef = block_excl_scan(in ? pflag[i] : 0ull, &tf, lds);
+    if (in) {
+      psize[i] = cs + es;
+      pflag[i] = cf + ef;
+    }
+    cs += ts;
+    cf += tf;
+  }
+  if (threadIdx.x == 0) {
+    *pay_total = cs;  // ck_pay[nchunks]
+    *nblocks = cf;
+  }
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_chunk_apply(const uint8_t *__restrict__ span, uint64_t nchunks,
+                                                              DevBufs d, int32_t codec,
+                                                              const unsigned long long *psize,
+                                                              const unsigned long long *pflag) {
+  __shared__ unsigned long long lds[17];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  uint32_t sz[kScanItems], st[kScanItems];
+  unsigned long long ss = 0, sf = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++) {
+    const bool in = i0 + k < nchunks;
+    const uint32_t s = in ? d.ck_size[i0 + k] : 0u;
+    sz[k] = s > (uint32_t)kMaxPayload ? 0u : s;
+    st[k] = in && d.ck_index[i0 + k] == 0 ? 1u : 0u;
+    ss += sz[k];
+    sf += st[k];
+  }
+  unsigned long long ts, tf;
+  unsigned long long es = block_excl_scan(ss, &ts, lds) + psize[blockIdx.x];
+  unsigned long long ef = block_excl_scan(sf, &tf, lds) + pflag[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++) {
+    const uint64_t i = i0 + k;
+    if (i >= nchunks) break;
+    d.ck_pay[i] = es;
+    d.ck_block[i] = (ef + st[k] == 0) ? kNoBlock : (uint32_t)(ef + st[k] - 1);  // chunks before any start: none
+    if (st[k]) {  // a block starts here: its descriptor (block ef)
+      const uint32_t total = d.ck_total[i];
+      const uint32_t cls = d.ck_info[i] & 0xffu;
+      unsigned long long meta = (unsigned long long)total | ((unsigned long long)cls << kMetaClsShift);
+      unsigned long long len = 0, nres = 0;
+      if (total != 0 && i + total <= nchunks) {
+        meta |= kMetaComplete;
+        // the block's payload bytes (its chunks' sizes, as the payload prefix
+        // counts them) and whether every chunk but the last is full
+        bool regular = true;
+        for (uint32_t q = 0; q < total; q++) {
+          const uint32_t s = d.ck_size[i + q];
+          const uint32_t v = s > (uint32_t)kMaxPayload ? 0u : s;
+          len += v;
+          if (q + 1 < total && v != (uint32_t)kMaxPayload) regular = false;
+        }
+        if (regular) meta |= kMetaRegular;
+        if (codec == RIO_CODEC_NONE) nres = first_uvarint(span, d, i, total, len);
+      }
+      d.blk_c0[ef] = i;
+      d.blk_meta[ef] = meta;
+      d.blk_len[ef] = len;
+      d.blk_nitems[ef] = nres;
+    }
+    es += sz[k];
+    ef += st[k];
+  }
+}
 
 // ---------------------------------------------------------------- launchers
 static inline unsigned grid_for(uint64_t n, unsigned per, unsigned cap) {
@@ -232,8 +304,15 @@ void launch_reset(const DevBufs &d, unsigned long long *nblocks_dev, hipStream_t
   hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, d.ctl, nblocks_dev);
 }
 
-void launch_chunk_meta(const uint8_t *span, uint64_t nchunks, const DevBufs &d, hipStream_t st) {
-  hipLaunchKernelGGL(k_chunk_meta, dim3(grid_for(nchunks, 256, 4096)), dim3(256), 0, st, span, nchunks, d);
+void launch_chunk_pass(const uint8_t *span, uint64_t nchunks, const DevBufs &d, unsigned long long *nblocks_dev,
+                       int32_t codec, hipStream_t st) {
+  const uint64_t tiles = (nchunks + kScanTile - 1) / kScanTile;
+  const unsigned g = (unsigned)(tiles ? tiles : 1);
+  unsigned long long *psize = d.scan_tmp, *pflag = d.scan_tmp + g;
+  hipLaunchKernelGGL(k_chunk_tiles, dim3(g), dim3(kScanThreads), 0, st, span, nchunks, d, psize, pflag);
+  hipLaunchKernelGGL(k_chunk_partials, dim3(1), dim3(1024), 0, st, nchunks, psize, pflag, d.ck_pay + nchunks,
+                     nblocks_dev);
+  hipLaunchKernelGGL(k_chunk_apply, dim3(g), dim3(kScanThreads), 0, st, span, nchunks, d, codec, psize, pflag);
 }
 
 template <class F, class O>
@@ -245,14 +324,6 @@ static void scan(F f, O o, const unsigned long long *n_dev, uint64_t n_host, uin
   hipLaunchKernelGGL(k_scan_reduce<F>, dim3(g), dim3(kScanThreads), 0, st, f, n_dev, n_host, partial);
   hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, st, n_dev, n_host, partial, total_out, total_at);
   hipLaunchKernelGGL((k_scan_apply<F, O>), dim3(g), dim3(kScanThreads), 0, st, f, o, n_dev, n_host, partial);
-}
-
-void launch_chunk_scans(const uint8_t *span, uint64_t nchunks, const DevBufs &d, unsigned long long *nblocks_dev,
-                        int32_t codec, hipStream_t st) {
-  // payload prefix first: the block descriptors read it
-  scan(SizeLoad{d.ck_size}, U64Out{d.ck_pay}, nullptr, nchunks, nchunks, d.scan_tmp, nullptr, d.ck_pay, st);
-  scan(FlagLoad{d.ck_index}, FlagOut{d, span, nchunks, codec}, nullptr, nchunks, nchunks, d.scan_tmp, nblocks_dev,
-       nullptr, st);
 }
 
 // exclusive scan of a per-chunk u64 array into out (n + 1 entries)

@@ -29,10 +29,9 @@
 
 namespace rio {
 // kernels.hip
-void launch_chunk_meta(const uint8_t *span, uint64_t nchunks, const DevBufs &d, hipStream_t st);
+void launch_chunk_pass(const uint8_t *span, uint64_t nchunks, const DevBufs &d, unsigned long long *nblocks_dev,
+                       int32_t codec, hipStream_t st);
 void launch_reset(const DevBufs &d, unsigned long long *nblocks_dev, hipStream_t st);
-void launch_chunk_scans(const uint8_t *span, uint64_t nchunks, const DevBufs &d, unsigned long long *nblocks_dev,
-                        int32_t codec, hipStream_t st);
 void launch_chunk_scan(const unsigned long long *in, unsigned long long *out, unsigned long long *tmp, uint64_t n,
                        hipStream_t st);
 void launch_block_scan(const unsigned long long *in, unsigned long long *out, unsigned long long *tmp,
@@ -50,7 +49,7 @@ void launch_block_files(const DevBufs &d, const unsigned long long *seg_end, con
                         uint64_t nseg, uint64_t max_blocks, hipStream_t st);
 // crc.hip
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
-                hipStream_t st, const ParseArgs *fused, bool meta);
+                hipStream_t st, const ParseArgs *fused);
 // codec.hip
 void launch_compact(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
@@ -117,7 +116,6 @@ struct rio_ctx {
   hipEvent_t ev[kNumEv] = {};
   hipEvent_t evA = nullptr, evB = nullptr;  // stream hand-offs (no timing)
   bool last_had_dec = false;
-  bool last_crc_first = false;  // the last run's k_crc also checked the chunk headers (ran before the scans)
   int ev_parse0 = kEvParse0, ev_crc0 = kEvCrc0;  // the events the last run's parse / CRC stages start at
   bool item_end_mode = false;  // RIO_CFG_ITEM_END: device results carry item_end (cumSize)
   bool last_cmp = false;  // the last host result's records are the compacted blocks (d.cmp)
@@ -212,7 +210,7 @@ static int alloc_bufs(rio_ctx *c) {
       dalloc(&d.blk_need, nb) || dalloc(&d.fl, nb) || dalloc(&d.blk_coff, 2 * (nb + 1)) || dalloc(&d.blk_data, nb) ||
       dalloc(&d.blk_file_off, nb) || dalloc(&d.blk_seg, nb))
     return -1;
-  if (dalloc(&d.scan_tmp, (n + 2047) / 2048 + 16) || dalloc(&d.strad, n)) return -1;
+  if (dalloc(&d.scan_tmp, 2 * ((n + 2047) / 2048) + 16) || dalloc(&d.strad, n)) return -1;
   if (dalloc(&d.item_off, c->item_cap) || dalloc(&d.item_len, c->item_cap) || dalloc(&d.side, c->side_cap))
     return -1;
   return 0;
@@ -453,21 +451,13 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   // that checksums a block's first chunk parses the block
   const bool fused = RIO_FUSED_PARSE && codec == RIO_CODEC_NONE && run_parse && run_crc && nchunks > 0;
   const CrcArgs ca{RIO_ABLATE, 0};
-  // order: k_chunk_meta, scans, (decode), parse, k_crc, resolve. Ablation
-  // builds with -DRIO_CRC_META=1 check the chunk headers inside k_crc, which
-  // then runs first (spans without a CRC pass still take k_chunk_meta)
-  const bool meta_in_crc = RIO_CRC_META && run_crc && !fused && nchunks > 0;
-  c->last_crc_first = meta_in_crc;
+  // order: chunk pass (headers + scans), (decode), parse, k_crc, resolve
   c->ev_crc0 = kEvCrc0;
-  if (meta_in_crc || !run_crc || fused || nchunks == 0) {  // (no CRC pass later: a zero-length interval here)
+  if (!run_crc || fused || nchunks == 0) {  // (no CRC pass later: a zero-length interval)
     HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
-    if (meta_in_crc) launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr, true);
     HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
   }
-  if (nchunks > 0) {
-    if (!meta_in_crc) launch_chunk_meta(span, nchunks, d, st);
-    launch_chunk_scans(span, nchunks, d, c->nblocks_dev, codec, st);
-  }
+  if (nchunks > 0) launch_chunk_pass(span, nchunks, d, c->nblocks_dev, codec, st);
   HIP_OK(hipEventRecord(c->ev[kEvScans], st));
   c->last_had_dec = false;
   if (codec != RIO_CODEC_NONE && nchunks > 0) {
@@ -502,7 +492,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     launch_block_scan(d.blk_nitems, d.blk_item_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
     if (fused) {
       HIP_OK(hipEventRecord(c->ev[kEvCrc0], st2));
-      launch_crc(span, nchunks, d, ca, c->ncu, st2, &pa, false);
+      launch_crc(span, nchunks, d, ca, c->ncu, st2, &pa);
       HIP_OK(hipEventRecord(c->ev[kEvCrc1], st2));
     } else if (codec == RIO_CODEC_NONE && mode == kModeBody && !no_items) {
       // the common block shape in a lean kernel, the rest listed for k_parse
@@ -526,13 +516,13 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   }
   HIP_OK(hipEventRecord(c->ev[kEvParse1], st2));
   if (st2 != st) HIP_OK(hipEventRecord(c->evB, st2));
-  if (!meta_in_crc && !fused && run_crc && nchunks > 0) {
+  if (!fused && run_crc && nchunks > 0) {
     c->ev_crc0 = kEvParse1;
     if (st2 != st) {
       HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
       c->ev_crc0 = kEvCrc0;
     }
-    launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr, false);
+    launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr);
     HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
   }
   if (st2 != st) HIP_OK(hipStreamWaitEvent(st, c->evB, 0));
@@ -971,7 +961,6 @@ extern "C" int rio_stage_times(rio_ctx *ctx, float *ms, int n) {
   if (ctx->last_had_dec) hipEventElapsedTime(&t[1], ctx->ev[kEvScans], ctx->ev[kEvDec]);
   hipEventElapsedTime(&t[2], ctx->ev[ctx->ev_crc0], ctx->ev[kEvCrc1]);
   hipEventElapsedTime(&t[3], ctx->ev[kEvStart], ctx->ev[kEvScans]);
-  if (ctx->last_crc_first) t[3] -= t[2];  // (the headers were checked inside k_crc)
   hipEventElapsedTime(&t[4], ctx->ev[kEvStart], ctx->ev[kEvEnd]);
   const int k = n < 5 ? n : 5;
   for (int i = 0; i < k; i++) ms[i] = t[i];

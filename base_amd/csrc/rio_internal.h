@@ -64,12 +64,6 @@ enum Mode : int32_t { kModeBody = 0, kModeHeader = 1, kModeTrailer = 2, kModeLas
 #ifndef RIO_TWO_STREAMS
 #define RIO_TWO_STREAMS 0
 #endif
-// Ablation: k_crc also checks the chunk headers (k_chunk_meta's work, on the
-// header rows it streams) and runs first. Measured slower on C2 (k_crc 2.92
-// against 2.81 ms), so the shipped library runs k_chunk_meta.
-#ifndef RIO_CRC_META
-#define RIO_CRC_META 0
-#endif
 // Ablation: the none-codec parse fused into k_crc (crc.hip). Measured slower
 // (DESIGN.md §5), so the shipped library runs k_crc and k_parse separately.
 #ifndef RIO_FUSED_PARSE

@@ -60,6 +60,11 @@ while [ $# -gt 0 ]; do
         step c2_meta_$i 300 $C2
         RIO_GPU_LIB=exp_lib/nometa/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_CRC_META=0" step c2_nometa_$i 300 $C2
       done ;;
+    ab_ctx)  # C2 with steps alternating over 2 contexts (default) vs 1 context
+      for i in 1 2; do
+        step c2_ctx2_$i 300 $C2
+        step c2_ctx1_$i 300 $C2 --c2-contexts 1
+      done ;;
     enc_zstd) step enc_zstd 300 python3 tools/bench_encode.py --codec 2 ;;
     enc_flate) step enc_flate 300 python3 tools/bench_encode.py --codec 1 ;;
     *) echo "unknown step $1"; exit 2 ;;
