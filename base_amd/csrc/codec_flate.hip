@@ -1475,8 +1475,17 @@ __global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *
     uint32_t *tok = d.tok + c0 * (uint64_t)kTokPerChunk;
     uint64_t bit = 0;
     uint32_t olen = 0, ntok = 0, res = 0;  // res: 0 ok, else a CodecErr for k_inflate_exact
+    uint32_t ck_next = 1;                  // the next input chunk's checkpoint (split copy pass)
     bool fin = false, fixed = false;
+    // checkpoints for k_flate_plan: (tokens, output) at the first DEFLATE block
+    // header or body round in each input chunk
+    auto checkpoint = [&]() {
+      const uint64_t kc = (bit >> 3) / (uint64_t)kMaxPayload;
+      for (; ck_next <= kc && ck_next < total; ck_next++)
+        if (l == 0) d.fl_ck[c0 + ck_next] = (unsigned long long)ntok | ((unsigned long long)olen << 32);
+    };
     while (!decline && !res && !fin) {
+      checkpoint();
       // ---- DEFLATE block header (wave-uniform)
       TokDec t;
       t.in = in;
@@ -1533,6 +1542,7 @@ __global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *
           res = kCodecEof;
           break;
         }
+        checkpoint();
         const uint64_t w0 = bit >> 5;  // staged window: dwords [w0, w0 + kSyncWinDw)
         wave_lds_sync();
         for (uint32_t k = (uint32_t)l; k < kSyncWinDw; k += 64) S.win[sync_at(k)] = fetch_dword(in, 4 * (w0 + k));
@@ -1618,6 +1628,7 @@ __global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *
         sp->mode = kFlDone;
         sp->ntok = ntok;
         sp->olen = olen;
+        d.fl_ck[c0] = ck_next;  // checkpoints 1 .. ck_next - 1
       }
     }
   }
@@ -1630,6 +1641,13 @@ __device__ __forceinline__ uint32_t umod_small(uint32_t k, uint32_t d) {
   if (r < 0) r += (int32_t)d;
   if (r >= (int32_t)d) r -= (int32_t)d;
   return (uint32_t)r;
+}
+
+// this wave's global stores complete before its next loads of the same bytes
+__device__ __forceinline__ void zmem_sync_dev() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // Copy-pass window: a ring of 36 KiB = the 32 KiB DEFLATE history + one batch
@@ -1821,6 +1839,195 @@ __global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long 
 #define RIO_LZ2_WPE 5
 #endif
 #define RIO_LZ2_ATTR __attribute__((amdgpu_waves_per_eu(RIO_LZ2_WPE)))
+
+// The copy pass over one token list (k_flate_lz2; k_flate_seg's segments):
+// `ntok` tokens at tk, output from position olen (> 0: resumed) into out
+// through a kRingB-byte ring, batches of at most kSpanB bytes. Returns the end
+// position. Positions count symbol bytes: kSym = 1, the decoded bytes; kSym =
+// 2, a split block's later segment as u16 symbols (k_flate_seg): every length
+// and distance doubles, a literal byte b is the symbol (b, 0), and the
+// segment's 32 KiB of unknown history are the symbols 256 + i (i = the
+// position's offset in that window) -- synthesized in the ring here, written
+// before `out` by the caller (syn_a: the segment's start modulo 16, see
+// k_flate_seg). Every byte-level step is the same for both widths.
+#ifdef RIO_FLSTAT
+__device__ Ctl *st_ctl;
+#endif
+template <int kSym, uint32_t kRingB, uint32_t kSpanB>
+__device__ __forceinline__ uint32_t lz2_run(uint8_t *ring, uint8_t *out, const uint32_t *tk, uint32_t ntok,
+                                            uint32_t olen, uint32_t syn_a = 0) {
+  constexpr uint32_t kMaskB = kRingB - 1, kNearB = kRingB - kSpanB - 16;
+  static_assert(kNearB >= kSpanB + 16 + 2 * 258, "HBM sources must be flushed two batches back");
+  const int l = lane_id();
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(out);
+  wave_lds_sync();
+  if (olen > 0) {  // resumed: the history before olen, into the ring
+    const uint32_t h0 = (olen > kNearB ? olen - kNearB : 0u) & ~15u;
+    for (uint32_t x = h0 + 16 * (uint32_t)l; x < olen; x += 1024) {
+      uint4 v;
+      if (kSym == 1) {
+        v = *reinterpret_cast<const uint4 *>(out + x);
+      } else {  // the synthetic window: symbol at x = 256 + x/2 - syn_a
+        const uint32_t s0 = 256u + (x >> 1) - syn_a;
+        v = make_uint4(s0 | ((s0 + 1) << 16), (s0 + 2) | ((s0 + 3) << 16), (s0 + 4) | ((s0 + 5) << 16),
+                       (s0 + 6) | ((s0 + 7) << 16));
+      }
+      *reinterpret_cast<uint4 *>(ring + (x & kMaskB)) = v;
+    }
+  }
+  uint32_t pre[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) pre[k] = (64u * k + (uint32_t)l < ntok) ? tk[64 * k + l] : 0u;
+  uint32_t cur = 0;
+  while (cur < ntok) {
+    uint32_t t[4], len[4], p[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) t[k] = pre[k];
+    // output positions (relative to the batch) and the tokens this batch takes
+    uint32_t carry = 0, take = 0, emax = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const bool valid = cur + 64u * k + (uint32_t)l < ntok;
+      len[k] = valid ? kSym * tok_len(t[k]) : 0u;
+      const uint32_t incl = wave_incl_sum_dpp(len[k]) + carry;
+      p[k] = incl - len[k];
+      const bool ok = valid && incl <= kSpanB;  // a prefix of the tokens (positions only grow)
+      take += (uint32_t)__popcll(__ballot(ok));
+      if (ok) emax = incl;
+      else len[k] = 0;
+      carry = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+    }
+    const uint32_t total = (uint32_t)__reduce_max_sync(~0ull, emax);
+    const uint32_t B0 = olen;
+#ifdef RIO_FLSTAT  // (statistics builds: batches, tokens, rounds, pending tokens -> ctl->zprof)
+    uint32_t st_rounds = 0;
+#endif
+    {  // zero the batch's ring bytes (their dwords; the history bytes of the first one stay)
+      uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
+      const uint32_t z0 = (B0 + 3) >> 2, z1 = (B0 + total + 3) >> 2;
+      for (uint32_t z = z0 + (uint32_t)l; z < z1; z += 64) rw[z & (kMaskB >> 2)] = 0u;
+      if ((B0 & 3) && l == 0) atomicAnd(&rw[(B0 >> 2) & (kMaskB >> 2)], (1u << (8 * (B0 & 3))) - 1);
+      wave_lds_sync();
+    }
+    const uint32_t near = B0 > kNearB ? B0 - kNearB : 0u;  // positions >= near: in the ring
+    // literals now; matches sourced before the batch now; the others pending
+    bool pend[4];
+    uint32_t cs[4], cn[4], glob = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      pend[k] = false;
+      cn[k] = 0;
+      const uint32_t n = len[k];
+      const uint32_t x = B0 + p[k];
+      cs[k] = x - kSym * ((t[k] & 0xffffu) + 1);
+      if (n == 0) continue;
+      if (!(t[k] >> 31)) {  // 1-3 literal bytes
+        uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
+        const uint32_t v = t[k] & 0xffffffu, o = 8 * (x & 3);
+        if (kSym == 1) {
+          atomicOr(&rw[(x >> 2) & (kMaskB >> 2)], v << o);
+          if ((x & 3) + n > 4) atomicOr(&rw[((x >> 2) + 1) & (kMaskB >> 2)], v >> (32 - o));
+        } else {  // bytes b0 0 b1 0 b2 0 at an even x
+          const uint64_t w = ((uint64_t)((v & 0xffu) | ((v & 0xff00u) << 8)) | ((uint64_t)(v >> 16) << 32)) << o;
+          atomicOr(&rw[(x >> 2) & (kMaskB >> 2)], (uint32_t)w);
+          if ((x & 3) + n > 4) atomicOr(&rw[((x >> 2) + 1) & (kMaskB >> 2)], (uint32_t)(w >> 32));
+        }
+      } else if (cs[k] < near) {
+        cn[k] = n;
+        glob |= 1u << k;
+      } else if (cs[k] + n <= B0) {
+        cn[k] = n;
+      } else {
+        pend[k] = true;
+      }
+    }
+#ifdef RIO_FLSTAT
+    {
+      uint32_t np = 0, ng = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        np += (uint32_t)__popcll(__ballot(pend[k]));
+        ng += (uint32_t)__popcll(__ballot((glob >> k) & 1));
+      }
+      if (l == 0) {
+        atomicAdd(&st_ctl->zprof[0], 1ull);
+        atomicAdd(&st_ctl->zprof[1], (unsigned long long)take);
+        atomicAdd(&st_ctl->zprof[2], (unsigned long long)np);
+        atomicAdd(&st_ctl->zprof[3], (unsigned long long)ng);
+      }
+    }
+#endif
+    // the next batch's tokens (issued before this batch's stores: see above)
+    const uint32_t nx = cur + take;
+#pragma unroll
+    for (int k = 0; k < 4; k++) pre[k] = (nx + 64u * k + (uint32_t)l < ntok) ? tk[nx + 64 * k + l] : 0u;
+    // the copies above (every slot, ring or HBM sources), then the matches
+    // sourced inside the batch in rounds: each round copies only from the ring,
+    // slot by slot, and only the slots some lane copies in it (a batch has ~6
+    // rounds for ~14 pending tokens: full four-slot copies there were most of
+    // the pass's instructions)
+    l2_copy4<kMaskB>(ring, gw, cs, B0, p, cn, glob);
+    for (;;) {
+#ifdef RIO_FLSTAT
+      st_rounds++;
+#endif
+      wave_lds_sync();
+      int kf = -1, lf = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const unsigned long long m = __ballot(pend[k]);
+        if (kf < 0 && m) {
+          kf = k;
+          lf = __ffsll((long long)m) - 1;
+        }
+      }
+      if (kf < 0) break;
+      // R: the first pending match; every byte before it is final
+      const uint32_t R = (uint32_t)__builtin_amdgcn_readlane(pick4(p, kf), lf);
+      const uint32_t Df = kSym * (((uint32_t)__builtin_amdgcn_readlane(pick4(t, kf), lf) & 0xffffu) + 1);
+      const uint32_t Nf = (uint32_t)__builtin_amdgcn_readlane(pick4(len, kf), lf);
+      const bool run = Df < Nf;  // it overlaps its own output: the whole wave copies it
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint32_t n = 0;
+        if (pend[k]) {
+          const bool first = k == kf && l == lf;
+          if (first || cs[k] + len[k] <= B0 + R) {  // source ends at or before R
+            if (!first || !run) n = len[k];
+            pend[k] = false;
+          }
+        }
+        if (__ballot(n != 0)) l2_copy1_ring<kMaskB>(ring, cs[k], B0 + p[k], n);
+      }
+      if (run) {  // byte k of the run = byte (k mod dist) of the dist bytes before it (final)
+        const uint32_t xs = B0 + R - Df, xd = B0 + R;
+        for (uint32_t k0 = 0; k0 < Nf; k0 += 64) {
+          const uint32_t k = k0 + (uint32_t)l;
+          if (k < Nf) {
+            const uint32_t v = ring[(xs + umod_small(k, Df)) & kMaskB];
+            atomicOr(reinterpret_cast<uint32_t *>(ring) + (((xd + k) >> 2) & (kMaskB >> 2)), v << (8 * ((xd + k) & 3)));
+          }
+        }
+      }
+    }
+#ifdef RIO_FLSTAT
+    if (l == 0) atomicAdd(&st_ctl->flstat_esc, (unsigned long long)st_rounds);
+#endif
+    // complete 16 B units of the batch to HBM
+    const uint32_t e = B0 + total;
+    for (uint32_t x = (B0 & ~15u) + 16 * (uint32_t)l; x + 16 <= e; x += 1024)
+      *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kMaskB));
+    olen = e;
+    cur += take;
+  }
+  // the last partial unit (decode regions and segment scratch are 256-aligned and sized in 256 B steps)
+  if ((olen & 15) && l == 0) {
+    const uint32_t x = olen & ~15u;
+    *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kMaskB));
+  }
+  return olen;
+}
+
 __global__ void __launch_bounds__(64) RIO_LZ2_ATTR k_flate_lz2(DevBufs d, const unsigned long long *nblocks, int round) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[kL2Ring];
   const int l = lane_id();
@@ -1829,137 +2036,223 @@ __global__ void __launch_bounds__(64) RIO_LZ2_ATTR k_flate_lz2(DevBufs d, const 
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     FlState *sp = &d.fl[b];
     const uint32_t mode = uni(sp->mode);
-    if (uni(sp->round) != (uint32_t)round || mode == kFlError || mode == kFlSkip) continue;
-    uint32_t olen = (uint32_t)uni64(sp->olen2);
-    const uint32_t ntok = uni(sp->ntok);
+    if (uni(sp->round) != (uint32_t)round || mode == kFlError || mode == kFlSkip || mode == kFlSplit) continue;
     uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
-    const uint32_t *gw = reinterpret_cast<const uint32_t *>(out);
     const uint32_t *tk = d.tok + uni64(d.blk_c0[b]) * (uint64_t)kTokPerChunk;
-    wave_lds_sync();
-    if (olen > 0) {  // resumed: the history this block has already written, into the ring
-      const uint32_t h0 = (olen > kL2Near ? olen - kL2Near : 0u) & ~15u;
-      for (uint32_t x = h0 + 16 * (uint32_t)l; x < olen; x += 1024)
-        *reinterpret_cast<uint4 *>(ring + (x & kL2Mask)) = *reinterpret_cast<const uint4 *>(out + x);
-    }
-    uint32_t pre[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) pre[k] = (64u * k + (uint32_t)l < ntok) ? tk[64 * k + l] : 0u;
-    uint32_t cur = 0;
-    while (cur < ntok) {
-      uint32_t t[4], len[4], p[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) t[k] = pre[k];
-      // output positions (relative to the batch) and the tokens this batch takes
-      uint32_t carry = 0, take = 0, emax = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const bool valid = cur + 64u * k + (uint32_t)l < ntok;
-        len[k] = valid ? tok_len(t[k]) : 0u;
-        const uint32_t incl = wave_incl_sum_dpp(len[k]) + carry;
-        p[k] = incl - len[k];
-        const bool ok = valid && incl <= kL2Span;  // a prefix of the tokens (positions only grow)
-        take += (uint32_t)__popcll(__ballot(ok));
-        if (ok) emax = incl;
-        else len[k] = 0;
-        carry = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-      }
-      const uint32_t total = (uint32_t)__reduce_max_sync(~0ull, emax);
-      const uint32_t B0 = olen;
-      {  // zero the batch's ring bytes (their dwords; the history bytes of the first one stay)
-        uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
-        const uint32_t z0 = (B0 + 3) >> 2, z1 = (B0 + total + 3) >> 2;
-        for (uint32_t z = z0 + (uint32_t)l; z < z1; z += 64) rw[z & (kL2Mask >> 2)] = 0u;
-        if ((B0 & 3) && l == 0) atomicAnd(&rw[(B0 >> 2) & (kL2Mask >> 2)], (1u << (8 * (B0 & 3))) - 1);
-        wave_lds_sync();
-      }
-      const uint32_t near = B0 > kL2Near ? B0 - kL2Near : 0u;  // positions >= near: in the ring
-      // literals now; matches sourced before the batch now; the others pending
-      bool pend[4];
-      uint32_t cs[4], cn[4], glob = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        pend[k] = false;
-        cn[k] = 0;
-        const uint32_t n = len[k];
-        const uint32_t x = B0 + p[k];
-        cs[k] = x - ((t[k] & 0xffffu) + 1);
-        if (n == 0) continue;
-        if (!(t[k] >> 31)) {  // 1-3 literal bytes
-          uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
-          const uint32_t v = t[k] & 0xffffffu, o = 8 * (x & 3);
-          atomicOr(&rw[(x >> 2) & (kL2Mask >> 2)], v << o);
-          if ((x & 3) + n > 4) atomicOr(&rw[((x >> 2) + 1) & (kL2Mask >> 2)], v >> (32 - o));
-        } else if (cs[k] < near) {
-          cn[k] = n;
-          glob |= 1u << k;
-        } else if (cs[k] + n <= B0) {
-          cn[k] = n;
-        } else {
-          pend[k] = true;
-        }
-      }
-      // the next batch's tokens (issued before this batch's stores: see above)
-      const uint32_t nx = cur + take;
-#pragma unroll
-      for (int k = 0; k < 4; k++) pre[k] = (nx + 64u * k + (uint32_t)l < ntok) ? tk[nx + 64 * k + l] : 0u;
-      // the copies above, then the matches sourced inside the batch, in rounds
-      bool run = false;
-      uint32_t R = 0, Df = 0, Nf = 0;
-      for (;;) {
-        l2_copy4(ring, gw, cs, B0, p, cn, glob);
-        if (run) {  // byte k of the run = byte (k mod dist) of the dist bytes before it (final)
-          const uint32_t xs = B0 + R - Df, xd = B0 + R;
-          for (uint32_t k0 = 0; k0 < Nf; k0 += 64) {
-            const uint32_t k = k0 + (uint32_t)l;
-            if (k < Nf) {
-              const uint32_t v = ring[(xs + umod_small(k, Df)) & kL2Mask];
-              atomicOr(reinterpret_cast<uint32_t *>(ring) + (((xd + k) >> 2) & (kL2Mask >> 2)), v << (8 * ((xd + k) & 3)));
-            }
-          }
-        }
-        wave_lds_sync();
-        int kf = -1, lf = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const unsigned long long m = __ballot(pend[k]);
-          if (kf < 0 && m) {
-            kf = k;
-            lf = __ffsll((long long)m) - 1;
-          }
-        }
-        if (kf < 0) break;
-        // R: the first pending match; every byte before it is final
-        R = (uint32_t)__builtin_amdgcn_readlane(pick4(p, kf), lf);
-        Df = ((uint32_t)__builtin_amdgcn_readlane(pick4(t, kf), lf) & 0xffffu) + 1;
-        Nf = (uint32_t)__builtin_amdgcn_readlane(pick4(len, kf), lf);
-        run = Df < Nf;  // it overlaps its own output: the whole wave copies it
-        glob = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          cn[k] = 0;
-          if (!pend[k]) continue;
-          const bool first = k == kf && l == lf;
-          if (first || cs[k] + len[k] <= B0 + R) {  // source ends at or before R
-            if (!first || !run) cn[k] = len[k];
-            pend[k] = false;
-          }
-        }
-      }
-      // complete 16 B units of the batch to HBM
-      const uint32_t e = B0 + total;
-      for (uint32_t x = (B0 & ~15u) + 16 * (uint32_t)l; x + 16 <= e; x += 1024)
-        *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
-      olen = e;
-      cur += take;
-    }
-    // the last partial unit (the decode region is 256-aligned and sized in 256 B steps)
-    if ((olen & 15) && l == 0) {
-      const uint32_t x = olen & ~15u;
-      *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
-    }
+    const uint32_t olen = lz2_run<1, kL2Ring, kL2Span>(ring, out, tk, uni(sp->ntok), (uint32_t)uni64(sp->olen2));
     if (l == 0) {
       sp->olen2 = olen;
       if (mode == kFlDone) d.blk_out_len[b] = olen;
+    }
+  }
+}
+
+// ================================================================ split copy pass
+// A recordio block at the writer's default MaxItems (16,384 records: ~5 MB
+// decoded) is one copy-pass wave, so a span of such blocks keeps far fewer
+// waves in flight than the pass needs to hide its latency (C3 at MaxItems =
+// 16384: 2,158 waves for 5,120 slots). When a span has fewer blocks than
+// copy-pass slots, k_flate_plan cuts each block's token list at the Huffman
+// pass's checkpoints (the (token, output) position at each input chunk) into
+// up to kSegMax segments of >= kSegMin bytes. Segment 0 is copied as usual;
+// every later segment is copied at the same time without its history, as u16
+// symbols (lz2_run<2>): a byte whose value comes, through any chain of
+// matches, from the 32 KiB before the segment is the symbol 256 + its
+// position in that window. k_flate_segfix then resolves each block's segments
+// in order -- the window is final once the segment before it is -- by one
+// lookup per byte. Blocks the scratch cannot hold are copied whole as before.
+constexpr uint32_t kSegRing = 8192, kSegSpan = 3072;
+constexpr uint64_t kSegWin = 65536;  // the synthetic window's symbol bytes before a later segment's output
+
+__device__ __forceinline__ uint64_t seg_scratch_bytes(uint32_t o0, uint32_t o1) {
+  // window + the segment's symbols from its 16-aligned start to its 16-rounded end (+ slack unit), 256-aligned
+  return (kSegWin + 2ull * ((((uint64_t)o1 + 15) & ~15ull) - (o0 & ~15u)) + 32 + 255) & ~255ull;
+}
+
+// per block (thread): the split points and each later segment's scratch
+__global__ void k_flate_plan(DevBufs d, const unsigned long long *nblocks) {
+  const uint64_t nb = *nblocks;
+  if (nb == 0) return;
+  uint64_t want = (d.seg_items + nb - 1) / nb;
+  if (want > (uint64_t)kSegMax) want = kSegMax;
+  if (want < 2) return;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
+    FlState *sp = &d.fl[b];
+    if (sp->mode != kFlDone || sp->round != 0) continue;
+    const uint32_t olen = (uint32_t)sp->olen, ntok = sp->ntok;
+    uint32_t S = (uint32_t)want;
+    if (S > olen / kSegMin) S = olen / kSegMin;
+    if (S < 2) continue;
+    const uint64_t c0 = d.blk_c0[b];
+    const uint32_t K = (uint32_t)d.fl_ck[c0];  // checkpoints 1 .. K-1
+    uint32_t tb[kSegMax + 1], ob[kSegMax + 1], n = 1;
+    tb[0] = ob[0] = 0;
+    uint32_t k = 1;
+    for (uint32_t j = 1; j < S; j++) {
+      const uint32_t target = (uint32_t)((uint64_t)olen * j / S);
+      unsigned long long e = 0;
+      while (k < K) {
+        e = d.fl_ck[c0 + k];
+        if ((uint32_t)(e >> 32) >= target) break;
+        k++;
+      }
+      if (k >= K) break;
+      const uint32_t t = (uint32_t)e, o = (uint32_t)(e >> 32);
+      k++;
+      if (o - ob[n - 1] >= kSegMin / 2 && olen - o >= kSegMin / 2 && t > tb[n - 1] && t < ntok) {
+        tb[n] = t;
+        ob[n] = o;
+        n++;
+      }
+    }
+    if (n < 2) continue;
+    tb[n] = ntok;
+    ob[n] = olen;
+    uint64_t need = 0;
+    for (uint32_t j = 1; j < n; j++) need += seg_scratch_bytes(ob[j], ob[j + 1]);
+    const uint64_t off = atomicAdd(&d.ctl->seg_used, (unsigned long long)need);
+    if (!d.seg_scr || off + need > d.seg_cap) continue;  // copied whole (the host grows the scratch for next time)
+    unsigned long long *e = d.fl_seg + 2 * b * (uint64_t)kSegMax;
+    uint64_t so = off;
+    for (uint32_t j = 0; j < n; j++) {
+      e[2 * j] = (unsigned long long)tb[j] | ((unsigned long long)ob[j] << 32);
+      e[2 * j + 1] = j ? so : 0ull;
+      if (j) so += seg_scratch_bytes(ob[j], ob[j + 1]);
+    }
+    sp->stored_left = n;
+    sp->mode = kFlSplit;
+    atomicAdd(&d.ctl->seg_blocks, 1ull);
+  }
+}
+
+// segment j of a split block (read by k_flate_seg / k_flate_segfix)
+struct SegRef {
+  uint32_t t0, t1, o0, o1;
+  uint64_t scr;
+};
+__device__ __forceinline__ SegRef seg_ref(const DevBufs &d, uint64_t b, uint32_t j, uint32_t S, const FlState *sp) {
+  const unsigned long long *e = d.fl_seg + 2 * (b * (uint64_t)kSegMax + j);
+  SegRef r;
+  const uint64_t e0 = uni64(e[0]);
+  r.t0 = (uint32_t)e0;
+  r.o0 = (uint32_t)(e0 >> 32);
+  r.scr = uni64(e[1]);
+  if (j + 1 < S) {
+    const uint64_t e1 = uni64(e[2]);
+    r.t1 = (uint32_t)e1;
+    r.o1 = (uint32_t)(e1 >> 32);
+  } else {
+    r.t1 = uni(sp->ntok);
+    r.o1 = (uint32_t)uni64(sp->olen);
+  }
+  return r;
+}
+
+__global__ void __launch_bounds__(64) RIO_LZ2_ATTR k_flate_seg(DevBufs d, const unsigned long long *nblocks) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kSegRing];
+  const int l = lane_id();
+  const uint64_t nb = uni64(*nblocks);
+  for (uint64_t i = blockIdx.x; i < nb * kSegMax; i += gridDim.x) {
+    const uint64_t b = i % nb;
+    const uint32_t j = (uint32_t)(i / nb);  // every block's segment 0 first, then segment 1, ...
+    const FlState *sp = &d.fl[b];
+    if (uni(sp->mode) != kFlSplit) continue;
+    const uint32_t S = uni(sp->stored_left);
+    if (j >= S) continue;
+    const SegRef r = seg_ref(d, b, j, S, sp);
+    const uint32_t *tk = d.tok + uni64(d.blk_c0[b]) * (uint64_t)kTokPerChunk + r.t0;
+    if (j == 0) {
+      lz2_run<1, kSegRing, kSegSpan>(ring, d.dec + uni64(d.blk_dec_off[b]), tk, r.t1, 0);
+      continue;
+    }
+    // position p of the segment is symbol byte x = kSegWin + 2 (p - (o0 & ~15)):
+    // 16-aligned positions at 32-aligned symbol bytes. The window before it
+    // holds the symbols 256 + i for positions o0 - 32768 + i.
+    uint8_t *out = d.seg_scr + r.scr;
+    const uint32_t a = r.o0 & 15u;
+    const uint32_t x0 = (uint32_t)kSegWin + 2 * a;
+    for (uint32_t x = 16 * (uint32_t)l; x < x0; x += 1024) {
+      const uint32_t s0 = 256u + (x >> 1) - a;  // (below 2a: never read)
+      *reinterpret_cast<uint4 *>(out + x) = make_uint4(s0 | ((s0 + 1) << 16), (s0 + 2) | ((s0 + 3) << 16),
+                                                       (s0 + 4) | ((s0 + 5) << 16), (s0 + 6) | ((s0 + 7) << 16));
+    }
+    zmem_sync_dev();  // the window's stores complete before the copies read it back (agent-scope loads)
+    lz2_run<2, kSegRing, kSegSpan>(ring, out, tk, r.t1 - r.t0, x0, a);
+  }
+}
+
+// Resolve a split block's later segments in order (workgroup per block): the
+// final 32 KiB before segment j into LDS, then each 16 B output unit from its
+// 16 symbols (< 256: the byte; else the window's byte).
+constexpr int kSegFixThreads = 256;
+__global__ void __launch_bounds__(kSegFixThreads) k_flate_segfix(DevBufs d, const unsigned long long *nblocks) {
+  __shared__ uint32_t win[8192 + 4];
+  const uint64_t nb = *nblocks;
+  const int tid = (int)threadIdx.x;
+  const uint8_t *wb = reinterpret_cast<const uint8_t *>(win);
+  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    FlState *sp = &d.fl[b];
+    if (sp->mode != kFlSplit) continue;  // (the same for every thread of the workgroup)
+    const uint32_t S = sp->stored_left;
+    uint8_t *dec = d.dec + d.blk_dec_off[b];
+    for (uint32_t j = 1; j < S; j++) {
+      const unsigned long long *e = d.fl_seg + 2 * (b * (uint64_t)kSegMax + j);
+      const uint32_t o0 = (uint32_t)(e[0] >> 32);
+      const uint32_t o1 = j + 1 < S ? (uint32_t)(e[2] >> 32) : (uint32_t)sp->olen;
+      const uint8_t *scr = d.seg_scr + e[1] + kSegWin;
+      const uint32_t w0 = o0 - 32768u, sh = w0 & 3u;  // (o0 >= kSegMin / 2)
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(dec + (w0 - sh));
+      __syncthreads();  // the previous segment's window reads are done
+      for (int k = tid; k < 8193; k += kSegFixThreads)
+        win[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const uint32_t U0 = o0 & ~15u, nu = (o1 - U0 + 15) >> 4;
+      for (uint32_t u = (uint32_t)tid; u < nu; u += kSegFixThreads) {
+        const uint32_t U = U0 + 16 * u;
+        const uint4 s0 = *reinterpret_cast<const uint4 *>(scr + 32 * (size_t)u);
+        const uint4 s1 = *reinterpret_cast<const uint4 *>(scr + 32 * (size_t)u + 16);
+        const uint32_t sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        uint32_t ov[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          uint32_t w = 0;
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const uint32_t pair = sv[2 * q + h];
+#pragma unroll
+            for (int m = 0; m < 2; m++) {
+              const uint32_t v = (pair >> (16 * m)) & 0xffffu;
+              const uint32_t byte = v < 256u ? v : (uint32_t)wb[sh + (v - 256u)];
+              w |= byte << (8 * (2 * h + m));
+            }
+          }
+          ov[q] = w;
+        }
+        uint4 *dp = reinterpret_cast<uint4 *>(dec + U);
+        if (U < o0 || U + 16 > o1) {  // bytes of the neighbouring segments stay
+          const uint32_t *cw = reinterpret_cast<const uint32_t *>(dp);
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const uint32_t cur = __hip_atomic_load(cw + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t keep = 0;
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+              const uint32_t p = U + 4 * q + m;
+              if (p < o0 || p >= o1) keep |= 0xffu << (8 * m);
+            }
+            ov[q] = (ov[q] & ~keep) | (cur & keep);
+          }
+        }
+        *dp = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+      }
+      __threadfence();  // this segment's bytes visible before the next window is read
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t olen = (uint32_t)sp->olen;
+      sp->olen2 = olen;
+      d.blk_out_len[b] = olen;
+      sp->mode = kFlDone;
     }
   }
 }
@@ -2008,6 +2301,14 @@ __global__ void __launch_bounds__(64) k_inflate_exact(const uint8_t *__restrict_
   }
 }
 
+uint64_t flate_seg_items(int ncu) { return (uint64_t)(ncu > 0 ? ncu : 256) * kL2Waves; }
+
+static unsigned grid256(uint64_t n) {
+  uint64_t g = (n + 255) / 256;
+  if (g > 1024) g = 1024;
+  return (unsigned)(g ? g : 1);
+}
+
 void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
                     uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st) {
   (void)hipMemsetAsync(d.fl_more, 0, sizeof(unsigned long long) * rounds, st);
@@ -2031,6 +2332,16 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
     if (gs < 1) gs = 1;
     hipLaunchKernelGGL(k_flate_sync, dim3((unsigned)gs), dim3(64), 0, st, span, d, nblocks, nchunks, dec_cap);
   }
+#ifdef RIO_FLSTAT
+  {
+    Ctl *p = d.ctl;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(st_ctl), &p, sizeof(p), 0, hipMemcpyHostToDevice, st);
+  }
+#endif
+  // few blocks: the copy pass split into segments (k_flate_plan marks the blocks; the
+  // rounds below skip them)
+  const bool split = kFlateSync && d.seg_items > 0;
+  if (split) hipLaunchKernelGGL(k_flate_plan, dim3(grid256(max_blocks)), dim3(256), 0, st, d, nblocks);
   for (int r = 0; r < rounds; r++) {
     hipLaunchKernelGGL(k_flate_tok, dim3((unsigned)g1), dim3(64), 0, st, span, d, nblocks, nchunks,
                        dec_cap, r, (int)(r == rounds - 1));
@@ -2038,6 +2349,14 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
       hipLaunchKernelGGL(k_flate_lz2, dim3((unsigned)g3), dim3(64), 0, st, d, nblocks, r);
     else
       hipLaunchKernelGGL(k_flate_lz, dim3((unsigned)g2), dim3(64), 0, st, d, nblocks, r);
+  }
+  if (split) {
+    uint64_t gs = max_blocks * kSegMax;
+    if (gs > (uint64_t)ncu * kL2Waves) gs = (uint64_t)ncu * kL2Waves;
+    hipLaunchKernelGGL(k_flate_seg, dim3((unsigned)(gs ? gs : 1)), dim3(64), 0, st, d, nblocks);
+    uint64_t gf = max_blocks;
+    if (gf > (uint64_t)ncu * 4) gf = (uint64_t)ncu * 4;
+    hipLaunchKernelGGL(k_flate_segfix, dim3((unsigned)(gf ? gf : 1)), dim3(kSegFixThreads), 0, st, d, nblocks);
   }
   uint64_t ge = (max_blocks + 63) / 64;
   if (ge > 1024) ge = 1024;

@@ -298,6 +298,8 @@ __global__ void k_reset(Ctl *ctl, unsigned long long *nblocks) {
   else if (t < 14) ctl->zprof[t - 10] = 0;
   else if (t == 14) ctl->zjob_n = 0;
   else if (t < 17) nblocks[t - 15] = 0;
+  else if (t == 17) ctl->seg_used = 0;
+  else if (t == 18) ctl->seg_blocks = 0;
 }
 
 void launch_reset(const DevBufs &d, unsigned long long *nblocks_dev, hipStream_t st) {

@@ -32,6 +32,8 @@ __device__ __forceinline__ uint32_t pick4(const uint32_t (&a)[4], int k) {
 // destination dwords (an LDS atomic, in any order) -- no byte stores, no races
 // with the neighbours sharing its end dwords. Source dwords are read aligned
 // and funnel-shifted; each step issues every slot's loads before using any.
+// kMask: the ring's size - 1 (k_flate_seg's rings are 8 KiB).
+template <uint32_t kMask = kL2Mask>
 __device__ __forceinline__ void l2_copy4(uint8_t *ring, const uint32_t *gw, const uint32_t (&s)[4], uint32_t B0,
                                          const uint32_t (&p)[4], const uint32_t (&n)[4], uint32_t glob,
                                          const uint32_t *gl = nullptr, uint32_t litm = 0) {
@@ -64,7 +66,7 @@ __device__ __forceinline__ void l2_copy4(uint8_t *ring, const uint32_t *gw, cons
                                       __HIP_MEMORY_SCOPE_AGENT);
       } else if (act) {
 #pragma unroll
-        for (int i = 0; i < 5; i++) w[k][i] = rw[(q + i) & (kL2Mask >> 2)];
+        for (int i = 0; i < 5; i++) w[k][i] = rw[(q + i) & (kMask >> 2)];
       }
     }
     if (!__builtin_amdgcn_ballot_w64(any)) break;
@@ -81,12 +83,38 @@ __device__ __forceinline__ void l2_copy4(uint8_t *ring, const uint32_t *gw, cons
           const uint32_t lo = t > x0 ? t - x0 : 0u;                         // 0..3
           const uint32_t hi = t + n[k] < x0 + 4 ? t + n[k] - x0 : 4u;      // 1..4
           const uint32_t m = (0xffffffffu << (8 * lo)) & (0xffffffffu >> (8 * (4 - hi)));
-          atomicOr(&rw[Dj & (kL2Mask >> 2)], v & m);
+          atomicOr(&rw[Dj & (kMask >> 2)], v & m);
         }
       }
     }
   }
 }
 
+// One copy per lane, ring to ring (the pending rounds: sources inside the
+// batch, every byte final by then): n bytes from position s to t (t - s >= n),
+// the same aligned reads, funnel shifts and OR-writes as l2_copy4.
+template <uint32_t kMask = kL2Mask>
+__device__ __forceinline__ void l2_copy1_ring(uint8_t *ring, uint32_t s, uint32_t t, uint32_t n) {
+  uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
+  const uint32_t d0 = t >> 2, d1 = n ? (t + n + 3) >> 2 : d0, sh = 8 * ((s - t) & 3);
+  const uint32_t q0 = (s >> 2) - ((s & 3) < (t & 3) ? 1u : 0u);
+  for (uint32_t D = 0; __builtin_amdgcn_ballot_w64(d0 + D < d1); D += 4) {
+    uint32_t w[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) w[i] = rw[(q0 + D + i) & (kMask >> 2)];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t Dj = d0 + D + j;
+      if (Dj < d1) {
+        const uint32_t v = __builtin_amdgcn_alignbit(w[j + 1], w[j], sh);
+        const uint32_t x0 = 4 * Dj;
+        const uint32_t lo = t > x0 ? t - x0 : 0u;
+        const uint32_t hi = t + n < x0 + 4 ? t + n - x0 : 4u;
+        const uint32_t m = (0xffffffffu << (8 * lo)) & (0xffffffffu >> (8 * (4 - hi)));
+        atomicOr(&rw[Dj & (kMask >> 2)], v & m);
+      }
+    }
+  }
+}
 
 }  // namespace rio

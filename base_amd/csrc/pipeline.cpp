@@ -118,6 +118,8 @@ struct rio_ctx {
   bool last_had_dec = false;
   int ev_parse0 = kEvParse0, ev_crc0 = kEvCrc0;  // the events the last run's parse / CRC stages start at
   bool item_end_mode = false;  // RIO_CFG_ITEM_END: device results carry item_end (cumSize)
+  bool flate_split = true;     // not RIO_CFG_FLATE_NO_SPLIT
+  uint64_t seg_want = 0;       // split copy pass: scratch the last flate run asked for
   bool last_cmp = false;  // the last host result's records are the compacted blocks (d.cmp)
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
   uint64_t side_cap = 0, item_cap = 0, dec_cap = 0;
@@ -220,7 +222,7 @@ static void free_all(rio_ctx *c) {
   DevBufs &d = c->d;
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.blk_data, d.blk_file_off, d.blk_seg, d.cmp, d.item_off, d.item_len, d.side,
-                d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
+                d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.fl_ck, d.fl_seg, d.seg_scr, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len,
                 c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan, c->d_seg, c->d_chain[0], c->d_chain[1], c->d_chain_meta};
   for (void *p : ps)
@@ -249,6 +251,7 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   c->d.tok_limit = cfg ? cfg->flate_tok_limit : 0;
   c->d.fl_grid = cfg ? cfg->flate_grid : 0;
   c->item_end_mode = cfg && (cfg->flags & RIO_CFG_ITEM_END);
+  c->flate_split = !(cfg && (cfg->flags & RIO_CFG_FLATE_NO_SPLIT));
   uint64_t span = (cfg && cfg->max_span_bytes) ? cfg->max_span_bytes : (256ull << 20);
   span = (span + kChunk - 1) / kChunk * kChunk;
   c->max_span = span;
@@ -396,6 +399,38 @@ static int ensure_tok(rio_ctx *c, uint64_t nchunks, uint64_t per_chunk) {
   return 0;
 }
 
+// flate split copy pass: checkpoints per chunk, segment table per block, and
+// the later segments' scratch -- grown to what the last run asked for (a
+// block the scratch cannot hold is copied whole meanwhile), at most 6x the
+// span or 2x the decode regions
+static int ensure_split(rio_ctx *c, uint64_t nchunks) {
+  DevBufs &d = c->d;
+  if (!d.fl_ck || c->max_chunks + 1 > d.fl_ck_n) {
+    if (dalloc(&d.fl_ck, c->max_chunks + 1) || dalloc(&d.fl_seg, 2 * (uint64_t)kSegMax * (c->max_blocks + 1)))
+      return -1;
+    d.fl_ck_n = c->max_chunks + 1;
+  }
+  d.seg_items = c->flate_split ? flate_seg_items(c->ncu) : 0;
+  uint64_t want = c->seg_want;
+  uint64_t lim = 6 * nchunks * (uint64_t)kChunk;  // (or twice the decode regions: highly compressible blocks)
+  if (lim < 2 * c->dec_cap) lim = 2 * c->dec_cap;
+  if (want > lim) want = lim;
+  if (d.seg_items && want > d.seg_cap) {
+    want += want / 8;
+    if (d.seg_scr) hipFree(d.seg_scr);
+    d.seg_scr = nullptr;
+    d.seg_cap = 0;
+    if (hipMalloc((void **)&d.seg_scr, want) == hipSuccess) d.seg_cap = want;
+    else (void)hipGetLastError();  // no scratch: blocks are copied whole
+  }
+  return 0;
+}
+
+// the scratch the last flate run's split asked for (read from its control block)
+static void note_split(rio_ctx *c) {
+  if (c->h_ctl->seg_used > c->d.seg_cap && c->h_ctl->seg_used > c->seg_want) c->seg_want = c->h_ctl->seg_used;
+}
+
 // zstd job list: kZJobsPerChunk per chunk of the span
 static int ensure_zjob(rio_ctx *c, uint64_t nchunks) {
   const uint64_t need = nchunks * (uint64_t)kZJobsPerChunk + 64;
@@ -464,7 +499,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     // decode regions: factor x the compressed bytes per block (+4 KiB each)
     if (ensure_dec(c, (uint64_t)c->dec_factor * nchunks * kChunk + nchunks * 4352ull)) return -1;
     // flate tokens / flattened zstd blocks
-    if (codec == RIO_CODEC_FLATE && ensure_tok(c, nchunks, kTokPerChunk)) return -1;
+    if (codec == RIO_CODEC_FLATE && (ensure_tok(c, nchunks, kTokPerChunk) || ensure_split(c, nchunks))) return -1;
     if (codec == RIO_CODEC_ZSTD && ensure_tok(c, nchunks, kZTokPerChunk)) return -1;
     if (codec == RIO_CODEC_ZSTD && (ensure_zlit(c) || ensure_zjob(c, nchunks))) return -1;
     launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
@@ -683,6 +718,7 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
       return -1;
     HIP_OK(hipMemcpyAsync(c->h_ctl, c->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipStreamSynchronize(c->st));
+    note_split(c);
     if (c->h_ctl->out_overflow == 0) break;
     if (grow_for_overflow(c, codec)) return -1;
     // decode regions: blocks that overflowed theirs carry their exact size (blk_need)
@@ -922,11 +958,18 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
   HIP_OK(hipSetDevice(ctx->device));
   HIP_OK(hipMemcpyAsync(ctx->h_ctl, ctx->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->st));
   HIP_OK(hipStreamSynchronize(ctx->st));
+  note_split(ctx);
 #ifdef RIO_ZPROF  // profiling builds: where the zstd entropy pass spends its cycles
   if (ctx->last_codec == RIO_CODEC_ZSTD)
     fprintf(stderr, "rio: zstd blocks on the serial path: %llu; entropy-pass cycles lit %llu tables %llu seq %llu block %llu\n",
             (unsigned long long)ctx->h_ctl->pad[1], ctx->h_ctl->zprof[0], ctx->h_ctl->zprof[1], ctx->h_ctl->zprof[2],
             ctx->h_ctl->zprof[3]);
+#endif
+#ifdef RIO_FLSTAT  // statistics builds: the flate copy pass's batches
+  if (ctx->last_codec == RIO_CODEC_FLATE)
+    fprintf(stderr, "rio flstat: batches %llu tokens %llu pending %llu hbm-sourced %llu rounds %llu split-blocks %llu\n",
+            ctx->h_ctl->zprof[0], ctx->h_ctl->zprof[1], ctx->h_ctl->zprof[2], ctx->h_ctl->zprof[3],
+            ctx->h_ctl->flstat_esc, ctx->h_ctl->seg_blocks);
 #endif
   float ms = 0;
   hipEventElapsedTime(&ms, ctx->ev[kEvStart], ctx->ev[kEvEnd]);
@@ -953,6 +996,8 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
   }
   return 0;
 }
+
+extern "C" uint64_t rio_flate_split_blocks(rio_ctx *ctx) { return ctx ? ctx->h_ctl->seg_blocks : 0; }
 
 extern "C" int rio_stage_times(rio_ctx *ctx, float *ms, int n) {
   if (!ctx || !ms || n <= 0) return 0;
@@ -1021,6 +1066,7 @@ static int decode_raw(rio_ctx *c, const uint8_t *const *payloads, const uint32_t
     if (enqueue(c, c->d_span, nch, UINT64_MAX, 1, 0, codec, kModeRaw, false, attempt)) return -1;
     HIP_OK(hipMemcpyAsync(c->h_ctl, c->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipStreamSynchronize(c->st));
+    note_split(c);
     const unsigned long long ov = c->h_ctl->out_overflow;
     if (ov == 0) break;
     if ((ov & 0x40) && ensure_dec(c, c->h_ctl->dec_need)) return -1;

@@ -99,6 +99,8 @@ struct Ctl {
   unsigned long long n_retry;                     // blocks k_parse_lean left to k_parse (listed in blk_coff)
   unsigned long long zprof[4];                    // (RIO_ZPROF builds: zstd entropy-pass cycles per phase)
   unsigned long long zjob_n;                      // zstd jobs made (k_zstd_ent)
+  unsigned long long seg_used;                    // flate split copy: scratch bytes the blocks asked for (k_flate_plan)
+  unsigned long long seg_blocks;                  // flate split copy: blocks split
 };
 
 constexpr unsigned long long kNone = ~0ull;
@@ -129,6 +131,7 @@ enum FlMode : uint32_t {
   kFlDone = 4,     // final block decoded
   kFlError = 5,    // decode failed (k_inflate_exact classifies it)
   kFlSkip = 6,     // not decoded (incomplete block, header magic, region overflow)
+  kFlSplit = 7,    // tokens complete, copy pass split into segments (k_flate_seg; stored_left = segments)
 };
 struct FlState {
   unsigned long long bitpos;  // logical bit offset of the next symbol / header
@@ -143,6 +146,10 @@ constexpr int kFlRounds = 6;          // Huffman/copy rounds launched per span
 constexpr int kTokPerChunk = kChunk;  // token region: 32,768 u32 per chunk of the block
 constexpr int kZTokPerChunk = 4 * kTokPerChunk;  // zstd scratch: input copy, literals, entries | jobs
 constexpr int kZJobsPerChunk = 16;               // zstd job list capacity (a block past it takes the serial path)
+// Split copy pass (codec_flate.hip k_flate_plan / k_flate_seg / k_flate_segfix):
+// segments per block at most, and the shortest segment
+constexpr int kSegMax = 8;
+constexpr uint32_t kSegMin = 65536;
 
 // Device arrays of one context (capacities fixed at rio_open, grown on demand).
 struct DevBufs {
@@ -186,6 +193,13 @@ struct DevBufs {
   uint64_t tok_limit;            // tokens per block and round (0: the whole region; rio_config.flate_tok_limit)
   uint64_t fl_grid;              // Huffman-pass workgroups (0: all resident; rio_config.flate_grid)
   unsigned long long *fl_more;   // per round: blocks whose token region filled (kFlRounds)
+  unsigned long long *fl_ck;     // per chunk: the Huffman pass's (ntok | olen << 32) at the block's input
+                                 // chunk k (entry c0 + k; entry c0 = entries written) -- split points
+  unsigned long long *fl_seg;    // per block x kSegMax: (tok | out << 32, scratch offset) of each segment
+  uint8_t *seg_scr;              // later segments' u16 symbols (0: no split)
+  uint64_t seg_cap;              // bytes at seg_scr
+  uint64_t seg_items;            // copy-pass waves the split aims to fill (ncu x kL2Waves; 0: no split)
+  uint64_t fl_ck_n;              // entries at fl_ck
   uint8_t *zlit;                 // zstd: one literal buffer per decoder wave (codec_zstd.hip)
   unsigned long long *zjob;      // zstd: job header offsets (bytes from tok)
   uint64_t zjob_cap;
@@ -201,6 +215,7 @@ struct DevBufs {
 // zstd decoder sizing (codec_zstd.hip)
 uint64_t zstd_grid(int ncu);             // decoder waves launched
 uint64_t zstd_lit_bytes(uint64_t grid);  // literal buffers for that many waves
+uint64_t flate_seg_items(int ncu);       // copy-pass slots the split copy pass fills
 
 // Kernel argument blocks (kernels.hip, codec.hip; filled by pipeline.cpp).
 struct ParseArgs {

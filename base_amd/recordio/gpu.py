@@ -52,6 +52,7 @@ class RioError(ctypes.Structure):
 
 
 RIO_CFG_ITEM_END = 1  # device results carry item_end (cumSize) + block_data / block_first_off
+RIO_CFG_FLATE_NO_SPLIT = 2  # never split a flate block's copy pass (tuning / tests)
 
 
 class RioConfig(ctypes.Structure):
@@ -103,7 +104,7 @@ EXPORTS = [
     "rio_scanner_header_len", "rio_scanner_header_kv", "rio_scanner_trailer", "rio_scanner_seek",
     "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish", "rio_scanner_gather",
     "rio_memory_reader", "rio_scan_v1_span", "rio_encode", "rio_encode_device", "rio_build_id",
-    "rio_scan_device_segments_async",
+    "rio_scan_device_segments_async", "rio_flate_split_blocks",
 ]
 
 _lib = None
@@ -122,6 +123,8 @@ def load(path: str = LIB_PATH):
         B.check_lib(path)  # refuses a library not built from this tree's sources
         L = ctypes.CDLL(path)
         L.rio_build_id.restype = ctypes.c_char_p
+        L.rio_flate_split_blocks.restype = ctypes.c_uint64
+        L.rio_flate_split_blocks.argtypes = [ctypes.c_void_p]
         L.rio_scan_device_segments_async.restype = ctypes.c_int
         L.rio_scan_device_segments_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
@@ -208,10 +211,11 @@ class Context:
     """One rio_ctx: a device, a HIP stream and fixed-capacity buffers."""
 
     def __init__(self, device: int = 0, max_span_bytes: int = 0, max_out_bytes: int = 0, max_items: int = 0,
-                 item_end: bool = False, flate_tok_limit: int = 0, flate_grid: int = 0):
+                 item_end: bool = False, flate_tok_limit: int = 0, flate_grid: int = 0,
+                 flate_split: bool = True):
         self.L = load()
-        cfg = RioConfig(device, RIO_CFG_ITEM_END if item_end else 0, max_span_bytes, max_out_bytes, max_items,
-                        flate_tok_limit, flate_grid)
+        flags = (RIO_CFG_ITEM_END if item_end else 0) | (0 if flate_split else RIO_CFG_FLATE_NO_SPLIT)
+        cfg = RioConfig(device, flags, max_span_bytes, max_out_bytes, max_items, flate_tok_limit, flate_grid)
         self.item_end = item_end
         self.h = self.L.rio_open(ctypes.byref(cfg))
         if not self.h:
@@ -324,6 +328,10 @@ class Context:
         if self.L.rio_sync(self.h, ctypes.byref(out)) != 0:
             raise RuntimeError("rio_sync: " + self.L.rio_last_error().decode())
         return out
+
+    def flate_split_blocks(self) -> int:
+        """Flate blocks of the last completed run copied as segments (split copy pass)."""
+        return int(self.L.rio_flate_split_blocks(self.h))
 
     def stage_times(self):
         """Device ms of the last run: [parse path, codec, k_crc, chunk meta+scans, total]."""

@@ -110,6 +110,9 @@ typedef struct rio_error {
                                 cumSize-shaped item output: rio_batch.item_end,
                                 block_data, block_first_off instead of item_off /
                                 item_len (8 B per item instead of 16) */
+#define RIO_CFG_FLATE_NO_SPLIT 2u  /* tuning / test: never split a flate block's copy pass into
+                                     * segments (by default a span of few large blocks is split,
+                                     * see DESIGN.md "split copy pass") */
 
 typedef struct rio_config {
     int32_t device;             /* HIP device ordinal */
@@ -263,6 +266,12 @@ int rio_scan_device_segments_async(rio_ctx *ctx, const void *dev_span, uint64_t 
  * [3] chunk headers + chunk scans, [4] the whole pipeline.
  * Returns the number of stages written. */
 int rio_stage_times(rio_ctx *ctx, float *ms, int n);
+
+/* Flate blocks of the last completed run whose copy pass was split into
+ * segments (DESIGN.md "split copy pass"; 0 with RIO_CFG_FLATE_NO_SPLIT, for
+ * many small blocks, or before the split scratch has been sized). For tests
+ * and measurement; no reference counterpart. */
+uint64_t rio_flate_split_blocks(rio_ctx *ctx);
 
 /* TransformFunc analogue (recordio.go:12): untransform one block given its
  * chunk payload views (in order, any lengths; their concatenation is the

@@ -21,6 +21,12 @@ def pytest_configure(config):
         import torch  # noqa: F401
 
 
+def pytest_collection_modifyitems(config, items):
+    # the same when GPU test files are named without -m gpu
+    if any(it.get_closest_marker("gpu") for it in items) and "not gpu" not in (config.option.markexpr or ""):
+        import torch  # noqa: F401
+
+
 @pytest.fixture(scope="session")
 def oracle():
     """The CPU restatement (test infrastructure only)."""

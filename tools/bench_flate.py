@@ -22,7 +22,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, warmup, device=0, check=True):
+def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, warmup, device=0, check=True,
+            flate_split=True):
     """One compressed workload on cuda:`device`: the base file `data` copied to
     HBM, its body replicated `replicas` times; one step = the scan pipeline over
     the whole device-resident span. Parity: the base file's items (device path)
@@ -53,7 +54,8 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
         ctx1.close()
 
     span_len = total - CH
-    ctx = gpu.Context(device, max_span_bytes=total, max_items=nrec * replicas + 1024, item_end=True)
+    ctx = gpu.Context(device, max_span_bytes=total, max_items=nrec * replicas + 1024, item_end=True,
+                      flate_split=flate_split)
     ptr = dev.data_ptr() + CH
 
     def step():
@@ -83,6 +85,7 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
         timed_parity = {"ok": bool(chk["ok"]), "items_checked": chk["items_checked"],
                         "bytes_checked": chk["bytes_checked"]}
     out_bytes = rec_bytes * replicas
+    split_blocks = ctx.flate_split_blocks() if codec == gpu.RIO_CODEC_FLATE else 0
     ctx.close()
     del dev
     torch.cuda.empty_cache()
@@ -97,7 +100,8 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
                    "base_record_bytes": rec_bytes, "replicas": replicas, "span_bytes": span_len,
                    "records_bytes": out_bytes},
         "parity": parity and bool(timed_parity and timed_parity["ok"]),
-        "parity_timed_output": timed_parity}
+        "parity_timed_output": timed_parity,
+        "split_blocks": split_blocks}
 
 
 TARGET_RECORD_BYTES = 10 << 30  # configs[2]: 10 GiB of uncompressed records
@@ -108,7 +112,8 @@ def replicas_for(rec_bytes: int) -> int:
     return -(-TARGET_RECORD_BYTES // rec_bytes)
 
 
-def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0):
+def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0,
+           flate_split=True):
     """The C3 workload on cuda:`device` (replicas=0: enough for 10 GiB of records);
     returns the measurement dict (no print). cpu_s > 0 adds the one-core and
     all-core CPU baselines (zlib inflate) on the base file."""
@@ -128,7 +133,8 @@ def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0
     if replicas <= 0:
         replicas = replicas_for(rec_bytes)
     res = measure(data, nrec, rec_bytes, want, gpu.RIO_CODEC_FLATE,
-                  "C3-like flate FASTQ, %d records/block" % per_block, replicas, steps, warmup, device, check)
+                  "C3-like flate FASTQ, %d records/block" % per_block, replicas, steps, warmup, device, check,
+                  flate_split)
     res["config"]["gen_s"] = round(gen_s, 1)
     if cpu_s > 0:
         import cpu_base
@@ -145,9 +151,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--per-block", type=int, default=1024)
     ap.add_argument("--cpu-s", type=float, default=0.0)
+    ap.add_argument("--no-split", action="store_true", help="copy every block whole (RIO_CFG_FLATE_NO_SPLIT)")
     args = ap.parse_args()
     print(json.dumps(run_c3(args.base_mib, args.replicas, args.steps, args.warmup, args.per_block,
-                            cpu_s=args.cpu_s)), flush=True)
+                            cpu_s=args.cpu_s, flate_split=not args.no_split)), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Split copy pass session: its tests, the flate suites, C3 at MaxItems 16384
+# with and without the split, C3 at 1024 per block. Stops at a crash / timeout.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 tmo=$2
+  shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$tmo" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 4 "gpurun_out/$name.log" | cut -c1-1200
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: $name exited with $rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case "$s" in
+    tests) step split_tests 600 python -u -m pytest tests/test_flate_split_gpu.py -x -v --timeout 150 --timeout-method thread ;;
+    flate) step flate_tests 600 python -u -m pytest tests/test_flate_gpu.py tests/test_headline_gpu.py tests/test_chain_gpu.py -x -v --timeout 150 --timeout-method thread ;;
+    all) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread ;;
+    b16k) step b16k 400 python3 tools/bench_flate.py --per-block 16384 --steps 3 ;;
+    b16k_ns) step b16k_ns 400 python3 tools/bench_flate.py --per-block 16384 --steps 3 --no-split ;;
+    b1k) step b1k 400 python3 tools/bench_flate.py --steps 3 ;;
+    prof16k) step prof16k 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof16k -o run -- \
+        python3 tools/bench_flate.py --per-block 16384 --steps 2 ;;
+    stat1k) RIO_GPU_LIB=exp_lib/flstat/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_FLSTAT" RIO_BUILD_DIR=exp_lib/flstat \
+        step stat1k 300 python3 tools/bench_flate.py --steps 1 --warmup 0 --replicas 4 ;;
+    stat16k) RIO_GPU_LIB=exp_lib/flstat/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_FLSTAT" RIO_BUILD_DIR=exp_lib/flstat \
+        step stat16k 300 python3 tools/bench_flate.py --steps 1 --warmup 1 --replicas 4 --per-block 16384 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
