@@ -484,10 +484,13 @@ constexpr uint32_t kEobExtra = 7;
 enum : int { kTabLit = 0, kTabDist = 1, kTabClen = 2 };
 enum : int { kTokDone = 0, kTokYield = -1 };
 #ifndef RIO_LIT_ROOT
-#define RIO_LIT_ROOT 9
+#define RIO_LIT_ROOT 10  // (round 3: 9 -> 10, C3 49.8 -> 51.2 GiB/s A/B; 11 and 12, or a 9-bit distance root: ~40)
 #endif
 constexpr int kTokLitRoot = RIO_LIT_ROOT;  // literal/length root table bits
-constexpr int kTokDistRoot = 8;
+#ifndef RIO_DIST_ROOT
+#define RIO_DIST_ROOT 8
+#endif
+constexpr int kTokDistRoot = RIO_DIST_ROOT;  // distance root table bits
 #ifndef RIO_FLATE_SYNC
 #define RIO_FLATE_SYNC 1
 #endif
@@ -1333,18 +1336,44 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
 // size beyond this kernel's 32-bit positions -- declines the block to
 // k_flate_tok; corrupt or oversized streams go to k_inflate_exact as there.
 constexpr uint32_t kSyncSeg = 1024;                       // bits per lane per round
-constexpr uint32_t kSyncBits = 64 * kSyncSeg;             // bits per round
-constexpr uint32_t kSyncWinDw = kSyncBits / 32 + 32;      // staged dwords (+ run-out margin)
+constexpr uint32_t kSyncBits = 64 * kSyncSeg;             // bits per round and wave
 constexpr int kSyncIters = 8;
 #ifndef RIO_SYNC_WAVES
 #define RIO_SYNC_WAVES 12
 #endif
-constexpr int kSyncWaves = RIO_SYNC_WAVES;                 // per CU (launch sizing)
+constexpr int kSyncWaves = RIO_SYNC_WAVES;                 // per CU (launch sizing, one wave per block)
+// Ablation builds (-DRIO_SYNC_WIDE=1): spans of fewer blocks than one-wave
+// slots decoded with kSyncW waves per block (128 segments per round). Measured
+// slower for C3 at MaxItems = 16384 (2,158 blocks): 51.3 ms at 2 waves, 58.1 at
+// 4, against 50.0 at one -- only 1,536 two-wave blocks are resident at a time
+// (registers), and the barriers cost more than the extra segments gain.
+#ifndef RIO_SYNC_WIDE
+#define RIO_SYNC_WIDE 0
+#endif
+constexpr int kSyncW = 2;
 
-struct SyncLds {
+template <int kW>
+constexpr uint32_t sync_win_dw() { return kW * kSyncBits / 32 + 32; }  // staged dwords (+ run-out margin)
+
+// cross-wave exchange of a kW-wave block (parity-double-buffered where it is
+// written every convergence iteration)
+template <int kW>
+struct SyncX {
+  uint32_t eob[2][kW], ex63[2][kW], need[2][kW];
+  uint32_t tsum[kW], osum[kW], bad[kW], fall[kW];
+  uint32_t exk;
+  uint32_t h_act, h_fin, h_res, h_decl, h_ntok, h_olen;  // the header wave's results
+  unsigned long long h_bit;
+};
+template <>
+struct SyncX<1> {};
+
+template <int kW>
+struct SyncLdsT {
   StreamLds T;  // the DEFLATE block's tables (ring / tbuf unused)
   WaveLds W;
-  uint32_t win[kSyncWinDw + kSyncWinDw / 32 + 1];  // skewed: see sync_at
+  uint32_t win[sync_win_dw<kW>() + sync_win_dw<kW>() / 32 + 1];  // skewed: see sync_at
+  SyncX<kW> x;
 };
 
 // 32 bits of the staged window at relative bit r
@@ -1358,12 +1387,122 @@ __device__ __forceinline__ uint32_t sync_bits(const uint32_t *win, uint32_t r) {
 }
 
 enum : uint32_t { kSyEob = 1, kSyBad = 2, kSyHist = 4, kSyFull = 8 };
+// Literals per token in this pass (ablation builds: -DRIO_SYNC_MERGE=3): 3 cut
+// C3's tokens by 8 % without a measurable gain (50.4 against 51.0 GiB/s).
+#ifndef RIO_SYNC_MERGE
+#define RIO_SYNC_MERGE 1
+#endif
+constexpr uint32_t kSyncMerge = RIO_SYNC_MERGE;
 
 // Decode tokens from relative bit r while r < end (or to the end-of-block
 // symbol). Counting mode skips an undecodable code by one bit (a lane off the
 // true chain); writing mode stops there. Returns the exit position.
+// Consecutive literals may share a token (kSyncMerge, up to 3 bytes as stored
+// blocks' tokens): both modes group them alike, so the counts place the
+// written tokens.
+// Bits come through a per-lane 64-bit buffer (bits [r, r + nb) of the window),
+// topped up to > 32 bits before the literal/length code (<= 15 + 5 bits) and
+// before the distance code (<= 15 + 13): the next window dword is loaded one
+// top-up ahead, so a symbol's dependent LDS reads are its table lookups only.
 template <bool kWrite>
 __device__ __forceinline__ uint32_t sync_decode(const StreamLds &T, const uint32_t *win, uint32_t r, uint32_t end,
+                                                uint32_t lim, uint32_t &ntok, uint32_t &nout, uint32_t &flags,
+                                                uint32_t *tk, uint32_t olen0, uint32_t cap) {
+  uint32_t lacc = 0, lcnt = 0;  // the literal run not yet written
+  auto flush = [&]() {
+    if (lcnt) {
+      if (kWrite) tk[ntok] = lacc | (lcnt << 24);
+      ntok++;
+      lacc = lcnt = 0;
+    }
+  };
+  uint32_t dn = (r >> 5) + 2;  // the next window dword into the buffer
+  uint64_t buf = (((uint64_t)win[sync_at(dn - 1)] << 32) | win[sync_at(dn - 2)]) >> (r & 31);
+  uint32_t nb = 64 - (r & 31), nxt = win[sync_at(dn)];
+  auto top_up = [&]() {
+    const bool low = nb <= 32;
+    buf |= low ? ((uint64_t)nxt << nb) : 0ull;
+    dn += low ? 1u : 0u;
+    nb += low ? 32u : 0u;
+    nxt = win[sync_at(dn)];  // (the same dword again when nothing was taken)
+  };
+  auto take = [&](uint32_t k) {
+    buf >>= k;
+    nb -= k;
+    r += k;
+  };
+  while (r < end && r < lim) {
+    top_up();
+    const uint32_t w = (uint32_t)buf;
+    uint32_t e = T.lit[w & ((1u << kTokLitRoot) - 1)];
+    if ((e & 15) == 0 && (e & kEnLenBit)) e = slow_walk<kTokLitRoot>(T.lfco, T.lent, w);
+    const uint32_t L = e & 15, E = (e >> 5) & 7;
+    if (L == 0) {
+      flags |= kSyBad;
+      if (kWrite) break;
+      take(1);
+      continue;
+    }
+    if (!(e & kEnLenBit)) {
+      if (kWrite && olen0 + nout >= cap) {
+        flags |= kSyFull;
+        break;
+      }
+      if (lcnt == kSyncMerge) flush();
+      lacc |= (e >> 8) << (8 * lcnt);
+      lcnt++;
+      take(L);
+      nout++;
+      continue;
+    }
+    flush();
+    if (E == kEobExtra) {
+      take(L);
+      flags |= kSyEob;
+      break;
+    }
+    const uint32_t len = (e >> 8) + 3 + __builtin_amdgcn_ubfe(w, L, E);
+    take(L + E);
+    top_up();
+    const uint32_t w2 = (uint32_t)buf;
+    uint32_t dd = T.dst[w2 & ((1u << kTokDistRoot) - 1)];
+    if ((dd & 15) == 0 && (dd & kEnLenBit)) dd = slow_walk<kTokDistRoot>(T.dfco, T.dent, w2);
+    const uint32_t L2 = dd & 15, E2 = (dd >> 7) & 15;
+    if (L2 == 0) {
+      flags |= kSyBad;
+      if (kWrite) break;
+      continue;
+    }
+    const uint32_t dist = (((dd >> 5) & 3) << E2) + 1 + __builtin_amdgcn_ubfe(w2, L2, E2);
+    if (kWrite) {
+      const uint32_t at = olen0 + nout, hist = at < 32768u ? at : 32768u;
+      if (dist > hist) {
+        flags |= kSyHist;
+        break;
+      }
+      if (len > cap - at) {
+        flags |= kSyFull;
+        break;
+      }
+      tk[ntok] = 0x80000000u | ((len - 3) << 16) | (dist - 1);
+    }
+    take(L2 + E2);
+    ntok++;
+    nout += len;
+  }
+  flush();
+  return r;
+}
+
+// (ablation builds, -DRIO_SYNC_BITBUF=0: the previous decoder, which reads each
+// code's bits from the window at its position -- two LDS reads before every
+// table lookup)
+#ifndef RIO_SYNC_BITBUF
+#define RIO_SYNC_BITBUF 1
+#endif
+#if !RIO_SYNC_BITBUF
+template <bool kWrite>
+__device__ __forceinline__ uint32_t sync_decode_win(const StreamLds &T, const uint32_t *win, uint32_t r, uint32_t end,
                                                 uint32_t lim, uint32_t &ntok, uint32_t &nout, uint32_t &flags,
                                                 uint32_t *tk, uint32_t olen0, uint32_t cap) {
   while (r < end && r < lim) {
@@ -1427,18 +1566,36 @@ __device__ __forceinline__ uint32_t sync_decode(const StreamLds &T, const uint32
   return r;
 }
 
+#endif
+
 #ifdef RIO_SYNC_WPE  // (experiments: waves per SIMD the Huffman pass is register-allocated for)
 #define RIO_SYNC_ATTR __attribute__((amdgpu_waves_per_eu(RIO_SYNC_WPE)))
 #else
 #define RIO_SYNC_ATTR
 #endif
-__global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *__restrict__ span, DevBufs d,
+// kW waves per block: segment g = 64 * wave + lane. Wave 0 reads the DEFLATE
+// block headers and builds the tables; the waves meet at barriers to exchange
+// the first end-of-block segment, the exits at their edges, the convergence
+// test, token / byte counts and flags (one wave: all within the wave, as before).
+// wide_below: the span's block count decides the variant -- the one-wave
+// kernel runs spans of >= wide_below blocks, the kSyncW-wave one the others.
+template <int kW>
+__global__ void __launch_bounds__(64 * kW) RIO_SYNC_ATTR k_flate_sync(const uint8_t *__restrict__ span, DevBufs d,
                                                    const unsigned long long *nblocks, uint64_t nchunks,
-                                                   uint64_t dec_cap) {
-  __shared__ SyncLds S;
+                                                   uint64_t dec_cap, uint64_t wide_below) {
+  constexpr uint32_t kWinDw = sync_win_dw<kW>();
+  __shared__ SyncLdsT<kW> S;
   StreamLds &T = S.T;
   const int l = lane_id();
+  const int wv = kW == 1 ? 0 : (int)(threadIdx.x >> 6);
+  const uint32_t g = (uint32_t)(64 * wv + l);  // this lane's segment
+  const bool lead = kW == 1 ? l == 0 : threadIdx.x == 0;
   const uint64_t nb = uni64(*nblocks);
+  if ((kW == 1) != (nb >= wide_below)) return;  // the other variant's span
+  auto bar = [&]() {
+    if constexpr (kW == 1) wave_lds_sync();
+    else __syncthreads();
+  };
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     FlState *sp = &d.fl[b];
     const uint64_t c0 = uni64(d.blk_c0[b]);
@@ -1450,13 +1607,13 @@ __global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *
     const uint64_t doff = uni64(d.blk_dec_off[b]), cp = uni64(d.blk_out_len[b]);
     if (!skip && doff + cp > dec_cap) {  // the regions need a larger buffer (host retries)
       skip = true;
-      if (l == 0) {
+      if (lead) {
         atomicOr(&d.ctl->out_overflow, 0x40ull);
         atomicMax(&d.ctl->dec_need, (unsigned long long)(doff + cp));
       }
     }
     if (skip) {
-      if (l == 0) {
+      if (lead) {
         sp->mode = kFlSkip;
         sp->round = 0;
         d.blk_out_len[b] = 0;
@@ -1482,88 +1639,147 @@ __global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *
     auto checkpoint = [&]() {
       const uint64_t kc = (bit >> 3) / (uint64_t)kMaxPayload;
       for (; ck_next <= kc && ck_next < total; ck_next++)
-        if (l == 0) d.fl_ck[c0 + ck_next] = (unsigned long long)ntok | ((unsigned long long)olen << 32);
+        if (lead) d.fl_ck[c0 + ck_next] = (unsigned long long)ntok | ((unsigned long long)olen << 32);
     };
     while (!decline && !res && !fin) {
       checkpoint();
-      // ---- DEFLATE block header (wave-uniform)
-      TokDec t;
-      t.in = in;
-      t.T = &T;
-      t.W = &S.W;
-      t.seek(bit);
-      if (t.nb < 32) t.refill();
-      fin = t.take(1) != 0;
-      const uint32_t type = t.take(2);
-      if (type == 0) {  // stored: its bytes become literal tokens, 3 per token
-        t.take(t.nb & 7);
+      // ---- DEFLATE block header (wave 0; wave-uniform). act: 0 a stored
+      // block done (next header), 1 a Huffman body follows, 2 stop
+      uint32_t act = 2;
+      if (wv == 0) {
+        TokDec t;
+        t.in = in;
+        t.T = &T;
+        t.W = &S.W;
+        t.seek(bit);
         if (t.nb < 32) t.refill();
-        const uint32_t len = t.take(16), nlen = t.take(16);
-        const uint64_t at = t.bitpos() / 8;
-        if ((uint16_t)nlen != (uint16_t)~len) {
-          res = kCodecCorrupt;
-        } else if (at + len > n) {
-          res = kCodecEof;
-        } else if (len > cap - olen) {
-          res = kCodecFull;
+        fin = t.take(1) != 0;
+        const uint32_t type = t.take(2);
+        if (type == 0) {  // stored: its bytes become literal tokens, 3 per token
+          t.take(t.nb & 7);
+          if (t.nb < 32) t.refill();
+          const uint32_t len = t.take(16), nlen = t.take(16);
+          const uint64_t at = t.bitpos() / 8;
+          act = 0;
+          if ((uint16_t)nlen != (uint16_t)~len) {
+            res = kCodecCorrupt;
+          } else if (at + len > n) {
+            res = kCodecEof;
+          } else if (len > cap - olen) {
+            res = kCodecFull;
+          } else {
+            const uint32_t nt = (len + 2) / 3;
+            if ((uint64_t)ntok + nt > tcap) {
+              decline = true;
+              act = 2;
+            } else {
+              for (uint32_t k = (uint32_t)l; k < nt; k += 64) {
+                const uint32_t c = (len - 3 * k) < 3 ? len - 3 * k : 3u;
+                uint32_t v = 0;
+                for (uint32_t q = 0; q < c; q++) v |= in.byte(at + 3 * k + q) << (8 * q);
+                tok[ntok + k] = v | (c << 24);
+              }
+              ntok += nt;
+              olen += len;
+              bit = 8 * (at + len);
+            }
+          }
         } else {
-          const uint32_t nt = (len + 2) / 3;
-          if ((uint64_t)ntok + nt > tcap) {
-            decline = true;
-            break;
+          if (type == 1) {
+            if (!fixed) fixed_tables(T, S.W);
+            fixed = true;
+          } else if (type == 2) {
+            if (read_dynamic(t)) res = kCodecCorrupt;
+            fixed = false;
+          } else {
+            res = kCodecCorrupt;
           }
-          for (uint32_t k = (uint32_t)l; k < nt; k += 64) {
-            const uint32_t c = (len - 3 * k) < 3 ? len - 3 * k : 3u;
-            uint32_t v = 0;
-            for (uint32_t q = 0; q < c; q++) v |= in.byte(at + 3 * k + q) << (8 * q);
-            tok[ntok + k] = v | (c << 24);
-          }
-          ntok += nt;
-          olen += len;
-          bit = 8 * (at + len);
+          if (!res && t.overrun()) res = kCodecEof;
+          act = res ? 2u : 1u;
+          if (!res) bit = t.bitpos();
         }
-        continue;
       }
-      if (type == 1) {
-        if (!fixed) fixed_tables(T, S.W);
-        fixed = true;
-      } else if (type == 2) {
-        if (read_dynamic(t)) res = kCodecCorrupt;
-        fixed = false;
-      } else {
-        res = kCodecCorrupt;
+      if constexpr (kW > 1) {  // the header wave's results (and its tables) to every wave
+        if (lead) {
+          S.x.h_act = act;
+          S.x.h_fin = fin;
+          S.x.h_res = res;
+          S.x.h_decl = decline;
+          S.x.h_ntok = ntok;
+          S.x.h_olen = olen;
+          S.x.h_bit = bit;
+        }
+        __syncthreads();
+        act = S.x.h_act;
+        fin = S.x.h_fin != 0;
+        res = S.x.h_res;
+        decline = S.x.h_decl != 0;
+        ntok = S.x.h_ntok;
+        olen = S.x.h_olen;
+        bit = S.x.h_bit;
       }
-      if (!res && t.overrun()) res = kCodecEof;
-      if (res) break;
-      bit = t.bitpos();
-      // ---- the block body, kSyncBits per round
+      if (act == 0) continue;
+      if (act == 2) break;
+      // ---- the block body, kW * kSyncBits per round
       for (;;) {
         if (bit > 8 * n + 64) {  // ran past the input without an end-of-block
           res = kCodecEof;
           break;
         }
         checkpoint();
-        const uint64_t w0 = bit >> 5;  // staged window: dwords [w0, w0 + kSyncWinDw)
-        wave_lds_sync();
-        for (uint32_t k = (uint32_t)l; k < kSyncWinDw; k += 64) S.win[sync_at(k)] = fetch_dword(in, 4 * (w0 + k));
-        wave_lds_sync();
-        const uint32_t r0 = (uint32_t)(bit - 32 * w0), lim = 32 * (kSyncWinDw - 2);
-        const uint32_t seg_end = r0 + kSyncSeg * (uint32_t)(l + 1);
-        uint32_t st = r0 + kSyncSeg * (uint32_t)l, ex = 0, nt = 0, no = 0, fl = 0;
+        const uint64_t w0 = bit >> 5;  // staged window: dwords [w0, w0 + kWinDw)
+        bar();
+        for (uint32_t k = (uint32_t)threadIdx.x; k < kWinDw; k += 64 * kW) S.win[sync_at(k)] = fetch_dword(in, 4 * (w0 + k));
+        bar();
+        const uint32_t r0 = (uint32_t)(bit - 32 * w0), lim = 32 * (kWinDw - 2);
+        const uint32_t seg_end = r0 + kSyncSeg * (g + 1);
+        uint32_t st = r0 + kSyncSeg * g, ex = 0, nt = 0, no = 0, fl = 0;
         bool need = true, conv = false;
+        uint32_t ke = 64 * kW - 1, eob_any = 0;  // the first segment that reached end-of-block
         for (int it = 0; it < kSyncIters; it++) {
           if (need) {
             nt = no = fl = 0;
+#if RIO_SYNC_BITBUF
             ex = sync_decode<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, 0, 0);
+#else
+            ex = sync_decode_win<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, 0, 0);
+#endif
           }
-          // the true chain ends at the first lane reaching end-of-block
+          // the true chain ends at the first segment reaching end-of-block
           const unsigned long long eobm = __ballot((fl & kSyEob) != 0);
-          const int ke = eobm ? __ffsll((long long)eobm) - 1 : 63;
           uint32_t prev = __shfl_up(ex, 1, 64);
-          const uint32_t nst = l == 0 ? r0 : prev;
-          need = l <= ke && nst != st;  // lanes after the end keep their start until the end moves
-          if (need) st = nst;
-          if (!__ballot(need)) {
+          bool anyneed;
+          if constexpr (kW == 1) {
+            eob_any = eobm != 0;
+            ke = eobm ? __ffsll((long long)eobm) - 1 : 63;
+            const uint32_t nst = l == 0 ? r0 : prev;
+            need = g <= ke && nst != st;  // segments after the end keep their start until the end moves
+            if (need) st = nst;
+            anyneed = __ballot(need) != 0;
+          } else {
+            const int par = it & 1;
+            if (l == 0) {
+              S.x.eob[par][wv] = eobm ? (uint32_t)(64 * wv + __ffsll((long long)eobm) - 1) : 64u * kW;
+              S.x.ex63[par][wv] = (uint32_t)__builtin_amdgcn_readlane(ex, 63);
+            }
+            __syncthreads();
+            uint32_t fe = 64u * kW;
+#pragma unroll
+            for (int w = 0; w < kW; w++) fe = min(fe, S.x.eob[par][w]);
+            eob_any = fe < 64u * kW;
+            ke = eob_any ? fe : 64u * kW - 1;
+            if (l == 0 && wv > 0) prev = S.x.ex63[par][wv - 1];
+            const uint32_t nst = g == 0 ? r0 : prev;
+            need = g <= ke && nst != st;
+            if (need) st = nst;
+            const bool wneed = __ballot(need) != 0;  // (the whole wave votes, lane 0 writes)
+            if (l == 0) S.x.need[par][wv] = wneed;
+            __syncthreads();
+            anyneed = false;
+#pragma unroll
+            for (int w = 0; w < kW; w++) anyneed |= S.x.need[par][w] != 0;
+          }
+          if (!anyneed) {
             conv = true;
             break;
           }
@@ -1572,17 +1788,37 @@ __global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *
           decline = true;
           break;
         }
-        const unsigned long long eobm = __ballot((fl & kSyEob) != 0);
-        const int ke = eobm ? __ffsll((long long)eobm) - 1 : 63;
-        const bool live = l <= ke;
-        if (__ballot(live && (fl & kSyBad))) {  // an undecodable code on the true chain
+        const bool live = g <= ke;
+        const uint32_t tn = live ? nt : 0u, on = live ? no : 0u;
+        const uint32_t ti = wave_incl_sum_dpp(tn), oi = wave_incl_sum_dpp(on);
+        uint32_t tpre = 0, opre = 0, ttot, otot;
+        bool bad = __ballot(live && (fl & kSyBad)) != 0;
+        if constexpr (kW == 1) {
+          ttot = (uint32_t)__builtin_amdgcn_readlane(ti, 63);
+          otot = (uint32_t)__builtin_amdgcn_readlane(oi, 63);
+        } else {
+          if (l == 0) {
+            S.x.tsum[wv] = (uint32_t)__builtin_amdgcn_readlane(ti, 63);
+            S.x.osum[wv] = (uint32_t)__builtin_amdgcn_readlane(oi, 63);
+            S.x.bad[wv] = bad;
+          }
+          __syncthreads();
+          ttot = otot = 0;
+#pragma unroll
+          for (int w = 0; w < kW; w++) {
+            if (w < wv) {
+              tpre += S.x.tsum[w];
+              opre += S.x.osum[w];
+            }
+            ttot += S.x.tsum[w];
+            otot += S.x.osum[w];
+            bad |= S.x.bad[w] != 0;
+          }
+        }
+        if (bad) {  // an undecodable code on the true chain
           res = kCodecCorrupt;
           break;
         }
-        const uint32_t tn = live ? nt : 0u, on = live ? no : 0u;
-        const uint32_t ti = wave_incl_sum_dpp(tn), oi = wave_incl_sum_dpp(on);
-        const uint32_t ttot = (uint32_t)__builtin_amdgcn_readlane(ti, 63);
-        const uint32_t otot = (uint32_t)__builtin_amdgcn_readlane(oi, 63);
         if ((uint64_t)ntok + ttot > tcap) {
           decline = true;
           break;
@@ -1590,9 +1826,31 @@ __global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *
         uint32_t f2 = 0;
         if (live) {
           uint32_t wt = 0, wo = 0;
-          sync_decode<true>(T, S.win, st, seg_end, lim, wt, wo, f2, tok + ntok + (ti - tn), olen + (oi - on), cap);
+#if RIO_SYNC_BITBUF
+          const uint32_t wx = sync_decode<true>(T, S.win, st, seg_end, lim, wt, wo, f2, tok + ntok + tpre + (ti - tn),
+                                                olen + opre + (oi - on), cap);
+#else
+          const uint32_t wx = sync_decode_win<true>(T, S.win, st, seg_end, lim, wt, wo, f2,
+                                                    tok + ntok + tpre + (ti - tn), olen + opre + (oi - on), cap);
+#endif
+#ifdef RIO_SYNC_DEBUG
+          if (wt != nt || wo != no || wx != ex)
+            printf("sync kW=%d b=%llu g=%u st=%u end=%u ke=%u: count nt=%u no=%u ex=%u fl=%u | write wt=%u wo=%u wx=%u f2=%u\n",
+                   kW, (unsigned long long)b, g, st, seg_end, ke, nt, no, ex, fl, wt, wo, wx, f2);
+#endif
         }
-        const uint32_t fall = (uint32_t)__reduce_or_sync(~0ull, f2);
+        uint32_t fall = (uint32_t)__reduce_or_sync(~0ull, f2);
+        uint32_t exk;
+        if constexpr (kW == 1) {
+          exk = (uint32_t)__builtin_amdgcn_readlane(ex, ke);
+        } else {
+          if (l == 0) S.x.fall[wv] = fall;
+          if (g == ke) S.x.exk = ex;
+          __syncthreads();
+#pragma unroll
+          for (int w = 0; w < kW; w++) fall |= S.x.fall[w];
+          exk = S.x.exk;
+        }
         if (fall & kSyHist) {
           res = kCodecCorrupt;
           break;
@@ -1603,13 +1861,12 @@ __global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *
         }
         ntok += ttot;
         olen += otot;
-        const uint32_t exk = (uint32_t)__builtin_amdgcn_readlane(ex, ke);
         bit = 32 * w0 + exk;
-        if (eobm) break;  // the DEFLATE block ended
+        if (eob_any) break;  // the DEFLATE block ended
       }
     }
     if (!decline && !res && bit > 8 * n) res = kCodecEof;  // the final block ran past the input
-    if (l == 0) {
+    if (lead) {
       sp->round = 0;
       sp->olen2 = 0;
       if (decline) {
@@ -1631,6 +1888,7 @@ __global__ void __launch_bounds__(64) RIO_SYNC_ATTR k_flate_sync(const uint8_t *
         d.fl_ck[c0] = ck_next;  // checkpoints 1 .. ck_next - 1
       }
     }
+    if constexpr (kW > 1) __syncthreads();  // (S.x and the tables are reused by the next block)
   }
 }
 
@@ -2326,11 +2584,21 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
   if (g3 > (uint64_t)ncu * kL2Waves) g3 = (uint64_t)ncu * kL2Waves;
   if (g3 < 1) g3 = 1;
   if (kFlateSync) {  // the wave-per-block Huffman pass first; k_flate_tok takes what it declines
-    uint64_t gs = max_blocks;
+    // one variant runs, by the span's block count (device): one wave per block
+    // when the blocks fill the one-wave slots, else kSyncW waves per block
     const uint64_t rs = (uint64_t)ncu * kSyncWaves;
-    if (gs > rs) gs = rs;
-    if (gs < 1) gs = 1;
-    hipLaunchKernelGGL(k_flate_sync, dim3((unsigned)gs), dim3(64), 0, st, span, d, nblocks, nchunks, dec_cap);
+    uint64_t gs = max_blocks < rs ? max_blocks : rs;
+#if RIO_SYNC_WIDE  // (ablation builds: measured slower)
+    hipLaunchKernelGGL(k_flate_sync<1>, dim3((unsigned)(gs ? gs : 1)), dim3(64), 0, st, span, d, nblocks, nchunks,
+                       dec_cap, rs);
+    const uint64_t rw = (uint64_t)ncu * (163840 / sizeof(SyncLdsT<kSyncW>));
+    gs = max_blocks < rw ? max_blocks : rw;
+    hipLaunchKernelGGL(k_flate_sync<kSyncW>, dim3((unsigned)(gs ? gs : 1)), dim3(64 * kSyncW), 0, st, span, d, nblocks,
+                       nchunks, dec_cap, rs);
+#else
+    hipLaunchKernelGGL(k_flate_sync<1>, dim3((unsigned)(gs ? gs : 1)), dim3(64), 0, st, span, d, nblocks, nchunks,
+                       dec_cap, 0);
+#endif
   }
 #ifdef RIO_FLSTAT
   {

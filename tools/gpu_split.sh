@@ -29,6 +29,23 @@ for s in "$@"; do
         step stat1k 300 python3 tools/bench_flate.py --steps 1 --warmup 0 --replicas 4 ;;
     stat16k) RIO_GPU_LIB=exp_lib/flstat/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_FLSTAT" RIO_BUILD_DIR=exp_lib/flstat \
         step stat16k 300 python3 tools/bench_flate.py --steps 1 --warmup 1 --replicas 4 --per-block 16384 ;;
+    nomerge) RIO_GPU_LIB=exp_lib/nomerge/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_SYNC_MERGE=1" RIO_BUILD_DIR=exp_lib/nomerge \
+        step nomerge 300 python -u -m pytest tests/test_flate_gpu.py -x -v --timeout 150 --timeout-method thread ;;
+    flate1) step flate1 300 python -u -m pytest tests/test_flate_gpu.py -x -v --timeout 150 --timeout-method thread ;;
+    dbg) RIO_GPU_LIB=exp_lib/dbg/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_DEBUG_DUMP -DRIO_SYNC_DEBUG" RIO_BUILD_DIR=exp_lib/dbg \
+        step dbg 300 python -u -m pytest "tests/test_flate_gpu.py::test_levels_and_styles" -x -s --timeout 150 --timeout-method thread ;;
+    prof1k) step prof1k 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof1k -o run -- \
+        python3 tools/bench_flate.py --steps 2 ;;
+    roots) for v in 10_8 11_8 12_8 10_9; do
+          RIO_GPU_LIB=exp_lib/root$v/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_LIT_ROOT=${v%_*} -DRIO_DIST_ROOT=${v#*_}" \
+            RIO_BUILD_DIR=exp_lib/root$v step b1k_root$v 300 python3 tools/bench_flate.py --steps 3
+        done
+        step b1k_base 300 python3 tools/bench_flate.py --steps 3 ;;
+    ab_bitbuf) for i in 1 2; do
+          step b1k_bitbuf_$i 300 python3 tools/bench_flate.py --steps 3
+          RIO_GPU_LIB=exp_lib/nobitbuf/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_SYNC_BITBUF=0" RIO_BUILD_DIR=exp_lib/nobitbuf \
+            step b1k_nobitbuf_$i 300 python3 tools/bench_flate.py --steps 3
+        done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
