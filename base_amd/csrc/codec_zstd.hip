@@ -1518,6 +1518,49 @@ __global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
 // (offset <= 28 bits, extras <= 16 + 16, states <= 9 + 9 + 8), so a sequence
 // takes at most 3 dwords.
 constexpr int kZs2Ring = 32;
+#ifndef RIO_ZS2_PREFETCH
+#define RIO_ZS2_PREFETCH 1
+#endif
+#ifndef RIO_ZS2_CODES_ALU
+#define RIO_ZS2_CODES_ALU 1
+#endif
+// LL / ML code -> baseline | extra bits << 24 (RFC 8878 3.1.1.3.2.1.1 tables),
+// computed (round 3) instead of looked up: the lookup was a second dependent LDS
+// read per sequence (ablation builds: -DRIO_ZS2_CODES_ALU=0)
+__device__ __forceinline__ uint32_t zs_llx(uint32_t c) {
+  const uint32_t k = c - 20u, p = (k >> 1) & 3u, b = p + 2u;
+  uint32_t base = 16u + (8u << p) + ((k & 1u) << b), bits = b;
+  if (c < 20u) {
+    base = 16u + 2u * (c - 16u);
+    bits = 1u;
+  }
+  if (c >= 25u) {
+    bits = c - 19u;
+    base = 1u << (bits & 31u);
+  }
+  if (c < 16u) {
+    base = c;
+    bits = 0u;
+  }
+  return base | (bits << 24);
+}
+__device__ __forceinline__ uint32_t zs_mlx(uint32_t c) {
+  const uint32_t k = c - 36u, p = (k >> 1) & 3u, b = p + 2u;
+  uint32_t base = 35u + (8u << p) + ((k & 1u) << b), bits = b;
+  if (c < 36u) {
+    base = 35u + 2u * (c - 32u);
+    bits = 1u;
+  }
+  if (c >= 43u) {
+    bits = c - 36u;
+    base = (1u << (bits & 31u)) + 3u;
+  }
+  if (c < 32u) {
+    base = c + 3u;
+    bits = 0u;
+  }
+  return base | (bits << 24);
+}
 struct ZBr64 {
   const uint32_t *w;
   uint64_t win;
@@ -1530,6 +1573,23 @@ struct ZBr64 {
   // which is an error whatever they hold
   __device__ __forceinline__ uint32_t Dc(int32_t i) const { return w[max(qtop - i, 0)]; }
   // ring: this lane's kZs2Ring dwords (D_i at i mod kZs2Ring)
+#if RIO_ZS2_PREFETCH
+  // the ring dword the next reload takes, loaded one reload ahead (round 3): a
+  // reload then waits for no LDS read. Valid: within a group the lane consumes
+  // <= 24 dwords of the >= 24 the ring holds, and the group's refill writes
+  // only slots past them.
+  uint32_t nx;
+  __device__ __forceinline__ void prime(const uint32_t (&ring)[kZs2Ring]) { nx = ring[cons & (kZs2Ring - 1)]; }
+  __device__ __forceinline__ void reload(const uint32_t (&ring)[kZs2Ring]) {
+    if (avail <= 32) {
+      win = (win << 32) | nx;
+      cons++;
+      avail += 32;
+      nx = ring[cons & (kZs2Ring - 1)];
+    }
+  }
+#else
+  __device__ __forceinline__ void prime(const uint32_t (&)[kZs2Ring]) {}
   __device__ __forceinline__ void reload(const uint32_t (&ring)[kZs2Ring]) {
 #if RIO_ZS2_BRANCHLESS
     // (experiment) the ring dword read every time, the refill selected: no
@@ -1552,6 +1612,7 @@ struct ZBr64 {
     }
 #endif
   }
+#endif
   __device__ __forceinline__ uint32_t read(int nb) {  // nb <= 31
     avail -= nb;
     return (uint32_t)(win >> avail) & ((1u << nb) - 1u);
@@ -1692,6 +1753,7 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
         sll = r.read(llg);
         sof = r.read(ofg);
         sml = r.read(mlg);
+        r.prime(rings[wv][ls]);
         r.reload(rings[wv][ls]);
       }
       active = err == 0;
@@ -1756,7 +1818,11 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
           } else if (ofc > 28) {
             err = kZSlow;
           } else {
+#if RIO_ZS2_CODES_ALU
+            const uint32_t mlx = zs_mlx(mlc), llx = zs_llx(llc);
+#else
             const uint32_t mlx = codes.ml[mlc], llx = codes.ll[llc];
+#endif
             const uint32_t ofv = (1u << ofc) + r.read((int)ofc);
             r.reload(rings[wv][ls]);
             const uint32_t ml = (mlx & 0xFFFFFFu) + r.read((int)(mlx >> 24));
@@ -2481,21 +2547,11 @@ __global__ void __launch_bounds__(64) k_zstd_exec2(DevBufs d, const unsigned lon
 #pragma unroll
       for (int k = 0; k < 2; k++)
         pre[k] = (nx + 64u * k + (uint32_t)l < ntok) ? ents[-1 - (int64_t)(nx + 64 * k + l)] : 0ull;
-      // the copies above, then the matches sourced inside the batch, in rounds
-      bool run = false;
-      uint32_t R = 0, Df = 0, Nf = 0;
+      // the copies above (every slot), then the matches sourced inside the
+      // batch in rounds, ring to ring, slot by slot, only the slots some lane
+      // copies in that round (as k_flate_lz2)
+      l2_copy4(ring, gw, cs, B0, cp, cn, glob, gl, litm);
       for (;;) {
-        l2_copy4(ring, gw, cs, B0, cp, cn, glob, gl, litm);
-        if (run) {  // byte k of the run = byte (k mod dist) of the dist bytes before it (final)
-          const uint32_t xs = B0 + R - Df, xd = B0 + R;
-          for (uint32_t k0 = 0; k0 < Nf; k0 += 64) {
-            const uint32_t k = k0 + (uint32_t)l;
-            if (k < Nf) {
-              const uint32_t v = ring[(xs + z_umod(k, Df)) & kL2Mask];
-              atomicOr(reinterpret_cast<uint32_t *>(ring) + (((xd + k) >> 2) & (kL2Mask >> 2)), v << (8 * ((xd + k) & 3)));
-            }
-          }
-        }
         wave_lds_sync();
         int kf = -1, lf = 0;
 #pragma unroll
@@ -2508,20 +2564,30 @@ __global__ void __launch_bounds__(64) k_zstd_exec2(DevBufs d, const unsigned lon
         }
         if (kf < 0) break;
         // R: the first pending match; every byte before it is final
-        R = (uint32_t)__builtin_amdgcn_readlane(pick4(cp, kf), lf);
-        Df = (uint32_t)__builtin_amdgcn_readlane(pick4(dist, kf), lf);
-        Nf = (uint32_t)__builtin_amdgcn_readlane(pick4(clen, kf), lf);
-        run = Df < Nf;  // it overlaps its own output: the whole wave copies it
-        glob = 0;
-        litm = 0;
+        const uint32_t R = (uint32_t)__builtin_amdgcn_readlane(pick4(cp, kf), lf);
+        const uint32_t Df = (uint32_t)__builtin_amdgcn_readlane(pick4(dist, kf), lf);
+        const uint32_t Nf = (uint32_t)__builtin_amdgcn_readlane(pick4(clen, kf), lf);
+        const bool run = Df < Nf;  // it overlaps its own output: the whole wave copies it
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          cn[k] = 0;
-          if (!pend[k]) continue;
-          const bool first = k == kf && l == lf;
-          if (first || cs[k] + clen[k] <= B0 + R) {  // source ends at or before R
-            if (!first || !run) cn[k] = clen[k];
-            pend[k] = false;
+        for (int k = 1; k < 4; k += 2) {  // (only match slots are ever pending)
+          uint32_t n = 0;
+          if (pend[k]) {
+            const bool first = k == kf && l == lf;
+            if (first || cs[k] + clen[k] <= B0 + R) {  // source ends at or before R
+              if (!first || !run) n = clen[k];
+              pend[k] = false;
+            }
+          }
+          if (__ballot(n != 0)) l2_copy1_ring(ring, cs[k], B0 + cp[k], n);
+        }
+        if (run) {  // byte k of the run = byte (k mod dist) of the dist bytes before it (final)
+          const uint32_t xs = B0 + R - Df, xd = B0 + R;
+          for (uint32_t k0 = 0; k0 < Nf; k0 += 64) {
+            const uint32_t k = k0 + (uint32_t)l;
+            if (k < Nf) {
+              const uint32_t v = ring[(xs + z_umod(k, Df)) & kL2Mask];
+              atomicOr(reinterpret_cast<uint32_t *>(ring) + (((xd + k) >> 2) & (kL2Mask >> 2)), v << (8 * ((xd + k) & 3)));
+            }
           }
         }
       }

@@ -46,6 +46,19 @@ for s in "$@"; do
           RIO_GPU_LIB=exp_lib/nobitbuf/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_SYNC_BITBUF=0" RIO_BUILD_DIR=exp_lib/nobitbuf \
             step b1k_nobitbuf_$i 300 python3 tools/bench_flate.py --steps 3
         done ;;
+    ab_exec2) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        for i in 1 2; do
+          step c4_exec_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+          RIO_GPU_LIB=exp_lib/exec2/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZSTD_EXEC2=1" RIO_BUILD_DIR=exp_lib/exec2 \
+            step c4_exec2_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+        done ;;
+    ab_zs2) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        for i in 1 2; do
+          step c4_new_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+          RIO_GPU_LIB=exp_lib/zs2old/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZS2_PREFETCH=0 -DRIO_ZS2_CODES_ALU=0" \
+            RIO_BUILD_DIR=exp_lib/zs2old step c4_old_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+        done ;;
+    zstdt) step zstd_tests 600 python -u -m pytest tests/test_zstd_gpu.py tests/test_zstd_libzstd.py -x -v --timeout 150 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
