@@ -510,6 +510,81 @@ __device__ bool z_huf_streams(ZLds &L, int max_bits, const uint8_t *src, int64_t
   return __ballot(l < ns && !ok) == 0;
 }
 
+// The literal streams with every lane decoding (round 3): each stream is cut
+// into 64 / ns segments of its bits, lane j of a stream decoding its segment
+// downwards from the segment's top -- a guessed symbol boundary; Huffman codes
+// self-synchronise (as in k_flate_sync), so a lane restarts from its
+// predecessor's exit until no start changes, then a prefix sum of the lanes'
+// symbol counts places each lane's bytes and a second decode writes them.
+// Valid iff every stream's chain ends exactly at the stream's first bit after
+// exactly its count of symbols -- the serial decoder's exact-consumption
+// check. Returns 1 ok, 0 a corrupt stream, -1 no convergence (the caller then
+// decodes serially).
+constexpr int kZHufIters = 8;
+__device__ int z_huf_sync(ZLds &L, int max_bits, const uint8_t *src, int64_t st, int64_t sn, int ns, uint8_t *out,
+                          int64_t seg, int64_t cnt) {
+  const int l = lane_id();
+  const int per = 64 / ns;                 // lanes per stream
+  const int t = l / per, j = l % per;      // stream, segment
+  const int64_t st_t = (int64_t)__shfl((long long)st, t, 64), sn_t = (int64_t)__shfl((long long)sn, t, 64);
+  const int64_t cnt_t = (int64_t)__shfl((long long)cnt, t, 64);
+  ZBr r;
+  bool ok = r.init(src, st_t, sn_t);
+  if (__ballot(!ok)) return 0;
+  const int32_t lo = r.lo, top = r.bit;
+  const int32_t S = (top - lo + per - 1) / per;  // bits per segment
+  const int32_t seg_lo = top - (j + 1) * S < lo ? lo : top - (j + 1) * S;
+  int32_t start = top - j * S < lo ? lo : top - j * S;
+  // one decode of this lane's segment from `from`: symbols whose top is above
+  // seg_lo; the exit is the first symbol boundary at or below it
+  auto decode = [&](int32_t from, bool write, int64_t at, uint32_t &n, bool &bad) -> int32_t {
+    r.bit = from;
+    n = 0;
+    bad = false;
+    while (r.bit > seg_lo) {
+      const uint32_t e = L.huf[r.get(r.bit - max_bits, max_bits)];
+      const int32_t nb = (int32_t)(e & 15);
+      if (nb == 0) {  // (no code: a malformed table or a lane off the chain)
+        bad = true;
+        r.bit -= 1;
+        continue;
+      }
+      if (write) out[at + n] = (uint8_t)(e >> 4);
+      r.bit -= nb;
+      n++;
+    }
+    return r.bit;
+  };
+  uint32_t n = 0;
+  bool bad = false, need = true, conv = false;
+  int32_t ex = 0;
+  for (int it = 0; it < kZHufIters; it++) {
+    if (need) ex = decode(start, false, 0, n, bad);
+    const int32_t prev = __shfl_up(ex, 1, 64);
+    const int32_t nst = j == 0 ? top : prev;
+    need = nst != start;
+    if (need) start = nst;
+    if (!__ballot(need)) {
+      conv = true;
+      break;
+    }
+  }
+  if (!conv) return -1;
+  // every stream: its last lane's exit at the stream's first bit, its symbols
+  // its count, no undecodable code on the chain
+  const uint32_t incl = wave_incl_sum_dpp(n);
+  const uint32_t before = (uint32_t)__shfl((int)incl, t > 0 ? t * per - 1 : 0, 64);
+  const uint32_t pre = t > 0 ? before : 0u;  // the symbols of the streams before this one
+  const uint32_t excl = incl - n - pre;
+  const uint32_t tot = (uint32_t)__shfl((int)incl, t * per + per - 1, 64) - pre;
+  const bool bad_stream = (j == per - 1 && ex != lo) || (j == 0 && (int64_t)tot != cnt_t) || bad;
+  if (__ballot(bad_stream)) return 0;
+  uint32_t n2 = 0;
+  bool bad2 = false;
+  decode(start, true, (int64_t)t * seg + excl, n2, bad2);
+  return 1;
+}
+
 // ---------------------------------------------------------------- sequence tables
 // (oracle seq_table) mode 0 predefined, 1 RLE, 2 compressed, 3 repeat; bytes used or -1
 __device__ int z_seq_table(uint32_t *t, uint16_t *next, int16_t *norm, int *have, int *log_io, int mode,
@@ -667,7 +742,8 @@ __device__ uint32_t z_literals(ZFrame &z, ZLds &L, int64_t bstart, int64_t n, in
     bool ok;
     if (streams == 1) {
       if (regen > max_regen) return kZSlow;
-      ok = z_huf_streams(L, z.max_bits, src, hs, hn, 1, z.lit, 0, regen);
+      const int sy = z_huf_sync(L, z.max_bits, src, hs, hn, 1, z.lit, 0, regen);
+      ok = sy > 0 || (sy < 0 && z_huf_streams(L, z.max_bits, src, hs, hn, 1, z.lit, 0, regen));
     } else {
       if (hn < 6) return kZCorrupt;
       const int64_t s1 = src[hs] | (src[hs + 1] << 8), s2 = src[hs + 2] | (src[hs + 3] << 8),
@@ -682,7 +758,8 @@ __device__ uint32_t z_literals(ZFrame &z, ZLds &L, int64_t bstart, int64_t n, in
       const int64_t st = hs + 6 + (l > 0 ? s1 : 0) + (l > 1 ? s2 : 0) + (l > 2 ? s3 : 0);
       const int64_t sn = l == 0 ? s1 : l == 1 ? s2 : l == 2 ? s3 : s4;
       const int64_t cnt = l < 3 ? seg : regen - 3 * seg;
-      ok = z_huf_streams(L, z.max_bits, src, st, sn, 4, z.lit, seg, cnt);
+      const int sy = z_huf_sync(L, z.max_bits, src, st, sn, 4, z.lit, seg, cnt);
+      ok = sy > 0 || (sy < 0 && z_huf_streams(L, z.max_bits, src, st, sn, 4, z.lit, seg, cnt));
     }
     if (!ok) return kZCorrupt;
     pos += csize;
@@ -1518,15 +1595,18 @@ __global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
 // (offset <= 28 bits, extras <= 16 + 16, states <= 9 + 9 + 8), so a sequence
 // takes at most 3 dwords.
 constexpr int kZs2Ring = 32;
+// Measured and kept out (round 3, ablation switches; A/B on one box, C4 ms per
+// step): the ring dword of the next reload loaded a reload ahead
+// (-DRIO_ZS2_PREFETCH=1: 150.2 against 147.0) and the LL / ML code baselines
+// computed instead of looked up (-DRIO_ZS2_CODES_ALU=1: 153.2; both 155.0) --
+// this pass's pace is set by where the compiler places its LDS waits.
 #ifndef RIO_ZS2_PREFETCH
-#define RIO_ZS2_PREFETCH 1
+#define RIO_ZS2_PREFETCH 0
 #endif
 #ifndef RIO_ZS2_CODES_ALU
-#define RIO_ZS2_CODES_ALU 1
+#define RIO_ZS2_CODES_ALU 0
 #endif
-// LL / ML code -> baseline | extra bits << 24 (RFC 8878 3.1.1.3.2.1.1 tables),
-// computed (round 3) instead of looked up: the lookup was a second dependent LDS
-// read per sequence (ablation builds: -DRIO_ZS2_CODES_ALU=0)
+// LL / ML code -> baseline | extra bits << 24 (RFC 8878 3.1.1.3.2.1.1 tables)
 __device__ __forceinline__ uint32_t zs_llx(uint32_t c) {
   const uint32_t k = c - 20u, p = (k >> 1) & 3u, b = p + 2u;
   uint32_t base = 16u + (8u << p) + ((k & 1u) << b), bits = b;

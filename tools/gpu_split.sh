@@ -58,6 +58,15 @@ for s in "$@"; do
           RIO_GPU_LIB=exp_lib/zs2old/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZS2_PREFETCH=0 -DRIO_ZS2_CODES_ALU=0" \
             RIO_BUILD_DIR=exp_lib/zs2old step c4_old_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
         done ;;
+    ab_zs2b) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        step c4_11 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+        for v in 01 10 00; do
+          RIO_GPU_LIB=exp_lib/zs2_$v/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZS2_PREFETCH=${v:0:1} -DRIO_ZS2_CODES_ALU=${v:1:1}" \
+            RIO_BUILD_DIR=exp_lib/zs2_$v step c4_$v 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+        done ;;
+    profc4) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        step profc4 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc4 -o run -- \
+          python3 tools/bench_zstd.py --steps 2 --warmup 1 --data /tmp/c4.bin ;;
     zstdt) step zstd_tests 600 python -u -m pytest tests/test_zstd_gpu.py tests/test_zstd_libzstd.py -x -v --timeout 150 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
