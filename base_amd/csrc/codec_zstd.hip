@@ -770,6 +770,78 @@ __device__ uint32_t z_literals(ZFrame &z, ZLds &L, int64_t bstart, int64_t n, in
 
 // Sequences section header and its three FSE tables (lane 0 builds them into
 // L): nseq, pos advanced to the sequence bitstream.
+// FSE decoding table by the whole wave (round 3; z_fse_build's cells): lane 0
+// walking the 512 cells twice -- the spread, then each cell's state from a
+// per-symbol counter in LDS -- was over half of k_zstd_ent. Here (1) the
+// low-probability symbols take the top cells by a ballot rank; (2) the spread
+// writes the k-th symbol occurrence (symbols in order, norm[s] each) to the k-th
+// valid cell of the sequence i * step mod size (valid: below the low symbols),
+// k from a ballot prefix over i, the symbol of k by binary search of the
+// counts' inclusive prefix; (3) a cell's occurrence number within its symbol
+// comes from ballots over the 64 cells of a chunk, one per distinct symbol,
+// with per-symbol running counts. False: the counts do not fill the table.
+// cum / cnt: 64 u16 of LDS scratch each.
+__device__ bool z_fse_build_wave(uint32_t *t, const int16_t *norm, int max_sym, int log, uint16_t *cum,
+                                 uint16_t *cnt) {
+  const int l = lane_id();
+  const uint32_t size = 1u << log, mask = size - 1;
+  const unsigned long long lt = (1ull << l) - 1;
+  const int nv = l <= max_sym ? norm[l] : 0;
+  const bool low = l <= max_sym && nv == -1;
+  const unsigned long long ml = __ballot(low);
+  const uint32_t nlow = (uint32_t)__popcll(ml);
+  if (low) t[size - 1 - (uint32_t)__popcll(ml & lt)] = (uint32_t)l;
+  const uint32_t high = size - 1 - nlow;
+  const uint32_t pc = nv > 0 ? (uint32_t)nv : 0u;
+  const uint32_t incl = wave_incl_sum_dpp(pc);
+  if ((uint32_t)__builtin_amdgcn_readlane(incl, 63) != high + 1) return false;
+  cum[l] = (uint16_t)incl;
+  cnt[l] = (uint16_t)(low ? 1 : nv);  // the next state's counter (FSE's symbolNext)
+  zsync();
+  const uint32_t step = (size >> 1) + (size >> 3) + 3;
+  uint32_t carry = 0;
+  for (uint32_t i0 = 0; i0 < size; i0 += 64) {
+    const uint32_t i = i0 + (uint32_t)l, q = (i * step) & mask;
+    const bool v = i < size && q <= high;
+    const unsigned long long m = __ballot(v);
+    const uint32_t k = carry + (uint32_t)__popcll(m & lt);
+    carry += (uint32_t)__popcll(m);
+    if (v) {  // the first symbol whose inclusive count passes k
+      int lo_s = 0, hi_s = max_sym;
+      while (lo_s < hi_s) {
+        const int mid = (lo_s + hi_s) >> 1;
+        if (cum[mid] > k) hi_s = mid;
+        else lo_s = mid + 1;
+      }
+      t[q] = (uint32_t)lo_s;
+    }
+  }
+  zsync();
+  for (uint32_t u0 = 0; u0 < size; u0 += 64) {
+    const uint32_t u = u0 + (uint32_t)l;
+    const bool in = u < size;
+    const uint32_t sym = in ? (t[u] & 0xffu) : 0xffffu;
+    unsigned long long left = __ballot(in);
+    uint32_t ns = 0;
+    while (left) {
+      const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)sym, __ffsll((long long)left) - 1);
+      const unsigned long long m = __ballot(in && sym == s0);
+      const uint32_t c = cnt[s0];
+      if (in && sym == s0) ns = c + (uint32_t)__popcll(m & lt);
+      zsync();
+      if (l == 0) cnt[s0] = (uint16_t)(c + (uint32_t)__popcll(m));
+      zsync();
+      left &= ~m;
+    }
+    if (in) {
+      const int nb = log - highbit(ns);
+      t[u] = sym | ((uint32_t)nb << 8) | (((ns << nb) - size) << 16);
+    }
+  }
+  zsync();
+  return true;
+}
+
 __device__ uint32_t z_seq_header(ZFrame &z, ZLds &L, int64_t bstart, int64_t n, int64_t &pos, int64_t &nseq_out) {
   const int l = lane_id();
   const uint8_t *src = z.src;
@@ -798,29 +870,54 @@ __device__ uint32_t z_seq_header(ZFrame &z, ZLds &L, int64_t bstart, int64_t n, 
   if (modes & 3) return kZCorrupt;
   // tables: lane 0 builds them from the staged descriptions (three NCounts:
   // < 300 bytes together), every lane learns the bytes used / a failure
-  int u = 0, uo = 0, um = 0;
   const int64_t sn = n - pos < kZDesc ? n - pos : kZDesc;
   const uint8_t *dsc = ((modes >> 2) & 0x3f) ? z_stage(L, src, bstart + pos, n - pos) : nullptr;
-  if (l == 0) {
-    u = z_seq_table(L.ll, L.next, L.norm, &z.have_ll, &z.ll_log, (modes >> 6) & 3, dsc, 0, sn, kLLDef, 6, 35, 9);
-    if (u >= 0)
-      uo = z_seq_table(L.of, L.next, L.norm, &z.have_of, &z.of_log, (modes >> 4) & 3, dsc, u, sn - u, kOFDef, 5, 31,
-                       8);
-    if (u >= 0 && uo >= 0)
-      um = z_seq_table(L.ml, L.next, L.norm, &z.have_ml, &z.ml_log, (modes >> 2) & 3, dsc, u + uo, sn - u - uo,
-                       kMLDef, 6, 52, 9);
-  }
-  u = zbcast(L, 0, u);
-  uo = zbcast(L, 1, uo);
-  um = zbcast(L, 2, um);
-  z.have_ll = zbcast(L, 3, z.have_ll);
-  z.have_of = zbcast(L, 4, z.have_of);
-  z.have_ml = zbcast(L, 5, z.have_ml);
-  z.ll_log = zbcast(L, 6, z.ll_log);
-  z.of_log = zbcast(L, 7, z.of_log);
-  z.ml_log = zbcast(L, 8, z.ml_log);
-  if (u < 0 || uo < 0 || um < 0) return kZCorrupt;
-  pos += u + uo + um;
+  // per table (z_seq_table's modes): lane 0 reads the description (predefined
+  // counts, RLE symbol, NCount or repeat), the wave builds the decoding table
+  uint16_t *cum = reinterpret_cast<uint16_t *>(L.hout[0]), *cnt = reinterpret_cast<uint16_t *>(L.hout[1]);
+  int64_t at = 0;
+  auto table = [&](uint32_t *t, int &have, int &logv, int mode, const int16_t *def, int def_log, int max_sym,
+                   int max_log) -> bool {
+    int k = 0, ms = max_sym, lg = logv, build = 0;
+    if (l == 0) {
+      if (mode == 0) {
+        for (int q = 0; q <= max_sym; q++) L.norm[q] = def[q];
+        lg = def_log;
+        build = 1;
+      } else if (mode == 1) {
+        if (sn - at < 1 || dsc[at] > max_sym) {
+          k = -1;
+        } else {
+          t[0] = dsc[at];  // log 0: nbits 0, base 0
+          lg = 0;
+          k = 1;
+        }
+      } else if (mode == 2) {
+        k = z_read_ncount(L.norm, &ms, &lg, dsc + at, sn - at, max_log);
+        if (k > sn - at) k = -1;
+        build = k >= 0;
+      } else if (!have) {
+        k = -1;
+      }
+    }
+    k = zbcast(L, 0, k);
+    ms = zbcast(L, 1, ms);
+    lg = zbcast(L, 2, lg);
+    build = zbcast(L, 3, build);
+    if (build && !z_fse_build_wave(t, L.norm, ms, lg, cum, cnt)) k = -1;
+    if (k < 0) return false;
+    if (mode != 3) {
+      have = 1;
+      logv = lg;
+    }
+    at += k;
+    return true;
+  };
+  if (!table(L.ll, z.have_ll, z.ll_log, (modes >> 6) & 3, kLLDef, 6, 35, 9) ||
+      !table(L.of, z.have_of, z.of_log, (modes >> 4) & 3, kOFDef, 5, 31, 8) ||
+      !table(L.ml, z.have_ml, z.ml_log, (modes >> 2) & 3, kMLDef, 6, 52, 9))
+    return kZCorrupt;
+  pos += at;
   return 0;
 }
 
@@ -1083,10 +1180,14 @@ struct ZJobSink {
   __device__ uint32_t block(ZFrame &z, ZLds &L, int64_t bstart, int64_t n) {
     int64_t pos = 0, regen = 0, nseq = 0;
     z.lit = tok8 + region + lit_w;
+    ZPROF_T(t0);
     uint32_t e = z_literals(z, L, bstart, n, pos, regen, half - 64 - lit_w);
     if (e) return e;
+    ZPROF_ADD(0, t0);
+    ZPROF_T(t1);
     e = z_seq_header(z, L, bstart, n, pos, nseq);
     if (e) return e;
+    ZPROF_ADD(1, t1);
     const int nll = 1 << z.ll_log, nml = 1 << z.ml_log, nof = 1 << z.of_log;
     const int64_t tabsz = nseq ? 4 * (int64_t)(nll + nml + nof) : 0;
     const int64_t at = new_job(tabsz, nseq, (uint32_t)regen, 0);

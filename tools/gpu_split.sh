@@ -67,6 +67,11 @@ for s in "$@"; do
     profc4) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
         step profc4 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc4 -o run -- \
           python3 tools/bench_zstd.py --steps 2 --warmup 1 --data /tmp/c4.bin ;;
+    zprof) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        RIO_GPU_LIB=exp_lib/zprof/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZPROF" RIO_BUILD_DIR=exp_lib/zprof \
+          step zprof 300 python3 tools/bench_zstd.py --steps 1 --warmup 0 --replicas 8 --data /tmp/c4.bin ;;
+    c4) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        step c4 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin ;;
     zstdt) step zstd_tests 600 python -u -m pytest tests/test_zstd_gpu.py tests/test_zstd_libzstd.py -x -v --timeout 150 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
