@@ -2273,6 +2273,12 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
 #ifndef RIO_ZEXEC_NOREADY
 #define RIO_ZEXEC_NOREADY 0
 #endif
+#ifndef RIO_ZEXEC_NOREST
+#define RIO_ZEXEC_NOREST 0
+#endif
+#ifndef RIO_ZEXEC_READY_MAX
+#define RIO_ZEXEC_READY_MAX 32  // longest match a lane copies on its own in the parallel round
+#endif
 constexpr uint32_t kZRingK = RIO_ZRING_K;  // ring = kZRingK x 4 KiB
 constexpr uint32_t kZRing = kZRingK * 4096;
 constexpr uint32_t kZPart = 2 * kZPiece;
@@ -2419,7 +2425,7 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
             // part's first match, each by its own lane ...
             const uint32_t R = zrl(dst, (uint32_t)(__ffsll((long long)mm) - 1));
             const uint32_t src_end = src + (myml < off ? myml : off);
-            const bool ready = m && src_end <= R && myml <= 32;
+            const bool ready = m && src_end <= R && myml <= (uint32_t)RIO_ZEXEC_READY_MAX;
             if (ready && !RIO_ZEXEC_NOREADY) {  // (RIO_ZEXEC_NOREADY: measurement only, wrong bytes)
               // the source wholly in the ring or wholly flushed (src + kZHist vs base is
               // monotone in the byte), neither ring range wrapping: 12 aligned bytes per
@@ -2453,7 +2459,14 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
             }
             // ... then the rest in order, each by the whole wave (every byte it
             // reads precedes it and is final by then)
-            unsigned long long rest = mm & ~__ballot(ready);
+            unsigned long long rest = RIO_ZEXEC_NOREST ? 0ull : mm & ~__ballot(ready);  // (NOREST: measurement only)
+#ifdef RIO_ZPROF
+            if (l == 0) {
+              atomicAdd(&d.ctl->zx[1], 1ull);
+              atomicAdd(&d.ctl->zx[2], (unsigned long long)__popcll(mm));
+              atomicAdd(&d.ctl->zx[3], (unsigned long long)__popcll(rest));
+            }
+#endif
             while (rest) {
               const uint32_t f = (uint32_t)(__ffsll((long long)rest) - 1);
               rest &= rest - 1;

@@ -964,6 +964,9 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
     fprintf(stderr, "rio: zstd blocks on the serial path: %llu; entropy-pass cycles lit %llu tables %llu seq %llu block %llu\n",
             (unsigned long long)ctx->h_ctl->pad[1], ctx->h_ctl->zprof[0], ctx->h_ctl->zprof[1], ctx->h_ctl->zprof[2],
             ctx->h_ctl->zprof[3]);
+  if (ctx->last_codec == RIO_CODEC_ZSTD)
+    fprintf(stderr, "rio: zstd execution parts with matches %llu, matches %llu, copied in order %llu\n",
+            ctx->h_ctl->zx[1], ctx->h_ctl->zx[2], ctx->h_ctl->zx[3]);
 #endif
 #ifdef RIO_FLSTAT  // statistics builds: the flate copy pass's batches
   if (ctx->last_codec == RIO_CODEC_FLATE)

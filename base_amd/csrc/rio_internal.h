@@ -101,6 +101,7 @@ struct Ctl {
   unsigned long long zjob_n;                      // zstd jobs made (k_zstd_ent)
   unsigned long long seg_used;                    // flate split copy: scratch bytes the blocks asked for (k_flate_plan)
   unsigned long long seg_blocks;                  // flate split copy: blocks split
+  unsigned long long zx[4];                       // (RIO_ZPROF builds: zstd execution pass groups, parts, ready, rest matches)
 };
 
 constexpr unsigned long long kNone = ~0ull;

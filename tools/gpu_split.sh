@@ -72,6 +72,22 @@ for s in "$@"; do
           step zprof 300 python3 tools/bench_zstd.py --steps 1 --warmup 0 --replicas 8 --data /tmp/c4.bin ;;
     c4) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
         step c4 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin ;;
+    norest) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        step c4_base 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+        RIO_GPU_LIB=exp_lib/norest/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZEXEC_NOREST=1" RIO_BUILD_DIR=exp_lib/norest \
+          step c4_norest 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin ;;
+    rmax) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        step c4_base 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+        for v in 64 128 256; do
+          RIO_GPU_LIB=exp_lib/rmax$v/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZEXEC_READY_MAX=$v" RIO_BUILD_DIR=exp_lib/rmax$v \
+            step c4_rmax$v 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+        done ;;
+    ab_rp) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        for i in 1 2; do
+          step c4_rp_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+          RIO_GPU_LIB=exp_lib/norp/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZEXEC_RESTPAR=0" RIO_BUILD_DIR=exp_lib/norp \
+            step c4_norp_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+        done ;;
     zstdt) step zstd_tests 600 python -u -m pytest tests/test_zstd_gpu.py tests/test_zstd_libzstd.py -x -v --timeout 150 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
