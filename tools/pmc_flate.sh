@@ -8,7 +8,8 @@ mkdir -p gpurun_out
 groups=(
   "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU"
   "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU"
-  "FETCH_SIZE WRITE_SIZE"
+  "FETCH_SIZE"
+  "WRITE_SIZE"
 )
 i=0
 for g in "${groups[@]}"; do
