@@ -222,7 +222,7 @@ static void free_all(rio_ctx *c) {
   DevBufs &d = c->d;
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.blk_data, d.blk_file_off, d.blk_seg, d.cmp, d.item_off, d.item_len, d.side,
-                d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.fl_ck, d.fl_seg, d.seg_scr, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
+                d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.fl_ck, d.fl_seg, d.seg_scr, d.fl_stage, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len,
                 c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan, c->d_seg, c->d_chain[0], c->d_chain[1], c->d_chain_meta};
   for (void *p : ps)
@@ -411,6 +411,11 @@ static int ensure_split(rio_ctx *c, uint64_t nchunks) {
     d.fl_ck_n = c->max_chunks + 1;
   }
   d.seg_items = c->flate_split ? flate_seg_items(c->ncu) : 0;
+  if (!d.fl_stage) {  // the Huffman pass's token staging (a wave decodes once per round, then copies)
+    const uint64_t w = flate_stage_words(c->ncu);
+    if (hipMalloc((void **)&d.fl_stage, w * 4) == hipSuccess) d.fl_stage_waves = w / (64ull * 256);
+    else (void)hipGetLastError(), d.fl_stage = nullptr, d.fl_stage_waves = 0;
+  }
   uint64_t want = c->seg_want;
   uint64_t lim = 6 * nchunks * (uint64_t)kChunk;  // (or twice the decode regions: highly compressible blocks)
   if (lim < 2 * c->dec_cap) lim = 2 * c->dec_cap;

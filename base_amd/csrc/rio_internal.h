@@ -201,6 +201,8 @@ struct DevBufs {
   uint64_t seg_cap;              // bytes at seg_scr
   uint64_t seg_items;            // copy-pass waves the split aims to fill (ncu x kL2Waves; 0: no split)
   uint64_t fl_ck_n;              // entries at fl_ck
+  uint32_t *fl_stage;            // Huffman pass: per-wave token staging (k_flate_sync), 0: none
+  uint64_t fl_stage_waves;       // waves it holds columns for
   uint8_t *zlit;                 // zstd: one literal buffer per decoder wave (codec_zstd.hip)
   unsigned long long *zjob;      // zstd: job header offsets (bytes from tok)
   uint64_t zjob_cap;
@@ -217,6 +219,7 @@ struct DevBufs {
 uint64_t zstd_grid(int ncu);             // decoder waves launched
 uint64_t zstd_lit_bytes(uint64_t grid);  // literal buffers for that many waves
 uint64_t flate_seg_items(int ncu);       // copy-pass slots the split copy pass fills
+uint64_t flate_stage_words(int ncu);     // the Huffman pass's token staging (u32 words)
 
 // Kernel argument blocks (kernels.hip, codec.hip; filled by pipeline.cpp).
 struct ParseArgs {

@@ -88,6 +88,12 @@ for s in "$@"; do
           RIO_GPU_LIB=exp_lib/norp/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZEXEC_RESTPAR=0" RIO_BUILD_DIR=exp_lib/norp \
             step c4_norp_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
         done ;;
+    ab_pf) python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        for i in 1 2; do
+          step c4_pf2_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+          RIO_GPU_LIB=exp_lib/pf1/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_ZFIX_PF2=0" RIO_BUILD_DIR=exp_lib/pf1 \
+            step c4_pf1_$i 300 python3 tools/bench_zstd.py --steps 3 --data /tmp/c4.bin
+        done ;;
     zstdt) step zstd_tests 600 python -u -m pytest tests/test_zstd_gpu.py tests/test_zstd_libzstd.py -x -v --timeout 150 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
