@@ -2358,6 +2358,10 @@ __global__ void __launch_bounds__(64) RIO_LZ2_ATTR k_flate_lz2(DevBufs d, const 
 // in order -- the window is final once the segment before it is -- by one
 // lookup per byte. Blocks the scratch cannot hold are copied whole as before.
 constexpr uint32_t kSegRing = 8192, kSegSpan = 3072;
+#ifndef RIO_SEG_W10
+#define RIO_SEG_W10 18  // measured: a u16 segment costs ~1.8x a byte segment per output byte
+#endif
+constexpr uint32_t kSegW10 = RIO_SEG_W10;
 constexpr uint64_t kSegWin = 65536;  // the synthetic window's symbol bytes before a later segment's output
 
 __device__ __forceinline__ uint64_t seg_scratch_bytes(uint32_t o0, uint32_t o1) {
@@ -2369,7 +2373,10 @@ __device__ __forceinline__ uint64_t seg_scratch_bytes(uint32_t o0, uint32_t o1) 
 __global__ void k_flate_plan(DevBufs d, const unsigned long long *nblocks) {
   const uint64_t nb = *nblocks;
   if (nb == 0) return;
-  uint64_t want = (d.seg_items + nb - 1) / nb;
+  // as many segments per block as every one gets a copy-pass slot of its own:
+  // the pass takes as long as its longest wave, so a second segment on a wave
+  // costs more than the split gains
+  uint64_t want = d.seg_items / nb;
   if (want > (uint64_t)kSegMax) want = kSegMax;
   if (want < 2) return;
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
@@ -2385,7 +2392,9 @@ __global__ void k_flate_plan(DevBufs d, const unsigned long long *nblocks) {
     tb[0] = ob[0] = 0;
     uint32_t k = 1;
     for (uint32_t j = 1; j < S; j++) {
-      const uint32_t target = (uint32_t)((uint64_t)olen * j / S);
+      // cut for equal cost: a later segment's byte costs kSegW10 / 10 of segment 0's
+      const uint32_t target =
+          (uint32_t)((uint64_t)olen * (kSegW10 + 10 * (j - 1)) / (kSegW10 + 10 * (S - 1)));
       unsigned long long e = 0;
       while (k < K) {
         e = d.fl_ck[c0 + k];

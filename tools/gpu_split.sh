@@ -41,6 +41,10 @@ for s in "$@"; do
             RIO_BUILD_DIR=exp_lib/root$v step b1k_root$v 300 python3 tools/bench_flate.py --steps 3
         done
         step b1k_base 300 python3 tools/bench_flate.py --steps 3 ;;
+    segw) for w in 10 14 24; do
+          RIO_GPU_LIB=exp_lib/segw$w/librio_gpu.so RIO_BUILD_DIR=exp_lib/segw$w RIO_EXTRA_FLAGS="-DRIO_SEG_W10=$w" \
+            step b16k_segw$w 400 python3 tools/bench_flate.py --per-block 16384 --steps 3
+        done ;;
     ab_bitbuf) for i in 1 2; do
           step b1k_bitbuf_$i 300 python3 tools/bench_flate.py --steps 3
           RIO_GPU_LIB=exp_lib/nobitbuf/librio_gpu.so RIO_EXTRA_FLAGS="-DRIO_SYNC_BITBUF=0" RIO_BUILD_DIR=exp_lib/nobitbuf \
