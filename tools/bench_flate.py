@@ -23,11 +23,14 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
 def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, warmup, device=0, check=True,
-            flate_split=True):
+            flate_split=True, contexts=1):
     """One compressed workload on cuda:`device`: the base file `data` copied to
     HBM, its body replicated `replicas` times; one step = the scan pipeline over
     the whole device-resident span. Parity: the base file's items (device path)
-    against want_fn() by SHA-256 and lengths. Returns the measurement dict."""
+    against want_fn() by SHA-256 and lengths. Returns the measurement dict.
+    contexts > 1: the span is cut at replica boundaries into that many parts, each
+    scanned by its own context (own stream), all launched before any is collected
+    -- a scanner's consecutive spans in flight together."""
     import numpy as np
     import torch
     from base_amd.recordio import gpu
@@ -54,25 +57,30 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
         ctx1.close()
 
     span_len = total - CH
-    ctx = gpu.Context(device, max_span_bytes=total, max_items=nrec * replicas + 1024, item_end=True,
-                      flate_split=flate_split)
-    ptr = dev.data_ptr() + CH
+    nctx = max(1, min(contexts, replicas))
+    cuts = [replicas * k // nctx for k in range(nctx + 1)]  # replica ranges of the parts
+    parts = [(CH + a * len(body), (z - a) * len(body), z - a) for a, z in zip(cuts[:-1], cuts[1:])]
+    ctxs = [gpu.Context(device, max_span_bytes=n + CH, max_items=nrec * r + 1024, item_end=True,
+                        flate_split=flate_split) for _, n, r in parts]
+    base = dev.data_ptr()
 
     def step():
-        ctx.scan_device_async(ptr, span_len, CH, codec)
-        return ctx.sync()
+        for c, (o, n, _) in zip(ctxs, parts):
+            c.scan_device_async(base + o, n, o, codec)
+        return [c.sync() for c in ctxs]
 
-    bb = step()
-    assert bb.stop == gpu.RIO_STOP_EOF and bb.err.code == 0, bb.err.msg
-    assert bb.n_items == nrec * replicas
+    bbs = step()
+    for bb, (_, _, r) in zip(bbs, parts):
+        assert bb.stop == gpu.RIO_STOP_EOF and bb.err.code == 0, bb.err.msg
+        assert bb.n_items == nrec * r
     for _ in range(warmup):
         step()
     stages = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        bb = step()
-        stages.append(ctx.stage_times())
+        bbs = step()
+        stages.append(ctxs[0].stage_times())
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     st = np.mean(np.array(stages), axis=0)
@@ -80,13 +88,17 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
     if check:  # the last timed step's output: every record of every replica, on the GPU
         import devcheck
         w, wl = devcheck.records_tensors(want, dev.device)
-        chk = devcheck.check_replicated(bb, dev[CH:], w, wl, replicas)
+        timed_parity = {"ok": True, "items_checked": 0, "bytes_checked": 0}
+        for bb, (o, n, r) in zip(bbs, parts):
+            chk = devcheck.check_replicated(bb, dev[o:o + n], w, wl, r)
+            timed_parity["ok"] = timed_parity["ok"] and bool(chk["ok"])
+            timed_parity["items_checked"] += chk["items_checked"]
+            timed_parity["bytes_checked"] += chk["bytes_checked"]
         del w, wl
-        timed_parity = {"ok": bool(chk["ok"]), "items_checked": chk["items_checked"],
-                        "bytes_checked": chk["bytes_checked"]}
     out_bytes = rec_bytes * replicas
-    split_blocks = ctx.flate_split_blocks() if codec == gpu.RIO_CODEC_FLATE else 0
-    ctx.close()
+    split_blocks = sum(c.flate_split_blocks() for c in ctxs) if codec == gpu.RIO_CODEC_FLATE else 0
+    for c in ctxs:
+        c.close()
     del dev
     torch.cuda.empty_cache()
     return {
@@ -101,7 +113,7 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
                    "records_bytes": out_bytes},
         "parity": parity and bool(timed_parity and timed_parity["ok"]),
         "parity_timed_output": timed_parity,
-        "split_blocks": split_blocks}
+        "split_blocks": split_blocks, "contexts": nctx}
 
 
 TARGET_RECORD_BYTES = 10 << 30  # configs[2]: 10 GiB of uncompressed records
@@ -113,7 +125,7 @@ def replicas_for(rec_bytes: int) -> int:
 
 
 def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0,
-           flate_split=True):
+           flate_split=True, contexts=1):
     """The C3 workload on cuda:`device` (replicas=0: enough for 10 GiB of records);
     returns the measurement dict (no print). cpu_s > 0 adds the one-core and
     all-core CPU baselines (zlib inflate) on the base file."""
@@ -134,7 +146,7 @@ def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0
         replicas = replicas_for(rec_bytes)
     res = measure(data, nrec, rec_bytes, want, gpu.RIO_CODEC_FLATE,
                   "C3-like flate FASTQ, %d records/block" % per_block, replicas, steps, warmup, device, check,
-                  flate_split)
+                  flate_split, contexts)
     res["config"]["gen_s"] = round(gen_s, 1)
     if cpu_s > 0:
         import cpu_base
@@ -152,9 +164,10 @@ def main():
     ap.add_argument("--per-block", type=int, default=1024)
     ap.add_argument("--cpu-s", type=float, default=0.0)
     ap.add_argument("--no-split", action="store_true", help="copy every block whole (RIO_CFG_FLATE_NO_SPLIT)")
+    ap.add_argument("--contexts", type=int, default=1, help="parts of the span scanned by their own contexts, in flight together")
     args = ap.parse_args()
     print(json.dumps(run_c3(args.base_mib, args.replicas, args.steps, args.warmup, args.per_block,
-                            cpu_s=args.cpu_s, flate_split=not args.no_split)), flush=True)
+                            cpu_s=args.cpu_s, flate_split=not args.no_split, contexts=args.contexts)), flush=True)
 
 
 if __name__ == "__main__":

@@ -41,6 +41,13 @@ for s in "$@"; do
             RIO_BUILD_DIR=exp_lib/root$v step b1k_root$v 300 python3 tools/bench_flate.py --steps 3
         done
         step b1k_base 300 python3 tools/bench_flate.py --steps 3 ;;
+    ctx2) step b16k_c2 400 python3 tools/bench_flate.py --per-block 16384 --steps 3 --contexts 2
+        step b1k_c2 400 python3 tools/bench_flate.py --steps 3 --contexts 2
+        python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        step c4_c1 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 3
+        step c4_c2 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 3 --contexts 2 ;;
+    ctxchk) step ctxchk 300 python3 tools/ctx_check.py --steps 4
+        step ctxchk_serial 300 python3 tools/ctx_check.py --steps 2 --serial ;;
     segw) for w in 10 14 24; do
           RIO_GPU_LIB=exp_lib/segw$w/librio_gpu.so RIO_BUILD_DIR=exp_lib/segw$w RIO_EXTRA_FLAGS="-DRIO_SEG_W10=$w" \
             step b16k_segw$w 400 python3 tools/bench_flate.py --per-block 16384 --steps 3
