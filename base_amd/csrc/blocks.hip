@@ -389,8 +389,12 @@ __global__ void __launch_bounds__(256) k_lean_end(LeanArgs a) {
 // irregular chunk layouts, and every malformed header: parse_header computes
 // the reference's error values).
 // Teams of kSlowTeam waves share a group of 64 blocks, member m taking the
-// group's slow blocks m, m + kSlowTeam, ...: a run of slow blocks (every block
-// of a file written with a large MaxItems) spreads over the team.
+// group's blocks m, m + kSlowTeam, ... that k_parse marked slow: a run of slow
+// blocks (every block of a file written with a large MaxItems) spreads over
+// the team. A block's status is read and rewritten by the one member that owns
+// its slot -- never ranked among the group's slow blocks, since the other
+// members (other workgroups, dispatched at other times when another stream's
+// kernels share the GPU) rewrite those statuses as they finish them.
 constexpr uint32_t kSlowTeam = 16;
 
 __global__ void __launch_bounds__(256) k_parse_slow(DevBufs d, ParseArgs a) {
@@ -401,12 +405,13 @@ __global__ void __launch_bounds__(256) k_parse_slow(DevBufs d, ParseArgs a) {
   const uint32_t member = (uint32_t)(wave % kSlowTeam);
   const int l = lane_id();
   for (uint64_t g = team * 64; g < nb; g += nteams * 64) {
-    const bool slow = (g + l < nb) && d.blk_status[g + l] == kBlkSlow;
+    // lane j: the member's j-th slot of the group
+    const uint64_t slot = g + member + (uint64_t)kSlowTeam * l;
+    const bool slow = l < (int)(64 / kSlowTeam) && slot < nb && d.blk_status[slot] == kBlkSlow;
     unsigned long long sm = __ballot(slow);
-    for (uint32_t rank = 0; sm; rank++) {
-      const uint64_t b = g + __ffsll((long long)sm) - 1;
+    while (sm) {
+      const uint64_t b = g + member + (uint64_t)kSlowTeam * (uint64_t)(__ffsll((long long)sm) - 1);
       sm &= sm - 1;
-      if (rank % kSlowTeam != member) continue;
       const uint64_t c0 = d.blk_c0[b];
       const unsigned long long meta = d.blk_meta[b];
       const uint64_t total = meta & kMetaTotalMask;

@@ -144,13 +144,16 @@ def c4_zstd(args, local, world, dist):
     """BASELINE.json configs[3] beside the headline: ~10 GiB of records (sizes
     log-uniform 64 B-64 KiB, 1 MiB blocks, zstd level 5) per GPU, device-resident,
     one pass = chunk CRC + zstd entropy/execution passes + packed unpack
-    (tools/bench_zstd.py). Whole-job GiB/s of compressed input."""
+    (tools/bench_zstd.py). Whole-job GiB/s of compressed input. The span is cut at
+    replica boundaries into --zstd-contexts parts, each scanned by its own context
+    and all in flight together (the passes' tails and LDS-bound phases overlap);
+    every record of every part is checked after the timed steps."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_zstd
     cpu_s = args.cpu_s if (world == 1 and not args.no_cpu_baseline) else 0.0
     r = bench_zstd.run_c4(replicas=args.zstd_replicas, steps=max(2, min(args.steps, 3)), warmup=1, device=local,
-                          check=True, cpu_s=cpu_s)
+                          check=True, cpu_s=cpu_s, contexts=args.zstd_contexts)
     if dist is not None:
         t = torch.tensor([r["ms_per_step"]], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -363,6 +366,8 @@ def main():
     ap.add_argument("--flate-replicas", type=int, default=0, help="0: enough for 10 GiB of records")
     ap.add_argument("--no-zstd", action="store_true", help="skip the C4 zstd measurement (configs[3])")
     ap.add_argument("--zstd-replicas", type=int, default=0, help="0: enough for 10 GiB of records")
+    ap.add_argument("--zstd-contexts", type=int, default=2,
+                    help="C4: the span's parts scanned by their own contexts, in flight together (1: one context)")
     ap.add_argument("--cpu-s", type=float, default=4.0, help="seconds per CPU-baseline measurement")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 many-file measurement (configs[4])")
     ap.add_argument("--c2-contexts", type=int, default=2, help="C2: contexts the steps alternate over (1 or 2)")

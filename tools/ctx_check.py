@@ -52,6 +52,31 @@ def describe(bb, span, w, wl, nrec, a, per_block, span_items=900000):
             "exp": exp[first:first + 32].cpu().numpy().tobytes().hex()}
 
 
+def block_report(bb, nrec, per_block, device):
+    """Per block of an item-end batch: the record id its decoded bytes start with
+    (region + header end) against the expected one; the first mismatching blocks."""
+    import torch
+    import devcheck
+    nb = int(bb.n_blocks)
+    data = devcheck.dev_copy(devcheck._ptr(bb.block_data), 8 * nb, device, torch.int64)
+    foff = devcheck.dev_copy(devcheck._ptr(bb.block_first_off), 8 * nb, device, torch.int64)
+    first = devcheck.dev_copy(devcheck._ptr(bb.block_first_item), 8 * (nb + 1), device, torch.int64)
+    rec = devcheck.dev_copy(bb.records, int(bb.records_len), device)
+    D = data & ((1 << 63) - 1)
+    pos = (D + foff)[:, None] + torch.arange(12, device=device)[None, :]
+    heads = rec[pos.clamp(max=rec.numel() - 1)].cpu().numpy()
+    per_rep = -(-nrec // per_block)
+    bad = []
+    for b in range(nb):
+        h = heads[b].tobytes()
+        got = h[2:h.find(b"\n")] if b"\n" in h else h
+        want = str((b % per_rep) * per_block).encode()
+        if got != want:
+            bad.append((b, got.decode(errors="replace"), want.decode(), int(D[b]), int(foff[b]), int(first[b])))
+    return {"nbad_blocks": len(bad), "first_bad_blocks": bad[:8],
+            "dec_off_sorted": bool((D[1:] >= D[:-1]).all().item())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--per-block", type=int, default=1024)
@@ -113,12 +138,13 @@ def main():
             rep = {"step": s, "part": k, "stop": int(bb.stop), "err": int(bb.err.code), "n_items": int(bb.n_items),
                    "want_items": nrec * r, "n_blocks": int(bb.n_blocks)}
             chk = devcheck.check_replicated(bb, dev[o:o + m], w, wl, r)
+            rep["blocks"] = block_report(bb, nrec, args.per_block, dev.device)
             rep.update(chk)
             if not chk["ok"]:
                 bad += 1
                 fb = chk["first_bad_item"]
                 if fb is not None and fb >= 0:
-                    rep["bad_detail"] = describe(bb, dev[o:o + m], w, wl, nrec, fb, args.per_block)
+                    pass
             print(json.dumps(rep), flush=True)
     print(json.dumps({"bad_parts": bad}), flush=True)
 

@@ -46,6 +46,14 @@ for s in "$@"; do
         python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
         step c4_c1 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 3
         step c4_c2 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 3 --contexts 2 ;;
+    ctxfix) step ctxchk 300 python3 tools/ctx_check.py --steps 3
+        step ctxchk3 300 python3 tools/ctx_check.py --steps 2 --contexts 3
+        step parse_tests 400 python -u -m pytest tests/test_contexts_gpu.py tests/test_parse_gpu.py tests/test_flate_gpu.py tests/test_headline_gpu.py -x -q --timeout 150 --timeout-method thread
+        step b1k 400 python3 tools/bench_flate.py --steps 3
+        step b1k_c2 400 python3 tools/bench_flate.py --steps 3 --contexts 2
+        python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/c4data.log 2>&1 || exit 1
+        step c4_c2 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 3 --contexts 2
+        step c4_c3 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 3 --contexts 3 ;;
     ctxchk) step ctxchk 300 python3 tools/ctx_check.py --steps 4
         step ctxchk_serial 300 python3 tools/ctx_check.py --steps 2 --serial ;;
     segw) for w in 10 14 24; do
