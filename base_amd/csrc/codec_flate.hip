@@ -1515,6 +1515,78 @@ __device__ __forceinline__ uint32_t sync_decode(const StreamLds &T, const uint32
   return r;
 }
 
+// Counting decode, one code per step (round 4). sync_decode decodes a whole
+// symbol per loop trip -- a literal, or a length code and its distance code --
+// so in a wave whose lanes hold both kinds every trip runs the literal path and
+// the match path one after the other under exec masks (~170 VALU + 66 SALU per
+// trip). Here a trip decodes ONE Huffman code: `sd` says which table (0:
+// literal/length, 1: distance), the entry's fields are picked by selects, and
+// the token, counts and state follow without branches; a match takes two trips,
+// a literal one. Same tokens, counts, staging and exit as sync_decode<false>
+// (the writing decode and this one must agree on the true chain): an
+// undecodable literal/length code skips one bit, an undecodable distance code
+// none (the next trip reads a literal/length code there), a match started
+// before `end` is finished past it, and end-of-block ends the segment.
+template <bool kCount>
+__device__ __forceinline__ uint32_t sync_count(const StreamLds &T, const uint32_t *win, uint32_t r, uint32_t end,
+                                               uint32_t lim, uint32_t &ntok, uint32_t &nout, uint32_t &flags,
+                                               uint32_t *sg, int32_t &slack) {
+  uint32_t dn = (r >> 5) + 2;
+  uint64_t buf = (((uint64_t)win[sync_at(dn - 1)] << 32) | win[sync_at(dn - 2)]) >> (r & 31);
+  uint32_t nb = 64 - (r & 31), nxt = win[sync_at(dn)];
+  uint32_t sd = 0, plen = 0, tn = ntok, on = nout, fl = flags;
+  int32_t sl = slack;
+  const uint32_t endl = end < lim ? end : lim;
+  while ((sd | (uint32_t)(r < endl)) != 0) {
+    const uint32_t low = nb <= 32 ? 1u : 0u;
+    buf |= (uint64_t)(nxt & (0u - low)) << (nb & 63u);
+    dn += low;
+    nb += low << 5;
+    nxt = win[sync_at(dn)];
+    const uint32_t w = (uint32_t)buf;
+    const uint32_t idx = w & (sd ? (1u << kTokDistRoot) - 1 : (1u << kTokLitRoot) - 1);
+    const uint16_t *tab = sd ? T.dst : T.lit;
+    uint32_t e = tab[idx];
+    if ((e & 31) == kLongMark)
+      e = sd ? slow_walk<kTokDistRoot>(T.dfco, T.dent, w) : slow_walk<kTokLitRoot>(T.lfco, T.lent, w);
+    const uint32_t L = e & 15;
+    // extra bits: literal/length (7:5; 7 = end-of-block), distance (10:7)
+    const uint32_t E = __builtin_amdgcn_ubfe(e, sd ? 7u : 5u, sd ? 4u : 3u);
+    const uint32_t lenbit = (e >> 4) & 1u & (sd ^ 1u);  // a length or end-of-block code
+    const uint32_t ok = L != 0 ? 1u : 0u;
+    const uint32_t eob = lenbit & (E == kEobExtra ? 1u : 0u) & ok;
+    const uint32_t lit = (sd | lenbit | (ok ^ 1u)) ^ 1u;
+    const uint32_t len = lenbit & (eob ^ 1u) & ok;
+    const uint32_t dst = sd & ok;
+    const uint32_t k = ok ? (eob ? L : L + E) : (sd ^ 1u);
+    buf >>= k;
+    nb -= k;
+    r += k;
+    fl |= ((ok ^ 1u) * (uint32_t)kSyBad) | (eob * (uint32_t)kSyEob);
+    if (eob) break;
+    // value: literal byte / length - 3 / distance
+    const uint32_t base = sd ? (__builtin_amdgcn_ubfe(e, 5, 2) << E) + 1 : e >> 8;
+    const uint32_t val = base + __builtin_amdgcn_ubfe(w, L, E);
+    if constexpr (kCount) {
+      const uint32_t em = lit | dst;
+      const uint32_t tm = 0x80000000u | (plen << 16) | (val - 1), tl = val | (1u << 24);
+      const uint32_t tv = tm ^ ((tm ^ tl) & (0u - lit));
+      if (em && sg && tn < kSyncStageCap) sg[64 * tn] = tv;
+      const int32_t s2 = (int32_t)on - (int32_t)val;
+      sl = (dst && s2 < sl) ? s2 : sl;
+      on += lit + dst * (plen + 3);
+      tn += em;
+    }
+    plen = len ? val : plen;
+    sd = len;
+  }
+  ntok = tn;
+  nout = on;
+  flags = fl;
+  slack = sl;
+  return r;
+}
+
 // (ablation builds, -DRIO_SYNC_BITBUF=0: the previous decoder, which reads each
 // code's bits from the window at its position -- two LDS reads before every
 // table lookup)
@@ -1761,18 +1833,31 @@ __global__ void __launch_bounds__(64 * kW) RIO_SYNC_ATTR k_flate_sync(const uint
         uint32_t st = r0 + kSyncSeg * g, ex = 0, nt = 0, no = 0, fl = 0;
         int32_t slack = 0;
         bool need = true, conv = false, stg = false;  // stg: this lane's last decode was staged
+        // cnt: this lane's last decode counted its tokens. The first decode of a
+        // round (from the guessed starts) only finds each segment's exit: every
+        // lane but lane 0 decodes again from its predecessor's exit anyway, so
+        // it neither counts nor stages (lane 0 counts in the second iteration)
+        bool cnt = false;
         uint32_t ke = 64 * kW - 1, eob_any = 0;  // the first segment that reached end-of-block
         for (int it = 0; it < kSyncIters; it++) {
-          if (need) {
+          if (need && it == 0) {
+            nt = no = fl = 0;
+            stg = false;
+#if RIO_SYNC_BITBUF
+            ex = sync_count<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, slack);
+#else
+            ex = sync_decode_win<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, 0, 0);
+#endif
+          } else if (need) {
             nt = no = fl = 0;
             slack = 0x7fffffff;
-            // every decode is staged: staging only the ones that are usually the
-            // last (segment 0's first, every later one) left a lane without a
+            cnt = true;
+            // every counted decode is staged: staging only the ones that are usually
+            // the last (segment 0's first, every later one) left a lane without a
             // staged decode in most rounds (41.0 against 35.4 ms for C3)
             stg = sgl != nullptr;
 #if RIO_SYNC_BITBUF
-            ex = sync_decode<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, 0, 0, stg ? sgl : nullptr,
-                                    &slack);
+            ex = sync_count<true>(T, S.win, st, seg_end, lim, nt, no, fl, stg ? sgl : nullptr, slack);
 #else
             ex = sync_decode_win<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, 0, 0);
 #endif
@@ -1785,7 +1870,8 @@ __global__ void __launch_bounds__(64 * kW) RIO_SYNC_ATTR k_flate_sync(const uint
             eob_any = eobm != 0;
             ke = eobm ? __ffsll((long long)eobm) - 1 : 63;
             const uint32_t nst = l == 0 ? r0 : prev;
-            need = g <= ke && nst != st;  // segments after the end keep their start until the end moves
+            // segments after the end keep their start until the end moves
+            need = g <= ke && (nst != st || !cnt);
             if (need) st = nst;
             anyneed = __ballot(need) != 0;
           } else {
@@ -1802,7 +1888,7 @@ __global__ void __launch_bounds__(64 * kW) RIO_SYNC_ATTR k_flate_sync(const uint
             ke = eob_any ? fe : 64u * kW - 1;
             if (l == 0 && wv > 0) prev = S.x.ex63[par][wv - 1];
             const uint32_t nst = g == 0 ? r0 : prev;
-            need = g <= ke && nst != st;
+            need = g <= ke && (nst != st || !cnt);
             if (need) st = nst;
             const bool wneed = __ballot(need) != 0;  // (the whole wave votes, lane 0 writes)
             if (l == 0) S.x.need[par][wv] = wneed;
@@ -2607,7 +2693,8 @@ __global__ void __launch_bounds__(64) k_inflate_exact(const uint8_t *__restrict_
 }
 
 uint64_t flate_seg_items(int ncu) { return (uint64_t)(ncu > 0 ? ncu : 256) * kL2Waves; }
-uint64_t flate_stage_words(int ncu) { return (uint64_t)(ncu > 0 ? ncu : 256) * kSyncWaves * 64 * kSyncStageCap; }
+uint64_t flate_stage_waves(int ncu) { return (uint64_t)(ncu > 0 ? ncu : 256) * kSyncWaves; }
+uint64_t flate_stage_words(int ncu) { return flate_stage_waves(ncu) * 64 * kSyncStageCap; }
 
 static unsigned grid256(uint64_t n) {
   uint64_t g = (n + 255) / 256;
@@ -2615,22 +2702,14 @@ static unsigned grid256(uint64_t n) {
   return (unsigned)(g ? g : 1);
 }
 
-void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
-                    uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st) {
+void launch_inflate_plan(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st);
+
+// The flate decode in two phases, so that the host can size the split copy
+// pass's scratch between them (pipeline.cpp: a context's first split plan).
+// Phase 1: the Huffman pass (k_flate_sync) and the split plan.
+void launch_inflate_huff(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks,
+                         uint64_t max_blocks, uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st) {
   (void)hipMemsetAsync(d.fl_more, 0, sizeof(unsigned long long) * rounds, st);
-  uint64_t g1 = (max_blocks + kVS - 1) / kVS;
-  // resident waves of 8 streams per CU: LDS-bound
-  const uint64_t r1 = (uint64_t)ncu * (163840 / (sizeof(StreamLds) * kVS + sizeof(WaveLds)));
-  if (g1 > r1) g1 = r1;
-  if (d.fl_grid && g1 > d.fl_grid) g1 = d.fl_grid;
-  if (g1 < 1) g1 = 1;
-  uint64_t g2 = max_blocks;
-  const uint64_t r2 = (uint64_t)ncu * 4;  // 36 KiB windows: 4 per CU
-  if (g2 > r2) g2 = r2;
-  if (g2 < 1) g2 = 1;
-  uint64_t g3 = max_blocks;
-  if (g3 > (uint64_t)ncu * kL2Waves) g3 = (uint64_t)ncu * kL2Waves;
-  if (g3 < 1) g3 = 1;
   if (kFlateSync) {  // the wave-per-block Huffman pass first; k_flate_tok takes what it declines
     // one variant runs, by the span's block count (device): one wave per block
     // when the blocks fill the one-wave slots, else kSyncW waves per block
@@ -2654,10 +2733,35 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
     (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(st_ctl), &p, sizeof(p), 0, hipMemcpyHostToDevice, st);
   }
 #endif
-  // few blocks: the copy pass split into segments (k_flate_plan marks the blocks; the
-  // rounds below skip them)
+  launch_inflate_plan(d, nblocks, max_blocks, st);
+}
+
+// few blocks: the copy pass split into segments (k_flate_plan marks the blocks;
+// the copy rounds skip them). Relaunched by the host after it sized the scratch
+// (with ctl->seg_used / seg_blocks reset): blocks it marks are planned once.
+void launch_inflate_plan(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st) {
+  if (kFlateSync && d.seg_items > 0)
+    hipLaunchKernelGGL(k_flate_plan, dim3(grid256(max_blocks)), dim3(256), 0, st, d, nblocks);
+}
+
+// Phase 2: the fallback Huffman pass and copy rounds, the split copy pass, and
+// the exact pass for failing blocks.
+void launch_inflate_copy(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks,
+                         uint64_t max_blocks, uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st) {
+  uint64_t g1 = (max_blocks + kVS - 1) / kVS;
+  // resident waves of 8 streams per CU: LDS-bound
+  const uint64_t r1 = (uint64_t)ncu * (163840 / (sizeof(StreamLds) * kVS + sizeof(WaveLds)));
+  if (g1 > r1) g1 = r1;
+  if (d.fl_grid && g1 > d.fl_grid) g1 = d.fl_grid;
+  if (g1 < 1) g1 = 1;
+  uint64_t g2 = max_blocks;
+  const uint64_t r2 = (uint64_t)ncu * 4;  // 36 KiB windows: 4 per CU
+  if (g2 > r2) g2 = r2;
+  if (g2 < 1) g2 = 1;
+  uint64_t g3 = max_blocks;
+  if (g3 > (uint64_t)ncu * kL2Waves) g3 = (uint64_t)ncu * kL2Waves;
+  if (g3 < 1) g3 = 1;
   const bool split = kFlateSync && d.seg_items > 0;
-  if (split) hipLaunchKernelGGL(k_flate_plan, dim3(grid256(max_blocks)), dim3(256), 0, st, d, nblocks);
   for (int r = 0; r < rounds; r++) {
     hipLaunchKernelGGL(k_flate_tok, dim3((unsigned)g1), dim3(64), 0, st, span, d, nblocks, nchunks,
                        dec_cap, r, (int)(r == rounds - 1));
@@ -2678,6 +2782,12 @@ void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long l
   if (ge > 1024) ge = 1024;
   if (ge < 1) ge = 1;
   hipLaunchKernelGGL(k_inflate_exact, dim3((unsigned)ge), dim3(64), 0, st, span, d, nblocks);
+}
+
+void launch_inflate(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
+                    uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st) {
+  launch_inflate_huff(span, d, nblocks, max_blocks, nchunks, dec_cap, rounds, ncu, st);
+  launch_inflate_copy(span, d, nblocks, max_blocks, nchunks, dec_cap, rounds, ncu, st);
 }
 
 }  // namespace rio

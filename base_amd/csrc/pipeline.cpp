@@ -57,6 +57,12 @@ void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_de
 void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks_dev,
                          uint64_t max_blocks, uint64_t nchunks, int codec, uint64_t dec_cap, int rounds, int ncu,
                          hipStream_t st);
+// codec_flate.hip: the flate decode's two phases (launch_codec_decode runs both)
+void launch_inflate_huff(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks,
+                         uint64_t max_blocks, uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st);
+void launch_inflate_plan(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st);
+void launch_inflate_copy(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks,
+                         uint64_t max_blocks, uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st);
 }  // namespace rio
 
 using namespace rio;
@@ -119,6 +125,7 @@ struct rio_ctx {
   int ev_parse0 = kEvParse0, ev_crc0 = kEvCrc0;  // the events the last run's parse / CRC stages start at
   bool item_end_mode = false;  // RIO_CFG_ITEM_END: device results carry item_end (cumSize)
   bool flate_split = true;     // not RIO_CFG_FLATE_NO_SPLIT
+  bool split_probed = false;   // the first flate run sized the split scratch mid-run (enqueue)
   uint64_t seg_want = 0;       // split copy pass: scratch the last flate run asked for
   bool last_cmp = false;  // the last host result's records are the compacted blocks (d.cmp)
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
@@ -413,7 +420,7 @@ static int ensure_split(rio_ctx *c, uint64_t nchunks) {
   d.seg_items = c->flate_split ? flate_seg_items(c->ncu) : 0;
   if (!d.fl_stage) {  // the Huffman pass's token staging (a wave decodes once per round, then copies)
     const uint64_t w = flate_stage_words(c->ncu);
-    if (hipMalloc((void **)&d.fl_stage, w * 4) == hipSuccess) d.fl_stage_waves = w / (64ull * 256);
+    if (hipMalloc((void **)&d.fl_stage, w * 4) == hipSuccess) d.fl_stage_waves = flate_stage_waves(c->ncu);
     else (void)hipGetLastError(), d.fl_stage = nullptr, d.fl_stage_waves = 0;
   }
   uint64_t want = c->seg_want;
@@ -508,7 +515,30 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     if (codec == RIO_CODEC_ZSTD && ensure_tok(c, nchunks, kZTokPerChunk)) return -1;
     if (codec == RIO_CODEC_ZSTD && (ensure_zlit(c) || ensure_zjob(c, nchunks))) return -1;
     launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
-    launch_codec_decode(span, d, c->nblocks_dev, max_blocks, nchunks, codec, c->dec_cap, c->fl_rounds, c->ncu, st);
+    if (codec == RIO_CODEC_FLATE) {
+      launch_inflate_huff(span, d, c->nblocks_dev, max_blocks, nchunks, c->dec_cap, c->fl_rounds, c->ncu, st);
+      if (d.seg_items && !c->split_probed && d.seg_cap == 0) {
+        // a context's first flate run: the split copy pass needs scratch the
+        // Huffman pass's output decides. Read what the plan asked for, size the
+        // scratch and plan again (seg_used / seg_blocks reset), so the first
+        // scan of a span of few large blocks splits too (later runs grow the
+        // scratch for the next call instead, without a mid-run sync)
+        c->split_probed = true;
+        HIP_OK(hipMemcpyAsync(&c->h_ctl->seg_used, &d.ctl->seg_used, sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (c->h_ctl->seg_used) {
+          c->seg_want = c->h_ctl->seg_used;
+          if (ensure_split(c, nchunks)) return -1;
+          HIP_OK(hipMemsetAsync(&d.ctl->seg_used, 0, sizeof(unsigned long long), st));
+          HIP_OK(hipMemsetAsync(&d.ctl->seg_blocks, 0, sizeof(unsigned long long), st));
+          launch_inflate_plan(d, c->nblocks_dev, max_blocks, st);
+        }
+      }
+      launch_inflate_copy(span, d, c->nblocks_dev, max_blocks, nchunks, c->dec_cap, c->fl_rounds, c->ncu, st);
+    } else {
+      launch_codec_decode(span, d, c->nblocks_dev, max_blocks, nchunks, codec, c->dec_cap, c->fl_rounds, c->ncu, st);
+    }
     c->last_had_dec = true;
   }
   // (an event record costs ~5 us of GPU time between kernels: the stage

@@ -220,6 +220,7 @@ uint64_t zstd_grid(int ncu);             // decoder waves launched
 uint64_t zstd_lit_bytes(uint64_t grid);  // literal buffers for that many waves
 uint64_t flate_seg_items(int ncu);       // copy-pass slots the split copy pass fills
 uint64_t flate_stage_words(int ncu);     // the Huffman pass's token staging (u32 words)
+uint64_t flate_stage_waves(int ncu);     // waves those words hold a staging column set for
 
 // Kernel argument blocks (kernels.hip, codec.hip; filled by pipeline.cpp).
 struct ParseArgs {

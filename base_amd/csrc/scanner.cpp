@@ -367,8 +367,27 @@ void read_header(rio_scanner *s) {
     s->read_serial(hdr, sizeof(hdr), 0, &st);
     uint32_t total;
     memcpy(&total, hdr + 20, 4);
-    if (st == 0 && total > 0) {  // the whole header block, however long (the span grows to it)
-      n = (uint64_t)total * kCk;
+    if (st == 0 && total > 0) {
+      // the header block's chunks as far as their own headers confirm them (same
+      // magic and total, index i at chunk i: ChunkScanner.Scan's checks,
+      // chunk.go:273-286), plus the first chunk that does not -- the GPU pass
+      // reports its error as the reference does. A corrupt `total` (or a file
+      // that is not recordio) thus reads one or two chunks, not the whole file
+      // into the span (the span only grows to a header the headers confirm).
+      uint64_t nck = 1;
+      for (uint64_t i = 1; i < total; i++) {
+        if (i * kCk >= s->file_size) break;
+        nck = i + 1;
+        if ((i + 1) * kCk > s->file_size) break;  // a truncated chunk (unexpected EOF)
+        uint8_t h[RIO_CHUNK_HEADER_SIZE];
+        s->read_serial(h, sizeof(h), i * kCk, &st);
+        if (st != 0) break;
+        uint32_t t2, ix;
+        memcpy(&t2, h + 20, 4);
+        memcpy(&ix, h + 24, 4);
+        if (memcmp(h, hdr, 8) != 0 || t2 != total || ix != i) break;
+      }
+      n = nck * kCk;
       if (n > s->file_size) n = s->file_size;
     }
   }

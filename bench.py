@@ -331,8 +331,23 @@ def c5_flate(args, local, rank, world, dist):
         t = torch.tensor([dt, 0.0 if ok else 1.0], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, ok = float(t[0].item()), t[1].item() == 0.0
-        # the ordered-output prefix: where this rank's records land in the file-set order
-        shard.ordered_prefix(n_items, sum(metas[f % c5_data.N_BASE]["rec_bytes"] for f in mine))
+    # the ordered-output prefix: where this rank's records land in the file-set
+    # order (RCCL all_gather; at N = 1 through a one-rank RCCL group of its own)
+    import torch.distributed as tdist
+    own = not tdist.is_initialized()
+    if own:
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        tdist.init_process_group("gloo" if REHEARSE else "nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                 world_size=1, device_id=None if REHEARSE else torch.device("cuda", local))
+    my_bytes = sum(metas[f % c5_data.N_BASE]["rec_bytes"] for f in mine)
+    pre = shard.ordered_prefix(n_items, my_bytes)
+    prefix = {"backend": tdist.get_backend(), "world": tdist.get_world_size(), "item_offset": pre[0],
+              "byte_offset": pre[1], "total_items": pre[2], "total_bytes": pre[3]}
+    if own:
+        tdist.destroy_process_group()
     for c in ctxs:
         c.close()
     del dev
@@ -340,7 +355,7 @@ def c5_flate(args, local, rank, world, dist):
     return {"metric": "recordio scan GiB/s device-resident (compressed in), C5 1024 trailer-indexed flate files",
             "value": round(all_bytes / dt / 2 ** 30, 2), "unit": "GiB/s", "n_gpus": world,
             "scaling": "strong", "ms_per_step": round(dt * 1e3, 3), "steps": steps, "parity": ok,
-            "parity_files_checked": len(mine), "parity_files_ok": files_ok,
+            "parity_files_checked": len(mine), "parity_files_ok": files_ok, "ordered_prefix": prefix,
             "config": {"files": c5_data.N_FILES, "file_record_bytes": c5_data.FILE_RECORD_BYTES,
                        "records_per_block": c5_data.PER_BLOCK, "distinct_base_files": c5_data.N_BASE,
                        "note": "file f is a copy of base f mod %d (each decoded and checked on its own)"

@@ -48,7 +48,14 @@ enum rio_codec {
  * are untransformed tn-1 first, t0 last (registry.go:121-146). As a codec
  * argument: RIO_CODEC_CHAIN(n, t0 | t1 << 2 | t2 << 4 | t3 << 6). Host-
  * synchronous calls only (rio_scan_span, rio_scan_device, rio_decode_block,
- * the scanner layer): each stage is a launch over the previous stage's output. */
+ * the scanner layer): each stage is a launch over the previous stage's output.
+ * Known divergence (parity with the reference unpinned for chains): the
+ * reference's combined untransformer passes the same `scratch` to every stage
+ * (registry.go:127-140), so a later stage may write its output over the earlier
+ * stage's output while still reading it (zstd.Decompress(scratch, in[0]) with
+ * in[0] inside scratch, recordiozstd.go:71-72; FlateUncompress into
+ * bytes.Buffer(scratch[:0]), recordioflate.go:54-65). The GPU decodes the clean
+ * composition of the stages; the chain test cases are oracle-derived. */
 #define RIO_CODEC_CHAIN_FLAG 0x10000
 #define RIO_CODEC_CHAIN(n, codes) (RIO_CODEC_CHAIN_FLAG | ((n) << 8) | (codes))
 

@@ -6,9 +6,11 @@ Every record must equal the generator's and the unsplit decode's, for DEFLATE
 streams of every block type (stored, fixed, dynamic; levels 0-9) and for long
 runs that cross the segment boundaries.
 
-The first scan on a context sizes the split scratch (its blocks are copied
-whole unless a retry of that call already has it); the second one splits. Both are checked, and the split count is read
-back (rio_flate_split_blocks) so the test fails if nothing was split.
+A context's first flate scan sizes the split scratch between the Huffman pass
+and the copy pass (round 4; before, the first scan copied its blocks whole and
+only later scans split), so the first scan splits as well as the second. Both
+are checked, and the split count is read back (rio_flate_split_blocks) so the
+test fails if nothing was split.
 """
 import os
 import sys
@@ -67,7 +69,7 @@ def _check(blocks):
     want = [r for recs, _ in blocks for r in recs]
     data = _file(blocks)
     got, nsplit = _scans(data, len(want), True)
-    assert nsplit[1] > 0, nsplit  # sized by the first run (or its retry), split in the second
+    assert nsplit[0] > 0 and nsplit[1] > 0, nsplit  # the first run sizes the scratch mid-run and splits
     for items in got:
         assert len(items) == len(want)
         assert items == want

@@ -97,9 +97,10 @@ def test_rank_shard_and_file_assignment():
     assert sorted(loads, reverse=True) == [64, 45, 41]  # largest first onto the least-loaded rank
 
 
-def _split_worker(rank, world, port, data, q, on_gpu=False):
+def _split_worker(rank, world, port, data, q, on_gpu=False, backend="gloo"):
     """scan_file_split on one rank: trailer index broadcast from rank 0, this
-    rank's block range decoded (GPU batch, or the oracle on CPU)."""
+    rank's block range decoded (GPU batch, or the oracle on CPU). backend "nccl"
+    (RCCL) needs on_gpu: the collectives' tensors live on cuda:0."""
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -108,7 +109,13 @@ def _split_worker(rank, world, port, data, q, on_gpu=False):
     import torch.distributed as dist
     import c5_data
     from base_amd.recordio import shard
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", 0))
+        assert dist.get_backend() == "nccl"
+    else:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         hdr_end = int.from_bytes(data[20:24], "little") * 32768
         if on_gpu:
@@ -132,12 +139,17 @@ def _split_worker(rank, world, port, data, q, on_gpu=False):
                 return O.scan(d).trailer
         recs, off, total = shard.scan_file_split(data, rank, world, c5_data.parse_index, scan_range,
                                                  read_trailer=read_trailer)
+        if backend == "nccl":  # the other two collectives on their own (RCCL on this rank's GPU)
+            blob = bytes(range(256)) * 3 + b"index"
+            assert shard.broadcast_bytes(blob if rank == 0 else None, 0) == blob
+            assert shard.broadcast_bytes(b"" if rank == 0 else None, 0) == b""
+            assert shard.ordered_prefix(7, 1000) == (7 * rank, 1000 * rank, 7 * world, 1000 * world)
         q.put((rank, off, total, recs))
     finally:
         dist.destroy_process_group()
 
 
-def _run_split(world, on_gpu=False):
+def _run_split(world, on_gpu=False, backend="gloo"):
     import sys
     import torch.multiprocessing as mp
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -148,7 +160,7 @@ def _run_split(world, on_gpu=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_split_worker, args=(r, world, port, data, q, on_gpu)) for r in range(world)]
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, data, q, on_gpu, backend)) for r in range(world)]
     for p in procs:
         p.start()
     got = sorted(q.get(timeout=300) for _ in range(world))
@@ -184,3 +196,12 @@ def test_split_blocks_ranges():
 @pytest.mark.gpu
 def test_index_split_two_ranks_gpu(gpu_lib):
     _run_split(2, on_gpu=True)
+
+
+@pytest.mark.gpu
+def test_index_split_rccl_world1(gpu_lib):
+    """The RCCL ("nccl") branches of shard.broadcast_bytes / ordered_prefix /
+    scan_file_split on the GPU box: a world-size-1 process group on cuda:0 in a
+    fresh spawned process (no GPU call before its init), a C5-shaped file split by
+    its trailer index and decoded on the GPU (the 8-rank run is the driver's)."""
+    _run_split(1, on_gpu=True, backend="nccl")

@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
 def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, warmup, device=0, check=True,
-            flate_split=True, contexts=1):
+            flate_split=True, contexts=1, pipeline=1):
     """One compressed workload on cuda:`device`: the base file `data` copied to
     HBM, its body replicated `replicas` times; one step = the scan pipeline over
     the whole device-resident span. Parity: the base file's items (device path)
@@ -60,29 +60,55 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
     nctx = max(1, min(contexts, replicas))
     cuts = [replicas * k // nctx for k in range(nctx + 1)]  # replica ranges of the parts
     parts = [(CH + a * len(body), (z - a) * len(body), z - a) for a, z in zip(cuts[:-1], cuts[1:])]
-    ctxs = [gpu.Context(device, max_span_bytes=n + CH, max_items=nrec * r + 1024, item_end=True,
-                        flate_split=flate_split) for _, n, r in parts]
+    npipe = max(1, pipeline)
+    # pipeline > 1: consecutive steps alternate over that many context sets, step i
+    # launched before step i - 1 is collected (a scanner's read-ahead: one span's
+    # copy pass beside the next span's Huffman pass)
+    sets = [[gpu.Context(device, max_span_bytes=n + CH, max_items=nrec * r + 1024, item_end=True,
+                         flate_split=flate_split) for _, n, r in parts] for _ in range(npipe)]
+    ctxs = sets[0]
     base = dev.data_ptr()
 
-    def step():
-        for c, (o, n, _) in zip(ctxs, parts):
+    def launch(cs):
+        for c, (o, n, _) in zip(cs, parts):
             c.scan_device_async(base + o, n, o, codec)
-        return [c.sync() for c in ctxs]
 
-    bbs = step()
-    for bb, (_, _, r) in zip(bbs, parts):
-        assert bb.stop == gpu.RIO_STOP_EOF and bb.err.code == 0, bb.err.msg
-        assert bb.n_items == nrec * r
-    for _ in range(warmup):
-        step()
+    for cs in sets:  # (every context's first scan sizes its buffers)
+        launch(cs)
+        bbs = [c.sync() for c in cs]
+        for bb, (_, _, r) in zip(bbs, parts):
+            assert bb.stop == gpu.RIO_STOP_EOF and bb.err.code == 0, bb.err.msg
+            assert bb.n_items == nrec * r
+
+    def run(n, record):
+        out, pending = None, None
+        for i in range(n):
+            cs = sets[i % npipe]
+            launch(cs)
+            if npipe == 1:
+                out = [c.sync() for c in cs]
+                if record:
+                    stages.append(cs[0].stage_times())
+                continue
+            if pending is not None:
+                out = [c.sync() for c in pending]
+                if record:
+                    stages.append(pending[0].stage_times())
+            pending = cs
+        if pending is not None:
+            out = [c.sync() for c in pending]
+            if record:
+                stages.append(pending[0].stage_times())
+        return out, (pending or ctxs)
+
     stages = []
+    run(warmup, False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        bbs = step()
-        stages.append(ctxs[0].stage_times())
+    bbs, last = run(steps, True)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    stages = stages or [[0.0] * 5]
     st = np.mean(np.array(stages), axis=0)
     timed_parity = None
     if check:  # the last timed step's output: every record of every replica, on the GPU
@@ -96,9 +122,10 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
             timed_parity["bytes_checked"] += chk["bytes_checked"]
         del w, wl
     out_bytes = rec_bytes * replicas
-    split_blocks = sum(c.flate_split_blocks() for c in ctxs) if codec == gpu.RIO_CODEC_FLATE else 0
-    for c in ctxs:
-        c.close()
+    split_blocks = sum(c.flate_split_blocks() for c in last) if codec == gpu.RIO_CODEC_FLATE else 0
+    for cs in sets:
+        for c in cs:
+            c.close()
     del dev
     torch.cuda.empty_cache()
     return {
@@ -113,7 +140,7 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
                    "records_bytes": out_bytes},
         "parity": parity and bool(timed_parity and timed_parity["ok"]),
         "parity_timed_output": timed_parity,
-        "split_blocks": split_blocks, "contexts": nctx}
+        "split_blocks": split_blocks, "contexts": nctx, "pipeline": npipe}
 
 
 TARGET_RECORD_BYTES = 10 << 30  # configs[2]: 10 GiB of uncompressed records
@@ -125,7 +152,7 @@ def replicas_for(rec_bytes: int) -> int:
 
 
 def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0,
-           flate_split=True, contexts=1):
+           flate_split=True, contexts=1, pipeline=1):
     """The C3 workload on cuda:`device` (replicas=0: enough for 10 GiB of records);
     returns the measurement dict (no print). cpu_s > 0 adds the one-core and
     all-core CPU baselines (zlib inflate) on the base file."""
@@ -146,7 +173,7 @@ def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0
         replicas = replicas_for(rec_bytes)
     res = measure(data, nrec, rec_bytes, want, gpu.RIO_CODEC_FLATE,
                   "C3-like flate FASTQ, %d records/block" % per_block, replicas, steps, warmup, device, check,
-                  flate_split, contexts)
+                  flate_split, contexts, pipeline)
     res["config"]["gen_s"] = round(gen_s, 1)
     if cpu_s > 0:
         import cpu_base
@@ -165,9 +192,12 @@ def main():
     ap.add_argument("--cpu-s", type=float, default=0.0)
     ap.add_argument("--no-split", action="store_true", help="copy every block whole (RIO_CFG_FLATE_NO_SPLIT)")
     ap.add_argument("--contexts", type=int, default=1, help="parts of the span scanned by their own contexts, in flight together")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="steps alternate over this many context sets, each launched before the previous is collected")
     args = ap.parse_args()
     print(json.dumps(run_c3(args.base_mib, args.replicas, args.steps, args.warmup, args.per_block,
-                            cpu_s=args.cpu_s, flate_split=not args.no_split, contexts=args.contexts)), flush=True)
+                            cpu_s=args.cpu_s, flate_split=not args.no_split, contexts=args.contexts,
+                            pipeline=args.pipeline)), flush=True)
 
 
 if __name__ == "__main__":

@@ -40,7 +40,7 @@ def load_or_make(base_mib, workers, path=None):
 
 
 def run_c4(base_mib=128, replicas=0, steps=5, warmup=1, device=0, check=True, cpu_s=0.0, workers=16, data_path=None,
-           contexts=1):
+           contexts=1, pipeline=1):
     """The C4 workload (replicas=0: enough for 10 GiB of records); cpu_s > 0 adds
     the one-core and all-core CPU baselines (libzstd) on the base file."""
     import bench_flate
@@ -54,7 +54,8 @@ def run_c4(base_mib=128, replicas=0, steps=5, warmup=1, device=0, check=True, cp
         replicas = bench_flate.replicas_for(rec_bytes)
     res = bench_flate.measure(data, nrec, rec_bytes, lambda: c4_data.all_records(nblk), gpu.RIO_CODEC_ZSTD,
                               "C4-like zstd level 5, records 64 B-64 KiB log-uniform, 1 MiB blocks",
-                              replicas, steps, warmup, device, check, contexts=contexts)
+                              replicas, steps, warmup, device, check, contexts=contexts,
+                              pipeline=pipeline)
     res["config"]["gen_s"] = round(gen_s, 1)
     if cpu_s > 0:
         import cpu_base
@@ -74,12 +75,15 @@ def main():
     ap.add_argument("--data", default=None, help="cache the base file here (load it if present)")
     ap.add_argument("--make-data", action="store_true", help="only write --data, no GPU")
     ap.add_argument("--contexts", type=int, default=1, help="parts of the span scanned by their own contexts, in flight together")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="steps alternate over this many context sets, each launched before the previous is collected")
     args = ap.parse_args()
     if args.make_data:
         load_or_make(args.base_mib, args.workers, args.data)
         return
     print(json.dumps(run_c4(args.base_mib, args.replicas, args.steps, args.warmup, cpu_s=args.cpu_s,
-                            workers=args.workers, data_path=args.data, contexts=args.contexts)), flush=True)
+                            workers=args.workers, data_path=args.data, contexts=args.contexts,
+                            pipeline=args.pipeline)), flush=True)
 
 
 if __name__ == "__main__":

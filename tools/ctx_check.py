@@ -143,8 +143,8 @@ def main():
             if not chk["ok"]:
                 bad += 1
                 fb = chk["first_bad_item"]
-                if fb is not None and fb >= 0:
-                    pass
+                if fb is not None and fb >= 0:  # the first bad item's block and bytes
+                    rep["bad_detail"] = describe(bb, dev[o:o + m], w, wl, nrec, fb, args.per_block)
             print(json.dumps(rep), flush=True)
     print(json.dumps({"bad_parts": bad}), flush=True)
 
