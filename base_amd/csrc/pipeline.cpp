@@ -126,6 +126,7 @@ struct rio_ctx {
   bool item_end_mode = false;  // RIO_CFG_ITEM_END: device results carry item_end (cumSize)
   bool flate_split = true;     // not RIO_CFG_FLATE_NO_SPLIT
   bool split_probed = false;   // the first flate run sized the split scratch mid-run (enqueue)
+  rio_stats stats{};           // host-path counters (rio_ctx_stats)
   uint64_t seg_want = 0;       // split copy pass: scratch the last flate run asked for
   bool last_cmp = false;  // the last host result's records are the compacted blocks (d.cmp)
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
@@ -663,6 +664,7 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
   HIP_OK(hipMemcpyAsync(first, c->d.blk_item_base, (nb + 1) * 8, hipMemcpyDeviceToHost, c->st));
   if (nb) HIP_OK(hipMemcpyAsync(foff, c->d.blk_c0, nb * 8, hipMemcpyDeviceToHost, c->st));
   HIP_OK(hipStreamSynchronize(c->st));
+  c->stats.d2h_bytes += k.rec_bytes + 16 * k.n_items + 8 * (2 * nb + 1);
   for (uint64_t b = 0; b < nb; b++) foff[b] = file_off + foff[b] * kChunk;
   out->records = r.records;
   out->item_off = reinterpret_cast<const uint64_t *>(h_off);
@@ -895,6 +897,13 @@ extern "C" int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbyt
 static int stage_span(rio_ctx *c, const uint8_t *span, uint64_t nbytes) {
   if (!c->d_span) HIP_OK(hipMalloc((void **)&c->d_span, c->max_span + kChunk));
   HIP_OK(hipMemcpyAsync(c->d_span, span, nbytes, hipMemcpyHostToDevice, c->st));
+  c->stats.h2d_bytes += nbytes;
+  return 0;
+}
+
+extern "C" int rio_ctx_stats(rio_ctx *ctx, rio_stats *out) {
+  if (!ctx || !out) return -1;
+  *out = ctx->stats;
   return 0;
 }
 
@@ -920,6 +929,8 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
   float ms = 0;
   hipEventElapsedTime(&ms, t0, t1);
   out->total_ms = ms;
+  ctx->stats.spans++;
+  ctx->stats.device_ms += ms;
   hipEventDestroy(t0);
   hipEventDestroy(t1);
   return rc;
@@ -1456,6 +1467,7 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
       for (const V1Job &j : rj) memcpy(c->h_v1 + j.off, span + j.span_off, j.hbytes);
       HIP_OK(hipMemcpyAsync(c->d_v1, c->h_v1, staged, hipMemcpyHostToDevice, c->st));
       HIP_OK(hipMemcpyAsync(c->d_v1_jobs, rj.data(), rj.size() * sizeof(V1Job), hipMemcpyHostToDevice, c->st));
+      c->stats.h2d_bytes += staged + rj.size() * sizeof(V1Job);
       HIP_OK(hipEventRecord(c->ev[kEvStart], c->st));
       launch_v1_unpack(c->d_v1, c->d_v1_jobs, rj.size(), c->d_v1_off, c->d_v1_len, c->d_v1_res, c->st);
       HIP_OK(hipGetLastError());
@@ -1476,6 +1488,7 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
     HIP_OK(hipMemcpyAsync(h_off, c->d_v1_off, items * 8, hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipMemcpyAsync(h_len, c->d_v1_len, items * 8, hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipStreamSynchronize(c->st));
+    c->stats.d2h_bytes += 16 * items;
     for (size_t k = 0; k < jobs.size(); k++) {  // the first packed record that failed ends the batch there
       const V1Res &x = jr[k];
       if (x.status == kV1Ok) continue;
@@ -1539,6 +1552,8 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
   out->stop = stop;
   out->in_bytes = nbytes;
   out->kernel_ms = kms;
+  c->stats.spans++;
+  c->stats.device_ms += kms;
   if (err) out->err = e;
   else if (stop == RIO_STOP_MORE && nrec == 0) out->err.a = need;  // the next record needs a span this large
   return 0;

@@ -92,6 +92,11 @@ class RioEncodeArgs(ctypes.Structure):
 RIO_BLOCK_BODY, RIO_BLOCK_HEADER, RIO_BLOCK_TRAILER = 0, 1, 2
 
 
+class RioStats(ctypes.Structure):
+    _fields_ = [("spans", ctypes.c_uint64), ("h2d_bytes", ctypes.c_uint64), ("d2h_bytes", ctypes.c_uint64),
+                ("device_ms", ctypes.c_double)]
+
+
 class RioMemory(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("size", ctypes.c_uint64)]
 
@@ -104,7 +109,7 @@ EXPORTS = [
     "rio_scanner_header_len", "rio_scanner_header_kv", "rio_scanner_trailer", "rio_scanner_seek",
     "rio_scanner_location", "rio_scanner_version", "rio_scanner_finish", "rio_scanner_gather",
     "rio_memory_reader", "rio_scan_v1_span", "rio_encode", "rio_encode_device", "rio_build_id",
-    "rio_scan_device_segments_async", "rio_flate_split_blocks",
+    "rio_scan_device_segments_async", "rio_flate_split_blocks", "rio_ctx_stats",
 ]
 
 _lib = None
@@ -123,6 +128,8 @@ def load(path: str = LIB_PATH):
         B.check_lib(path)  # refuses a library not built from this tree's sources
         L = ctypes.CDLL(path)
         L.rio_build_id.restype = ctypes.c_char_p
+        L.rio_ctx_stats.restype = ctypes.c_int
+        L.rio_ctx_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(RioStats)]
         L.rio_flate_split_blocks.restype = ctypes.c_uint64
         L.rio_flate_split_blocks.argtypes = [ctypes.c_void_p]
         L.rio_scan_device_segments_async.restype = ctypes.c_int
@@ -328,6 +335,13 @@ class Context:
         if self.L.rio_sync(self.h, ctypes.byref(out)) != 0:
             raise RuntimeError("rio_sync: " + self.L.rio_last_error().decode())
         return out
+
+    def stats(self) -> dict:
+        """rio_ctx_stats: host spans scanned, bytes copied in and out, device ms."""
+        st = RioStats()
+        self.L.rio_ctx_stats(self.h, ctypes.byref(st))
+        return {"spans": int(st.spans), "h2d_bytes": int(st.h2d_bytes), "d2h_bytes": int(st.d2h_bytes),
+                "device_ms": float(st.device_ms)}
 
     def flate_split_blocks(self) -> int:
         """Flate blocks of the last completed run copied as segments (split copy pass)."""

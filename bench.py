@@ -140,6 +140,33 @@ def c3_flate(args, local, world, dist):
     return r
 
 
+def c3_flate_16k(args, local, world, dist):
+    """BASELINE.json configs[2] at the reference writer's default block size:
+    MaxItems = 16384 (recordio/writerv2.go:28-29), i.e. 16,385 records per block
+    (~5 MB blocks; SURVEY.md §8(d) C3's sensitivity point), the same ~10 GiB of
+    records. Steps alternate over two contexts (--flate16k-pipeline), each
+    launched before the previous step is collected -- a scanner's read-ahead of
+    its next span: one step's copy pass runs beside the next step's Huffman pass
+    (a span of 2,158 blocks fills neither pass alone). `serial` is the same steps
+    one at a time. Every record of the last timed step is checked."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_flate
+    r = bench_flate.run_c3(replicas=args.flate_replicas, steps=max(2, min(args.steps, 5)), warmup=2,
+                           per_block=16384, device=local, check=True, pipeline=args.flate16k_pipeline)
+    if dist is not None:
+        t = torch.tensor([r["ms_per_step"]], device=coll_dev(local), dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+        r["value"] = round(r["config"]["span_bytes"] * world / (ms * 1e-3) / 2 ** 30, 2)
+        r["ms_per_step"] = round(ms, 3)
+    r["n_gpus"] = world
+    r["target_GiBs"] = 40.0
+    moved = (r["config"]["span_bytes"] + r["config"]["records_bytes"]) * world
+    r["hbm_frac"] = round(moved / (r["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    return r
+
+
 def c4_zstd(args, local, world, dist):
     """BASELINE.json configs[3] beside the headline: ~10 GiB of records (sizes
     log-uniform 64 B-64 KiB, 1 MiB blocks, zstd level 5) per GPU, device-resident,
@@ -153,7 +180,7 @@ def c4_zstd(args, local, world, dist):
     import bench_zstd
     cpu_s = args.cpu_s if (world == 1 and not args.no_cpu_baseline) else 0.0
     r = bench_zstd.run_c4(replicas=args.zstd_replicas, steps=max(2, min(args.steps, 3)), warmup=1, device=local,
-                          check=True, cpu_s=cpu_s, contexts=args.zstd_contexts)
+                          check=True, cpu_s=cpu_s, contexts=args.zstd_contexts, pipeline=args.zstd_pipeline)
     if dist is not None:
         t = torch.tensor([r["ms_per_step"]], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -381,8 +408,15 @@ def main():
     ap.add_argument("--flate-replicas", type=int, default=0, help="0: enough for 10 GiB of records")
     ap.add_argument("--no-zstd", action="store_true", help="skip the C4 zstd measurement (configs[3])")
     ap.add_argument("--zstd-replicas", type=int, default=0, help="0: enough for 10 GiB of records")
-    ap.add_argument("--zstd-contexts", type=int, default=2,
+    ap.add_argument("--zstd-contexts", type=int, default=1,
                     help="C4: the span's parts scanned by their own contexts, in flight together (1: one context)")
+    ap.add_argument("--zstd-pipeline", type=int, default=2,
+                    help="C4: steps alternate over this many contexts, each launched before the previous is "
+                         "collected (1: one step at a time; the line reports that rate as `serial` too)")
+    ap.add_argument("--no-flate16k", action="store_true", help="skip C3 at MaxItems 16384 (configs[2] sensitivity)")
+    ap.add_argument("--flate16k-pipeline", type=int, default=2, help="C3 at MaxItems 16384: contexts steps alternate over")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host file in, records out) line")
+    ap.add_argument("--e2e-gib", type=float, default=2.0, help="end-to-end: file size per workload")
     ap.add_argument("--cpu-s", type=float, default=4.0, help="seconds per CPU-baseline measurement")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 many-file measurement (configs[4])")
     ap.add_argument("--c2-contexts", type=int, default=2, help="C2: contexts the steps alternate over (1 or 2)")
@@ -548,10 +582,16 @@ def main():
     torch.cuda.empty_cache()
     if not args.no_flate:
         out["c3_flate"] = c3_flate(args, local, world, dist)
+    if not args.no_flate16k:
+        out["c3_flate_16k"] = c3_flate_16k(args, local, world, dist)
     if not args.no_zstd:
         out["c4_zstd"] = c4_zstd(args, local, world, dist)
     if not args.no_c5:
         out["c5_flate"] = c5_flate(args, local, rank, world, dist)
+    if world == 1 and not args.no_e2e:  # the drop-in path, PCIe included (north_star)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_e2e
+        out["e2e"] = bench_e2e.run_e2e(local, args.e2e_gib)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["cpu_baseline_all_cores"], out["c1_cpu"] = cpu_baselines(args)
     if rank == 0:

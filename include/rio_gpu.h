@@ -214,6 +214,17 @@ const char *rio_build_id(void);
 /* the HIP stream the ctx launches on (hipStream_t as void*) */
 void *rio_stream(rio_ctx *ctx);
 
+/* Host-path counters of a ctx since rio_open: the end-to-end (PCIe-inclusive)
+ * accounting of rio_scan_span / rio_scan_v1_span and the scanner layer's spans
+ * (no reference counterpart: the Go scanner reads and copies on the host). */
+typedef struct rio_stats {
+    uint64_t spans;     /* host spans scanned */
+    uint64_t h2d_bytes; /* bytes copied host -> device (the spans) */
+    uint64_t d2h_bytes; /* bytes copied device -> host (records, item views, block tables) */
+    double device_ms;   /* HIP-event time of those calls: copies in, pipeline, copies out */
+} rio_stats;
+int rio_ctx_stats(rio_ctx *ctx, rio_stats *out);
+
 /* Transformer registry lookup (registry.go:113-148 + recordioflate/zstd Init):
  * resolves the header's "transformer" values to a codec -- none, flate, zstd,
  * or a RIO_CODEC_CHAIN of 2-4 of flate / zstd. Returns 0 and sets *codec, or

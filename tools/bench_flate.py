@@ -103,6 +103,15 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
 
     stages = []
     run(warmup, False)
+    serial = None
+    if npipe > 1:  # the same steps one at a time on one context set, for comparison
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            launch(ctxs)
+            for c in ctxs:
+                c.sync()
+        serial = (time.perf_counter() - t0) / steps
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     bbs, last = run(steps, True)
@@ -140,7 +149,10 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
                    "records_bytes": out_bytes},
         "parity": parity and bool(timed_parity and timed_parity["ok"]),
         "parity_timed_output": timed_parity,
-        "split_blocks": split_blocks, "contexts": nctx, "pipeline": npipe}
+        "split_blocks": split_blocks, "contexts": nctx, "pipeline": npipe,
+        "serial": None if serial is None else {
+            "value": round(span_len / serial / 2 ** 30, 2), "ms_per_step": round(serial * 1e3, 3),
+            "note": "the same steps one at a time (each collected before the next is launched)"}}
 
 
 TARGET_RECORD_BYTES = 10 << 30  # configs[2]: 10 GiB of uncompressed records

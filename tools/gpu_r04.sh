@@ -48,6 +48,8 @@ while [ $# -gt 0 ]; do
     c4_c2) c4data; step c4_c2 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 3 --contexts 2 ;;
     c4_p2) c4data; step c4_p2 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 4 --pipeline 2 ;;
     bench) step bench 900 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchnc5) step benchnc5 900 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-c5 --no-e2e ;;
+    e2e) c4data; step e2e 600 python3 tools/bench_e2e.py ;;
     full) step full 1100 python3 bench.py ;;
     prof16k) step prof16k 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof16k -o run -- \
         python3 tools/bench_flate.py --per-block 16384 --steps 2 ;;
