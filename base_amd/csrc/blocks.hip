@@ -252,6 +252,9 @@ struct LeanArgs {
   uint64_t limit_chunk, item_cap;
 };
 
+constexpr int kLeanHdrLanes = 32;  // header window lanes loaded (16 B each)
+constexpr int kLeanBndLanes = 16;  // boundary window lanes loaded either side of the chunk boundary
+
 __global__ void __launch_bounds__(256) k_lean_end(LeanArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_win[4][1040];
   __shared__ __attribute__((aligned(16))) uint16_t s_tpos[4][264];
@@ -261,33 +264,60 @@ __global__ void __launch_bounds__(256) k_lean_end(LeanArgs a) {
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const int l = lane_id();
-  // lane j < 4 holds descriptor field j of the wave's next block
+  // lane j < 4 holds descriptor field j of a block. Software-pipelined (round
+  // 4): while block b is parsed, block b + nwaves's windows and block
+  // b + 2 nwaves's descriptor are in flight, so a block's loads are waited for
+  // one block later (gfx9 vmcnt counts in order)
   const unsigned long long *dsrc = l == 0 ? a.blk_c0 : l == 1 ? a.blk_meta : l == 2 ? a.blk_len : a.blk_item_base;
+  auto lean_ok = [&](unsigned long long dsc) {
+    const uint64_t c0 = readlane_u64(dsc, 0);
+    const unsigned long long meta = readlane_u64(dsc, 1), len = readlane_u64(dsc, 2);
+    const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
+    return (meta & kMetaComplete) && (meta & kMetaRegular) && cls == kMagicPacked && c0 < a.limit_chunk &&
+           len < (1ull << 32);
+  };
+  // the header window's first 512 B and 256 B either side of the chunk
+  // boundary (a C2 block's 508-byte header and 256-byte straddler); a longer
+  // header or a straddler outside goes to k_parse (was: both 1 KiB windows
+  // whole, 2 KiB fetched per 65 KiB block)
+  auto fetch = [&](unsigned long long dsc, bool ok, uint32_t (&w)[4], uint32_t (&bnd)[4]) {
+    w[0] = w[1] = w[2] = w[3] = 0x80808080u;
+    bnd[0] = bnd[1] = bnd[2] = bnd[3] = 0;
+    if (!ok) return;
+    const uint64_t c0 = readlane_u64(dsc, 0);
+    const unsigned long long meta = readlane_u64(dsc, 1), len = readlane_u64(dsc, 2);
+    const uint8_t *ck = a.span + c0 * kChunk;
+    const uint32_t size0 = len < (uint64_t)kMaxPayload ? (uint32_t)len : (uint32_t)kMaxPayload;
+    if (l < kLeanHdrLanes && 16u * l + 16 <= size0) {  // 4-byte aligned: 28 + 16 l
+      const uint4 v = *reinterpret_cast<const uint4 *>(ck + kChunkHdr + 16 * l);
+      w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+    }
+    if ((meta & kMetaTotalMask) >= 2 && l >= 32 - kLeanBndLanes && l < 32 + kLeanBndLanes) {
+      // payload kBndW0 + 16 l: chunk c0's tail, then c0 + 1's head
+      const uint8_t *src = (l < 32) ? ck + kChunkHdr + kBndW0 + 16 * l : ck + kChunk + kChunkHdr + 16 * (l - 32);
+      const uint4 v = *reinterpret_cast<const uint4 *>(src);
+      bnd[0] = v.x, bnd[1] = v.y, bnd[2] = v.z, bnd[3] = v.w;
+    }
+  };
   unsigned long long desc = (l < 4 && wave < nb) ? dsrc[wave] : 0;
+  bool ok_nx = wave < nb && lean_ok(desc);
+  uint32_t w_nx[4], bnd_nx[4];
+  fetch(desc, ok_nx, w_nx, bnd_nx);
+  unsigned long long desc_nx = (l < 4 && wave + nwaves < nb) ? dsrc[wave + nwaves] : 0;
   for (uint64_t b = wave; b < nb; b += nwaves) {
     const uint64_t c0 = readlane_u64(desc, 0);
     const unsigned long long meta = readlane_u64(desc, 1), len = readlane_u64(desc, 2);
     const uint64_t base = readlane_u64(desc, 3);
-    const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
-    const uint64_t nck = meta & kMetaTotalMask;
-    const bool ok = (meta & kMetaComplete) && (meta & kMetaRegular) && cls == kMagicPacked && c0 < a.limit_chunk &&
-                    len < (1ull << 32);
-    uint32_t w[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u}, bnd[4] = {0, 0, 0, 0};
-    const uint8_t *ck = a.span + c0 * kChunk;
-    if (ok) {
-      const uint32_t size0 = len < (uint64_t)kMaxPayload ? (uint32_t)len : (uint32_t)kMaxPayload;
-      if (16u * l + 16 <= size0) {  // 4-byte aligned: 28 + 16 l
-        const uint4 v = *reinterpret_cast<const uint4 *>(ck + kChunkHdr + 16 * l);
-        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
-      }
-      if (nck >= 2) {  // payload kBndW0 + 16 l: chunk c0's tail, then c0 + 1's head
-        const uint8_t *src = (l < 32) ? ck + kChunkHdr + kBndW0 + 16 * l : ck + kChunk + kChunkHdr + 16 * (l - 32);
-        const uint4 v = *reinterpret_cast<const uint4 *>(src);
-        bnd[0] = v.x, bnd[1] = v.y, bnd[2] = v.z, bnd[3] = v.w;
-      }
-    }
-    const uint64_t bn = b + nwaves;  // the next block's descriptor, in flight while this one is parsed
-    desc = (l < 4 && bn < nb) ? dsrc[bn] : 0;
+    const bool ok = ok_nx;
+    uint32_t w[4], bnd[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[k] = w_nx[k], bnd[k] = bnd_nx[k];
+    // the next block's windows and the one after's descriptor, in flight while this one is parsed
+    const uint64_t bn = b + nwaves;
+    ok_nx = bn < nb && lean_ok(desc_nx);
+    fetch(desc_nx, ok_nx, w_nx, bnd_nx);
+    desc = desc_nx;
+    desc_nx = (l < 4 && bn + nwaves < nb) ? dsrc[bn + nwaves] : 0;
     bool done = false;
     uint32_t hdr = 0;
     if (ok) {
@@ -335,15 +365,17 @@ __global__ void __launch_bounds__(256) k_lean_end(LeanArgs a) {
           wrap |= carry + add < carry;
           carry += add;
         }
-        // straddlers: only across the first chunk boundary, inside the boundary
-        // window (written from the registers); any other crossing is declined
+        // straddlers: only across the first chunk boundary, inside the loaded
+        // part of the boundary window (written from the registers); any other
+        // crossing is declined
+        constexpr uint32_t W0 = (uint32_t)kMaxPayload - 16 * kLeanBndLanes, W1 = W0 + 32 * kLeanBndLanes;
         bool far = false, sd[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           const uint32_t s_ = st[k], e_ = st[k] + v[k];
           sd[k] = v[k] > 0 && s_ < (uint32_t)kMaxPayload && e_ > (uint32_t)kMaxPayload;
           far |= v[k] > 0 && s_ / (uint32_t)kMaxPayload != (e_ - 1) / (uint32_t)kMaxPayload &&
-                 !(sd[k] && s_ >= kBndW0 && e_ <= kBndW0 + 1024);
+                 !(sd[k] && s_ >= W0 && e_ <= W1);
         }
         if (!__ballot(lng || bad || wrap || far) && carry == plen) {
           done = true;

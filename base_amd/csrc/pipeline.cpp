@@ -152,8 +152,8 @@ struct rio_ctx {
   // transformed payloads; host-path staging of items, ends and output
   unsigned long long *e_blk = nullptr;
   uint64_t e_blk_cap = 0;
-  uint8_t *e_hdr = nullptr, *e_comp = nullptr, *e_data = nullptr, *e_out = nullptr;
-  uint64_t e_hdr_cap = 0, e_comp_cap = 0, e_data_cap = 0, e_out_cap = 0;
+  uint8_t *e_hdr = nullptr, *e_comp = nullptr, *e_comp2 = nullptr, *e_data = nullptr, *e_out = nullptr;
+  uint64_t e_hdr_cap = 0, e_comp_cap = 0, e_comp2_cap = 0, e_data_cap = 0, e_out_cap = 0;
   unsigned long long *e_zscr = nullptr;  // zstd / dynamic flate encode: the waves' sequence / token lists
   uint64_t e_zscr_cap = 0;
   ZeTabs *e_ztab = nullptr;              // zstd encode: predefined FSE tables (uploaded once)
@@ -232,7 +232,7 @@ static void free_all(rio_ctx *c) {
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.blk_data, d.blk_file_off, d.blk_seg, d.cmp, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.fl_ck, d.fl_seg, d.seg_scr, d.fl_stage, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len,
-                c->e_blk, c->e_hdr, c->e_comp, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan, c->d_seg, c->d_chain[0], c->d_chain[1], c->d_chain_meta};
+                c->e_blk, c->e_hdr, c->e_comp, c->e_comp2, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan, c->d_seg, c->d_chain[0], c->d_chain[1], c->d_chain_meta};
   for (void *p : ps)
     if (p) hipFree(p);
   if (c->h_ctl) hipHostFree(c->h_ctl);
@@ -1622,32 +1622,55 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
   if (egrow(&c->e_hdr, &c->e_hdr_cap, hdr_total + 16)) return -1;
   ea.hdr = c->e_hdr;
   launch_enc_header(ea, st);
-  if (ea.codec == RIO_CODEC_FLATE) {  // the payloads compressed into comp (deflate_enc.hip)
-    launch_deflate_bound(ea, st);
-    launch_chunk_scan(ea.nck, ea.comp_off, c->e_scan, nb, st);
-    unsigned long long comp_total = 0;
-    HIP_OK(hipMemcpyAsync(&comp_total, ea.comp_off + nb, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (egrow(&c->e_comp, &c->e_comp_cap, comp_total + 64)) return -1;
-    if (ea.level != 0 && ea.level != 1 && egrow(&c->e_zscr, &c->e_zscr_cap, deflate_scratch_words(c->ncu))) return -1;
-    ea.comp = c->e_comp;
-    launch_deflate(ea, c->e_zscr, c->ncu, st);
-  } else if (ea.codec == RIO_CODEC_ZSTD) {  // one frame per payload (zstd_enc.hip)
-    launch_zstd_enc_bound(ea, st);
-    launch_chunk_scan(ea.nck, ea.comp_off, c->e_scan, nb, st);
-    unsigned long long comp_total = 0;
-    HIP_OK(hipMemcpyAsync(&comp_total, ea.comp_off + nb, 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (egrow(&c->e_comp, &c->e_comp_cap, comp_total + 64)) return -1;
-    if (egrow(&c->e_zscr, &c->e_zscr_cap, zstd_enc_scratch_words(c->ncu))) return -1;
-    if (!c->e_ztab) {
-      ZeTabs t;
-      ze_build_tabs(t);
-      if (dalloc(&c->e_ztab, 1)) return -1;
-      HIP_OK(hipMemcpy(c->e_ztab, &t, sizeof(t), hipMemcpyHostToDevice));
+  // the transformers in order (writerv2.go:432-441 with registry.go:75-111's
+  // combined transform: stage k transforms stage k - 1's output). A stage
+  // after the first reads the previous stage's compressed payloads as its
+  // blocks' "headers" (hdr_len = their lengths, no item bytes), the mirror of
+  // the scan's k_reframe; stages alternate between two compressed buffers.
+  int nst = 1;
+  int32_t stc[4] = {ea.codec, 0, 0, 0}, stl[4] = {ea.level, 0, 0, 0};
+  if (ea.codec & RIO_CODEC_CHAIN_FLAG) {
+    nst = (ea.codec >> 8) & 0xff;
+    for (int k = 0; k < nst; k++) {
+      stc[k] = (ea.codec >> (2 * k)) & 3;
+      stl[k] = (int32_t)(int8_t)(uint8_t)((uint32_t)ea.level >> (8 * k));  // a signed byte per stage
     }
-    ea.comp = c->e_comp;
-    launch_zstd_enc(ea, c->e_ztab, c->e_zscr, c->ncu, st);
+  }
+  for (int k = 0; k < nst && stc[0] != RIO_CODEC_NONE; k++) {
+    uint8_t **buf = (k & 1) ? &c->e_comp2 : &c->e_comp;
+    uint64_t *cap = (k & 1) ? &c->e_comp2_cap : &c->e_comp_cap;
+    if (k > 0) {  // the previous stage's payloads become this stage's input
+      HIP_OK(hipMemcpyAsync(ea.hdr_len, ea.pay_len, (nb + 1) * 8, hipMemcpyDeviceToDevice, st));
+      HIP_OK(hipMemcpyAsync(ea.hdr_off, ea.comp_off, (nb + 1) * 8, hipMemcpyDeviceToDevice, st));
+      ea.hdr = ea.comp;
+    }
+    ea.codec = stc[k];
+    ea.level = stl[k];
+    if (ea.codec == RIO_CODEC_FLATE) {  // the payloads compressed into comp (deflate_enc.hip)
+      launch_deflate_bound(ea, st);
+    } else {  // one zstd frame per payload (zstd_enc.hip)
+      launch_zstd_enc_bound(ea, st);
+    }
+    launch_chunk_scan(ea.nck, ea.comp_off, c->e_scan, nb, st);
+    unsigned long long comp_total = 0;
+    HIP_OK(hipMemcpyAsync(&comp_total, ea.comp_off + nb, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (egrow(buf, cap, comp_total + 64)) return -1;
+    ea.comp = *buf;
+    if (ea.codec == RIO_CODEC_FLATE) {
+      if (ea.level != 0 && ea.level != 1 && egrow(&c->e_zscr, &c->e_zscr_cap, deflate_scratch_words(c->ncu)))
+        return -1;
+      launch_deflate(ea, c->e_zscr, c->ncu, st);
+    } else {
+      if (egrow(&c->e_zscr, &c->e_zscr_cap, zstd_enc_scratch_words(c->ncu))) return -1;
+      if (!c->e_ztab) {
+        ZeTabs t;
+        ze_build_tabs(t);
+        if (dalloc(&c->e_ztab, 1)) return -1;
+        HIP_OK(hipMemcpy(c->e_ztab, &t, sizeof(t), hipMemcpyHostToDevice));
+      }
+      launch_zstd_enc(ea, c->e_ztab, c->e_zscr, c->ncu, st);
+    }
   }
   launch_enc_nck(ea, st);
   launch_chunk_scan(ea.nck, ea.ck0, c->e_scan, nb, st);
@@ -1677,8 +1700,19 @@ static int encode_dev(rio_ctx *c, const rio_encode_args *a, const uint8_t *data,
 
 static int encode_check(rio_ctx *ctx, const rio_encode_args *a, rio_error *err) {
   if (!ctx || !a) return -1;
-  if (a->codec != RIO_CODEC_NONE && a->codec != RIO_CODEC_FLATE && a->codec != RIO_CODEC_ZSTD) {
-    rio_set_error(err, RIO_ERR_ARG, 0, "encode: codec %d not supported (none, flate, zstd)", a->codec);
+  bool codec_ok = a->codec == RIO_CODEC_NONE || a->codec == RIO_CODEC_FLATE || a->codec == RIO_CODEC_ZSTD;
+  if (a->codec & RIO_CODEC_CHAIN_FLAG) {  // 1-4 stages, each flate or zstd
+    const int n = (a->codec >> 8) & 0xff;
+    codec_ok = n >= 1 && n <= 4 && (a->codec & ~(RIO_CODEC_CHAIN_FLAG | 0xffff)) == 0;
+    for (int k = 0; codec_ok && k < n; k++) {
+      const int ck = (a->codec >> (2 * k)) & 3;
+      codec_ok = ck == RIO_CODEC_FLATE || ck == RIO_CODEC_ZSTD;
+    }
+    if (codec_ok && (a->codec & 0xff) >> (2 * n)) codec_ok = false;  // codes past the n stages
+  }
+  if (!codec_ok) {
+    rio_set_error(err, RIO_ERR_ARG, 0, "encode: codec %d not supported (none, flate, zstd, a chain of 1-4 of those)",
+                  a->codec);
     return RIO_ERR_ARG;
   }
   if (a->kind < RIO_BLOCK_BODY || a->kind > RIO_BLOCK_TRAILER) {

@@ -11,9 +11,12 @@ here the items between two block-ending calls (Flush, SetTrailer, Finish) are
 kept and encoded by rio_encode calls of up to `batch_bytes` of whole blocks
 each -- once a run holds `batch_bytes`, its whole blocks are encoded early -- so
 thousands of blocks go through one launch. Errors stick as the reference's
-errors.Once does: a transformer config that does not parse (NewWriter), or a
-flate level outside [-2, 9] (the first transformed block), stops every later
-write and is reported by Err() / Finish().
+errors.Once does: an unknown transformer name or a config that does not parse
+(NewWriter sets them on err, writerv2.go:318-320), or a flate level outside
+[-2, 9] (the first transformed block), stops every later write and is reported
+by Err() / Finish(). Transformer chains (2-4 of flate / zstd) encode in one
+rio_encode call per batch (RIO_CODEC_CHAIN: each stage re-reads the previous
+stage's payloads).
 The Index callback runs after a block's location is known, as in the
 reference (writerv2.go:458-470: after serialisation, before the write)."""
 from __future__ import annotations
@@ -57,22 +60,40 @@ class GpuWriter:
         self.batch_bytes = batch_bytes
         self.n_written = 0
         self.err: Optional[Exception] = None
-        # transformers: none, or one "flate" / "flate N" (recordioflate.go:31-52: N = 0
-        # stored blocks, 1 fixed Huffman, otherwise dynamic Huffman per 32 KiB, the
-        # smaller of dynamic / fixed) or "zstd" / "zstd N" (recordiozstd.go:31-52)
+        # transformers (registry.go:75-111, applied in order at writerv2.go:432-441):
+        # none, or 1-4 of "flate" / "flate N" (recordioflate.go:31-52: N = 0 stored
+        # blocks, 1 fixed Huffman, otherwise dynamic Huffman per 32 KiB, the smaller
+        # of dynamic / fixed) and "zstd" / "zstd N" (recordiozstd.go:31-52); two or
+        # more are one RIO_CODEC_CHAIN encode, stage k transforming stage k - 1's
+        # output. As NewWriter does (writerv2.go:318-320), a name the registry does
+        # not hold or a config that does not parse is set on err, not raised.
         self.codec, self.level = gpu.RIO_CODEC_NONE, 0
-        if opts.Transformers:
-            name, _, arg = opts.Transformers[0].partition(" ")
-            if len(opts.Transformers) != 1 or name not in ("flate", "zstd"):
-                raise ValueError("GpuWriter encodes none or one flate / zstd transformer (got %r)"
-                                 % (opts.Transformers,))
-            self.codec = gpu.RIO_CODEC_FLATE if name == "flate" else gpu.RIO_CODEC_ZSTD
-            self.level = -1
+        self.stages = []  # (codec, level) per transformer
+        for t in opts.Transformers:
+            name, _, arg = t.partition(" ")  # registry.go:54-64: split on the first space
+            if name not in ("flate", "zstd"):
+                self._set_err(RuntimeError("Transformer %s not found" % t))
+                break
+            level = -1
             if arg:
-                try:  # a config error is NewWriter's: w.err.Set (writerv2.go:318-320)
-                    self.level = _atoi(arg)
+                try:  # strconv.Atoi of the config (recordioflate.go:76-81, recordiozstd.go:19-25)
+                    level = _atoi(arg)
                 except RuntimeError as e:
                     self._set_err(e)
+                    break
+            self.stages.append((gpu.RIO_CODEC_FLATE if name == "flate" else gpu.RIO_CODEC_ZSTD, level))
+        if self.err is None and len(self.stages) > 4:
+            self._set_err(RuntimeError("GpuWriter: at most 4 transformers encode on the GPU (got %d)"
+                                       % len(self.stages)))
+        if self.err is None and len(self.stages) == 1:
+            self.codec, self.level = self.stages[0]
+        elif self.err is None and self.stages:
+            self.codec = gpu.codec_chain(*[c for c, _ in self.stages])
+            self.level = 0
+            for k, (_, lv) in enumerate(self.stages):  # stage k's level: a signed byte (rio_gpu.h)
+                self.level |= (max(-128, min(127, lv)) & 0xFF) << (8 * k)
+            if self.level >= 1 << 31:
+                self.level -= 1 << 32  # (int32)
         self.header = []
         self.state = _BODY if opts.SkipHeader else _INITIAL
         if not opts.SkipHeader:
@@ -91,9 +112,11 @@ class GpuWriter:
     def _transform_err(self):
         """The error klauspost's flate.NewWriter returns on the first block a
         transform runs on (recordioflate.go:31-34: levels outside
-        [HuffmanOnly, BestCompression] = [-2, 9])."""
-        if self.codec == gpu.RIO_CODEC_FLATE and not -2 <= self.level <= 9:
-            return RuntimeError("flate: invalid compression level %d: want value in range [-2, 9]" % self.level)
+        [HuffmanOnly, BestCompression] = [-2, 9]); in a chain, the first flate
+        stage that has one (the stages run in order)."""
+        for codec, level in self.stages:
+            if codec == gpu.RIO_CODEC_FLATE and not -2 <= level <= 9:
+                return RuntimeError("flate: invalid compression level %d: want value in range [-2, 9]" % level)
         return None
 
     def _write(self, data: bytes):

@@ -331,7 +331,12 @@ typedef struct rio_encode_args {
     int32_t level;             /* flate: 0 stored blocks (NoCompression), 1 fixed-Huffman
                                   blocks, otherwise (the default -1 included) a dynamic- or
                                   fixed-Huffman block per 32 KiB, whichever is smaller; both
-                                  with greedy hash matches */
+                                  with greedy hash matches.
+                                  codec = RIO_CODEC_CHAIN(n, t0 | t1 << 2 | ...) (1 <= n <= 4,
+                                  each flate or zstd): the writer's transformers in order,
+                                  stage k transforming stage k - 1's output (registry.go:75-111,
+                                  writerv2.go:432-441); stage k's level is the signed byte
+                                  (level >> 8k) & 0xff (0xff = -1, the default) */
     int32_t reserved;
 } rio_encode_args;
 /* Host memory in and out: writes the chunk stream to out (out_cap bytes) and

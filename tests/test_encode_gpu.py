@@ -304,3 +304,85 @@ def test_encode_zstd_decodes(gpu_ctx, oracle):
         k += 1
     assert k == 4
     assert comp < 0.75 * plain, (comp, plain)
+
+
+def _undo_payload(pay, chain):
+    """A block payload with the chain's stages undone last first (zlib raw
+    inflate, libzstd) -- the reference's GetUntransformer order (registry.go:121-146)."""
+    import zlib
+    from base_amd.recordio.codecs import zstd_decompress_ref
+    for t in reversed(chain):
+        if t.split(" ")[0] == "flate":
+            pay = zlib.decompress(pay, -15)
+        else:
+            pay = zstd_decompress_ref(pay, 64 * len(pay) + (1 << 20))
+    return pay
+
+
+@pytest.mark.gpu
+def test_encode_chains_decode(gpu_ctx, oracle):
+    """Write-side transformer chains (registry.go:75-111, applied in order at
+    writerv2.go:432-441): 2- and 3-stage files written on the GPU (one
+    RIO_CODEC_CHAIN encode per batch) read back identical through the oracle and
+    the GPU scanner; every block payload is the stages applied in order (zlib /
+    libzstd undo them, last first)."""
+    from base_amd.recordio import gpu
+    from base_amd.recordio.codecs import have_zstd
+    from conftest import oracle_has_zstd
+    if not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    rng = random.Random(11)
+    sets = [fastq_records(rng, 2000), records(rng, 200), [b""] * 30, [b"y" * 90000] * 3]
+    chains = (["zstd", "flate"], ["flate 1", "zstd", "flate"], ["flate", "flate 0"], ["zstd 5", "zstd"],
+              ["flate", "zstd", "flate 1", "zstd"])
+    for chain in chains:
+        for i, recs in enumerate(sets):
+            data = gpu_write(recs, WriterOpts(Transformers=chain, MaxItems=rng.choice([1, 60, 700])),
+                             trailer=b"chain-trailer", ctx=gpu_ctx, batch_bytes=1 << 18)
+            ref = oracle.scan(data)
+            assert ref.err == "" and ref.items == recs and ref.trailer == b"chain-trailer", (chain, i)
+            sc = gpu.NewScanner(data, ctx=gpu_ctx)
+            got = []
+            while sc.Scan():
+                got.append(sc.Get())
+            assert sc.Finish() is None and got == recs, (chain, i)
+    if not have_zstd():
+        return
+    recs = fastq_records(rng, 600)
+    for chain in (["zstd", "flate"], ["flate 1", "zstd", "flate"]):
+        data = gpu_write(recs, WriterOpts(Transformers=chain, MaxItems=149), ctx=gpu_ctx)
+        off, k = 32768, 0
+        while off < len(data):
+            total = int.from_bytes(data[off + 20:off + 24], "little")
+            pay = b"".join(data[off + c * 32768 + 28: off + c * 32768 + 28 +
+                                int.from_bytes(data[off + c * 32768 + 16:off + c * 32768 + 20], "little")]
+                           for c in range(total))
+            assert _undo_payload(pay, chain) == F.packed_block_payload(recs[k * 150:(k + 1) * 150]), (chain, k)
+            off += total * 32768
+            k += 1
+        assert k == 4
+
+
+@pytest.mark.gpu
+def test_writer_transformer_list_errors(gpu_ctx):
+    """NewWriter's transformer errors go to err (writerv2.go:318-320), not raised:
+    a name the registry does not hold ("Transformer %s not found",
+    registry.go:58, the whole value), a config that does not parse, anywhere in
+    a chain; nothing is written. A chain's flate stage with a level outside
+    [-2, 9] fails the first transformed block (the header is written)."""
+    from base_amd.recordio.gpu_writer import GpuWriter
+    for tl, msg in ((["snappy"], "Transformer snappy not found"),
+                    (["zstd", "lz4 3"], "Transformer lz4 3 not found"),
+                    (["flate", "zstd x"], 'strconv.Atoi: parsing "x": invalid syntax')):
+        buf = io.BytesIO()
+        w = GpuWriter(buf, WriterOpts(Transformers=tl), ctx=gpu_ctx)
+        assert str(w.Err()) == msg
+        w.Append(b"abc")
+        assert str(w.Finish()) == msg and buf.getvalue() == b"", tl
+    buf = io.BytesIO()
+    w = GpuWriter(buf, WriterOpts(Transformers=["zstd", "flate 12"], MaxItems=3), ctx=gpu_ctx)
+    assert w.Err() is None
+    for i in range(10):
+        w.Append(b"item %d" % i)
+    assert str(w.Finish()) == "flate: invalid compression level 12: want value in range [-2, 9]"
+    assert len(buf.getvalue()) == 32768

@@ -37,9 +37,12 @@ while [ $# -gt 0 ]; do
         python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread -k "$1" ;;
     testf) shift; step "pytest_$(basename "$1" .py)" 600 \
         python -u -m pytest "$1" -v --timeout 150 --timeout-method thread ;;
-    c2) step c2 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-zstd --no-c5 ;;
-    c2c1) step c2c1 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-zstd --no-c5 \
-        --c2-contexts 1 ;;
+    c2) step c2 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-flate16k --no-zstd \
+        --no-c5 --no-e2e ;;
+    c2c1) step c2c1 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-flate16k --no-zstd \
+        --no-c5 --no-e2e --c2-contexts 1 ;;
+    profc2) step profc2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc2 -o run -- \
+        python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-flate --no-flate16k --no-zstd --no-c5 --no-e2e ;;
     b1k) step b1k 400 python3 tools/bench_flate.py --steps 3 ;;
     b1k_p2) step b1k_p2 400 python3 tools/bench_flate.py --steps 4 --pipeline 2 ;;
     b16k) step b16k 400 python3 tools/bench_flate.py --per-block 16384 --steps 3 ;;
