@@ -181,6 +181,15 @@ struct rio_ctx {
   unsigned long long *d_seg = nullptr;
   uint64_t d_seg_cap = 0;
   std::vector<uint64_t> seg_end_h, seg_file_h;
+  // transformer chains through the async entries: the stages ran at the call
+  // (each needs the previous one's block sizes on the host); rio_sync returns
+  // chain_batch. chain_c0: stage 1's block chunk indexes (the file's), on the
+  // host and (for segment scans) on the device
+  bool chain_async = false;
+  rio_batch chain_batch{};
+  std::vector<unsigned long long> chain_c0;
+  unsigned long long *d_chain_c0 = nullptr;
+  uint64_t d_chain_c0_cap = 0;
   // transformer chains: the reframed stage outputs (two, alternating) and their chunk offsets
   uint8_t *d_chain[2] = {nullptr, nullptr};
   uint64_t d_chain_cap[2] = {0, 0};
@@ -837,6 +846,7 @@ static int run_chain(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_spa
     HIP_OK(hipMemcpy(c0.data(), c->d.blk_c0, nv * 8, hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(olen.data(), c->d.blk_out_len, nv * 8, hipMemcpyDeviceToHost));
   }
+  c->chain_c0 = c0;
   Ctl last = s1;      // the latest stage's control block
   bool later_err = false;
   for (int k = n - 2; k >= 0 && nv > 0; k--) {
@@ -944,11 +954,21 @@ extern "C" int rio_scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes,
 extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes, uint64_t file_off,
                                      int32_t codec) {
   if (!ctx) return -1;
-  if (codec & RIO_CODEC_CHAIN_FLAG) {  // each stage needs the previous one's block sizes on the host
-    set_last_error("a transformer chain decodes through rio_scan_device / rio_scan_span, not the async entry");
-    return -1;
-  }
   HIP_OK(hipSetDevice(ctx->device));
+  if (codec & RIO_CODEC_CHAIN_FLAG) {
+    // a chain's stages run here, one after the other (each needs the previous
+    // one's block sizes on the host): the call returns when they are done and
+    // rio_sync hands back their batch
+    ctx->last_nseg = 0;
+    ctx->chain_async = false;
+    memset(&ctx->chain_batch, 0, sizeof(ctx->chain_batch));
+    if (run_span(ctx, (const uint8_t *)dev_span, (const uint8_t *)dev_span, nbytes, file_off, 1, UINT64_MAX, codec,
+                 kModeBody, nullptr, &ctx->chain_batch))
+      return -1;
+    ctx->chain_async = true;
+    ctx->last_codec = codec;
+    return 0;
+  }
   const uint64_t nchunks = nbytes / kChunk;
   if (nchunks > ctx->max_chunks) {
     set_last_error("span exceeds ctx capacity");
@@ -993,15 +1013,37 @@ extern "C" int rio_scan_device_segments_async(rio_ctx *ctx, const void *dev_span
   }
   if (rio_scan_device_async(ctx, dev_span, nbytes, 0, codec)) return -1;
   ctx->last_nseg = nseg;
-  if (nseg)
+  if (nseg && ctx->chain_async) {
+    // the last stage's blocks are stage 1's, in order: their segments and
+    // file offsets from stage 1's chunk indexes (the last stage's are of its
+    // reframed span)
+    const uint64_t nv = ctx->chain_c0.size();
+    if (ctx->d_chain_c0_cap < nv + 1) {
+      if (dalloc(&ctx->d_chain_c0, nv + 1)) return -1;
+      ctx->d_chain_c0_cap = nv + 1;
+    }
+    if (nv) HIP_OK(hipMemcpy(ctx->d_chain_c0, ctx->chain_c0.data(), nv * 8, hipMemcpyHostToDevice));
+    DevBufs d1 = ctx->d;
+    d1.blk_c0 = ctx->d_chain_c0;
+    launch_block_files(d1, ctx->d_seg, ctx->d_seg + nseg, nseg, nv ? nv : 1, ctx->st);
+  } else if (nseg) {
     launch_block_files(ctx->d, ctx->d_seg, ctx->d_seg + nseg, nseg, ctx->last_nchunks ? ctx->last_nchunks : 1,
                        ctx->st);
+  }
   return 0;
 }
+
+static int sync_segments(rio_ctx *ctx, rio_batch *out);
 
 extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
   if (!ctx || !out) return -1;
   HIP_OK(hipSetDevice(ctx->device));
+  if (ctx->chain_async) {  // a chain's batch (its stages ran at the async call)
+    ctx->chain_async = false;
+    HIP_OK(hipStreamSynchronize(ctx->st));
+    *out = ctx->chain_batch;
+    return sync_segments(ctx, out);
+  }
   HIP_OK(hipMemcpyAsync(ctx->h_ctl, ctx->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->st));
   HIP_OK(hipStreamSynchronize(ctx->st));
   note_split(ctx);
@@ -1030,7 +1072,12 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
     rio_set_error(&out->err, RIO_ERR_CAPACITY, 0, "output capacity exceeded");
     out->stop = RIO_STOP_ERROR;
   }
-  if (ctx->last_nseg) {  // segment scan: per-block files, and the error's file
+  return sync_segments(ctx, out);
+}
+
+// segment scans: per-block files, and the error's file
+static int sync_segments(rio_ctx *ctx, rio_batch *out) {
+  if (ctx->last_nseg) {
     out->block_file_off = reinterpret_cast<const uint64_t *>(ctx->d.blk_file_off);
     out->block_segment = reinterpret_cast<const uint64_t *>(ctx->d.blk_seg);
     if (out->stop == RIO_STOP_ERROR) {

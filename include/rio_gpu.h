@@ -46,9 +46,11 @@ enum rio_codec {
 /* A chain of transformers (the header's "transformer" values t0 .. tn-1, 2 <=
  * n <= 4, each flate or zstd): blocks were transformed by t0 first, so they
  * are untransformed tn-1 first, t0 last (registry.go:121-146). As a codec
- * argument: RIO_CODEC_CHAIN(n, t0 | t1 << 2 | t2 << 4 | t3 << 6). Host-
- * synchronous calls only (rio_scan_span, rio_scan_device, rio_decode_block,
- * the scanner layer): each stage is a launch over the previous stage's output.
+ * argument: RIO_CODEC_CHAIN(n, t0 | t1 << 2 | t2 << 4 | t3 << 6). Each stage
+ * is a launch over the previous stage's output and needs its block sizes on
+ * the host, so the async entries (rio_scan_device_async,
+ * rio_scan_device_segments_async) run a chain's stages at the call and
+ * rio_sync returns their batch (per-block segments and file offsets included).
  * Known divergence (parity with the reference unpinned for chains): the
  * reference's combined untransformer passes the same `scratch` to every stage
  * (registry.go:127-140), so a later stage may write its output over the earlier

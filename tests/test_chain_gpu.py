@@ -3,7 +3,8 @@ Transformers [t0, t1, ...] is untransformed tn-1 first. The golden chain cases
 run in test_gpu_parity.test_golden_cases; here the other entry points: the
 batch layer (host and device results, both output shapes), rio_decode_block,
 Seek / Gather, sharded scans, corrupt streams against the oracle, and the async
-entry's refusal (each stage needs the previous one's sizes on the host)."""
+entries (rio_scan_device_async, rio_scan_device_segments_async: a chain's
+stages run at the call, rio_sync returns the batch)."""
 import os
 import random
 import struct
@@ -92,8 +93,10 @@ def test_chain_batch_layer(oracle, chain_files, item_end):
                                  codec=_codec(trs))
             assert bd.stop == gpu.RIO_STOP_EOF and bd.err.code == 0, (trs, bd.err.msg)
             assert gpu.device_batch_items(bd, body) == recs
-            with pytest.raises(RuntimeError):
-                ctx.scan_device_async(dev.data_ptr(), len(body), _body(data), _codec(trs))
+            ctx.scan_device_async(dev.data_ptr(), len(body), _body(data), _codec(trs))
+            ba = ctx.sync()
+            assert ba.stop == gpu.RIO_STOP_EOF and ba.err.code == 0, (trs, ba.err.msg)
+            assert gpu.device_batch_items(ba, body) == recs
     finally:
         ctx.close()
 
@@ -164,3 +167,72 @@ def test_golden_chain_cases_decode(gpu_ctx, manifest):
             h.update(struct.pack("<Q", len(it)))
             h.update(it)
         assert len(items) == case["n_items"] and h.hexdigest() == case["items_sha256"]
+
+
+def test_chain_segments_scan(oracle, chain_files):
+    """Chained files through the many-file launch (rio_scan_device_segments_async,
+    configs[4]'s path): the bodies of every chain file of one chain back to back
+    with different records each; every block's file (block_segment) and its
+    ItemLocation.Block in that file (block_file_off, the oracle's locations), the
+    records of each file; a corrupt stream in the second file stops the batch
+    there in that file's coordinates, the first file's records delivered."""
+    import ctypes
+    import zlib
+    import numpy as np
+    import torch
+    from base_amd.recordio import gpu, shard
+    from base_amd.recordio.writer import WriterOpts, write_file
+    rng = random.Random(23)
+    for trs in (("zstd", "flate"), ("flate", "zstd", "flate 1")):
+        recs = [[rng.randbytes(rng.choice([5, 90, 2000])) * rng.choice([1, 8]) for _ in range(n)]
+                for n in (300, 77, 410)]
+        datas = [write_file(r, WriterOpts(Transformers=list(trs), MaxItems=29), trailer=b"T%d" % k)
+                 for k, r in enumerate(recs)]
+        bodies, ends, foffs = [], [], []
+        for d in datas:
+            bodies.append(d[_body(d):shard.trailer_offset(d)])
+            ends.append(sum(map(len, bodies)))
+            foffs.append(_body(d))
+        span = b"".join(bodies)
+        dev = torch.frombuffer(bytearray(span), dtype=torch.uint8).to("cuda:0")
+        ctx = gpu.Context(0, max_span_bytes=len(span) + 32768, item_end=True)
+        try:
+            ctx.scan_device_segments_async(dev.data_ptr(), len(span), ends, foffs, _codec(trs))
+            b = ctx.sync()
+            assert b.err.code == 0 and b.stop == gpu.RIO_STOP_EOF and b.err_segment == -1, b.err.msg
+            nb = int(b.n_blocks)
+            u64 = lambda p, n: np.frombuffer(gpu.dev_to_host(ctypes.cast(p, ctypes.c_void_p).value, 8 * n),
+                                             dtype=np.uint64)
+            seg, boff, first = u64(b.block_segment, nb), u64(b.block_file_off, nb), u64(b.block_first_item, nb + 1)
+            items = gpu.device_batch_items(b, span)
+            for k, d in enumerate(datas):
+                ref = oracle.scan(d)
+                assert ref.err == "" and ref.items == recs[k]
+                sel = np.nonzero(seg == k)[0]
+                assert boff[sel].tolist() == sorted({loc[0] for loc in ref.locations}), (trs, k)
+                assert items[int(first[sel[0]]):int(first[sel[-1] + 1])] == recs[k], (trs, k)
+            # file 1's middle chunk: a bit flip with its CRC fixed (the chain decodes or
+            # rejects it as the oracle's does), then the same flip with the CRC left
+            # stale (stage 1's chunk error); both in file 1's coordinates
+            o = ends[0] + (ends[1] - ends[0]) // 32768 // 2 * 32768
+            size = struct.unpack_from("<I", span, o + 16)[0]
+            for fix_crc in (True, False):
+                bad = bytearray(span)
+                bad[o + 28 + size // 2] ^= 0x10
+                if fix_crc:
+                    struct.pack_into("<I", bad, o + 8, zlib.crc32(bytes(bad[o + 12:o + 28 + size])))
+                ref = oracle.scan(bytes(datas[1][:foffs[1]]) + bytes(bad[ends[0]:ends[1]]), read_trailer=False)
+                assert fix_crc or ref.err.startswith("Chunk checksum mismatch"), ref.err
+                dev.copy_(torch.frombuffer(bad, dtype=torch.uint8))
+                ctx.scan_device_segments_async(dev.data_ptr(), len(span), ends, foffs, _codec(trs))
+                b = ctx.sync()
+                got = gpu.device_batch_items(b, bytes(bad))
+                if ref.err:
+                    assert b.stop == gpu.RIO_STOP_ERROR and b.err_segment == 1, (trs, fix_crc, b.err.msg)
+                    assert b.err.msg.decode() == ref.err, (trs, b.err.msg, ref.err)
+                    assert got == recs[0] + ref.items
+                else:
+                    assert b.err.code == 0 and b.stop == gpu.RIO_STOP_EOF, (trs, b.err.msg)
+                    assert got == recs[0] + ref.items + recs[2]
+        finally:
+            ctx.close()
