@@ -115,12 +115,7 @@ __global__ void __launch_bounds__(256) k_parse(DevBufs d, ParseArgs a) {
 #endif
 constexpr int kLeanBatch = RIO_LEAN_BATCH;
 
-#ifdef RIO_LEAN_WPE  // (experiments: waves per SIMD k_parse_lean is register-allocated for)
-#define RIO_LEAN_ATTR __attribute__((amdgpu_waves_per_eu(RIO_LEAN_WPE)))
-#else
-#define RIO_LEAN_ATTR
-#endif
-__global__ void __launch_bounds__(256) RIO_LEAN_ATTR k_parse_lean(DevBufs d, ParseArgs a) {
+__global__ void __launch_bounds__(256) k_parse_lean(DevBufs d, ParseArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_win[4][1040];
   __shared__ __attribute__((aligned(16))) uint16_t s_tpos[4][264];
   uint8_t *lwin = s_win[threadIdx.x >> 6];
@@ -762,9 +757,6 @@ void launch_parse_lean(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
       ncu = 256;
     cap = (unsigned)(per_cu * ncu);
-#ifdef RIO_LEAN_GRID
-    cap = RIO_LEAN_GRID;  // (experiments: leave CUs to a concurrent k_crc)
-#endif
   }
   hipLaunchKernelGGL(k_parse_lean, dim3(grid_of(max_blocks, 4 * kLeanBatch, cap)), dim3(256), 0, st, d, a);
 }

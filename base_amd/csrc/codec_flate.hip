@@ -7,7 +7,7 @@
 // IOVecReader view, recordioiov.go:14-58); decoding stops at the end of the
 // BFINAL block and trailing bytes are ignored, as in Go.
 //
-// The fast path (k_flate_tok + k_flate_lz, below) decodes valid streams. Go's
+// The fast path (k_flate_sync / k_flate_tok + k_flate_lz2, below) decodes valid streams. Go's
 // inflater pulls bytes lazily (moreBits), which only matters for *where* an
 // error is reported (CorruptInputError's offset is its roffset) and for
 // rejecting a truncated stream; so on any error the block is re-decoded by
@@ -452,13 +452,9 @@ __device__ void inflate_exact(const CompIn &in, InflLds &L, uint64_t cap, uint32
 //   DEFLATE block header, the table build for a dynamic block, picking up the
 //   next recordio block, writing a block's result -- "escape" to wave-uniform
 //   scalar code for that one stream (readlane in, cndmask back).
-// k_flate_lz -- copy pass: one wave per block with a 64 KiB LDS window (the
-//   DEFLATE history plus the largest token batch, so no match ever reads HBM
-//   and no write of a batch clobbers a source of the same batch): 64 tokens
-//   per step, output positions from a wave prefix sum, literals written in
-//   parallel, each match copied by its own lane once its source bytes are
-//   final, every completed 1 KiB flushed to the block's decode region with
-//   16 B/lane stores.
+// k_flate_lz2 -- copy pass (below): one wave per block, the 32 KiB history in
+//   HBM (the block's own decode region) and a 4 KiB LDS ring per batch of up
+//   to 256 tokens.
 //
 // A block whose token region fills yields (FlState) and resumes in the next
 // round: the Huffman pass re-reads the current block header to rebuild its
@@ -491,14 +487,6 @@ constexpr int kTokLitRoot = RIO_LIT_ROOT;  // literal/length root table bits
 #define RIO_DIST_ROOT 8
 #endif
 constexpr int kTokDistRoot = RIO_DIST_ROOT;  // distance root table bits
-#ifndef RIO_FLATE_SYNC
-#define RIO_FLATE_SYNC 1
-#endif
-constexpr bool kFlateSync = RIO_FLATE_SYNC != 0;  // k_flate_sync first (ablation builds: -DRIO_FLATE_SYNC=0)
-#ifndef RIO_FLATE_LZ2
-#define RIO_FLATE_LZ2 1
-#endif
-constexpr bool kFlateLz2 = RIO_FLATE_LZ2 != 0;  // HBM-history copy pass (ablation builds: -DRIO_FLATE_LZ2=0)
 
 // RFC 1951 §3.2.5 length / distance bases and extra bits
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -964,7 +952,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           const uint64_t c0 = uni64(d.blk_c0[sb]);
           const unsigned long long meta = uni64(d.blk_meta[sb]);
           uint32_t stm;
-          if (round == 0 && kFlateSync && uni(sp->mode) != kFlHeader) continue;  // k_flate_sync handled it
+          if (round == 0 && uni(sp->mode) != kFlHeader) continue;  // k_flate_sync handled it
           if (round == 0) {
             const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
             // incomplete blocks, and magics that are never untransformed (the header
@@ -1331,7 +1319,7 @@ __device__ __forceinline__ void zmem_sync_dev() {
 // lane is on the true chain (lane 0 starts at a known boundary, and lane i's
 // start is lane i-1's exit). A prefix sum of the lanes' token / byte counts
 // places each lane's tokens, and a last pass writes them (same token format as
-// k_flate_tok, so k_flate_lz is unchanged). The first lane that decodes the
+// k_flate_tok, so the copy pass is unchanged). The first lane that decodes the
 // end-of-block symbol ends the DEFLATE block; lanes after it were decoding the
 // next block's bits and are discarded.
 //
@@ -1349,15 +1337,12 @@ constexpr int kSyncIters = 8;
 #define RIO_SYNC_WAVES 12
 #endif
 constexpr int kSyncWaves = RIO_SYNC_WAVES;                 // per CU (launch sizing, one wave per block)
-// Ablation builds (-DRIO_SYNC_WIDE=1): spans of fewer blocks than one-wave
-// slots decoded with kSyncW waves per block (128 segments per round). Measured
-// slower for C3 at MaxItems = 16384 (2,158 blocks): 51.3 ms at 2 waves, 58.1 at
-// 4, against 50.0 at one -- only 1,536 two-wave blocks are resident at a time
+// The kernel is written for kW waves per block (segment g = 64 * wave + lane,
+// cross-wave exchanges at barriers); only kW = 1 is instantiated: kW = 2 / 4
+// for spans of fewer blocks than one-wave slots measured slower for C3 at
+// MaxItems = 16384 (2,158 blocks; round 3): 51.3 ms at 2 waves, 58.1 at 4,
+// against 50.0 at one -- only 1,536 two-wave blocks are resident at a time
 // (registers), and the barriers cost more than the extra segments gain.
-#ifndef RIO_SYNC_WIDE
-#define RIO_SYNC_WIDE 0
-#endif
-constexpr int kSyncW = 2;
 
 template <int kW>
 constexpr uint32_t sync_win_dw() { return kW * kSyncBits / 32 + 32; }  // staged dwords (+ run-out margin)
@@ -1394,12 +1379,9 @@ __device__ __forceinline__ uint32_t sync_bits(const uint32_t *win, uint32_t r) {
 }
 
 enum : uint32_t { kSyEob = 1, kSyBad = 2, kSyHist = 4, kSyFull = 8 };
-// Literals per token in this pass (ablation builds: -DRIO_SYNC_MERGE=3): 3 cut
-// C3's tokens by 8 % without a measurable gain (50.4 against 51.0 GiB/s).
-#ifndef RIO_SYNC_MERGE
-#define RIO_SYNC_MERGE 1
-#endif
-constexpr uint32_t kSyncMerge = RIO_SYNC_MERGE;
+// Literals per token in this pass: one (3, as stored blocks' tokens, cut C3's
+// tokens by 8 % without a measurable gain: 50.4 against 51.0 GiB/s, round 3).
+constexpr uint32_t kSyncMerge = 1;
 
 // Decode tokens from relative bit r while r < end (or to the end-of-block
 // symbol). Counting mode skips an undecodable code by one bit (a lane off the
@@ -1587,85 +1569,7 @@ __device__ __forceinline__ uint32_t sync_count(const StreamLds &T, const uint32_
   return r;
 }
 
-// (ablation builds, -DRIO_SYNC_BITBUF=0: the previous decoder, which reads each
-// code's bits from the window at its position -- two LDS reads before every
-// table lookup)
-#ifndef RIO_SYNC_BITBUF
-#define RIO_SYNC_BITBUF 1
-#endif
-#if !RIO_SYNC_BITBUF
-template <bool kWrite>
-__device__ __forceinline__ uint32_t sync_decode_win(const StreamLds &T, const uint32_t *win, uint32_t r, uint32_t end,
-                                                uint32_t lim, uint32_t &ntok, uint32_t &nout, uint32_t &flags,
-                                                uint32_t *tk, uint32_t olen0, uint32_t cap) {
-  while (r < end && r < lim) {
-    const uint32_t w = sync_bits(win, r);
-    uint32_t e = T.lit[w & ((1u << kTokLitRoot) - 1)];
-    if ((e & 15) == 0 && (e & kEnLenBit)) e = slow_walk<kTokLitRoot>(T.lfco, T.lent, w);
-    const uint32_t L = e & 15, E = (e >> 5) & 7;
-    if (L == 0) {
-      flags |= kSyBad;
-      if (kWrite) break;
-      r += 1;
-      continue;
-    }
-    if (!(e & kEnLenBit)) {
-      if (kWrite) {
-        if (olen0 + nout >= cap) {
-          flags |= kSyFull;
-          break;
-        }
-        tk[ntok] = (e >> 8) | (1u << 24);
-      }
-      r += L;
-      ntok++;
-      nout++;
-      continue;
-    }
-    if (E == kEobExtra) {
-      r += L;
-      flags |= kSyEob;
-      break;
-    }
-    const uint32_t len = (e >> 8) + 3 + __builtin_amdgcn_ubfe(w, L, E);
-    const uint32_t r1 = r + L + E;
-    const uint32_t w2 = sync_bits(win, r1);
-    uint32_t dd = T.dst[w2 & ((1u << kTokDistRoot) - 1)];
-    if ((dd & 15) == 0 && (dd & kEnLenBit)) dd = slow_walk<kTokDistRoot>(T.dfco, T.dent, w2);
-    const uint32_t L2 = dd & 15, E2 = (dd >> 7) & 15;
-    if (L2 == 0) {
-      flags |= kSyBad;
-      if (kWrite) break;
-      r = r1;
-      continue;
-    }
-    const uint32_t dist = (((dd >> 5) & 3) << E2) + 1 + __builtin_amdgcn_ubfe(w2, L2, E2);
-    if (kWrite) {
-      const uint32_t at = olen0 + nout, hist = at < 32768u ? at : 32768u;
-      if (dist > hist) {
-        flags |= kSyHist;
-        break;
-      }
-      if (len > cap - at) {
-        flags |= kSyFull;
-        break;
-      }
-      tk[ntok] = 0x80000000u | ((len - 3) << 16) | (dist - 1);
-    }
-    r = r1 + L2 + E2;
-    ntok++;
-    nout += len;
-  }
-  return r;
-}
 
-#endif
-
-#ifdef RIO_SYNC_WPE  // (experiments: waves per SIMD the Huffman pass is register-allocated for)
-#define RIO_SYNC_ATTR __attribute__((amdgpu_waves_per_eu(RIO_SYNC_WPE)))
-#else
-#define RIO_SYNC_ATTR
-#endif
 // kW waves per block: segment g = 64 * wave + lane. Wave 0 reads the DEFLATE
 // block headers and builds the tables; the waves meet at barriers to exchange
 // the first end-of-block segment, the exits at their edges, the convergence
@@ -1673,7 +1577,7 @@ __device__ __forceinline__ uint32_t sync_decode_win(const StreamLds &T, const ui
 // wide_below: the span's block count decides the variant -- the one-wave
 // kernel runs spans of >= wide_below blocks, the kSyncW-wave one the others.
 template <int kW>
-__global__ void __launch_bounds__(64 * kW) RIO_SYNC_ATTR k_flate_sync(const uint8_t *__restrict__ span, DevBufs d,
+__global__ void __launch_bounds__(64 * kW) k_flate_sync(const uint8_t *__restrict__ span, DevBufs d,
                                                    const unsigned long long *nblocks, uint64_t nchunks,
                                                    uint64_t dec_cap, uint64_t wide_below) {
   constexpr uint32_t kWinDw = sync_win_dw<kW>();
@@ -1843,11 +1747,7 @@ __global__ void __launch_bounds__(64 * kW) RIO_SYNC_ATTR k_flate_sync(const uint
           if (need && it == 0) {
             nt = no = fl = 0;
             stg = false;
-#if RIO_SYNC_BITBUF
             ex = sync_count<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, slack);
-#else
-            ex = sync_decode_win<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, 0, 0);
-#endif
           } else if (need) {
             nt = no = fl = 0;
             slack = 0x7fffffff;
@@ -1856,11 +1756,7 @@ __global__ void __launch_bounds__(64 * kW) RIO_SYNC_ATTR k_flate_sync(const uint
             // the last (segment 0's first, every later one) left a lane without a
             // staged decode in most rounds (41.0 against 35.4 ms for C3)
             stg = sgl != nullptr;
-#if RIO_SYNC_BITBUF
             ex = sync_count<true>(T, S.win, st, seg_end, lim, nt, no, fl, stg ? sgl : nullptr, slack);
-#else
-            ex = sync_decode_win<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, 0, 0);
-#endif
           }
           // the true chain ends at the first segment reaching end-of-block
           const unsigned long long eobm = __ballot((fl & kSyEob) != 0);
@@ -1957,13 +1853,8 @@ __global__ void __launch_bounds__(64 * kW) RIO_SYNC_ATTR k_flate_sync(const uint
           }
         } else if (live) {
           uint32_t wt = 0, wo = 0;
-#if RIO_SYNC_BITBUF
           const uint32_t wx = sync_decode<true>(T, S.win, st, seg_end, lim, wt, wo, f2, tok + ntok + tpre + (ti - tn),
                                                 olen + opre + (oi - on), cap);
-#else
-          const uint32_t wx = sync_decode_win<true>(T, S.win, st, seg_end, lim, wt, wo, f2,
-                                                    tok + ntok + tpre + (ti - tn), olen + opre + (oi - on), cap);
-#endif
 #ifdef RIO_SYNC_DEBUG
           if (wt != nt || wo != no || wx != ex)
             printf("sync kW=%d b=%llu g=%u st=%u end=%u ke=%u: count nt=%u no=%u ex=%u fl=%u | write wt=%u wo=%u wx=%u f2=%u\n",
@@ -2032,168 +1923,12 @@ __device__ __forceinline__ uint32_t umod_small(uint32_t k, uint32_t d) {
   return (uint32_t)r;
 }
 
-// Copy-pass window: a ring of 36 KiB = the 32 KiB DEFLATE history + one batch
-// of at most 4 KiB (a wider batch -- long matches -- goes in 8 parts of 8
-// tokens, <= 2,064 B each), flushed after every batch: a write at x replaces
-// x - 36 KiB, which is flushed and older than any source of the batch.
-constexpr uint32_t kLzWin = 36864;
-constexpr uint32_t kLzSpan = kLzWin - 32768;
-constexpr int kLzSuper = 4;  // batches of 64 tokens staged in LDS per super-batch
-
-// x mod 36864 (= 9 * 2^12) for any u32 x
-__device__ __forceinline__ uint32_t lz_slot(uint32_t x) {
-  const uint32_t q = __umulhi(x >> 12, 0x1C71C71Du);  // (x >> 12) / 9, exact below 2^20
-  return x - q * kLzWin;
-}
-__device__ __forceinline__ uint32_t lz_next(uint32_t slot, uint32_t k) {  // slot + k (k < kLzWin), wrapped
-  const uint32_t r = slot + k;
-  return r >= kLzWin ? r - kLzWin : r;
-}
-
-// write the completed 1 KiB units of [flushed, olen) to HBM, 16 B per lane
-// (a unit never wraps: 49152 is a multiple of 1024)
-__device__ __forceinline__ void lz_flush_units(const uint8_t *win, uint8_t *out, uint64_t &flushed, uint64_t olen) {
-  const int l = lane_id();
-  for (uint64_t u0 = flushed & ~1023ull; u0 + 1024 <= olen; u0 += 1024) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(win + lz_slot((uint32_t)u0) + 16 * l);
-    *reinterpret_cast<uint4 *>(out + u0 + 16 * l) = v;
-    flushed = u0 + 1024;
-  }
-}
-
-__global__ void __launch_bounds__(64) k_flate_lz(DevBufs d, const unsigned long long *nblocks, int round) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kLzWin];
-  __shared__ uint32_t tbuf[64 * kLzSuper];
-  const int l = lane_id();
-  if (round > 0 && uni64(d.fl_more[round - 1]) == 0) return;
-  const uint64_t nb = uni64(*nblocks);
-  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
-    FlState *sp = &d.fl[b];
-    const uint32_t mode = uni(sp->mode);
-    if (uni(sp->round) != (uint32_t)round || mode == kFlError || mode == kFlSkip) continue;
-    uint64_t olen = uni64(sp->olen2);
-    const uint32_t ntok = uni(sp->ntok);
-    uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
-    const uint32_t *tk = d.tok + uni64(d.blk_c0[b]) * (uint64_t)kTokPerChunk;
-    wave_lds_sync();
-    if (olen > 0) {  // resumed: the history this block has already written
-      const uint64_t h = olen < 32768ull ? olen : 32768ull;
-      for (uint64_t k = l; k < h; k += 64) win[lz_slot((uint32_t)(olen - h + k))] = out[olen - h + k];
-      wave_lds_sync();
-    }
-    uint64_t flushed = olen;
-    // Tokens stream through LDS one super-batch (256 tokens) at a time; the
-    // next super-batch is loaded into registers while this one is decoded.
-    uint32_t pre[kLzSuper];
-#pragma unroll
-    for (int q = 0; q < kLzSuper; q++) pre[q] = (64u * q + (uint32_t)l < ntok) ? tk[64 * q + l] : 0u;
-    for (uint32_t s0 = 0; s0 < ntok; s0 += 64 * kLzSuper) {
-      wave_lds_sync();
-#pragma unroll
-      for (int q = 0; q < kLzSuper; q++) tbuf[64 * q + l] = pre[q];
-      const uint32_t s1 = s0 + 64 * kLzSuper;
-#pragma unroll
-      for (int q = 0; q < kLzSuper; q++) pre[q] = (s1 + 64u * q + (uint32_t)l < ntok) ? tk[s1 + 64 * q + l] : 0u;
-      wave_lds_sync();
-      const uint32_t nbat = (ntok - s0 + 63) / 64 < (uint32_t)kLzSuper ? (ntok - s0 + 63) / 64 : (uint32_t)kLzSuper;
-      for (uint32_t bi = 0; bi < nbat; bi++) {
-        const uint32_t t0 = (s0 + 64 * bi + (uint32_t)l < ntok) ? tbuf[64 * bi + l] : 0u;
-        const uint32_t len0 = (t0 >> 31) ? ((t0 >> 16) & 0xffu) + 3 : (t0 >> 24) & 3u;
-        // a batch spanning more than kLzSpan bytes (long matches) goes in 8 parts
-        const uint32_t all = (uint32_t)__builtin_amdgcn_readlane(wave_incl_sum_dpp(len0), 63);
-        const int parts = all > kLzSpan ? 8 : 1;
-        for (int h = 0; h < parts; h++) {
-          const bool mine = parts == 1 || (l >> 3) == h;
-          const uint32_t t = mine ? t0 : 0u;
-          const bool m = (t >> 31) != 0;
-          const uint32_t len = mine ? len0 : 0u;
-          const uint32_t incl = wave_incl_sum_dpp(len);
-          const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-          const uint32_t p = incl - len;  // position relative to olen
-          const uint32_t base = (uint32_t)olen;
-          const uint32_t q0 = lz_slot(base + p);  // the token's first output slot
-          if (!m) {
-            if (len > 0) win[q0] = (uint8_t)t;
-            if (len > 1) win[lz_next(q0, 1)] = (uint8_t)(t >> 8);
-            if (len > 2) win[lz_next(q0, 2)] = (uint8_t)(t >> 16);
-          }
-          const uint32_t dist = (t & 0x7fffu) + 1;
-          const int src_end = (int)p - (int)dist + (int)(len < dist ? len : dist);
-          const unsigned long long mm = __ballot(m);
-          if (mm) {
-            // one parallel round: every short match whose source ends before the
-            // batch's first match, copied by its own lane 8 bytes at a time ...
-            const int R = (int)__builtin_amdgcn_readlane(p, __ffsll((long long)mm) - 1);
-            const bool ready = m && src_end <= R && len <= 16;
-            if (ready) {
-              const uint32_t a0 = lz_slot(base + p - dist);
-              if (dist >= 8 || len <= dist) {  // no byte of an 8-byte piece depends on another
-                for (uint32_t k = 0; k < len; k += 8) {
-                  const uint32_t sa = lz_next(a0, k), da = lz_next(q0, k);
-                  uint8_t v[8];
-                  if (sa + 8 <= kLzWin) {
-#pragma unroll
-                    for (int jj = 0; jj < 8; jj++) v[jj] = win[sa + jj];
-                  } else {
-#pragma unroll
-                    for (int jj = 0; jj < 8; jj++) v[jj] = win[lz_next(sa, jj)];
-                  }
-                  if (da + 8 <= kLzWin && k + 8 <= len) {
-#pragma unroll
-                    for (int jj = 0; jj < 8; jj++) win[da + jj] = v[jj];
-                  } else {
-#pragma unroll
-                    for (int jj = 0; jj < 8; jj++)
-                      if (k + jj < len) win[lz_next(da, jj)] = v[jj];
-                  }
-                }
-              } else {  // overlapping run: byte by byte, each byte reads one written before it
-                for (uint32_t k = 0; k < len; k++) win[lz_next(q0, k)] = win[lz_next(a0, k)];
-              }
-            }
-            // ... then the rest (sources inside this batch, or longer than 16 B) in
-            // order, each copied by the whole wave: every byte it reads precedes it
-            // and is final by then
-            unsigned long long rem = mm & ~__ballot(ready);
-            while (rem) {
-              const int f = __ffsll((long long)rem) - 1;
-              rem &= rem - 1;
-              const uint32_t P = base + (uint32_t)__builtin_amdgcn_readlane(p, f);
-              const uint32_t D = (uint32_t)__builtin_amdgcn_readlane(dist, f);
-              const uint32_t N = (uint32_t)__builtin_amdgcn_readlane(len, f);
-              const uint32_t sa = lz_slot(P - D), da = lz_slot(P);
-              for (uint32_t k0 = 0; k0 < N; k0 += 64) {
-                const uint32_t k = k0 + (uint32_t)l;
-                const uint32_t kk = D >= N ? k : umod_small(k, D);
-                const uint8_t v = k < N ? win[lz_next(sa, kk)] : 0;
-                if (k < N) win[lz_next(da, k)] = v;
-              }
-            }
-          }
-          olen += total;
-          if ((olen & ~1023ull) > flushed) {
-            wave_lds_sync();
-            lz_flush_units(win, out, flushed, olen);
-          }
-        }
-      }
-    }
-    wave_lds_sync();
-    lz_flush_units(win, out, flushed, olen);
-    for (uint64_t k = flushed + l; k < olen; k += 64) out[k] = win[lz_slot((uint32_t)k)];
-    if (l == 0) {
-      sp->olen2 = olen;
-      if (mode == kFlDone) d.blk_out_len[b] = olen;
-    }
-  }
-}
-
 // ================================================================ k_flate_lz2
 // Copy pass with the 32 KiB history in HBM: the block's own output region,
 // which the wave has already written. LDS holds only a 4 KiB ring per wave
 // (the batch being built plus the 2,544 bytes before it), so ~28 waves fit a
-// CU where k_flate_lz's 36 KiB windows fit 4: the copy pass is latency-bound,
-// and occupancy is what hides the latency.
+// CU where a 36 KiB window with the whole history (the round-1 pass) fits 4:
+// the copy pass is latency-bound, and occupancy is what hides the latency.
 //
 // A batch is up to 256 tokens (4 per lane, token order k-major) whose output
 // fits kL2Span bytes. Its bytes are produced in the ring:
@@ -2710,22 +2445,11 @@ void launch_inflate_plan(const DevBufs &d, const unsigned long long *nblocks, ui
 void launch_inflate_huff(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks,
                          uint64_t max_blocks, uint64_t nchunks, uint64_t dec_cap, int rounds, int ncu, hipStream_t st) {
   (void)hipMemsetAsync(d.fl_more, 0, sizeof(unsigned long long) * rounds, st);
-  if (kFlateSync) {  // the wave-per-block Huffman pass first; k_flate_tok takes what it declines
-    // one variant runs, by the span's block count (device): one wave per block
-    // when the blocks fill the one-wave slots, else kSyncW waves per block
+  {  // the wave-per-block Huffman pass first; k_flate_tok takes what it declines
     const uint64_t rs = (uint64_t)ncu * kSyncWaves;
-    uint64_t gs = max_blocks < rs ? max_blocks : rs;
-#if RIO_SYNC_WIDE  // (ablation builds: measured slower)
-    hipLaunchKernelGGL(k_flate_sync<1>, dim3((unsigned)(gs ? gs : 1)), dim3(64), 0, st, span, d, nblocks, nchunks,
-                       dec_cap, rs);
-    const uint64_t rw = (uint64_t)ncu * (163840 / sizeof(SyncLdsT<kSyncW>));
-    gs = max_blocks < rw ? max_blocks : rw;
-    hipLaunchKernelGGL(k_flate_sync<kSyncW>, dim3((unsigned)(gs ? gs : 1)), dim3(64 * kSyncW), 0, st, span, d, nblocks,
-                       nchunks, dec_cap, rs);
-#else
+    const uint64_t gs = max_blocks < rs ? max_blocks : rs;
     hipLaunchKernelGGL(k_flate_sync<1>, dim3((unsigned)(gs ? gs : 1)), dim3(64), 0, st, span, d, nblocks, nchunks,
                        dec_cap, 0);
-#endif
   }
 #ifdef RIO_FLSTAT
   {
@@ -2740,7 +2464,7 @@ void launch_inflate_huff(const uint8_t *span, const DevBufs &d, const unsigned l
 // the copy rounds skip them). Relaunched by the host after it sized the scratch
 // (with ctl->seg_used / seg_blocks reset): blocks it marks are planned once.
 void launch_inflate_plan(const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks, hipStream_t st) {
-  if (kFlateSync && d.seg_items > 0)
+  if (d.seg_items > 0)
     hipLaunchKernelGGL(k_flate_plan, dim3(grid256(max_blocks)), dim3(256), 0, st, d, nblocks);
 }
 
@@ -2754,21 +2478,14 @@ void launch_inflate_copy(const uint8_t *span, const DevBufs &d, const unsigned l
   if (g1 > r1) g1 = r1;
   if (d.fl_grid && g1 > d.fl_grid) g1 = d.fl_grid;
   if (g1 < 1) g1 = 1;
-  uint64_t g2 = max_blocks;
-  const uint64_t r2 = (uint64_t)ncu * 4;  // 36 KiB windows: 4 per CU
-  if (g2 > r2) g2 = r2;
-  if (g2 < 1) g2 = 1;
   uint64_t g3 = max_blocks;
   if (g3 > (uint64_t)ncu * kL2Waves) g3 = (uint64_t)ncu * kL2Waves;
   if (g3 < 1) g3 = 1;
-  const bool split = kFlateSync && d.seg_items > 0;
+  const bool split = d.seg_items > 0;
   for (int r = 0; r < rounds; r++) {
     hipLaunchKernelGGL(k_flate_tok, dim3((unsigned)g1), dim3(64), 0, st, span, d, nblocks, nchunks,
                        dec_cap, r, (int)(r == rounds - 1));
-    if (kFlateLz2)
-      hipLaunchKernelGGL(k_flate_lz2, dim3((unsigned)g3), dim3(64), 0, st, d, nblocks, r);
-    else
-      hipLaunchKernelGGL(k_flate_lz, dim3((unsigned)g2), dim3(64), 0, st, d, nblocks, r);
+    hipLaunchKernelGGL(k_flate_lz2, dim3((unsigned)g3), dim3(64), 0, st, d, nblocks, r);
   }
   if (split) {
     uint64_t gs = max_blocks * kSegMax;

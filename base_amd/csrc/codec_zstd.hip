@@ -25,14 +25,6 @@
 
 #include "device_common.h"
 #include "rio_internal.h"
-#include "lz_ring.h"
-
-// k_zstd_exec2 (the flate copy pass's ring machinery) measured slower than
-// k_zstd_exec on C4: 65.6 against 58.6 ms (134 VGPRs: 3 waves/SIMD; every
-// literal run a global read). Built with -DRIO_ZSTD_EXEC2=1.
-#ifndef RIO_ZSTD_EXEC2
-#define RIO_ZSTD_EXEC2 0
-#endif
 
 namespace rio {
 
@@ -56,15 +48,10 @@ constexpr uint64_t kZLitStride = kZBlockMax + 256;  // per-wave literal buffer
 #define RIO_ZWAVES 12
 #endif
 constexpr int kZWaves = RIO_ZWAVES;  // resident zstd waves per CU (LDS ~10 KiB each)
-constexpr int kZSeqWaves = 8;                        // k_zstd_seq waves per CU (64 jobs each; every job of a C4 span in flight)
 #ifndef RIO_ZFIX_WAVES
 #define RIO_ZFIX_WAVES 20  // 5 per SIMD (8: 162.0 ms for C4, 20: 156.1, 28: 159.8)
 #endif
 constexpr int kZFixWaves = RIO_ZFIX_WAVES;            // k_zstd_fix waves per CU
-#ifndef RIO_ZSTD_SEQ2
-#define RIO_ZSTD_SEQ2 1
-#endif
-constexpr bool kZstdSeq2 = RIO_ZSTD_SEQ2 != 0;  // LDS-table sequence pass (ablation builds: -DRIO_ZSTD_SEQ2=0)
 
 __constant__ uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,  12,   13,   14,   15,   16,   18,
                                      20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
@@ -1084,7 +1071,7 @@ struct ZSerialSink {
 // split so that each is at most kZPiece bytes (copying a long match in pieces
 // with the same offset is the same copy). Frame ends are marked: ll = 0xFFFF
 // with ml = 0xFFFF (checksum = offset field) or 0xFFFE (no checksum).
-constexpr uint32_t kZPiece = RIO_ZSTD_EXEC2 ? 512 : 2048;  // exec2: within its batch span and far-source margin
+constexpr uint32_t kZPiece = 2048;
 constexpr uint32_t kZMark = 0xFFFF;
 constexpr uint32_t kZMarkCk = 0xFFFF, kZMarkNoCk = 0xFFFE;
 
@@ -1095,10 +1082,15 @@ struct ZJob {
   uint32_t checksum, logs;  // frame checksum (kJCk); ll_log | of_log << 8 | ml_log << 16
   int64_t fcs;              // frame content size, at the frame's last job (-1: none)
   uint64_t tab_off;         // ll, ml, of cells (u32 x 2^log each)
-  uint64_t raw_off;         // raw sequences (u64 x nseq): ll | ml << 17 | offset value << 35
+  uint64_t raw_off;         // raw sequences (u64 x nseq): ll | ml << 17 | offset << 35 (kZSym: symbolic)
   uint64_t next;            // the block's next job header
-  uint32_t err, pad;        // k_zstd_seq: 0, kZCorrupt or kZSlow
+  uint32_t err, rep0;       // k_zstd_seq2: 0, kZCorrupt or kZSlow; the repeat offsets after the
+  uint32_t rep1, rep2;      // job's last sequence (kZSym: in terms of the ones before its first)
 };
+// An offset as k_zstd_seq2 writes it: the value (< 2^28), or kZSym | slot << 24 | c =
+// "repeat offset `slot` as it was before the job's first sequence, minus c" (the
+// job's starting history is its predecessor's final one, known only in file order)
+constexpr uint32_t kZSym = 1u << 28;
 constexpr int64_t kZJobHdr = (sizeof(ZJob) + 15) / 16 * 16;  // header bytes; 16-aligned tables follow
 constexpr uint32_t kJFirst = 1, kJLast = 2, kJCk = 4, kJLit = 8;
 
@@ -1142,7 +1134,9 @@ struct ZJobSink {
       h->raw_off = region + (uint64_t)(at + kZJobHdr + tabr);
       h->next = 0;
       h->err = 0;
-      h->pad = 0;
+      h->rep0 = kZSym;
+      h->rep1 = kZSym | (1u << 24);
+      h->rep2 = kZSym | (2u << 24);
       if (last >= 0) hdr(last)->next = region + (uint64_t)at;
     }
     pend_first = 0;
@@ -1586,103 +1580,19 @@ __global__ void __launch_bounds__(64) RIO_ZENT_ATTR k_zstd_ent(const uint8_t *__
   }
 }
 
-// ---------------------------------------------------------------- k_zstd_seq
-// Sequence pass: lane per job (grid-stride over DevBufs::zjob), every lane of
-// the wave decoding its own job's sequence bitstream (one vector instruction
-// advances 64 jobs); each sequence becomes a raw entry (ll, ml and the offset
-// value before repeat-offset resolution, which needs the previous block's last
-// offsets and is k_zstd_fix's). The FSE cells (u32, 5 KiB per job at most)
-// come from the job's tables in HBM: the grid is sized so that the tables of
-// the jobs in flight stay cache-resident. The code tables are in LDS and the
-// raw entries are staged in LDS and stored 16 at a time (a vector load or
-// store in the loop would be waited for behind the loads in flight: vmcnt
-// counts in order). The serial decoder's checks that need only this stream
-// (symbols in range, no overrun, exact end) are made here; an offset code
-// above 28 (windows beyond 256 MiB) sends the recordio block to the serial
-// path.
+// readlane of a u32
 __device__ __forceinline__ uint32_t zrl(uint32_t v, uint32_t lane) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
-}
-
-constexpr int kZStage = 16;  // raw entries per lane per store burst
-__global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
-  __shared__ ZCodes codes;
-  __shared__ __attribute__((aligned(16))) uint64_t stage[64][kZStage];
-  const int l = lane_id();
-  for (int u = l; u < 36; u += 64) codes.ll[u] = kZCodes.ll[u];
-  for (int u = l; u < 53; u += 64) codes.ml[u] = kZCodes.ml[u];
-  wave_lds_sync();
-  uint8_t *tok8 = reinterpret_cast<uint8_t *>(d.tok);
-  uint64_t *st = stage[l];
-  const uint64_t nj0 = d.ctl->zjob_n, nj = nj0 < d.zjob_cap ? nj0 : d.zjob_cap;
-  for (uint64_t j = (uint64_t)blockIdx.x * 64 + l; j < nj; j += (uint64_t)gridDim.x * 64) {
-    ZJob *hp = reinterpret_cast<ZJob *>(tok8 + d.zjob[j]);
-    const uint32_t flags = hp->flags, nseq = hp->nseq;
-    if ((flags & kJLit) || nseq == 0) continue;
-    const uint64_t seq_off = hp->seq_off, tab_off = hp->tab_off, raw_off = hp->raw_off;
-    const uint32_t seq_len = hp->seq_len, logs = hp->logs;
-    uint32_t err = 0;
-    ZBr r;
-    if (!r.init(tok8, (int64_t)seq_off, (int64_t)seq_len)) {
-      err = kZCorrupt;
-    } else {
-      const int llg = logs & 0xff, ofg = (logs >> 8) & 0xff, mlg = (logs >> 16) & 0xff;
-      const uint32_t *tll = reinterpret_cast<const uint32_t *>(tok8 + tab_off), *tml = tll + (1 << llg);
-      const uint32_t *tof = tml + (1 << mlg);
-      uint4 *raw = reinterpret_cast<uint4 *>(tok8 + raw_off);
-      uint32_t sll = r.read(llg), sof = r.read(ofg), sml = r.read(mlg);
-      uint32_t i = 0;
-      for (; i < nseq; i++) {
-        const uint32_t cl = tll[sll], cm = tml[sml], cof = tof[sof];
-        const uint32_t llc = cl & 0xff, mlc = cm & 0xff, ofc = cof & 0xff;
-        if (llc > 35 || mlc > 52 || ofc > 31) {
-          err = kZCorrupt;
-          break;
-        }
-        if (ofc > 28) {
-          err = kZSlow;
-          break;
-        }
-        const uint32_t mlx = codes.ml[mlc], llx = codes.ll[llc];
-        const uint32_t ofv = (1u << ofc) + r.read((int)ofc);
-        const uint32_t ml = (mlx & 0xFFFFFFu) + r.read((int)(mlx >> 24));
-        const uint32_t ll = (llx & 0xFFFFFFu) + r.read((int)(llx >> 24));
-        if (i + 1 < nseq) {
-          sll = (cl >> 16) + r.read((int)((cl >> 8) & 0xff));
-          sml = (cm >> 16) + r.read((int)((cm >> 8) & 0xff));
-          sof = (cof >> 16) + r.read((int)((cof >> 8) & 0xff));
-        }
-        if (r.overrun()) {
-          err = kZCorrupt;
-          break;
-        }
-        st[i & (kZStage - 1)] = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
-        if ((i & (kZStage - 1)) == kZStage - 1) {  // 16 entries (raw + 16 i is 16-aligned)
-          const uint4 *sv = reinterpret_cast<const uint4 *>(st);
-          uint4 *dv = raw + (i & ~(uint32_t)(kZStage - 1)) / 2;
-#pragma unroll
-          for (int k = 0; k < kZStage / 2; k++) dv[k] = sv[k];
-        }
-      }
-      if (!err) {  // the partial last burst
-        const uint32_t g = nseq & ~(uint32_t)(kZStage - 1);
-        uint64_t *dr = reinterpret_cast<uint64_t *>(raw);
-        for (uint32_t k = g; k < nseq; k++) dr[k] = st[k & (kZStage - 1)];
-        if (!r.exact()) err = kZCorrupt;
-      }
-    }
-    hp->err = err;
-  }
 }
 
 // ---------------------------------------------------------------- k_zstd_seq2
 // Sequence pass with the FSE tables in LDS: four waves per CU, each decoding
 // kZs2Jobs jobs at a time (a lane per job, lanes kZs2Jobs..63 idle), each job's
 // three tables in its own LDS slot as u16 cells. 60 jobs per CU is far fewer
-// than k_zstd_seq keeps in flight, but a cell load is an LDS access (~100
-// cycles) instead of an HBM/MALL miss: with every job of a span in flight
-// (82k for C4) the tables (up to 5 KiB each) outgrow every cache, and each
-// sequence waited on a DRAM access. A cell here is the symbol (6 bits) and
+// than the round-1 pass (a lane per job, u32 cells in HBM) kept in flight, but a
+// cell load is an LDS access (~100 cycles) instead of an HBM/MALL miss: with
+// every job of a span in flight (82k for C4) the tables (up to 5 KiB each)
+// outgrew every cache, and each sequence waited on a DRAM access. A cell here is the symbol (6 bits) and
 // FSE's nextState (10 bits); nbBits = log - highbit(nextState) and the new
 // state's base = (nextState << nbBits) - 2^log are recomputed per use. A job's
 // tables are loaded by the whole wave (u32 cells from k_zstd_ent); the lanes
@@ -1696,52 +1606,10 @@ __global__ void __launch_bounds__(64) k_zstd_seq(DevBufs d) {
 // (offset <= 28 bits, extras <= 16 + 16, states <= 9 + 9 + 8), so a sequence
 // takes at most 3 dwords.
 constexpr int kZs2Ring = 32;
-// Measured and kept out (round 3, ablation switches; A/B on one box, C4 ms per
-// step): the ring dword of the next reload loaded a reload ahead
-// (-DRIO_ZS2_PREFETCH=1: 150.2 against 147.0) and the LL / ML code baselines
-// computed instead of looked up (-DRIO_ZS2_CODES_ALU=1: 153.2; both 155.0) --
+// Measured and kept out (round 3; A/B on one box, C4 ms per step): the ring
+// dword of the next reload loaded a reload ahead (150.2 against 147.0) and the
+// LL / ML code baselines computed instead of looked up (153.2; both 155.0) --
 // this pass's pace is set by where the compiler places its LDS waits.
-#ifndef RIO_ZS2_PREFETCH
-#define RIO_ZS2_PREFETCH 0
-#endif
-#ifndef RIO_ZS2_CODES_ALU
-#define RIO_ZS2_CODES_ALU 0
-#endif
-// LL / ML code -> baseline | extra bits << 24 (RFC 8878 3.1.1.3.2.1.1 tables)
-__device__ __forceinline__ uint32_t zs_llx(uint32_t c) {
-  const uint32_t k = c - 20u, p = (k >> 1) & 3u, b = p + 2u;
-  uint32_t base = 16u + (8u << p) + ((k & 1u) << b), bits = b;
-  if (c < 20u) {
-    base = 16u + 2u * (c - 16u);
-    bits = 1u;
-  }
-  if (c >= 25u) {
-    bits = c - 19u;
-    base = 1u << (bits & 31u);
-  }
-  if (c < 16u) {
-    base = c;
-    bits = 0u;
-  }
-  return base | (bits << 24);
-}
-__device__ __forceinline__ uint32_t zs_mlx(uint32_t c) {
-  const uint32_t k = c - 36u, p = (k >> 1) & 3u, b = p + 2u;
-  uint32_t base = 35u + (8u << p) + ((k & 1u) << b), bits = b;
-  if (c < 36u) {
-    base = 35u + 2u * (c - 32u);
-    bits = 1u;
-  }
-  if (c >= 43u) {
-    bits = c - 36u;
-    base = (1u << (bits & 31u)) + 3u;
-  }
-  if (c < 32u) {
-    base = c + 3u;
-    bits = 0u;
-  }
-  return base | (bits << 24);
-}
 struct ZBr64 {
   const uint32_t *w;
   uint64_t win;
@@ -1754,33 +1622,8 @@ struct ZBr64 {
   // which is an error whatever they hold
   __device__ __forceinline__ uint32_t Dc(int32_t i) const { return w[max(qtop - i, 0)]; }
   // ring: this lane's kZs2Ring dwords (D_i at i mod kZs2Ring)
-#if RIO_ZS2_PREFETCH
-  // the ring dword the next reload takes, loaded one reload ahead (round 3): a
-  // reload then waits for no LDS read. Valid: within a group the lane consumes
-  // <= 24 dwords of the >= 24 the ring holds, and the group's refill writes
-  // only slots past them.
-  uint32_t nx;
-  __device__ __forceinline__ void prime(const uint32_t (&ring)[kZs2Ring]) { nx = ring[cons & (kZs2Ring - 1)]; }
-  __device__ __forceinline__ void reload(const uint32_t (&ring)[kZs2Ring]) {
-    if (avail <= 32) {
-      win = (win << 32) | nx;
-      cons++;
-      avail += 32;
-      nx = ring[cons & (kZs2Ring - 1)];
-    }
-  }
-#else
   __device__ __forceinline__ void prime(const uint32_t (&)[kZs2Ring]) {}
   __device__ __forceinline__ void reload(const uint32_t (&ring)[kZs2Ring]) {
-#if RIO_ZS2_BRANCHLESS
-    // (experiment) the ring dword read every time, the refill selected: no
-    // exec-mask branch per reload
-    const bool need = avail <= 32;
-    const uint32_t v = ring[cons & (kZs2Ring - 1)];
-    win = need ? ((win << 32) | v) : win;
-    cons += need ? 1 : 0;
-    avail += need ? 32 : 0;
-#else
     if (avail <= 32) {
       // in the ring once retired from the registers (else a direct load: rare)
       // the ring always holds it: >= 24 dwords at the start of every group of
@@ -1791,9 +1634,7 @@ struct ZBr64 {
       cons++;
       avail += 32;
     }
-#endif
   }
-#endif
   __device__ __forceinline__ uint32_t read(int nb) {  // nb <= 31
     avail -= nb;
     return (uint32_t)(win >> avail) & ((1u << nb) - 1u);
@@ -1846,6 +1687,7 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
   bool active = false, exhausted = !slot;
   ZJob *hp = nullptr;
   uint32_t nseq = 0, i = 0, err = 0, sll = 0, sml = 0, sof = 0;
+  uint32_t rp0 = 0, rp1 = 0, rp2 = 0;  // the job's repeat offsets (kZSym: relative to its start)
   int llg = 0, mlg = 0, ofg = 0;
   uint64_t *raw = nullptr;
   ZBr64 r;
@@ -1915,6 +1757,9 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
     if (starting) {  // the bitstream: container, ring, registers
       i = 0;
       err = 0;
+      rp0 = kZSym;
+      rp1 = kZSym | (1u << 24);
+      rp2 = kZSym | (2u << 24);
       const int64_t start = (int64_t)hp->seq_off, n = (int64_t)hp->seq_len;
       const uint32_t last = n > 0 ? tok8[start + n - 1] : 0u;
       if (last == 0) {  // empty stream or no end marker in its last byte
@@ -1996,14 +1841,10 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
           const uint32_t llc = cl & 63u, mlc = cm & 63u, ofc = cof & 63u;
           if (llc > 35 || mlc > 52 || ofc > 31) {
             err = kZCorrupt;
-          } else if (ofc > 28) {
+          } else if (ofc > 27) {  // (offsets >= 2^28: the serial path)
             err = kZSlow;
           } else {
-#if RIO_ZS2_CODES_ALU
-            const uint32_t mlx = zs_mlx(mlc), llx = zs_llx(llc);
-#else
             const uint32_t mlx = codes.ml[mlc], llx = codes.ll[llc];
-#endif
             const uint32_t ofv = (1u << ofc) + r.read((int)ofc);
             r.reload(rings[wv][ls]);
             const uint32_t ml = (mlx & 0xFFFFFFu) + r.read((int)(mlx >> 24));
@@ -2016,11 +1857,22 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
               sof = zs2_base(cof, no, ofg) + r.read((int)no);
               r.reload(rings[wv][ls]);
             }
-            if (r.overrun()) {
+            // repeat offsets (RFC 8878 3.1.2.5), in terms of the job's starting ones
+            // where they are still unknown: "rep0 - 1" of a symbolic offset adds to its c
+            const uint32_t idx = ofv > 3 ? 0u : ofv + (ll == 0 ? 1u : 0u);
+            const uint32_t dec = (rp0 & kZSym) ? rp0 + 1u : rp0 - 1u;
+            const uint32_t off = idx == 0 ? ofv - 3 : idx == 1 ? rp0 : idx == 2 ? rp1 : idx == 3 ? rp2 : dec;
+            if (idx != 1) {
+              const uint32_t n2 = idx == 2 ? rp2 : rp1;
+              rp1 = rp0;
+              rp0 = off;
+              rp2 = n2;
+            }
+            if (r.overrun() || off == 0) {  // (0: "rep0 - 1" of 1, the serial path's case)
               err = kZCorrupt;
             } else {
               uint64_t &Ek = k == 0 ? E0 : k == 1 ? E1 : k == 2 ? E2 : k == 3 ? E3 : k == 4 ? E4 : k == 5 ? E5 : k == 6 ? E6 : E7;
-              Ek = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
+              Ek = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)off << 35);
               i++;
               if (i == nseq && !r.exact()) err = kZCorrupt;
             }
@@ -2041,7 +1893,12 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
       if (c > 0) r.nf += c;
       pi0 = i0;
       pne = ne;
-      if (hp && !active && (err || (i == nseq && ne > 0))) hp->err = err;  // the job ended in this group
+      if (hp && !active && (err || (i == nseq && ne > 0))) {  // the job ended in this group
+        hp->err = err;
+        hp->rep0 = rp0;
+        hp->rep1 = rp1;
+        hp->rep2 = rp2;
+      }
     } while (!__ballot((slot && !active && !exhausted) || (active && r.nf - r.cons < 24)));
     if (pne > 0) raw[pi0 + 0] = E0;
     if (pne > 1) raw[pi0 + 1] = E1;
@@ -2054,34 +1911,15 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
   }
 }
 
-// One step of the repeat-offset history scan (k_zstd_fix): compose this
-// lane's op (src, c) after the op of the DPP source lane (g o f); lanes the
-// DPP pattern gives no source keep the identity op (slot k <- slot k, + 0).
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ void z_hist_step(uint32_t &src, uint32_t &c0, uint32_t &c1, uint32_t &c2) {
-  constexpr int kIdSrc = 0 | (1 << 2) | (2 << 4);
-  const uint32_t fs = (uint32_t)__builtin_amdgcn_update_dpp(kIdSrc, (int)src, kCtrl, kRowMask, 0xf, false);
-  const uint32_t f0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c0, kCtrl, kRowMask, 0xf, false);
-  const uint32_t f1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1, kCtrl, kRowMask, 0xf, false);
-  const uint32_t f2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c2, kCtrl, kRowMask, 0xf, false);
-  uint32_t ns = 0, nc[3];
-  const uint32_t cc[3] = {c0, c1, c2};
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const uint32_t gs = (src >> (2 * k)) & 3u;
-    const uint32_t fsel = gs == 0 ? f0 : (gs == 1 ? f1 : f2);
-    ns |= (gs == 3 ? 3u : (fs >> (2 * gs)) & 3u) << (2 * k);
-    nc[k] = gs == 3 ? cc[k] : fsel + cc[k];
-  }
-  src = ns;
-  c0 = nc[0];
-  c1 = nc[1];
-  c2 = nc[2];
-}
-
 // ---------------------------------------------------------------- k_zstd_fix
+// an offset of k_zstd_seq2's: its value, or a repeat offset as the job started
+__device__ __forceinline__ uint32_t z_resolve(uint32_t e, uint32_t r0, uint32_t r1, uint32_t r2) {
+  const uint32_t sl = (e >> 24) & 3u, from = sl == 0 ? r0 : (sl == 1 ? r1 : r2);
+  return (e & kZSym) ? from - (e & 0xFFFFFFu) : e;
+}
 // In file order, one wave per recordio block: every job's raw sequences 64 at
-// a time -- repeat offsets resolved by a wave scan of history ops, the serial decoder's
+// a time -- repeat offsets that k_zstd_seq2 left in terms of the job's starting
+// history resolved (round 4; a wave scan of history ops before), the serial decoder's
 // per-sequence checks made lane-parallel from prefix sums (literals left,
 // offset within the frame's output), execution entries written -- then the
 // frame checks (content size), then the frame walk's own error if it stopped
@@ -2125,6 +1963,7 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
     for (uint32_t j = 0; j < njobs && !zerr; j++) {
       const ZJob *hp = reinterpret_cast<const ZJob *>(tok8 + jo);
       const uint32_t flags = uni(hp->flags), regen = uni(hp->regen), nseq = uni(hp->nseq), jerr = uni(hp->err);
+      const uint32_t fr0 = uni(hp->rep0), fr1 = uni(hp->rep1), fr2 = uni(hp->rep2);
       const uint64_t raw_off = uni64(hp->raw_off), next = uni64(hp->next);
       const int64_t fcs = (int64_t)uni64((uint64_t)hp->fcs);
       const uint32_t cks = uni(hp->checksum);
@@ -2153,50 +1992,7 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
           const uint64_t rv = rv_nx;
           if (g0 + 64 < nseq) rv_nx = (uint32_t)l < nseq - g0 - 64 ? raw[g0 + 64 + l] : 0ull;
           const uint32_t ll = (uint32_t)rv & 0x1FFFFu, ml = (uint32_t)(rv >> 17) & 0x3FFFFu;
-          const uint32_t ofv = (uint32_t)(rv >> 35);
-          // Repeat offsets: a sequence maps the offset history (rep0, rep1, rep2)
-          // by an op "slot k <- slot src_k + c_k, or the constant c_k when
-          // src_k = 3" (RFC 8878 3.1.2.5); an inclusive scan of the composed ops
-          // gives each sequence the history after it, whose slot 0 is its offset.
-          uint32_t src, c0, c1 = 0, c2 = 0;
-          {
-            const uint32_t idx = ofv > 3 ? 0u : ofv + (ll == 0 ? 1u : 0u);
-            if (!v || idx == 1) {  // offset = rep0, history unchanged
-              src = 0u | (1u << 2) | (2u << 4);
-              c0 = 0;
-            } else if (idx == 0) {  // a new offset
-              src = 3u | (0u << 2) | (1u << 4);
-              c0 = ofv - 3;
-            } else if (idx == 2) {
-              src = 1u | (0u << 2) | (2u << 4);
-              c0 = 0;
-            } else if (idx == 3) {
-              src = 2u | (0u << 2) | (1u << 4);
-              c0 = 0;
-            } else {  // rep0 - 1 (0 is the error below)
-              src = 0u | (0u << 2) | (1u << 4);
-              c0 = ~0u;
-            }
-          }
-          // inclusive scan by DPP (row shifts, then the row broadcasts, as
-          // wave_incl_sum_dpp); lanes without a source lane compose the identity
-          z_hist_step<0x111, 0xf>(src, c0, c1, c2);  // row_shr:1
-          z_hist_step<0x112, 0xf>(src, c0, c1, c2);  // row_shr:2
-          z_hist_step<0x114, 0xf>(src, c0, c1, c2);  // row_shr:4
-          z_hist_step<0x118, 0xf>(src, c0, c1, c2);  // row_shr:8
-          z_hist_step<0x142, 0xa>(src, c0, c1, c2);  // row_bcast:15
-          z_hist_step<0x143, 0xc>(src, c0, c1, c2);  // row_bcast:31
-          auto apply = [&](uint32_t sk, uint32_t ck) {
-            return sk == 3 ? ck : (sk == 0 ? rep0 : (sk == 1 ? rep1 : rep2)) + ck;
-          };
-          const uint32_t off = apply(src & 3u, c0);
-          {  // the history after the group (lanes past cnt hold the identity)
-            const uint32_t ls = zrl(src, 63), l0 = zrl(c0, 63), l1 = zrl(c1, 63), l2 = zrl(c2, 63);
-            const uint32_t n0 = apply(ls & 3u, l0), n1 = apply((ls >> 2) & 3u, l1), n2 = apply((ls >> 4) & 3u, l2);
-            rep0 = n0;
-            rep1 = n1;
-            rep2 = n2;
-          }
+          const uint32_t off = z_resolve((uint32_t)(rv >> 35), rep0, rep1, rep2);
           // z_exec's checks per sequence: literals left, offset within the frame's output
           const uint32_t lin = wave_incl_sum_dpp(v ? ll : 0u), tin = wave_incl_sum_dpp(v ? ll + ml : 0u);
           const int64_t my_lp = lp + (int64_t)(lin - ll);
@@ -2218,6 +2014,12 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
           olen += zrl(tin, cnt - 1);
         }
         if (zerr) break;
+        // the history after the job, from the one it started with
+        const uint32_t n0 = z_resolve(fr0, rep0, rep1, rep2), n1 = z_resolve(fr1, rep0, rep1, rep2),
+                       n2 = z_resolve(fr2, rep0, rep1, rep2);
+        rep0 = n0;
+        rep1 = n1;
+        rep2 = n2;
       }
       if ((int64_t)regen > lp) pieces((uint64_t)((int64_t)regen - lp), 0, 0);  // the block's last literals
       olen += (int64_t)regen - lp;
@@ -2267,15 +2069,6 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
 #ifndef RIO_ZRING_K
 #define RIO_ZRING_K 5
 #endif
-#ifndef RIO_ZEXEC_NOLIT
-#define RIO_ZEXEC_NOLIT 0
-#endif
-#ifndef RIO_ZEXEC_NOREADY
-#define RIO_ZEXEC_NOREADY 0
-#endif
-#ifndef RIO_ZEXEC_NOREST
-#define RIO_ZEXEC_NOREST 0
-#endif
 #ifndef RIO_ZEXEC_READY_MAX
 #define RIO_ZEXEC_READY_MAX 32  // longest match a lane copies on its own in the parallel round
 #endif
@@ -2293,11 +2086,7 @@ __device__ __forceinline__ uint32_t zr_slot(uint32_t x) {
   return x - __umulhi(x >> 12, 0xFFFFFFFFu / kZRingK + 1u) * kZRing;
 }
 __device__ __forceinline__ uint8_t zr_src(const uint8_t *ring, const uint8_t *out, uint32_t pos, uint32_t base) {
-#if RIO_ZEXEC_NOFAR  // (measurement only: far sources read from the ring -- wrong bytes, the cost of their loads)
-  return ring[zr_slot(pos)];
-#else
   return pos + kZHist >= base ? ring[zr_slot(pos)] : out[pos];
-#endif
 }
 // k mod d for k < 2^20, d >= 1
 __device__ __forceinline__ uint32_t z_umod(uint32_t k, uint32_t dv) {
@@ -2338,6 +2127,14 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
     // (from dword-aligned pf_nx; ~0: not prefetched), so a group usually
     // starts without waiting for memory
     uint64_t e_nx = (uint32_t)l < ntok ? ents[-1 - (int64_t)l] : 0ull;
+    // entries two groups ahead, so that the next group's far match sources
+    // (<= 8 bytes, already flushed) are loaded while this group runs: fl_prev is
+    // `flushed` when the next group's entries were requested, so once they
+    // have arrived every flush store before that request has completed (vmcnt
+    // counts in order) and those bytes are visible without a drain
+    uint64_t e_nx2 = 64u + (uint32_t)l < ntok ? ents[-1 - (int64_t)(64 + l)] : 0ull;
+    uint32_t fl_prev = 0, cq0 = 0, cq1 = 0, cq2 = 0;
+    bool cqok = false;  // this group's lane entry has its source in cq0..cq2
     uint32_t pf_nx = ~0u, lit_nx = 0;
     if (lit0 + 256 <= ent_end) {
       pf_nx = 0;
@@ -2353,14 +2150,38 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
         litbuf[l] = lit_nx;
         lit_at = pf_nx;
       }
-      if (g0 + 64 < ntok)
-        e_nx = (uint32_t)l < ntok - g0 - 64 ? ents[-1 - (int64_t)(g0 + 64 + l)] : 0ull;
+      e_nx = e_nx2;
+      if (g0 + 128 < ntok)
+        e_nx2 = (uint32_t)l < ntok - g0 - 128 ? ents[-1 - (int64_t)(g0 + 128 + l)] : 0ull;
       const uint32_t ll0 = (uint32_t)e & 0xffffu, ml0 = (uint32_t)(e >> 16) & 0xffffu, off = (uint32_t)(e >> 32);
       const bool mark = ll0 == kZMark;
       const uint32_t len = mark ? 0u : ll0 + ml0, lits = mark ? 0u : ll0;
       const uint32_t incl = wave_incl_sum_dpp(len), lincl = wave_incl_sum_dpp(lits);
       const uint32_t excl = incl - len, lexcl = lincl - lits;
       const unsigned long long marks = __ballot(mark);
+      uint32_t nq0 = 0, nq1 = 0, nq2 = 0;
+      bool nqok = false;
+      {  // the next group's short far sources, loaded now (see fl_prev)
+        const uint32_t F = fl_prev;
+        fl_prev = flushed;
+        if (g0 + 64 < ntok) {
+          const uint32_t l1 = (uint32_t)e_nx & 0xffffu, m1 = (uint32_t)(e_nx >> 16) & 0xffffu;
+          const uint32_t o1 = (uint32_t)(e_nx >> 32);
+          const bool k1 = l1 == kZMark;
+          const uint32_t len1 = k1 ? 0u : l1 + m1;
+          const uint32_t inc1 = wave_incl_sum_dpp(len1);
+          const uint32_t base1 = olen + zrl(incl, n - 1);  // the next group's first output byte
+          const uint32_t dst1 = base1 + inc1 - len1 + l1, src1 = dst1 - o1;
+          nqok = (uint32_t)l < ntok - g0 - 64 && !k1 && m1 != 0 && m1 <= 8 && o1 <= dst1 && (o1 >= 8 || m1 <= o1) &&
+                 src1 + m1 <= F && src1 + m1 - 1 + kZHist < base1;
+          if (nqok) {
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(out + (src1 & ~3u));
+            nq0 = w[0];
+            nq1 = w[1];
+            nq2 = w[2];
+          }
+        }
+      }
       {  // the next group's literals start where this group's end
         const uint32_t na = (litpos + zrl(lincl, n - 1)) & ~3u;
         pf_nx = ~0u;
@@ -2393,7 +2214,7 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
             wave_lds_sync();
             const uint8_t *lb = reinterpret_cast<const uint8_t *>(litbuf) + (litpos - a0);
             const uint32_t lp = lexcl - ls;
-            if (myll && myll <= 32 && !RIO_ZEXEC_NOLIT) {  // (RIO_ZEXEC_NOLIT: measurement only, wrong bytes)
+            if (myll && myll <= 32) {
               const uint32_t q0 = base + p;
               for (uint32_t k = 0; k < myll; k++) ring[zr_slot(q0 + k)] = lb[lp + k];
             }
@@ -2416,7 +2237,7 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
             {  // bytes read from the decode region (pos + kZHist < base) visible first: drain
                // the wave's stores only when one of them lies at or above the last drain's mark
               const uint32_t hi = min(src + (myml < off ? myml : off), base - kZHist);
-              if (__ballot(m && src + kZHist < base && hi > synced)) {
+              if (__ballot(m && !cqok && src + kZHist < base && hi > synced)) {
                 zmem_sync();
                 synced = flushed;
               }
@@ -2426,7 +2247,7 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
             const uint32_t R = zrl(dst, (uint32_t)(__ffsll((long long)mm) - 1));
             const uint32_t src_end = src + (myml < off ? myml : off);
             const bool ready = m && src_end <= R && myml <= (uint32_t)RIO_ZEXEC_READY_MAX;
-            if (ready && !RIO_ZEXEC_NOREADY) {  // (RIO_ZEXEC_NOREADY: measurement only, wrong bytes)
+            if (ready) {
               // the source wholly in the ring or wholly flushed (src + kZHist vs base is
               // monotone in the byte), neither ring range wrapping: 12 aligned bytes per
               // 8-byte piece, two funnel shifts, byte stores at immediate offsets
@@ -2437,7 +2258,9 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
                 for (uint32_t k = 0; k < myml; k += 8) {
                   const uint32_t *w = all_ring ? reinterpret_cast<const uint32_t *>(ring + ((ss + k) & ~3u))
                                                : reinterpret_cast<const uint32_t *>(out + ((src + k) & ~3u));
-                  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = (src + k) & 3u;  // ss = src (mod 4)
+                  const bool pre = cqok;  // (a prefetched source is far and <= 8 bytes: k = 0 only)
+                  const uint32_t w0 = pre ? cq0 : w[0], w1 = pre ? cq1 : w[1], w2 = pre ? cq2 : w[2];
+                  const uint32_t sh = (src + k) & 3u;  // ss = src (mod 4)
                   const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
                   uint8_t *dp = ring + ds + k;
 #pragma unroll
@@ -2459,7 +2282,7 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
             }
             // ... then the rest in order, each by the whole wave (every byte it
             // reads precedes it and is final by then)
-            unsigned long long rest = RIO_ZEXEC_NOREST ? 0ull : mm & ~__ballot(ready);  // (NOREST: measurement only)
+            unsigned long long rest = mm & ~__ballot(ready);
 #ifdef RIO_ZPROF
             if (l == 0) {
               atomicAdd(&d.ctl->zx[1], 1ull);
@@ -2504,6 +2327,10 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
         }
         s = e1;
       }
+      cq0 = nq0;
+      cq1 = nq1;
+      cq2 = nq2;
+      cqok = nqok;
     }
     wave_lds_sync();
     zr_flush(ring, out, flushed, olen);
@@ -2596,220 +2423,6 @@ __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, D
   }
 }
 
-#if RIO_ZSTD_EXEC2
-// ---------------------------------------------------------------- k_zstd_exec2
-// Execution pass on the copy-pass machinery of k_flate_lz2 (lz_ring.h): one
-// wave per block, a 4 KiB LDS ring, history older than the ring read back
-// from the decode region (agent-scope loads), literals read from the block's
-// literal area the same way. A batch is up to 128 entries (2 per lane), each
-// two copies -- its literal run, then its match -- whose output fits kL2Span;
-// a frame-end mark ends a batch (checksummed frames are hashed from HBM once
-// their bytes are flushed). Entries are at most kZPiece + kZPiece bytes
-// (k_zstd_fix splits longer runs and matches).
-static_assert(kL2Near >= kL2Span + 16 + kZPiece, "zstd copies from HBM must be flushed two batches back");
-static_assert(2 * kZPiece <= kL2Span, "an entry must fit a batch");
-
-__global__ void __launch_bounds__(64) k_zstd_exec2(DevBufs d, const unsigned long long *nblocks) {
-  __shared__ __attribute__((aligned(16))) uint8_t ring[kL2Ring];
-  const int l = lane_id();
-  const uint64_t nb = uni64(*nblocks);
-  for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
-    FlState *sp = &d.fl[b];
-    const uint32_t mode = uni(sp->mode);
-    if (mode != kZsExec && mode != kZsErrCk) continue;
-    const uint8_t *region = reinterpret_cast<const uint8_t *>(d.tok + uni64(d.blk_c0[b]) * (uint64_t)kZTokPerChunk);
-    const uint64_t lit0 = uni64(sp->bitpos), ent_end = uni64(sp->hdrpos);
-    const uint32_t ntok = uni(sp->ntok);
-    const uint64_t *ents = reinterpret_cast<const uint64_t *>(region + ent_end);  // entry e at ents[-1 - e]
-    const uint32_t *gl = reinterpret_cast<const uint32_t *>(region + lit0);       // 16-aligned
-    uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
-    const uint32_t *gw = reinterpret_cast<const uint32_t *>(out);
-    uint32_t olen = 0, litpos = 0, fstart = 0, zerr = 0;
-    wave_lds_sync();
-    uint64_t pre[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) pre[k] = (64u * k + (uint32_t)l < ntok) ? ents[-1 - (int64_t)(64 * k + l)] : 0ull;
-    uint32_t cur = 0;
-    while (cur < ntok && !zerr) {
-      uint64_t e[2];
-#pragma unroll
-      for (int k = 0; k < 2; k++) e[k] = pre[k];
-      // a frame end first in line: flush, check the frame's checksum
-      const uint64_t e0 = readlane_u64(e[0], 0);
-      if ((e0 & 0xffffu) == kZMark) {
-        if (((e0 >> 16) & 0xffffu) == kZMarkCk) {
-          if (olen & 15) {
-            if (l == 0) {
-              const uint32_t x = olen & ~15u;
-              *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
-            }
-          }
-          zmem_sync();
-          const uint32_t got = (uint32_t)z_xxh64(out + fstart, olen - fstart);
-          if (got != (uint32_t)(e0 >> 32)) {
-            zerr = kZChecksum;
-            break;
-          }
-        }
-        fstart = olen;
-        cur++;
-#pragma unroll
-        for (int k = 0; k < 2; k++)
-          pre[k] = (cur + 64u * k + (uint32_t)l < ntok) ? ents[-1 - (int64_t)(cur + 64 * k + l)] : 0ull;
-        continue;
-      }
-      // this batch: entries up to the first mark, output within kL2Span
-      uint32_t fm = 128;
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const bool valid = cur + 64u * k + (uint32_t)l < ntok;
-        const unsigned long long m = __ballot(valid && (e[k] & 0xffffu) == kZMark);
-        if (fm == 128 && m) fm = 64 * k + (__ffsll((long long)m) - 1);
-      }
-      uint32_t ll[2], ml[2], p[2], lp[2];
-      uint32_t carry = 0, lcarry = 0, take = 0, emax = 0, lmax = 0;
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const uint32_t idx = 64 * k + (uint32_t)l;
-        const bool valid = cur + idx < ntok && idx < fm;
-        ll[k] = valid ? (uint32_t)e[k] & 0xffffu : 0u;
-        ml[k] = valid ? (uint32_t)(e[k] >> 16) & 0xffffu : 0u;
-        const uint32_t len = ll[k] + ml[k];
-        const uint32_t incl = wave_incl_sum_dpp(len) + carry;
-        const uint32_t lincl = wave_incl_sum_dpp(ll[k]) + lcarry;
-        p[k] = incl - len;
-        lp[k] = lincl - ll[k];
-        const bool ok = valid && incl <= kL2Span;  // a prefix of the entries
-        take += (uint32_t)__popcll(__ballot(ok));
-        if (ok) {
-          emax = incl;
-          lmax = lincl;
-        } else {
-          ll[k] = ml[k] = 0;
-        }
-        carry = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-        lcarry = (uint32_t)__builtin_amdgcn_readlane(lincl, 63);
-      }
-      const uint32_t total = (uint32_t)__reduce_max_sync(~0ull, emax);
-      const uint32_t ltotal = (uint32_t)__reduce_max_sync(~0ull, lmax);
-      const uint32_t B0 = olen;
-      {  // zero the batch's ring bytes (their dwords; the history bytes of the first one stay)
-        uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
-        const uint32_t z0 = (B0 + 3) >> 2, z1 = (B0 + total + 3) >> 2;
-        for (uint32_t z = z0 + (uint32_t)l; z < z1; z += 64) rw[z & (kL2Mask >> 2)] = 0u;
-        if ((B0 & 3) && l == 0) atomicAnd(&rw[(B0 >> 2) & (kL2Mask >> 2)], (1u << (8 * (B0 & 3))) - 1);
-        wave_lds_sync();
-      }
-      const uint32_t near = B0 > kL2Near ? B0 - kL2Near : 0u;  // positions >= near: in the ring
-      // slots 2k (entry k's literals, from the literal area) and 2k + 1 (its
-      // match): literals and matches sourced before the batch now, the others pending
-      uint32_t cs[4], cn[4], cp[4], dist[4], clen[4], glob = 0, litm = 0;
-      bool pend[4];
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const int a = 2 * k, m = 2 * k + 1;
-        cp[a] = p[k];
-        clen[a] = ll[k];
-        cs[a] = litpos + lp[k];
-        cn[a] = ll[k];
-        dist[a] = 0;
-        pend[a] = false;
-        if (ll[k]) {
-          glob |= 1u << a;
-          litm |= 1u << a;
-        }
-        cp[m] = p[k] + ll[k];
-        clen[m] = ml[k];
-        dist[m] = (uint32_t)(e[k] >> 32);
-        const uint32_t x = B0 + cp[m];
-        cs[m] = x - dist[m];
-        cn[m] = 0;
-        pend[m] = false;
-        if (ml[k]) {
-          if (cs[m] < near) {
-            cn[m] = ml[k];
-            glob |= 1u << m;
-          } else if (cs[m] + ml[k] <= B0) {
-            cn[m] = ml[k];
-          } else {
-            pend[m] = true;
-          }
-        }
-      }
-      // the next batch's entries (issued before this batch's stores: see k_flate_lz2)
-      const uint32_t nx = cur + take;
-#pragma unroll
-      for (int k = 0; k < 2; k++)
-        pre[k] = (nx + 64u * k + (uint32_t)l < ntok) ? ents[-1 - (int64_t)(nx + 64 * k + l)] : 0ull;
-      // the copies above (every slot), then the matches sourced inside the
-      // batch in rounds, ring to ring, slot by slot, only the slots some lane
-      // copies in that round (as k_flate_lz2)
-      l2_copy4(ring, gw, cs, B0, cp, cn, glob, gl, litm);
-      for (;;) {
-        wave_lds_sync();
-        int kf = -1, lf = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const unsigned long long mm = __ballot(pend[k]);
-          if (kf < 0 && mm) {
-            kf = k;
-            lf = __ffsll((long long)mm) - 1;
-          }
-        }
-        if (kf < 0) break;
-        // R: the first pending match; every byte before it is final
-        const uint32_t R = (uint32_t)__builtin_amdgcn_readlane(pick4(cp, kf), lf);
-        const uint32_t Df = (uint32_t)__builtin_amdgcn_readlane(pick4(dist, kf), lf);
-        const uint32_t Nf = (uint32_t)__builtin_amdgcn_readlane(pick4(clen, kf), lf);
-        const bool run = Df < Nf;  // it overlaps its own output: the whole wave copies it
-#pragma unroll
-        for (int k = 1; k < 4; k += 2) {  // (only match slots are ever pending)
-          uint32_t n = 0;
-          if (pend[k]) {
-            const bool first = k == kf && l == lf;
-            if (first || cs[k] + clen[k] <= B0 + R) {  // source ends at or before R
-              if (!first || !run) n = clen[k];
-              pend[k] = false;
-            }
-          }
-          if (__ballot(n != 0)) l2_copy1_ring(ring, cs[k], B0 + cp[k], n);
-        }
-        if (run) {  // byte k of the run = byte (k mod dist) of the dist bytes before it (final)
-          const uint32_t xs = B0 + R - Df, xd = B0 + R;
-          for (uint32_t k0 = 0; k0 < Nf; k0 += 64) {
-            const uint32_t k = k0 + (uint32_t)l;
-            if (k < Nf) {
-              const uint32_t v = ring[(xs + z_umod(k, Df)) & kL2Mask];
-              atomicOr(reinterpret_cast<uint32_t *>(ring) + (((xd + k) >> 2) & (kL2Mask >> 2)), v << (8 * ((xd + k) & 3)));
-            }
-          }
-        }
-      }
-      // complete 16 B units of the batch to HBM
-      const uint32_t end = B0 + total;
-      for (uint32_t x = (B0 & ~15u) + 16 * (uint32_t)l; x + 16 <= end; x += 1024)
-        *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
-      olen = end;
-      litpos += ltotal;
-      cur += take;
-    }
-    // the last partial unit (the decode region is 256-aligned and sized in 256 B steps)
-    if ((olen & 15) && l == 0) {
-      const uint32_t x = olen & ~15u;
-      *reinterpret_cast<uint4 *>(out + x) = *reinterpret_cast<const uint4 *>(ring + (x & kL2Mask));
-    }
-    if (l == 0) {
-      if (!zerr && mode == kZsExec) {
-        d.blk_out_len[b] = olen;
-      } else {  // a checksum mismatch: the exact decoder re-decodes the block and names the error
-        sp->mode = kZsSlow;
-        atomicAdd(&d.ctl->pad[1], 1ull);
-      }
-    }
-  }
-}
-
-#endif  // RIO_ZSTD_EXEC2
 
 uint64_t zstd_grid(int ncu) { return (uint64_t)ncu * kZWaves; }
 uint64_t zstd_lit_bytes(uint64_t grid) { return grid * kZLitStride; }
@@ -2821,10 +2434,8 @@ void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long
   uint64_t g = max_blocks < grid ? max_blocks : grid;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(k_zstd_ent, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
-  if (kZstdSeq2)  // 4-wave workgroups sharing the CU's LDS (kZs2Groups per CU)
-    hipLaunchKernelGGL(k_zstd_seq2, dim3((unsigned)(grid / kZWaves * kZs2Groups)), dim3(256), 0, st, d);
-  else
-    hipLaunchKernelGGL(k_zstd_seq, dim3((unsigned)(grid / kZWaves * kZSeqWaves)), dim3(64), 0, st, d);
+  // 4-wave workgroups sharing the CU's LDS (kZs2Groups per CU)
+  hipLaunchKernelGGL(k_zstd_seq2, dim3((unsigned)(grid / kZWaves * kZs2Groups)), dim3(256), 0, st, d);
   uint64_t g3 = grid / kZWaves * kZFixWaves;
   if (g3 > max_blocks) g3 = max_blocks;
   if (g3 < 1) g3 = 1;
@@ -2832,14 +2443,7 @@ void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long
   uint64_t g2 = grid / kZWaves * kZExecWaves;
   if (g2 > max_blocks) g2 = max_blocks;
   if (g2 < 1) g2 = 1;
-#if RIO_ZSTD_EXEC2
-  uint64_t g4 = (uint64_t)(grid / kZWaves) * kL2Waves;
-  if (g4 > max_blocks) g4 = max_blocks;
-  if (g4 < 1) g4 = 1;
-  hipLaunchKernelGGL(k_zstd_exec2, dim3((unsigned)g4), dim3(64), 0, st, d, nblocks);
-#else
   hipLaunchKernelGGL(k_zstd_exec, dim3((unsigned)g2), dim3(64), 0, st, d, nblocks);
-#endif
   hipLaunchKernelGGL(k_zstd, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
 }
 

@@ -21,7 +21,8 @@
 // while one stage is folded the next three are in flight (16 waves per CU keep
 // 192 KiB outstanding).
 //
-// Fused parse (ablation builds with -DRIO_FUSED_PARSE=1; none codec, k_crc<true>): the wave that checksums a block's
+// Fused parse (k_crc<true>, round 2; measured slower and not instantiated:
+// DESIGN.md §5; none codec): the wave that checksums a block's
 // first chunk also parses the block (parse_block.h: magic handling, the
 // varint header, one view per item, straddler copies). The header window --
 // payload bytes 0..1023 = chunk bytes 28..1051 -- is taken from the rows the
@@ -202,19 +203,13 @@ __global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restric
 }
 
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
-                hipStream_t st, const ParseArgs *fused) {
+                hipStream_t st) {
   uint64_t g = (nchunks + kCrcWaves - 1) / kCrcWaves;
   const uint64_t cap = (uint64_t)(ncu > 0 ? ncu : 256);
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   const CrcParseIn pin{d.ck_index, d.ck_block, d.blk_meta, d.blk_len, d.blk_item_base, d.ck_pay};
-#if RIO_FUSED_PARSE
-  if (fused)
-    hipLaunchKernelGGL(k_crc<true>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
-                       d.crc_fix_a, d.crc_fix_b, d, ca, pin, *fused);
-  else
-#endif
-    hipLaunchKernelGGL(k_crc<false>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
+  hipLaunchKernelGGL(k_crc<false>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
                        d.crc_fix_a, d.crc_fix_b, d, ca, pin, ParseArgs{});
 }
 

@@ -2,8 +2,8 @@
 // (include/rio_gpu.h). One rio_ctx = one device, two HIP streams, buffers sized
 // at rio_open and grown only when a span needs more.
 //
-// Launch order per span (one stream; an ablation build with -DRIO_TWO_STREAMS=1
-// puts the parse path on a second stream):
+// Launch order per span (one stream; the parse beside k_crc on a second stream
+// measured slower):
 //   none:       memsets, k_chunk_meta, chunk scans, block scan (item slots),
 //               k_parse, k_parse_slow, [straddler scan], k_strad, k_crc, k_resolve
 //   flate/zstd: memsets, k_chunk_meta, chunk scans, codec decode, item counts,
@@ -49,7 +49,7 @@ void launch_block_files(const DevBufs &d, const unsigned long long *seg_end, con
                         uint64_t nseg, uint64_t max_blocks, hipStream_t st);
 // crc.hip
 void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const CrcArgs &ca, int ncu,
-                hipStream_t st, const ParseArgs *fused);
+                hipStream_t st);
 // codec.hip
 void launch_compact(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
@@ -118,9 +118,8 @@ void rio_results_free(rio_results *r) {
 struct rio_ctx {
   int device = 0;
   int ncu = 256;
-  hipStream_t st = nullptr, st2 = nullptr;
+  hipStream_t st = nullptr;
   hipEvent_t ev[kNumEv] = {};
-  hipEvent_t evA = nullptr, evB = nullptr;  // stream hand-offs (no timing)
   bool last_had_dec = false;
   int ev_parse0 = kEvParse0, ev_crc0 = kEvCrc0;  // the events the last run's parse / CRC stages start at
   bool item_end_mode = false;  // RIO_CFG_ITEM_END: device results carry item_end (cumSize)
@@ -250,10 +249,7 @@ static void free_all(rio_ctx *c) {
   if (c->h_v1) hipHostFree(c->h_v1);
   for (hipEvent_t e : c->ev)
     if (e) hipEventDestroy(e);
-  if (c->evA) hipEventDestroy(c->evA);
-  if (c->evB) hipEventDestroy(c->evB);
   if (c->st) hipStreamDestroy(c->st);
-  if (c->st2 && c->st2 != c->st) hipStreamDestroy(c->st2);
 }
 
 static int ctx_init(rio_ctx *c, const rio_config *cfg) {
@@ -278,11 +274,7 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   c->item_cap = (cfg && cfg->max_items) ? cfg->max_items : span / 64 + 1024;
   c->dec_cap = 0;
   HIP_OK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-  if (RIO_TWO_STREAMS) HIP_OK(hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking));
-  else c->st2 = c->st;
   for (hipEvent_t &e : c->ev) HIP_OK(hipEventCreate(&e));
-  HIP_OK(hipEventCreateWithFlags(&c->evA, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&c->evB, hipEventDisableTiming));
   if (alloc_bufs(c)) return -1;
   DevBufs &d = c->d;
   if (dalloc(&d.ctl, 1) || dalloc(&c->nblocks_dev, 2) || dalloc(&d.fl_more, 64)) return -1;
@@ -305,7 +297,6 @@ int rio_ctx_reserve_span(rio_ctx *c, uint64_t bytes) {
   if (bytes <= c->max_span) return 0;
   HIP_OK(hipSetDevice(c->device));
   HIP_OK(hipStreamSynchronize(c->st));
-  if (c->st2 != c->st) HIP_OK(hipStreamSynchronize(c->st2));
   c->max_span = bytes;
   c->max_chunks = bytes / kChunk;
   c->max_blocks = c->max_chunks;
@@ -390,7 +381,6 @@ void rio_close(rio_ctx *ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->st);
-  if (ctx->st2 != ctx->st) hipStreamSynchronize(ctx->st2);
   for (auto &b : ctx->buf_pool) hipHostFree(b.first);
   for (rio_results *r : ctx->res_pool) rio_results_free(r);
   free_all(ctx);
@@ -490,7 +480,7 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
                    int tail_partial, int32_t codec, int32_t mode, bool sparse, int attempt, int stage_flags = 0) {
   if (sparse && codec == RIO_CODEC_NONE && ensure_side(c, nchunks * (uint64_t)kChunk)) return -1;
   DevBufs &d = c->d;
-  hipStream_t st = c->st, st2 = c->st2;
+  hipStream_t st = c->st;
   c->last_nchunks = nchunks;
   c->last_cmp = false;  // records are d.dec / d.side until a host result compacts them
   HIP_OK(hipEventRecord(c->ev[kEvStart], st));
@@ -504,13 +494,10 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   const bool run_parse = !(RIO_ABLATE & 2) && mode != kModeRaw,
              run_crc = !(RIO_ABLATE & 4) && mode != kModeRaw && !(stage_flags & kStageNoCrc);
   const bool no_items = (stage_flags & kStageNoItems) != 0;
-  // ablation builds (-DRIO_FUSED_PARSE=1): none codec in one pass -- the wave
-  // that checksums a block's first chunk parses the block
-  const bool fused = RIO_FUSED_PARSE && codec == RIO_CODEC_NONE && run_parse && run_crc && nchunks > 0;
   const CrcArgs ca{RIO_ABLATE, 0};
   // order: chunk pass (headers + scans), (decode), parse, k_crc, resolve
   c->ev_crc0 = kEvCrc0;
-  if (!run_crc || fused || nchunks == 0) {  // (no CRC pass later: a zero-length interval)
+  if (!run_crc || nchunks == 0) {  // (no CRC pass later: a zero-length interval)
     HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
     HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
   }
@@ -553,59 +540,42 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   }
   // (an event record costs ~5 us of GPU time between kernels: the stage
   // boundaries share events where they coincide -- parse starts at kEvDec or
-  // kEvScans, the CRC at kEvParse1 -- and the hand-offs run only when an
-  // ablation build splits the parse onto a second stream)
+  // kEvScans, the CRC at kEvParse1)
   if (c->last_had_dec) HIP_OK(hipEventRecord(c->ev[kEvDec], st));
   c->ev_parse0 = c->last_had_dec ? kEvDec : kEvScans;
-  if (st2 != st) {
-    HIP_OK(hipEventRecord(c->evA, st));
-    HIP_OK(hipStreamWaitEvent(st2, c->evA, 0));
-    HIP_OK(hipEventRecord(c->ev[kEvParse0], st2));
-    c->ev_parse0 = kEvParse0;
-  }
   if (nchunks > 0 && run_parse) {
     ParseArgs pa{span, nchunks, limit_chunk, mode, codec, c->nblocks_dev, c->item_cap, c->side_cap, sparse,
                  (c->item_end_mode && sparse) ? 1 : 0};
     pa.no_items = no_items ? 1 : 0;
-    if (no_items) HIP_OK(hipMemsetAsync(d.blk_nitems, 0, max_blocks * sizeof(unsigned long long), st2));
-    else if (codec != RIO_CODEC_NONE) launch_dec_nitems(d, c->nblocks_dev, max_blocks, st2);
-    launch_block_scan(d.blk_nitems, d.blk_item_base, d.scan_tmp, c->nblocks_dev, max_blocks, st2);
-    if (fused) {
-      HIP_OK(hipEventRecord(c->ev[kEvCrc0], st2));
-      launch_crc(span, nchunks, d, ca, c->ncu, st2, &pa);
-      HIP_OK(hipEventRecord(c->ev[kEvCrc1], st2));
-    } else if (codec == RIO_CODEC_NONE && mode == kModeBody && !no_items) {
+    if (no_items) HIP_OK(hipMemsetAsync(d.blk_nitems, 0, max_blocks * sizeof(unsigned long long), st));
+    else if (codec != RIO_CODEC_NONE) launch_dec_nitems(d, c->nblocks_dev, max_blocks, st);
+    launch_block_scan(d.blk_nitems, d.blk_item_base, d.scan_tmp, c->nblocks_dev, max_blocks, st);
+    if (codec == RIO_CODEC_NONE && mode == kModeBody && !no_items) {
       // the common block shape in a lean kernel, the rest listed for k_parse
-      if (pa.end_mode) launch_lean_end(d, pa, max_blocks, st2);  // (item-end device results)
-      else launch_parse_lean(d, pa, max_blocks, st2);
+      if (pa.end_mode) launch_lean_end(d, pa, max_blocks, st);  // (item-end device results)
+      else launch_parse_lean(d, pa, max_blocks, st);
       ParseArgs pl = pa;
       pl.list = d.blk_coff;
       pl.list_n = &d.ctl->n_retry;
-      launch_parse(d, pl, max_blocks, st2);
+      launch_parse(d, pl, max_blocks, st);
     } else {
-      launch_parse(d, pa, max_blocks, st2);
+      launch_parse(d, pa, max_blocks, st);
     }
-    launch_parse_slow(d, pa, max_blocks, st2);
+    launch_parse_slow(d, pa, max_blocks, st);
     if (codec == RIO_CODEC_NONE) {
-      if (!sparse) launch_chunk_scan(d.ck_ssz, d.ck_sbase, d.scan_tmp, nchunks, st2);
-      launch_strad(span, d, nchunks, c->side_cap, sparse, pa.end_mode, st2);
+      if (!sparse) launch_chunk_scan(d.ck_ssz, d.ck_sbase, d.scan_tmp, nchunks, st);
+      launch_strad(span, d, nchunks, c->side_cap, sparse, pa.end_mode, st);
     }
   } else if (nchunks == 0) {
-    HIP_OK(hipMemsetAsync(d.blk_item_base, 0, 8, st2));
-    HIP_OK(hipMemsetAsync(d.ck_sbase, 0, 8, st2));
+    HIP_OK(hipMemsetAsync(d.blk_item_base, 0, 8, st));
+    HIP_OK(hipMemsetAsync(d.ck_sbase, 0, 8, st));
   }
-  HIP_OK(hipEventRecord(c->ev[kEvParse1], st2));
-  if (st2 != st) HIP_OK(hipEventRecord(c->evB, st2));
-  if (!fused && run_crc && nchunks > 0) {
+  HIP_OK(hipEventRecord(c->ev[kEvParse1], st));
+  if (run_crc && nchunks > 0) {
     c->ev_crc0 = kEvParse1;
-    if (st2 != st) {
-      HIP_OK(hipEventRecord(c->ev[kEvCrc0], st));
-      c->ev_crc0 = kEvCrc0;
-    }
-    launch_crc(span, nchunks, d, ca, c->ncu, st, nullptr);
+    launch_crc(span, nchunks, d, ca, c->ncu, st);
     HIP_OK(hipEventRecord(c->ev[kEvCrc1], st));
   }
-  if (st2 != st) HIP_OK(hipStreamWaitEvent(st, c->evB, 0));
   if (mode != kModeRaw) {
     ResolveArgs ra{span, nchunks, is_file_end, tail_partial, mode, codec, c->nblocks_dev, limit_chunk, sparse, 0};
     launch_resolve(d, ra, st);

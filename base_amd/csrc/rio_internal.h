@@ -61,14 +61,6 @@ enum Mode : int32_t { kModeBody = 0, kModeHeader = 1, kModeTrailer = 2, kModeLas
 #ifndef RIO_ABLATE
 #define RIO_ABLATE 0
 #endif
-#ifndef RIO_TWO_STREAMS
-#define RIO_TWO_STREAMS 0
-#endif
-// Ablation: the none-codec parse fused into k_crc (crc.hip). Measured slower
-// (DESIGN.md §5), so the shipped library runs k_crc and k_parse separately.
-#ifndef RIO_FUSED_PARSE
-#define RIO_FUSED_PARSE 0
-#endif
 
 // Control block written by the kernels, read back by the host (one copy).
 struct Ctl {
@@ -261,11 +253,7 @@ struct ResolveArgs {
 // ---- host helpers: GF(2) arithmetic of the reflected CRC-32 polynomial ----
 constexpr uint32_t kPoly = 0xEDB88320u;
 #ifndef RIO_FOLD_COPIES
-#if RIO_FUSED_PARSE
-#define RIO_FOLD_COPIES 16  // LDS room for the fused parse's staging
-#else
 #define RIO_FOLD_COPIES 32
-#endif
 #endif
 constexpr int kFoldCopies = RIO_FOLD_COPIES;     // bank-private replicas of each fold table
 constexpr int kFoldShift = kFoldCopies == 32 ? 7 : (kFoldCopies == 16 ? 6 : 5);  // log2(4 * copies)
