@@ -1082,15 +1082,10 @@ struct ZJob {
   uint32_t checksum, logs;  // frame checksum (kJCk); ll_log | of_log << 8 | ml_log << 16
   int64_t fcs;              // frame content size, at the frame's last job (-1: none)
   uint64_t tab_off;         // ll, ml, of cells (u32 x 2^log each)
-  uint64_t raw_off;         // raw sequences (u64 x nseq): ll | ml << 17 | offset << 35 (kZSym: symbolic)
+  uint64_t raw_off;         // raw sequences (u64 x nseq): ll | ml << 17 | offset value << 35
   uint64_t next;            // the block's next job header
-  uint32_t err, rep0;       // k_zstd_seq2: 0, kZCorrupt or kZSlow; the repeat offsets after the
-  uint32_t rep1, rep2;      // job's last sequence (kZSym: in terms of the ones before its first)
+  uint32_t err, pad;        // k_zstd_seq: 0, kZCorrupt or kZSlow
 };
-// An offset as k_zstd_seq2 writes it: the value (< 2^28), or kZSym | slot << 24 | c =
-// "repeat offset `slot` as it was before the job's first sequence, minus c" (the
-// job's starting history is its predecessor's final one, known only in file order)
-constexpr uint32_t kZSym = 1u << 28;
 constexpr int64_t kZJobHdr = (sizeof(ZJob) + 15) / 16 * 16;  // header bytes; 16-aligned tables follow
 constexpr uint32_t kJFirst = 1, kJLast = 2, kJCk = 4, kJLit = 8;
 
@@ -1134,9 +1129,7 @@ struct ZJobSink {
       h->raw_off = region + (uint64_t)(at + kZJobHdr + tabr);
       h->next = 0;
       h->err = 0;
-      h->rep0 = kZSym;
-      h->rep1 = kZSym | (1u << 24);
-      h->rep2 = kZSym | (2u << 24);
+      h->pad = 0;
       if (last >= 0) hdr(last)->next = region + (uint64_t)at;
     }
     pend_first = 0;
@@ -1687,7 +1680,6 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
   bool active = false, exhausted = !slot;
   ZJob *hp = nullptr;
   uint32_t nseq = 0, i = 0, err = 0, sll = 0, sml = 0, sof = 0;
-  uint32_t rp0 = 0, rp1 = 0, rp2 = 0;  // the job's repeat offsets (kZSym: relative to its start)
   int llg = 0, mlg = 0, ofg = 0;
   uint64_t *raw = nullptr;
   ZBr64 r;
@@ -1757,9 +1749,6 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
     if (starting) {  // the bitstream: container, ring, registers
       i = 0;
       err = 0;
-      rp0 = kZSym;
-      rp1 = kZSym | (1u << 24);
-      rp2 = kZSym | (2u << 24);
       const int64_t start = (int64_t)hp->seq_off, n = (int64_t)hp->seq_len;
       const uint32_t last = n > 0 ? tok8[start + n - 1] : 0u;
       if (last == 0) {  // empty stream or no end marker in its last byte
@@ -1841,7 +1830,7 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
           const uint32_t llc = cl & 63u, mlc = cm & 63u, ofc = cof & 63u;
           if (llc > 35 || mlc > 52 || ofc > 31) {
             err = kZCorrupt;
-          } else if (ofc > 27) {  // (offsets >= 2^28: the serial path)
+          } else if (ofc > 28) {
             err = kZSlow;
           } else {
             const uint32_t mlx = codes.ml[mlc], llx = codes.ll[llc];
@@ -1857,22 +1846,11 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
               sof = zs2_base(cof, no, ofg) + r.read((int)no);
               r.reload(rings[wv][ls]);
             }
-            // repeat offsets (RFC 8878 3.1.2.5), in terms of the job's starting ones
-            // where they are still unknown: "rep0 - 1" of a symbolic offset adds to its c
-            const uint32_t idx = ofv > 3 ? 0u : ofv + (ll == 0 ? 1u : 0u);
-            const uint32_t dec = (rp0 & kZSym) ? rp0 + 1u : rp0 - 1u;
-            const uint32_t off = idx == 0 ? ofv - 3 : idx == 1 ? rp0 : idx == 2 ? rp1 : idx == 3 ? rp2 : dec;
-            if (idx != 1) {
-              const uint32_t n2 = idx == 2 ? rp2 : rp1;
-              rp1 = rp0;
-              rp0 = off;
-              rp2 = n2;
-            }
-            if (r.overrun() || off == 0) {  // (0: "rep0 - 1" of 1, the serial path's case)
+            if (r.overrun()) {
               err = kZCorrupt;
             } else {
               uint64_t &Ek = k == 0 ? E0 : k == 1 ? E1 : k == 2 ? E2 : k == 3 ? E3 : k == 4 ? E4 : k == 5 ? E5 : k == 6 ? E6 : E7;
-              Ek = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)off << 35);
+              Ek = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
               i++;
               if (i == nseq && !r.exact()) err = kZCorrupt;
             }
@@ -1893,12 +1871,7 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
       if (c > 0) r.nf += c;
       pi0 = i0;
       pne = ne;
-      if (hp && !active && (err || (i == nseq && ne > 0))) {  // the job ended in this group
-        hp->err = err;
-        hp->rep0 = rp0;
-        hp->rep1 = rp1;
-        hp->rep2 = rp2;
-      }
+      if (hp && !active && (err || (i == nseq && ne > 0))) hp->err = err;  // the job ended in this group
     } while (!__ballot((slot && !active && !exhausted) || (active && r.nf - r.cons < 24)));
     if (pne > 0) raw[pi0 + 0] = E0;
     if (pne > 1) raw[pi0 + 1] = E1;
@@ -1911,15 +1884,34 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
   }
 }
 
-// ---------------------------------------------------------------- k_zstd_fix
-// an offset of k_zstd_seq2's: its value, or a repeat offset as the job started
-__device__ __forceinline__ uint32_t z_resolve(uint32_t e, uint32_t r0, uint32_t r1, uint32_t r2) {
-  const uint32_t sl = (e >> 24) & 3u, from = sl == 0 ? r0 : (sl == 1 ? r1 : r2);
-  return (e & kZSym) ? from - (e & 0xFFFFFFu) : e;
+// One step of the repeat-offset history scan (k_zstd_fix): compose this
+// lane's op (src, c) after the op of the DPP source lane (g o f); lanes the
+// DPP pattern gives no source keep the identity op (slot k <- slot k, + 0).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void z_hist_step(uint32_t &src, uint32_t &c0, uint32_t &c1, uint32_t &c2) {
+  constexpr int kIdSrc = 0 | (1 << 2) | (2 << 4);
+  const uint32_t fs = (uint32_t)__builtin_amdgcn_update_dpp(kIdSrc, (int)src, kCtrl, kRowMask, 0xf, false);
+  const uint32_t f0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c0, kCtrl, kRowMask, 0xf, false);
+  const uint32_t f1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1, kCtrl, kRowMask, 0xf, false);
+  const uint32_t f2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c2, kCtrl, kRowMask, 0xf, false);
+  uint32_t ns = 0, nc[3];
+  const uint32_t cc[3] = {c0, c1, c2};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint32_t gs = (src >> (2 * k)) & 3u;
+    const uint32_t fsel = gs == 0 ? f0 : (gs == 1 ? f1 : f2);
+    ns |= (gs == 3 ? 3u : (fs >> (2 * gs)) & 3u) << (2 * k);
+    nc[k] = gs == 3 ? cc[k] : fsel + cc[k];
+  }
+  src = ns;
+  c0 = nc[0];
+  c1 = nc[1];
+  c2 = nc[2];
 }
+
+// ---------------------------------------------------------------- k_zstd_fix
 // In file order, one wave per recordio block: every job's raw sequences 64 at
-// a time -- repeat offsets that k_zstd_seq2 left in terms of the job's starting
-// history resolved (round 4; a wave scan of history ops before), the serial decoder's
+// a time -- repeat offsets resolved by a wave scan of history ops, the serial decoder's
 // per-sequence checks made lane-parallel from prefix sums (literals left,
 // offset within the frame's output), execution entries written -- then the
 // frame checks (content size), then the frame walk's own error if it stopped
@@ -1963,7 +1955,6 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
     for (uint32_t j = 0; j < njobs && !zerr; j++) {
       const ZJob *hp = reinterpret_cast<const ZJob *>(tok8 + jo);
       const uint32_t flags = uni(hp->flags), regen = uni(hp->regen), nseq = uni(hp->nseq), jerr = uni(hp->err);
-      const uint32_t fr0 = uni(hp->rep0), fr1 = uni(hp->rep1), fr2 = uni(hp->rep2);
       const uint64_t raw_off = uni64(hp->raw_off), next = uni64(hp->next);
       const int64_t fcs = (int64_t)uni64((uint64_t)hp->fcs);
       const uint32_t cks = uni(hp->checksum);
@@ -1992,7 +1983,50 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
           const uint64_t rv = rv_nx;
           if (g0 + 64 < nseq) rv_nx = (uint32_t)l < nseq - g0 - 64 ? raw[g0 + 64 + l] : 0ull;
           const uint32_t ll = (uint32_t)rv & 0x1FFFFu, ml = (uint32_t)(rv >> 17) & 0x3FFFFu;
-          const uint32_t off = z_resolve((uint32_t)(rv >> 35), rep0, rep1, rep2);
+          const uint32_t ofv = (uint32_t)(rv >> 35);
+          // Repeat offsets: a sequence maps the offset history (rep0, rep1, rep2)
+          // by an op "slot k <- slot src_k + c_k, or the constant c_k when
+          // src_k = 3" (RFC 8878 3.1.2.5); an inclusive scan of the composed ops
+          // gives each sequence the history after it, whose slot 0 is its offset.
+          uint32_t src, c0, c1 = 0, c2 = 0;
+          {
+            const uint32_t idx = ofv > 3 ? 0u : ofv + (ll == 0 ? 1u : 0u);
+            if (!v || idx == 1) {  // offset = rep0, history unchanged
+              src = 0u | (1u << 2) | (2u << 4);
+              c0 = 0;
+            } else if (idx == 0) {  // a new offset
+              src = 3u | (0u << 2) | (1u << 4);
+              c0 = ofv - 3;
+            } else if (idx == 2) {
+              src = 1u | (0u << 2) | (2u << 4);
+              c0 = 0;
+            } else if (idx == 3) {
+              src = 2u | (0u << 2) | (1u << 4);
+              c0 = 0;
+            } else {  // rep0 - 1 (0 is the error below)
+              src = 0u | (0u << 2) | (1u << 4);
+              c0 = ~0u;
+            }
+          }
+          // inclusive scan by DPP (row shifts, then the row broadcasts, as
+          // wave_incl_sum_dpp); lanes without a source lane compose the identity
+          z_hist_step<0x111, 0xf>(src, c0, c1, c2);  // row_shr:1
+          z_hist_step<0x112, 0xf>(src, c0, c1, c2);  // row_shr:2
+          z_hist_step<0x114, 0xf>(src, c0, c1, c2);  // row_shr:4
+          z_hist_step<0x118, 0xf>(src, c0, c1, c2);  // row_shr:8
+          z_hist_step<0x142, 0xa>(src, c0, c1, c2);  // row_bcast:15
+          z_hist_step<0x143, 0xc>(src, c0, c1, c2);  // row_bcast:31
+          auto apply = [&](uint32_t sk, uint32_t ck) {
+            return sk == 3 ? ck : (sk == 0 ? rep0 : (sk == 1 ? rep1 : rep2)) + ck;
+          };
+          const uint32_t off = apply(src & 3u, c0);
+          {  // the history after the group (lanes past cnt hold the identity)
+            const uint32_t ls = zrl(src, 63), l0 = zrl(c0, 63), l1 = zrl(c1, 63), l2 = zrl(c2, 63);
+            const uint32_t n0 = apply(ls & 3u, l0), n1 = apply((ls >> 2) & 3u, l1), n2 = apply((ls >> 4) & 3u, l2);
+            rep0 = n0;
+            rep1 = n1;
+            rep2 = n2;
+          }
           // z_exec's checks per sequence: literals left, offset within the frame's output
           const uint32_t lin = wave_incl_sum_dpp(v ? ll : 0u), tin = wave_incl_sum_dpp(v ? ll + ml : 0u);
           const int64_t my_lp = lp + (int64_t)(lin - ll);
@@ -2014,12 +2048,6 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
           olen += zrl(tin, cnt - 1);
         }
         if (zerr) break;
-        // the history after the job, from the one it started with
-        const uint32_t n0 = z_resolve(fr0, rep0, rep1, rep2), n1 = z_resolve(fr1, rep0, rep1, rep2),
-                       n2 = z_resolve(fr2, rep0, rep1, rep2);
-        rep0 = n0;
-        rep1 = n1;
-        rep2 = n2;
       }
       if ((int64_t)regen > lp) pieces((uint64_t)((int64_t)regen - lp), 0, 0);  // the block's last literals
       olen += (int64_t)regen - lp;
@@ -2127,14 +2155,6 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
     // (from dword-aligned pf_nx; ~0: not prefetched), so a group usually
     // starts without waiting for memory
     uint64_t e_nx = (uint32_t)l < ntok ? ents[-1 - (int64_t)l] : 0ull;
-    // entries two groups ahead, so that the next group's far match sources
-    // (<= 8 bytes, already flushed) are loaded while this group runs: fl_prev is
-    // `flushed` when the next group's entries were requested, so once they
-    // have arrived every flush store before that request has completed (vmcnt
-    // counts in order) and those bytes are visible without a drain
-    uint64_t e_nx2 = 64u + (uint32_t)l < ntok ? ents[-1 - (int64_t)(64 + l)] : 0ull;
-    uint32_t fl_prev = 0, cq0 = 0, cq1 = 0, cq2 = 0;
-    bool cqok = false;  // this group's lane entry has its source in cq0..cq2
     uint32_t pf_nx = ~0u, lit_nx = 0;
     if (lit0 + 256 <= ent_end) {
       pf_nx = 0;
@@ -2150,38 +2170,14 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
         litbuf[l] = lit_nx;
         lit_at = pf_nx;
       }
-      e_nx = e_nx2;
-      if (g0 + 128 < ntok)
-        e_nx2 = (uint32_t)l < ntok - g0 - 128 ? ents[-1 - (int64_t)(g0 + 128 + l)] : 0ull;
+      if (g0 + 64 < ntok)
+        e_nx = (uint32_t)l < ntok - g0 - 64 ? ents[-1 - (int64_t)(g0 + 64 + l)] : 0ull;
       const uint32_t ll0 = (uint32_t)e & 0xffffu, ml0 = (uint32_t)(e >> 16) & 0xffffu, off = (uint32_t)(e >> 32);
       const bool mark = ll0 == kZMark;
       const uint32_t len = mark ? 0u : ll0 + ml0, lits = mark ? 0u : ll0;
       const uint32_t incl = wave_incl_sum_dpp(len), lincl = wave_incl_sum_dpp(lits);
       const uint32_t excl = incl - len, lexcl = lincl - lits;
       const unsigned long long marks = __ballot(mark);
-      uint32_t nq0 = 0, nq1 = 0, nq2 = 0;
-      bool nqok = false;
-      {  // the next group's short far sources, loaded now (see fl_prev)
-        const uint32_t F = fl_prev;
-        fl_prev = flushed;
-        if (g0 + 64 < ntok) {
-          const uint32_t l1 = (uint32_t)e_nx & 0xffffu, m1 = (uint32_t)(e_nx >> 16) & 0xffffu;
-          const uint32_t o1 = (uint32_t)(e_nx >> 32);
-          const bool k1 = l1 == kZMark;
-          const uint32_t len1 = k1 ? 0u : l1 + m1;
-          const uint32_t inc1 = wave_incl_sum_dpp(len1);
-          const uint32_t base1 = olen + zrl(incl, n - 1);  // the next group's first output byte
-          const uint32_t dst1 = base1 + inc1 - len1 + l1, src1 = dst1 - o1;
-          nqok = (uint32_t)l < ntok - g0 - 64 && !k1 && m1 != 0 && m1 <= 8 && o1 <= dst1 && (o1 >= 8 || m1 <= o1) &&
-                 src1 + m1 <= F && src1 + m1 - 1 + kZHist < base1;
-          if (nqok) {
-            const uint32_t *w = reinterpret_cast<const uint32_t *>(out + (src1 & ~3u));
-            nq0 = w[0];
-            nq1 = w[1];
-            nq2 = w[2];
-          }
-        }
-      }
       {  // the next group's literals start where this group's end
         const uint32_t na = (litpos + zrl(lincl, n - 1)) & ~3u;
         pf_nx = ~0u;
@@ -2237,7 +2233,7 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
             {  // bytes read from the decode region (pos + kZHist < base) visible first: drain
                // the wave's stores only when one of them lies at or above the last drain's mark
               const uint32_t hi = min(src + (myml < off ? myml : off), base - kZHist);
-              if (__ballot(m && !cqok && src + kZHist < base && hi > synced)) {
+              if (__ballot(m && src + kZHist < base && hi > synced)) {
                 zmem_sync();
                 synced = flushed;
               }
@@ -2258,9 +2254,7 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
                 for (uint32_t k = 0; k < myml; k += 8) {
                   const uint32_t *w = all_ring ? reinterpret_cast<const uint32_t *>(ring + ((ss + k) & ~3u))
                                                : reinterpret_cast<const uint32_t *>(out + ((src + k) & ~3u));
-                  const bool pre = cqok;  // (a prefetched source is far and <= 8 bytes: k = 0 only)
-                  const uint32_t w0 = pre ? cq0 : w[0], w1 = pre ? cq1 : w[1], w2 = pre ? cq2 : w[2];
-                  const uint32_t sh = (src + k) & 3u;  // ss = src (mod 4)
+                  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = (src + k) & 3u;  // ss = src (mod 4)
                   const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
                   uint8_t *dp = ring + ds + k;
 #pragma unroll
@@ -2327,10 +2321,6 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
         }
         s = e1;
       }
-      cq0 = nq0;
-      cq1 = nq1;
-      cq2 = nq2;
-      cqok = nqok;
     }
     wave_lds_sync();
     zr_flush(ring, out, flushed, olen);

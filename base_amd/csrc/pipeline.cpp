@@ -130,6 +130,10 @@ struct rio_ctx {
   bool last_cmp = false;  // the last host result's records are the compacted blocks (d.cmp)
   uint64_t max_span = 0, max_chunks = 0, max_blocks = 0;
   uint64_t side_cap = 0, item_cap = 0, dec_cap = 0;
+  // growth for one call (a chain's later stages, rio_decode_block's long block):
+  // the sizes before it, restored at the next call (settle)
+  bool grown_tmp = false;
+  uint64_t base_span = 0, base_side = 0, base_item = 0;
   uint32_t dec_factor = 8;  // first-attempt decode-region bound: compressed bytes x this
   int fl_rounds = kFlRounds;  // flate Huffman/copy rounds per span (doubled if a block needs more)
   DevBufs d{};
@@ -292,7 +296,7 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   return 0;
 }
 
-int rio_ctx_reserve_span(rio_ctx *c, uint64_t bytes) {
+static int reserve(rio_ctx *c, uint64_t bytes) {
   bytes = (bytes + kChunk - 1) / kChunk * kChunk;
   if (bytes <= c->max_span) return 0;
   HIP_OK(hipSetDevice(c->device));
@@ -306,6 +310,74 @@ int rio_ctx_reserve_span(rio_ctx *c, uint64_t bytes) {
     hipFree(c->d_span);
     c->d_span = nullptr;
   }
+  return alloc_bufs(c);
+}
+
+// a lasting reservation (the scanner's header / long block): also the size a
+// temporary growth returns to
+int rio_ctx_reserve_span(rio_ctx *c, uint64_t bytes) {
+  if (c->grown_tmp) {
+    const uint64_t r = (bytes + kChunk - 1) / kChunk * kChunk;
+    if (r > c->base_span) c->base_span = r;
+    if (c->base_side < r / 8 + (1 << 20)) c->base_side = r / 8 + (1 << 20);
+    if (c->base_item < r / 64 + 1024) c->base_item = r / 64 + 1024;
+  }
+  return reserve(c, bytes);
+}
+
+// growth for this call only: a chain stage's decoded bytes can be several times
+// the file span, and one chain file should not leave a long-lived context that
+// large (the results stay valid until the next call, which shrinks it back)
+static int reserve_tmp(rio_ctx *c, uint64_t bytes) {
+  if ((bytes + kChunk - 1) / kChunk * kChunk <= c->max_span) return 0;
+  if (!c->grown_tmp) {
+    c->grown_tmp = true;
+    c->base_span = c->max_span;
+    c->base_side = c->side_cap;
+    c->base_item = c->item_cap;
+  }
+  return reserve(c, bytes);
+}
+
+template <class T>
+static void dfree(T **p) {
+  if (*p) hipFree(*p);
+  *p = nullptr;
+}
+
+// back to the sizes before a temporary growth (every buffer sized from the
+// grown span is released; the demand-sized ones regrow on use)
+static int settle(rio_ctx *c) {
+  if (!c->grown_tmp) return 0;
+  c->grown_tmp = false;
+  HIP_OK(hipSetDevice(c->device));
+  HIP_OK(hipStreamSynchronize(c->st));
+  c->max_span = c->base_span;
+  c->max_chunks = c->max_span / kChunk;
+  c->max_blocks = c->max_chunks;
+  c->side_cap = c->base_side;
+  c->item_cap = c->base_item;
+  DevBufs &d = c->d;
+  dfree(&c->d_span);
+  dfree(&d.dec);
+  c->dec_cap = d.dec_cap = 0;
+  dfree(&d.tok);
+  d.tok_cap = 0;
+  dfree(&d.zjob);
+  d.zjob_cap = 0;
+  dfree(&d.seg_scr);
+  d.seg_cap = 0;
+  c->seg_want = 0;
+  dfree(&d.fl_ck);
+  dfree(&d.fl_seg);
+  d.fl_ck_n = 0;
+  for (int k = 0; k < 2; k++) {
+    dfree(&c->d_chain[k]);
+    c->d_chain_cap[k] = 0;
+  }
+  if (c->h_stage) hipHostFree(c->h_stage);
+  c->h_stage = nullptr;
+  c->h_stage_cap = 0;
   return alloc_bufs(c);
 }
 
@@ -833,7 +905,8 @@ static int run_chain(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_spa
     launch_reframe(c->d.dec, c->d.blk_dec_off, c->d.blk_out_len, c->d_chain_meta, nv, magic, buf, c->st);
     HIP_OK(hipStreamSynchronize(c->st));
     // the stage's chunks may outnumber the file's (decoded bytes): the span grows
-    if (rio_ctx_reserve_span(c, sbytes)) return -1;
+    // for this call
+    if (reserve_tmp(c, sbytes)) return -1;
     if (run_span(c, buf, report_span, sbytes, file_off, 1, UINT64_MAX, at(k), mode, res, out,
                  kStageNoCrc | (k > 0 ? kStageNoItems : 0)))
       return -1;
@@ -870,6 +943,7 @@ extern "C" int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbyt
                                int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_batch *out) {
   if (!ctx || !out) return -1;
   memset(out, 0, sizeof(*out));
+  if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;  // (consecutive chain calls keep the growth)
   return run_span(ctx, (const uint8_t *)dev_span, (const uint8_t *)dev_span, nbytes, file_off, is_file_end,
                   limit_off, codec, kModeBody, nullptr, out);
 }
@@ -884,6 +958,7 @@ static int stage_span(rio_ctx *c, const uint8_t *span, uint64_t nbytes) {
 extern "C" int rio_ctx_stats(rio_ctx *ctx, rio_stats *out) {
   if (!ctx || !out) return -1;
   *out = ctx->stats;
+  out->span_cap = ctx->max_span;
   return 0;
 }
 
@@ -891,6 +966,7 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
                        uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res, rio_batch *out) {
   if (!ctx || !out) return -1;
   memset(out, 0, sizeof(*out));
+  if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;
   if (nbytes > ctx->max_span + kChunk) {
     rio_set_error(&out->err, RIO_ERR_CAPACITY, file_off, "span of %" PRIu64 " bytes exceeds ctx capacity", nbytes);
     out->stop = RIO_STOP_ERROR;
@@ -925,6 +1001,7 @@ extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_
                                      int32_t codec) {
   if (!ctx) return -1;
   HIP_OK(hipSetDevice(ctx->device));
+  if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;
   if (codec & RIO_CODEC_CHAIN_FLAG) {
     // a chain's stages run here, one after the other (each needs the previous
     // one's block sizes on the host): the call returns when they are done and
@@ -1096,7 +1173,7 @@ static int decode_raw(rio_ctx *c, const uint8_t *const *payloads, const uint32_t
   for (int i = 0; i < n; i++) total += lens[i];
   const uint64_t nch = total ? (total + kMaxPayload - 1) / kMaxPayload : 1;
   const uint64_t nbytes = nch * kChunk;
-  if (rio_ctx_reserve_span(c, nbytes)) return -1;  // a block longer than the span: the span grows to it
+  if (reserve_tmp(c, nbytes)) return -1;  // a block longer than the span: the span grows to it (this call)
   if (c->h_stage_cap < nbytes) {
     if (c->h_stage) hipHostFree(c->h_stage);
     c->h_stage = nullptr;
@@ -1165,6 +1242,7 @@ static int decode_raw(rio_ctx *c, const uint8_t *const *payloads, const uint32_t
 extern "C" int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, const uint32_t *lens, int n,
                                 int32_t codec, uint8_t *scratch, uint64_t cap, uint64_t *out_len, rio_error *err) {
   if (!ctx || n < 0 || (n > 0 && (!payloads || !lens)) || !out_len) return -1;
+  if (settle(ctx)) return -1;
   rio_error scratch_err;
   if (!err) err = &scratch_err;
   memset(err, 0, sizeof(*err));
@@ -1331,6 +1409,7 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
   if (!c || !out) return -1;
   memset(out, 0, sizeof(*out));
   HIP_OK(hipSetDevice(c->device));
+  if (settle(c)) return -1;
   rio_results &r = res ? *res : c->res;
   std::vector<V1Rec> &recs = c->v1_recs;
   std::vector<V1Job> &jobs = c->v1_jobs;

@@ -289,9 +289,10 @@ struct rio_scanner {
     *buf = nullptr;
     *cap = 0;
   }
-  // read [at, at+n) into *buf and decode it on the GPU into *rs
+  // read [at, at+n) into *buf and decode it on the GPU into *rs (ahead: the
+  // read-ahead of the bytes after it starts before the GPU decode)
   int decode_into(uint8_t **buf, uint64_t *cap, rio_results *rs, uint64_t at, uint64_t n, int32_t cdc, int32_t mode,
-                  uint64_t lim, rio_batch *out) {
+                  uint64_t lim, rio_batch *out, bool ahead = false) {
     if (ensure_buf(buf, cap, n ? n : 1)) {
       memset(out, 0, sizeof(*out));
       rio_set_error(&out->err, RIO_ERR_HIP, at, "pinned allocation failed");
@@ -307,6 +308,7 @@ struct rio_scanner {
       return 0;
     }
     const int is_end = (at + got >= file_size);
+    if (ahead) read_ahead(at + got);
     if (v1 && mode == 0) return rio_scan_v1_span_mode(ctx, *buf, got, at, is_end, rs, out);
     // a header / trailer block longer than the ctx's span: the span grows to it
     if (mode != 0 && rio_ctx_reserve_span(ctx, got) != 0) return -1;
@@ -316,6 +318,16 @@ struct rio_scanner {
     ra_drop();
     span_data = nullptr;
     return decode_into(&span, &span_cap, res, at, n, cdc, mode, lim, out);
+  }
+  // The file bytes from `end` (the span being decoded ends there), read on the
+  // thread while the GPU decodes the span and the caller consumes its batch.
+  // Only when the next span certainly starts there or earlier: a shard's
+  // spans end once one reaches its limit.
+  void read_ahead(uint64_t end) {
+    if (end < file_size && end < limit) {
+      const uint64_t left = file_size - end, maxspan = rio_ctx_max_span(ctx);
+      ra_start(end, left < maxspan ? left : maxspan);
+    }
   }
   // the body's next span [at, at + n): from the read-ahead when it holds it
   int decode_body(uint64_t at, uint64_t n, rio_batch *out) {
@@ -330,6 +342,7 @@ struct rio_scanner {
       std::swap(span, ra_buf);  // the batch's views will point into this buffer
       std::swap(span_cap, ra_cap);
       const int is_end = (at + n >= file_size);
+      read_ahead(at + n);  // (into the previous span's buffer: its batch is consumed)
       const int rc = v1 ? rio_scan_v1_span_mode(ctx, base, n, at, is_end, res, out)
                         : rio_scan_span_mode(ctx, base, n, at, is_end, limit, codec, 0, res, out);
       span_data = base;
@@ -338,7 +351,7 @@ struct rio_scanner {
       return rc;
     }
     ra_valid = false;
-    const int rc = decode_into(&span, &span_cap, res, at, n, codec, 0, limit, out);
+    const int rc = decode_into(&span, &span_cap, res, at, n, codec, 0, limit, out, true);
     span_data = span;
     span_at = at;
     span_n = n;
@@ -567,9 +580,10 @@ bool next_batch(rio_scanner *s) {
         continue;  // again, at the grown span
       }
       s->off += b.consumed;
-      // the bytes after this span, read while the batch is consumed
+      // the bytes after this span, read while the batch is consumed (usually
+      // started already, before the span's decode: decode_body)
       const uint64_t end = s->span_at + s->span_n;
-      if (end < s->file_size && s->off < s->limit) {
+      if (!(s->ra_valid && s->ra_at == end) && end < s->file_size && s->off < s->limit) {
         const uint64_t left = s->file_size - end;
         s->ra_start(end, left < maxspan ? left : maxspan);
       }

@@ -94,7 +94,7 @@ RIO_BLOCK_BODY, RIO_BLOCK_HEADER, RIO_BLOCK_TRAILER = 0, 1, 2
 
 class RioStats(ctypes.Structure):
     _fields_ = [("spans", ctypes.c_uint64), ("h2d_bytes", ctypes.c_uint64), ("d2h_bytes", ctypes.c_uint64),
-                ("device_ms", ctypes.c_double)]
+                ("device_ms", ctypes.c_double), ("span_cap", ctypes.c_uint64)]
 
 
 class RioMemory(ctypes.Structure):
@@ -337,11 +337,12 @@ class Context:
         return out
 
     def stats(self) -> dict:
-        """rio_ctx_stats: host spans scanned, bytes copied in and out, device ms."""
+        """rio_ctx_stats: host spans scanned, bytes copied in and out, device ms,
+        and the span the device buffers are sized for now."""
         st = RioStats()
         self.L.rio_ctx_stats(self.h, ctypes.byref(st))
         return {"spans": int(st.spans), "h2d_bytes": int(st.h2d_bytes), "d2h_bytes": int(st.d2h_bytes),
-                "device_ms": float(st.device_ms)}
+                "device_ms": float(st.device_ms), "span_cap": int(st.span_cap)}
 
     def flate_split_blocks(self) -> int:
         """Flate blocks of the last completed run copied as segments (split copy pass)."""

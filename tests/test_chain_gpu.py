@@ -101,6 +101,41 @@ def test_chain_batch_layer(oracle, chain_files, item_end):
         ctx.close()
 
 
+def test_chain_growth_is_temporary(chain_files):
+    """A chain's later stages decode spans larger than the file's (the decoded
+    bytes, reframed): the context grows for that call only. Consecutive chain
+    calls keep the growth; the next plain call (here a none-codec span, checked)
+    returns the device buffers to the configured span."""
+    import torch
+    from base_amd.recordio import gpu
+    from base_amd.recordio.writer import WriterOpts, write_file
+    recs = chain_files[0]
+    trs = ("flate 0", "zstd")  # stored DEFLATE under zstd: stage 2's span is ~the records' size
+    data = write_file(recs, WriterOpts(Transformers=list(trs), MaxItems=41))
+    body = data[_body(data):]
+    cap0 = (len(body) + 32767) // 32768 * 32768
+    assert sum(map(len, recs)) > 2 * cap0
+    plain_recs = [bytes([k % 251]) * (k * 7 % 900) for k in range(500)]
+    plain = write_file(plain_recs, WriterOpts(MaxItems=50))
+    ctx = gpu.Context(0, max_span_bytes=cap0)
+    try:
+        assert ctx.stats()["span_cap"] == cap0
+        for _ in range(2):
+            b = ctx.scan_span(body, file_off=_body(data), is_file_end=True, codec=_codec(trs))
+            assert b.err.code == 0 and gpu.batch_items(b) == recs, b.err.msg
+            assert ctx.stats()["span_cap"] > cap0
+        pb = plain[_body(plain):]
+        dev = torch.frombuffer(bytearray(pb), dtype=torch.uint8).to("cuda:0")
+        bd = ctx.scan_device(dev.data_ptr(), len(pb), file_off=_body(plain), is_file_end=True,
+                             codec=gpu.RIO_CODEC_NONE)
+        assert bd.err.code == 0 and gpu.device_batch_items(bd, pb) == plain_recs
+        assert ctx.stats()["span_cap"] == cap0
+        b = ctx.scan_span(body, file_off=_body(data), is_file_end=True, codec=_codec(trs))
+        assert b.err.code == 0 and gpu.batch_items(b) == recs  # grows again
+    finally:
+        ctx.close()
+
+
 def test_chain_decode_block(gpu_ctx, oracle, chain_files):
     """rio_decode_block with a chain codec: the combined untransform of one block."""
     from base_amd.recordio import format as F
