@@ -70,6 +70,11 @@ while [ $# -gt 0 ]; do
         python3 -u tools/bench_flate.py --steps 1 --warmup 0 --replicas 8
       step pmc1k_sq2 150 rocprofv3 --pmc $PMC_SQ2 --output-format csv -d gpurun_out/pmc1k_sq2 -o run -- \
         python3 -u tools/bench_flate.py --steps 1 --warmup 0 --replicas 8 ;;
+    pmcc2)  # FETCH_SIZE / WRITE_SIZE passes over the C2 bench (bench.py's roofline traffic)
+      step pmc_c2_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_c2_fetch -o run -- \
+        python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-flate --no-flate16k --no-zstd --no-c5 --no-e2e
+      step pmc_c2_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_c2_write -o run -- \
+        python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-flate --no-flate16k --no-zstd --no-c5 --no-e2e ;;
     pmcc4)
       c4data
       step pmcc4_fetch 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcc4_fetch -o run -- \
