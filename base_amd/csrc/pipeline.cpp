@@ -134,6 +134,14 @@ struct rio_ctx {
   // the sizes before it, restored at the next call (settle)
   bool grown_tmp = false;
   uint64_t base_span = 0, base_side = 0, base_item = 0;
+  rio_config cfg{};            // as opened (the sibling opens with it)
+  rio_ctx *sibling = nullptr;  // a scanner's second context (its span ahead), opened on first use
+  // rio_scan_span_begin: collect enqueues the result copies without waiting;
+  // rio_scan_span_end waits for them and finishes the batch
+  bool defer_collect = false, pend = false;
+  uint64_t pend_nb = 0, pend_file_off = 0, pend_d2h = 0;
+  unsigned long long *pend_foff = nullptr;
+  hipEvent_t pend_t0 = nullptr, pend_t1 = nullptr;
   uint32_t dec_factor = 8;  // first-attempt decode-region bound: compressed bytes x this
   int fl_rounds = kFlRounds;  // flate Huffman/copy rounds per span (doubled if a block needs more)
   DevBufs d{};
@@ -257,6 +265,7 @@ static void free_all(rio_ctx *c) {
 }
 
 static int ctx_init(rio_ctx *c, const rio_config *cfg) {
+  if (cfg) c->cfg = *cfg;
   c->device = cfg ? cfg->device : 0;
   HIP_OK(hipSetDevice(c->device));
   hipDeviceProp_t prop;
@@ -451,6 +460,8 @@ void rio_ctx_give_results(rio_ctx *c, rio_results *r) {
 
 void rio_close(rio_ctx *ctx) {
   if (!ctx) return;
+  rio_scan_span_end(ctx);
+  rio_close(ctx->sibling);
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->st);
   for (auto &b : ctx->buf_pool) hipHostFree(b.first);
@@ -714,9 +725,18 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
   }
   HIP_OK(hipMemcpyAsync(first, c->d.blk_item_base, (nb + 1) * 8, hipMemcpyDeviceToHost, c->st));
   if (nb) HIP_OK(hipMemcpyAsync(foff, c->d.blk_c0, nb * 8, hipMemcpyDeviceToHost, c->st));
-  HIP_OK(hipStreamSynchronize(c->st));
-  c->stats.d2h_bytes += k.rec_bytes + 16 * k.n_items + 8 * (2 * nb + 1);
-  for (uint64_t b = 0; b < nb; b++) foff[b] = file_off + foff[b] * kChunk;
+  const uint64_t d2h = k.rec_bytes + 16 * k.n_items + 8 * (2 * nb + 1);
+  if (c->defer_collect) {  // rio_scan_span_end waits and converts the block offsets
+    c->pend = true;
+    c->pend_nb = nb;
+    c->pend_foff = foff;
+    c->pend_file_off = file_off;
+    c->pend_d2h = d2h;
+  } else {
+    HIP_OK(hipStreamSynchronize(c->st));
+    c->stats.d2h_bytes += d2h;
+    for (uint64_t b = 0; b < nb; b++) foff[b] = file_off + foff[b] * kChunk;
+  }
   out->records = r.records;
   out->item_off = reinterpret_cast<const uint64_t *>(h_off);
   out->item_len = reinterpret_cast<const uint64_t *>(h_len);
@@ -943,6 +963,7 @@ extern "C" int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbyt
                                int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_batch *out) {
   if (!ctx || !out) return -1;
   memset(out, 0, sizeof(*out));
+  if (rio_scan_span_end(ctx)) return -1;
   if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;  // (consecutive chain calls keep the growth)
   return run_span(ctx, (const uint8_t *)dev_span, (const uint8_t *)dev_span, nbytes, file_off, is_file_end,
                   limit_off, codec, kModeBody, nullptr, out);
@@ -959,12 +980,19 @@ extern "C" int rio_ctx_stats(rio_ctx *ctx, rio_stats *out) {
   if (!ctx || !out) return -1;
   *out = ctx->stats;
   out->span_cap = ctx->max_span;
+  if (const rio_ctx *sb = ctx->sibling) {  // (a scanner's spans ahead ran there)
+    out->spans += sb->stats.spans;
+    out->h2d_bytes += sb->stats.h2d_bytes;
+    out->d2h_bytes += sb->stats.d2h_bytes;
+    out->device_ms += sb->stats.device_ms;
+  }
   return 0;
 }
 
-int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
-                       uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res, rio_batch *out) {
+static int scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
+                     uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res, rio_batch *out, bool defer) {
   if (!ctx || !out) return -1;
+  if (rio_scan_span_end(ctx)) return -1;  // (a deferred batch of this ctx: complete before its buffers are reused)
   memset(out, 0, sizeof(*out));
   if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;
   if (nbytes > ctx->max_span + kChunk) {
@@ -978,9 +1006,22 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
   hipEventCreate(&t1);
   hipEventRecord(t0, ctx->st);
   if (stage_span(ctx, span, nbytes)) return -1;
+  // (a chain's stages read their results on the host: never deferred)
+  ctx->defer_collect = defer && !(codec & RIO_CODEC_CHAIN_FLAG);
   const int rc = run_span(ctx, ctx->d_span, span, nbytes, file_off, is_file_end, limit_off, codec, mode,
                           res ? res : &ctx->res, out);
+  ctx->defer_collect = false;
   hipEventRecord(t1, ctx->st);
+  if (ctx->pend) {
+    if (rc) {  // (no batch to finish)
+      ctx->pend = false;
+      hipEventSynchronize(t1);
+    } else {
+      ctx->pend_t0 = t0;
+      ctx->pend_t1 = t1;
+      return 0;
+    }
+  }
   hipEventSynchronize(t1);
   float ms = 0;
   hipEventElapsedTime(&ms, t0, t1);
@@ -992,6 +1033,46 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
   return rc;
 }
 
+int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
+                       uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res, rio_batch *out) {
+  return scan_span(ctx, span, nbytes, file_off, is_file_end, limit_off, codec, mode, res, out, false);
+}
+
+int rio_scan_span_begin(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
+                        uint64_t limit_off, int32_t codec, rio_results *res, rio_batch *out) {
+  return scan_span(ctx, span, nbytes, file_off, is_file_end, limit_off, codec, 0, res, out, true);
+}
+
+int rio_scan_span_end(rio_ctx *ctx) {
+  if (!ctx || !ctx->pend) return 0;
+  ctx->pend = false;
+  HIP_OK(hipSetDevice(ctx->device));
+  const hipError_t e = hipEventSynchronize(ctx->pend_t1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, ctx->pend_t0, ctx->pend_t1);
+  hipEventDestroy(ctx->pend_t0);
+  hipEventDestroy(ctx->pend_t1);
+  if (e != hipSuccess) {
+    set_last_error("HIP error %d (%s) waiting for a span's results", (int)e, hipGetErrorString(e));
+    return -1;
+  }
+  for (uint64_t b = 0; b < ctx->pend_nb; b++) ctx->pend_foff[b] = ctx->pend_file_off + ctx->pend_foff[b] * kChunk;
+  ctx->stats.d2h_bytes += ctx->pend_d2h;
+  ctx->stats.spans++;
+  ctx->stats.device_ms += ms;
+  return 0;
+}
+
+rio_ctx *rio_ctx_sibling(rio_ctx *c) {
+  if (!c) return nullptr;
+  if (!c->sibling) {
+    rio_config cf = c->cfg;
+    cf.max_span_bytes = c->max_span;
+    c->sibling = rio_open(&cf);
+  }
+  return c->sibling;
+}
+
 extern "C" int rio_scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
                              int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_batch *out) {
   return rio_scan_span_mode(ctx, span, nbytes, file_off, is_file_end, limit_off, codec, kModeBody, nullptr, out);
@@ -1001,6 +1082,7 @@ extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_
                                      int32_t codec) {
   if (!ctx) return -1;
   HIP_OK(hipSetDevice(ctx->device));
+  if (rio_scan_span_end(ctx)) return -1;
   if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;
   if (codec & RIO_CODEC_CHAIN_FLAG) {
     // a chain's stages run here, one after the other (each needs the previous
@@ -1242,6 +1324,7 @@ static int decode_raw(rio_ctx *c, const uint8_t *const *payloads, const uint32_t
 extern "C" int rio_decode_block(rio_ctx *ctx, const uint8_t *const *payloads, const uint32_t *lens, int n,
                                 int32_t codec, uint8_t *scratch, uint64_t cap, uint64_t *out_len, rio_error *err) {
   if (!ctx || n < 0 || (n > 0 && (!payloads || !lens)) || !out_len) return -1;
+  if (rio_scan_span_end(ctx)) return -1;
   if (settle(ctx)) return -1;
   rio_error scratch_err;
   if (!err) err = &scratch_err;
@@ -1409,6 +1492,7 @@ int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint
   if (!c || !out) return -1;
   memset(out, 0, sizeof(*out));
   HIP_OK(hipSetDevice(c->device));
+  if (rio_scan_span_end(c)) return -1;
   if (settle(c)) return -1;
   rio_results &r = res ? *res : c->res;
   std::vector<V1Rec> &recs = c->v1_recs;

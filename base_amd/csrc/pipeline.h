@@ -16,6 +16,16 @@ void rio_results_free(rio_results *r);
 int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
                        int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res,
                        rio_batch *out);
+// the same with the result copies left in flight: *out's counts, stop and error
+// are final, its host arrays arrive by rio_scan_span_end (any later call on the
+// ctx waits for them first; total_ms is not set). Body mode; a chain codec runs
+// as rio_scan_span_mode.
+int rio_scan_span_begin(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
+                        int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_results *res, rio_batch *out);
+int rio_scan_span_end(rio_ctx *ctx);  // 0 (also when nothing is in flight) or -1 (rio_last_error)
+// a second context opened with this one's configuration on first use (a
+// scanner's span ahead) and closed with it
+rio_ctx *rio_ctx_sibling(rio_ctx *c);
 // v1 records of one span (rio_scan_v1_span) into *res (the ctx's own when null)
 int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
                           rio_results *res, rio_batch *out);

@@ -205,6 +205,80 @@ struct rio_scanner {
     ra_running = true;
     ra_th = std::thread([this] { ra_got = read_full(ra_buf + kRaRoom, ra_len, ra_at, &ra_st); });
   }
+  // Span ahead: the body's next span is decoded on a second context (the
+  // ctx's sibling) as soon as the current batch's extent is known -- before
+  // that batch's result copies have come back, so the next span's H2D copy and
+  // decode overlap them (PCIe is full duplex) -- and its own result copies
+  // come back while the caller consumes the current batch. Slots (context,
+  // results) alternate: the current batch's is `slot`, the span ahead's slot ^ 1.
+  // Three staging buffers rotate: the current batch's span (its views point
+  // there), the span ahead, and the read-ahead.
+  rio_ctx *cx[2] = {nullptr, nullptr};
+  rio_results *rs[2] = {nullptr, nullptr};
+  int slot = 0;
+  bool ahead = false;
+  int ahead_rc = 0;
+  rio_batch ahead_b{};
+  uint64_t ahead_at = 0, ahead_n = 0;
+  const uint8_t *ahead_base = nullptr;
+  uint8_t *ahead_buf = nullptr;
+  uint64_t ahead_cap = 0;
+  void ahead_drop() {
+    if (ahead) rio_scan_span_end(cx[slot ^ 1]);
+    ahead = false;
+  }
+  // the current batch's result copies (rio_scan_span_begin) in place
+  int finish_cur() { return rio_scan_span_end(cx[slot]); }
+  // a body span in host memory, decoded into the current slot (results deferred)
+  int scan_body(const uint8_t *base, uint64_t n, uint64_t at, rio_batch *out) {
+    const int is_end = (at + n >= file_size);
+    if (v1) return rio_scan_v1_span_mode(cx[slot], base, n, at, is_end, rs[slot], out);
+    return rio_scan_span_begin(cx[slot], base, n, at, is_end, limit, codec, rs[slot], out);
+  }
+  // the span begun ahead becomes the current batch
+  int take_ahead(rio_batch *out) {
+    ahead = false;
+    std::swap(span, ahead_buf);  // (the previous batch's buffer is free now)
+    std::swap(span_cap, ahead_cap);
+    span_data = ahead_base;
+    span_at = ahead_at;
+    span_n = ahead_n;
+    slot ^= 1;
+    *out = ahead_b;
+    return ahead_rc;
+  }
+  // begin the body's next span [off, off + n) on the other slot, from the
+  // current span's unconsumed tail and the read-ahead's bytes (only when they
+  // hold it all; otherwise the next batch decodes when it is asked for)
+  void begin_ahead() {
+    if (v1 || done || err_set || off >= limit || off >= file_size) return;
+    const uint64_t maxspan = rio_ctx_max_span(ctx);
+    const uint64_t n = file_size - off < maxspan ? file_size - off : maxspan;
+    ra_join();
+    const uint64_t pend = span_at + span_n;
+    if (!(ra_valid && span_data && ra_at == pend && off >= span_at && off <= pend && pend - off <= kRaRoom &&
+          ra_st == 0 && off + n <= pend + ra_got))
+      return;
+    if (!cx[1]) {
+      cx[1] = rio_ctx_sibling(ctx);
+      if (!cx[1]) return;
+      rs[1] = rio_ctx_take_results(ctx);
+    }
+    if (rio_ctx_reserve_span(cx[slot ^ 1], n) != 0) return;
+    const uint64_t t = pend - off;
+    uint8_t *base = ra_buf + kRaRoom - t;
+    if (t) memcpy(base, span_data + (off - span_at), t);
+    ra_valid = false;
+    std::swap(ahead_buf, ra_buf);
+    std::swap(ahead_cap, ra_cap);
+    ahead_base = base;
+    ahead_at = off;
+    ahead_n = n;
+    read_ahead(off + n);  // (into the buffer of the batch before the current one)
+    ahead_rc = rio_scan_span_begin(cx[slot ^ 1], base, n, off, off + n >= file_size ? 1 : 0, limit, codec,
+                                   rs[slot ^ 1], &ahead_b);
+    ahead = true;
+  }
   // rio_scanner_gather: staging, results and the gathered items' bytes
   uint8_t *gspan = nullptr;
   uint64_t gspan_cap = 0;
@@ -291,8 +365,8 @@ struct rio_scanner {
   }
   // read [at, at+n) into *buf and decode it on the GPU into *rs (ahead: the
   // read-ahead of the bytes after it starts before the GPU decode)
-  int decode_into(uint8_t **buf, uint64_t *cap, rio_results *rs, uint64_t at, uint64_t n, int32_t cdc, int32_t mode,
-                  uint64_t lim, rio_batch *out, bool ahead = false) {
+  int decode_into(uint8_t **buf, uint64_t *cap, rio_results *res_, uint64_t at, uint64_t n, int32_t cdc,
+                  int32_t mode, uint64_t lim, rio_batch *out, bool body = false) {
     if (ensure_buf(buf, cap, n ? n : 1)) {
       memset(out, 0, sizeof(*out));
       rio_set_error(&out->err, RIO_ERR_HIP, at, "pinned allocation failed");
@@ -308,14 +382,19 @@ struct rio_scanner {
       return 0;
     }
     const int is_end = (at + got >= file_size);
-    if (ahead) read_ahead(at + got);
-    if (v1 && mode == 0) return rio_scan_v1_span_mode(ctx, *buf, got, at, is_end, rs, out);
+    if (body) {  // the body's span (the current slot; the bytes after it read meanwhile)
+      read_ahead(at + got);
+      return scan_body(*buf, got, at, out);
+    }
+    if (v1 && mode == 0) return rio_scan_v1_span_mode(ctx, *buf, got, at, is_end, res_, out);
     // a header / trailer block longer than the ctx's span: the span grows to it
     if (mode != 0 && rio_ctx_reserve_span(ctx, got) != 0) return -1;
-    return rio_scan_span_mode(ctx, *buf, got, at, is_end, lim, cdc, mode, rs, out);
+    return rio_scan_span_mode(ctx, *buf, got, at, is_end, lim, cdc, mode, res_, out);
   }
   int decode(uint64_t at, uint64_t n, int32_t cdc, int32_t mode, uint64_t lim, rio_batch *out) {
     ra_drop();
+    ahead_drop();
+    slot = 0;
     span_data = nullptr;
     return decode_into(&span, &span_cap, res, at, n, cdc, mode, lim, out);
   }
@@ -341,10 +420,8 @@ struct rio_scanner {
       ra_valid = false;
       std::swap(span, ra_buf);  // the batch's views will point into this buffer
       std::swap(span_cap, ra_cap);
-      const int is_end = (at + n >= file_size);
       read_ahead(at + n);  // (into the previous span's buffer: its batch is consumed)
-      const int rc = v1 ? rio_scan_v1_span_mode(ctx, base, n, at, is_end, res, out)
-                        : rio_scan_span_mode(ctx, base, n, at, is_end, limit, codec, 0, res, out);
+      const int rc = scan_body(base, n, at, out);
       span_data = base;
       span_at = at;
       span_n = n;
@@ -518,8 +595,16 @@ bool next_batch(rio_scanner *s) {
     uint64_t n = s->file_size - s->off;
     if (n > maxspan) n = maxspan;
     rio_batch &b = s->batch;
-    if (s->decode_body(s->off, n, &b) != 0) {
+    int rc;
+    if (s->ahead && s->ahead_at == s->off && s->ahead_n == n) {
+      rc = s->take_ahead(&b);
+    } else {
+      s->ahead_drop();
+      rc = s->decode_body(s->off, n, &b);
+    }
+    if (rc != 0) {
       s->set_errf(RIO_ERR_HIP, s->off, "%s", rio_last_error());
+      s->finish_cur();
       return false;
     }
     s->have_batch = true;
@@ -587,6 +672,11 @@ bool next_batch(rio_scanner *s) {
         const uint64_t left = s->file_size - end;
         s->ra_start(end, left < maxspan ? left : maxspan);
       }
+      s->begin_ahead();  // (its copies and decode overlap this batch's result copies)
+    }
+    if (s->finish_cur() != 0) {
+      s->set_errf(RIO_ERR_HIP, s->off, "%s", rio_last_error());
+      return false;
     }
     if (b.n_items > 0) return true;
     if (s->pending_set) {
@@ -654,6 +744,8 @@ rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int l
   rio_scanner *s = new rio_scanner();
   s->ctx = ctx;
   s->res = ctx ? rio_ctx_take_results(ctx) : rio_results_new();
+  s->cx[0] = ctx;
+  s->rs[0] = s->res;
   s->shard_start = start;
   s->shard_limit = limit;
   s->shard_n = nshard;
@@ -869,6 +961,7 @@ void rio_scanner_seek(rio_scanner *s, uint64_t block, int64_t item) {
   }
   // Seek (scannerv2.go:348-361): restart at the block, skip `item` items
   s->ra_drop();
+  s->ahead_drop();
   s->have_batch = false;
   s->pending_set = false;
   s->done = false;
@@ -1032,12 +1125,16 @@ int rio_scanner_finish(rio_scanner *s, rio_error *err) {
   if (!s) return 0;
   int rc = rio_scanner_err(s, err);
   s->ra_drop();
+  s->ahead_drop();
+  for (rio_ctx *c : s->cx) rio_scan_span_end(c);  // (nothing of this scanner's left in flight)
   if (s->ctx) {  // buffers and result sets back to the ctx's pools
     s->give_buf(&s->span, &s->span_cap);
     s->give_buf(&s->ra_buf, &s->ra_cap);
+    s->give_buf(&s->ahead_buf, &s->ahead_cap);
     s->give_buf(&s->gspan, &s->gspan_cap);
     rio_ctx_give_results(s->ctx, s->gres);
     rio_ctx_give_results(s->ctx, s->res);
+    rio_ctx_give_results(s->ctx, s->rs[1]);
   } else {
     rio_results_free(s->res);
   }

@@ -223,7 +223,8 @@ typedef struct rio_stats {
     uint64_t spans;     /* host spans scanned */
     uint64_t h2d_bytes; /* bytes copied host -> device (the spans) */
     uint64_t d2h_bytes; /* bytes copied device -> host (records, item views, block tables) */
-    double device_ms;   /* HIP-event time of those calls: copies in, pipeline, copies out */
+    double device_ms;   /* HIP-event time of those calls: copies in, pipeline, copies out (a
+                           scanner's spans ahead run on a second context: included) */
     uint64_t span_cap;  /* the span the device buffers are sized for now (rio_config.max_span_bytes,
                            grown by a block longer than it; a chain's later stages grow it for that
                            call only) */

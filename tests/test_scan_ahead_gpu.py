@@ -1,0 +1,113 @@
+"""The scanner's span ahead (scanner.cpp begin_ahead): with a file of many
+spans, span i + 1 is decoded on the ctx's sibling context while batch i's
+result copies come back, and batches alternate between the two. Every record,
+error and location must be what the oracle's scanner (scannerv2.go's restated)
+gives, whichever context decoded it: many spans for each codec, a corrupt
+chunk in a later span, Seek in the middle of a scan, shards, and the byte
+accounting across both contexts."""
+import random
+import struct
+import zlib
+
+import pytest
+
+from conftest import oracle_has_zstd
+
+pytestmark = pytest.mark.gpu
+
+SPAN = 8 * 32768  # small spans: a few MB file is dozens of them
+
+
+def _file(trs, n, seed):
+    from base_amd.recordio.writer import WriterOpts, write_file
+    rng = random.Random(seed)
+    recs = [rng.randbytes(rng.choice([0, 5, 300, 2000])) * rng.choice([1, 1, 6]) for _ in range(n)]
+    return recs, write_file(recs, WriterOpts(Transformers=trs, MaxItems=23), trailer=b"AHEAD")
+
+
+def _scan(data, ctx, start=0, limit=1, nshard=1):
+    from base_amd.recordio import gpu
+    sc = gpu.NewShardScanner(data, gpu.ScannerOpts(), start, limit, nshard, ctx=ctx)
+    items = []
+    while sc.Scan():
+        items.append(sc.Get())
+    e = sc.Finish()
+    return items, ("" if e is None else str(e))
+
+
+@pytest.mark.parametrize("trs", [[], ["flate"], ["zstd"], ["zstd", "flate"]])
+def test_many_spans_every_record(oracle, trs):
+    from base_amd.recordio import gpu
+    if "zstd" in trs and not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    recs, data = _file(trs, 2500, 1)
+    ref = oracle.scan(data)
+    assert ref.err == "" and ref.items == recs
+    ctx = gpu.Context(0, max_span_bytes=SPAN)
+    try:
+        for _ in range(2):  # (the second scan reuses the sibling and the pools)
+            items, err = _scan(data, ctx)
+            assert err == "" and items == recs, trs
+        st = ctx.stats()
+        body = len(data) - 32768  # the spans cover the body at least once per scan
+        assert st["spans"] >= 2 * (body // SPAN) and st["h2d_bytes"] >= 2 * body
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("trs", [[], ["flate"], ["zstd"]])
+def test_corrupt_later_span_matches_oracle(oracle, trs):
+    """A bad chunk deep in the file (CRC left stale, or fixed so the codec or the
+    packed parse must notice): the same records before it and the same error."""
+    from base_amd.recordio import gpu
+    if "zstd" in trs and not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    recs, data = _file(trs, 2500, 2)
+    nck = len(data) // 32768
+    rng = random.Random(3)
+    ctx = gpu.Context(0, max_span_bytes=SPAN)
+    try:
+        for trial in range(6):
+            b = bytearray(data)
+            c = rng.randrange(nck // 2, nck - 2)
+            o = c * 32768
+            size = struct.unpack_from("<I", b, o + 16)[0]
+            if size == 0:
+                continue
+            b[o + 28 + rng.randrange(size)] ^= 1 << rng.randrange(8)
+            if trial % 2:
+                struct.pack_into("<I", b, o + 8, zlib.crc32(bytes(b[o + 12:o + 28 + size])))
+            d = bytes(b)
+            ref = oracle.scan(d, read_trailer=False)
+            items, err = _scan(d, ctx)
+            assert err == ref.err and items == ref.items, (trs, trial, c)
+    finally:
+        ctx.close()
+
+
+def test_seek_mid_scan_and_shards(oracle):
+    """Seek while a span ahead is in flight, then scan on; shards with small spans."""
+    from base_amd.recordio import gpu
+    from base_amd.recordio.writer import ItemLocation
+    recs, data = _file(["flate"], 3000, 4)
+    ref = oracle.scan(data)
+    ctx = gpu.Context(0, max_span_bytes=SPAN)
+    try:
+        sc = gpu.NewScanner(data, ctx=ctx)
+        for _ in range(700):  # some spans in: the next one has been begun ahead
+            assert sc.Scan()
+        for i in (2900, 10, 1500, 2999, 0):
+            sc.Seek(ItemLocation(*ref.locations[i]))
+            got = []
+            while len(got) < 300 and sc.Scan():
+                got.append(sc.Get())
+            assert got == recs[i:i + 300], i
+        assert sc.Finish() is None
+        parts = []
+        for s in range(4):
+            items, err = _scan(data, ctx, s, s + 1, 4)
+            assert err == ""
+            parts.extend(items)
+        assert parts == recs
+    finally:
+        ctx.close()
