@@ -200,9 +200,12 @@ def c5_flate(args, local, rank, world, dist):
     device-resident, decoded as batches of whole file bodies back to back, one
     rio_scan_device_segments_async launch per batch (each body a segment: its
     blocks' ItemLocation.Block offsets are their own file's). The 1024 files are
-    copies of c5_data.N_BASE distinct base files (generating 1024 distinct 64 MiB
-    files would take ~10 minutes per run); every file is decoded and checked on
-    its own. Strong scaling: the 1024 files are fixed as N grows; value = all
+    made from c5_data.N_BASE generated base files (generating 1024 distinct 64 MiB
+    files would take ~10 minutes per run): file f is base f mod N_BASE with its
+    blocks rotated by a file-specific count (blocks are independent, so it is a
+    valid recordio file of the same records in another order), so every file
+    has its own block layout, record order and trailer index; every file is
+    decoded and checked on its own. Strong scaling: the 1024 files are fixed as N grows; value = all
     files' bytes / max time over ranks. No record byte crosses xGMI; the one
     collective is the ordered-output prefix (RCCL).
 
@@ -248,6 +251,16 @@ def c5_flate(args, local, rank, world, dist):
     sizes = [len(bases[f % c5_data.N_BASE]) for f in range(c5_data.N_FILES)]
     mine = shard.assign_files(sizes, world)[rank]
     body_len = [spans[k][1] - spans[k][0] for k in range(c5_data.N_BASE)]
+    rel = [[o - index[k][0] for o in index[k]] for k in range(c5_data.N_BASE)]  # body-relative block starts
+
+    def rot(f):  # file f's first block (of its base's): its blocks are base blocks rot, rot + 1, ..., rot - 1
+        k = f % c5_data.N_BASE
+        return (f // c5_data.N_BASE) * 37 % len(index[k])
+
+    def file_index(f):  # file f's trailer index: its blocks' file offsets, in its block order
+        k, r = f % c5_data.N_BASE, rot(f)
+        nb_, n, cut = len(index[k]), body_len[k], rel[k][rot(f)]
+        return [spans[k][0] + (rel[k][(r + j) % nb_] - cut) % n for j in range(nb_)]
     # batches of whole file bodies, <= args.c5_batch_gib each
     cap = int(args.c5_batch_gib * 2 ** 30)
     batches, cur, cur_b = [], [], 0
@@ -270,8 +283,9 @@ def c5_flate(args, local, rank, world, dist):
         ends, foffs = [], []
         for f in bt:
             k = f % c5_data.N_BASE
-            n = body_len[k]
-            dev[pos:pos + n].copy_(dbase[k])
+            n, cut = body_len[k], rel[k][rot(f)]
+            dev[pos:pos + n - cut].copy_(dbase[k][cut:])  # blocks rot .. end, then 0 .. rot - 1
+            dev[pos + n - cut:pos + n].copy_(dbase[k][:cut])
             pos += n
             ends.append(pos - lo)
             foffs.append(spans[k][0])
@@ -295,10 +309,14 @@ def c5_flate(args, local, rank, world, dist):
     # parity pass: every file of the rank against its base's records and index
     files_ok = 0
     if mine:
-        want = {}
+        want, blk_bytes = {}, {}
         for k in range(c5_data.N_BASE):
-            w = b"".join(c5_data.base_records(k))
+            recs = c5_data.base_records(k)
+            w = b"".join(recs)
             want[k] = torch.frombuffer(bytearray(w), dtype=torch.uint8).to(dev.device)
+            lens = np.fromiter((len(x) for x in recs), dtype=np.int64, count=len(recs))
+            cum = np.concatenate([[0], np.cumsum(lens)])
+            blk_bytes[k] = cum[np.minimum(np.arange(len(index[k])) * c5_data.PER_BLOCK, len(recs))]
         for i, bt in enumerate(batches):
             launch(ctxs[0], i)
             r = ctxs[0].sync()
@@ -320,7 +338,10 @@ def c5_flate(args, local, rank, world, dist):
                 b0, b1 = bounds[j], bounds[j + 1]
                 got = torch.cat([rec[int(data_[b] + foff[b]):int(data_[b] + foff[b] + nbytes[b])]
                                  for b in range(b0, b1)])
-                if torch.equal(got, want[k]) and boff[b0:b1].tolist() == index[k]:
+                br = int(blk_bytes[k][rot(f)])  # the records of the base's blocks before rot
+                tail = want[k].numel() - br
+                if (got.numel() == want[k].numel() and torch.equal(got[:tail], want[k][br:])
+                        and torch.equal(got[tail:], want[k][:br]) and boff[b0:b1].tolist() == file_index(f)):
                     files_ok += 1
             del rec
         del want
@@ -385,7 +406,8 @@ def c5_flate(args, local, rank, world, dist):
             "parity_files_checked": len(mine), "parity_files_ok": files_ok, "ordered_prefix": prefix,
             "config": {"files": c5_data.N_FILES, "file_record_bytes": c5_data.FILE_RECORD_BYTES,
                        "records_per_block": c5_data.PER_BLOCK, "distinct_base_files": c5_data.N_BASE,
-                       "note": "file f is a copy of base f mod %d (each decoded and checked on its own)"
+                       "note": "file f is base f mod %d with its blocks rotated by a file-specific count: "
+                               "1024 distinct block layouts and indexes (each decoded and checked on its own)"
                                % c5_data.N_BASE,
                        "files_bytes_total": all_bytes, "files_this_rank": len(mine),
                        "batches_this_rank": len(batches), "launch": "rio_scan_device_segments_async, "

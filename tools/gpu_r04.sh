@@ -50,6 +50,7 @@ while [ $# -gt 0 ]; do
     c4) c4data; step c4 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 3 ;;
     c4_c2) c4data; step c4_c2 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 3 --contexts 2 ;;
     c4_p2) c4data; step c4_p2 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 4 --pipeline 2 ;;
+    c5) step c5 600 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-flate --no-flate16k --no-zstd --no-e2e ;;
     bench) step bench 900 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchnc5) step benchnc5 900 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-c5 --no-e2e ;;
     e2e) c4data; step e2e 600 python3 tools/bench_e2e.py ;;
