@@ -94,6 +94,13 @@ def pmc_traffic(kernel: str, replicas: int):
 
 
 REHEARSE = os.environ.get("RIO_BENCH_REHEARSE") == "1"  # N ranks on one GPU over gloo (rehearsal only)
+_T0 = time.perf_counter()
+
+
+def progress(rank, msg):
+    """A progress line on stderr (rank 0): stdout carries only the result line."""
+    if rank == 0:
+        print("[bench %7.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
 
 
 def coll_dev(local):
@@ -464,6 +471,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1 and REHEARSE:  # every rank on GPU 0, collectives over gloo
+        import faulthandler
+        faulthandler.dump_traceback_later(100, repeat=True)  # (a stalled rehearsal shows where)
         import torch.distributed as dist
         local = 0
         torch.cuda.set_device(0)
@@ -478,6 +487,7 @@ def main():
     from base_amd.recordio import gpu
     gpu.load()  # refuses a library whose build id is not this tree's (base_amd/build.py)
 
+    progress(rank, "C2: %d GPU(s)" % world)
     data, nrec = make_c2_file()
     body = data[CHUNK:]
     nbody = len(body)
@@ -602,19 +612,26 @@ def main():
         c.close()
     del dev
     torch.cuda.empty_cache()
+    progress(rank, "C2 %.2f GiB/s" % value)
     if not args.no_flate:
+        progress(rank, "C3 flate")
         out["c3_flate"] = c3_flate(args, local, world, dist)
     if not args.no_flate16k:
+        progress(rank, "C3 flate at MaxItems 16384")
         out["c3_flate_16k"] = c3_flate_16k(args, local, world, dist)
     if not args.no_zstd:
+        progress(rank, "C4 zstd")
         out["c4_zstd"] = c4_zstd(args, local, world, dist)
     if not args.no_c5:
+        progress(rank, "C5 1024 files")
         out["c5_flate"] = c5_flate(args, local, rank, world, dist)
     if world == 1 and not args.no_e2e:  # the drop-in path, PCIe included (north_star)
+        progress(rank, "end-to-end scans")
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import bench_e2e
         out["e2e"] = bench_e2e.run_e2e(local, args.e2e_gib)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress(rank, "CPU baselines")
         out["cpu_baseline"], out["cpu_baseline_all_cores"], out["c1_cpu"] = cpu_baselines(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
