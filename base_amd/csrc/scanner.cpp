@@ -10,8 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <string>
 #include <algorithm>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -830,6 +830,23 @@ int64_t rio_scanner_next_batch(rio_scanner *s, const uint8_t **data, uint64_t *l
   while (n < max) {
     // do not cross into a new GPU batch: views stay valid for the whole call
     if (n > 0 && !(s->have_batch && s->item < s->batch.n_items)) break;
+    if (s && !s->error_scanner && !s->err_set && s->have_batch && s->item < s->batch.n_items) {
+      // the current batch's next items in one pass (what rio_scanner_scan would
+      // return one by one: a view per item, then the scanner positioned on the
+      // last one -- its block and index for Location)
+      const rio_batch &b = s->batch;
+      const uint64_t k = std::min<uint64_t>(b.n_items - s->item, (uint64_t)(max - n));
+      for (uint64_t i = 0; i < k; i++) data[n + i] = batch_item(b, s->item + i, &lens[n + i]);
+      const uint64_t last = s->item + k - 1;
+      while (last >= b.block_first_item[s->blk + 1]) s->blk++;
+      s->cur = data[n + k - 1];
+      s->cur_len = lens[n + k - 1];
+      s->cur_block = b.block_file_off[s->blk];
+      s->cur_item = (int64_t)(last - b.block_first_item[s->blk]);
+      s->item = last + 1;
+      n += (int64_t)k;
+      continue;
+    }
     if (!rio_scanner_scan(s)) break;
     data[n] = s->cur;
     lens[n] = s->cur_len;

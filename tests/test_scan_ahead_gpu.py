@@ -111,3 +111,35 @@ def test_seek_mid_scan_and_shards(oracle):
         assert parts == recs
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("trs", [[], ["zstd"]])
+def test_scan_batch_views_and_location(oracle, trs):
+    """rio_scanner_next_batch (ScanBatch) hands a batch's items over in one pass:
+    the same items as Scan/Get, mixed with plain Scans, odd batch sizes, across
+    spans, and Location afterwards is the last item's (the reference's)."""
+    from base_amd.recordio import gpu
+    if "zstd" in trs and not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    recs, data = _file(trs, 2500, 5)
+    ref = oracle.scan(data)
+    ctx = gpu.Context(0, max_span_bytes=SPAN)
+    try:
+        sc = gpu.NewScanner(data, ctx=ctx)
+        got, sizes, i = [], [7, 1000, 1, 333, 1 << 16], 0
+        while True:
+            if i % 3 == 2:  # a plain Scan between batches
+                if not sc.Scan():
+                    break
+                got.append(sc.Get())
+            else:
+                part = sc.ScanBatch(sizes[i % len(sizes)])
+                if not part:
+                    break
+                got.extend(part)
+            loc = sc.Location()
+            assert (loc.Block, loc.Item) == tuple(ref.locations[len(got) - 1]), (i, len(got))
+            i += 1
+        assert sc.Finish() is None and got == recs
+    finally:
+        ctx.close()
