@@ -136,6 +136,38 @@ def test_chain_growth_is_temporary(chain_files):
         ctx.close()
 
 
+def test_decode_block_growth_is_temporary():
+    """rio_decode_block of a block longer than the context's span grows it for
+    that call; the next plain call returns it to the configured size."""
+    import os as _os
+    import torch
+    from base_amd.recordio import gpu
+    from base_amd.recordio import format as F
+    from base_amd.recordio.codecs import make_compressor
+    from base_amd.recordio.writer import WriterOpts, write_file
+    recs = [_os.urandom(3000) for _ in range(400)]  # ~1.2 MB, incompressible
+    payload = F.packed_block_payload(recs)
+    comp = make_compressor("flate 1")(payload)
+    cap0 = 4 * 32768
+    ctx = gpu.Context(0, max_span_bytes=cap0)
+    try:
+        assert len(comp) > 2 * cap0
+        pays = [comp[i:i + 30000] for i in range(0, len(comp), 30000)]
+        assert ctx.decode_block(pays, gpu.RIO_CODEC_FLATE) == payload
+        assert ctx.stats()["span_cap"] > cap0
+        plain_recs = [bytes([k % 251]) * 100 for k in range(300)]
+        plain = write_file(plain_recs, WriterOpts(MaxItems=1000))  # one block: a chunk
+        pb = plain[32768:]
+        assert len(pb) <= cap0
+        dev = torch.frombuffer(bytearray(pb), dtype=torch.uint8).to("cuda:0")
+        bd = ctx.scan_device(dev.data_ptr(), len(pb), file_off=32768, is_file_end=True,
+                             codec=gpu.RIO_CODEC_NONE)
+        assert bd.err.code == 0 and gpu.device_batch_items(bd, pb) == plain_recs, bd.err.msg
+        assert ctx.stats()["span_cap"] == cap0
+    finally:
+        ctx.close()
+
+
 def test_chain_decode_block(gpu_ctx, oracle, chain_files):
     """rio_decode_block with a chain codec: the combined untransform of one block."""
     from base_amd.recordio import format as F
