@@ -1,15 +1,16 @@
 // Chunk CRC32-IEEE verify (readChunk, recordio/internal/chunk.go:338-343) at
 // HBM read speed, no carry-less multiply.
 //
-// One wave per 32 KiB chunk, kCrcWaves waves per workgroup, one workgroup per CU.
+// One wave per 32 KiB chunk, kCrcWaves (12) waves per workgroup, one workgroup per CU.
 // Lane t loads the 16-byte units at chunk offsets 1024*i + 16*t (i = 0..31): every
 // load instruction is 1 KiB contiguous. Each of the lane's 4 dwords (k = 0..3)
 // is its own CRC stream with one dword per 1 KiB row; the 1020-byte gap to the
 // stream's next dword is folded into the tables, so one step is
 //   S_k <- fold0[b0] ^ fold1[b1] ^ fold2[b2] ^ fold3[b3],  b = bytes of (u_k ^ S_k),
 //   fold_j[b] = R(b || 0^(1023-j))     (R = raw CRC: zero init, no final xor).
-// Only 4 fold tables exist, so each is replicated 32x in LDS (128 KiB): lane l
-// reads copy l & 31 and every ds_read_b32 is bank-conflict free. A row's 16
+// Only 4 fold tables exist, so each is replicated 16x in LDS (64 KiB): lane l
+// reads copy l & 15 (32 copies, 128 KiB, made every read conflict-free but left
+// no room on the CU for anything else). A row's 16
 // lookups are independent and issue back to back; only the row-to-row chain
 // per stream is serial.
 // After row 31, stream (t, k) holds R(message) * x^(8(16t + 4k)); the lane
@@ -18,8 +19,17 @@
 // Bytes outside [12, 28+size) are zeroed, so V = R(0^12 || covered || 0^pad) and
 // crc = ~(~0 * x^(8(16+size)) ^ V * x^(-8 pad)).
 // Loads are software-pipelined in 4 KiB stages through 4 register buffers:
-// while one stage is folded the next three are in flight (16 waves per CU keep
-// 192 KiB outstanding).
+// while one stage is folded the next three are in flight (12 waves per CU keep
+// 144 KiB outstanding).
+//
+// Room beside it (round 4): the tables are dynamic LDS (92 KiB) and the
+// registers are allocated for 4 waves per SIMD (127 VGPRs) while the workgroup
+// has 12 waves (3 per SIMD) -- with static LDS the compiler sizes registers for
+// the 3 waves per SIMD the LDS allows (167 VGPRs) -- so one workgroup of another
+// kernel (k_lean_end: 6 KiB of LDS, 71 VGPRs per wave) fits on each CU beside
+// it: with two contexts in flight, step i + 1's parse runs during step i's
+// CRC pass (C2, A/B on one box: 3.114 -> 3.043 ms per step; alone k_crc 2.785
+// -> 2.75 ms).
 //
 // Fused parse (k_crc<true>, round 2; measured slower and not instantiated:
 // DESIGN.md §5; none codec): the wave that checksums a block's
@@ -42,9 +52,9 @@
 namespace rio {
 
 #ifndef RIO_CRC_WAVES
-#define RIO_CRC_WAVES 16
+#define RIO_CRC_WAVES 12
 #endif
-constexpr int kCrcWaves = RIO_CRC_WAVES;  // waves per workgroup (one workgroup per CU: 156 KiB LDS at 32 copies)
+constexpr int kCrcWaves = RIO_CRC_WAVES;  // waves per workgroup (one workgroup per CU: 92 KiB LDS at 16 copies)
 
 constexpr int kRows = 4;   // rows per pipeline stage (4 KiB per wave)
 constexpr int kBufs = 4;   // register buffers: kBufs - 1 stages in flight during a fold
@@ -106,14 +116,35 @@ struct CrcParseIn {
 };
 constexpr int kStageBytes = 1088;  // payload window staging: row 0 + 32 B of row 1 (then reused as the window)
 
+// the tables in dynamic LDS, so that the compiler sizes registers for
+// RIO_CRC_WPE waves per SIMD instead of the occupancy the static LDS allows
+#ifndef RIO_CRC_DYN
+#define RIO_CRC_DYN 1
+#endif
+#ifndef RIO_CRC_WPE
+#define RIO_CRC_WPE 4
+#endif
+#if RIO_CRC_DYN
+#define RIO_CRC_ATTR __attribute__((amdgpu_waves_per_eu(RIO_CRC_WPE)))
+#else
+#define RIO_CRC_ATTR
+#endif
+constexpr size_t kCrcDynLds = RIO_CRC_DYN ? 4 * (size_t)(kFoldWords + kMulTables * 1024) : 0;
+
 template <bool kParse>
-__global__ void __launch_bounds__(64 * kCrcWaves) k_crc(const uint8_t *__restrict__ span, uint64_t nchunks,
+__global__ void __launch_bounds__(64 * kCrcWaves) RIO_CRC_ATTR k_crc(const uint8_t *__restrict__ span, uint64_t nchunks,
                                                        const uint32_t *__restrict__ ck_size,
                                                        const uint32_t *__restrict__ fix_a,
                                                        const uint32_t *__restrict__ fix_b, DevBufs d, CrcArgs ca,
                                                        CrcParseIn pin, ParseArgs pa) {
+#if RIO_CRC_DYN
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+  uint32_t *const s_fold = s_dyn;
+  uint32_t *const s_mul = s_dyn + kFoldWords;
+#else
   __shared__ __attribute__((aligned(16))) uint32_t s_fold[kFoldWords];
   __shared__ __attribute__((aligned(16))) uint32_t s_mul[kMulTables * 1024];
+#endif
   __shared__ __attribute__((aligned(16))) uint8_t s_stage[kParse ? kCrcWaves : 1][kParse ? kStageBytes : 16];
   __shared__ __attribute__((aligned(16))) uint16_t s_tpos[kParse ? kCrcWaves : 1][kParse ? 1024 : 1];
   {
@@ -209,7 +240,7 @@ void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const C
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   const CrcParseIn pin{d.ck_index, d.ck_block, d.blk_meta, d.blk_len, d.blk_item_base, d.ck_pay};
-  hipLaunchKernelGGL(k_crc<false>, dim3((unsigned)g), dim3(64 * kCrcWaves), 0, st, span, nchunks, d.ck_size,
+  hipLaunchKernelGGL(k_crc<false>, dim3((unsigned)g), dim3(64 * kCrcWaves), kCrcDynLds, st, span, nchunks, d.ck_size,
                        d.crc_fix_a, d.crc_fix_b, d, ca, pin, ParseArgs{});
 }
 

@@ -253,11 +253,11 @@ struct ResolveArgs {
 // ---- host helpers: GF(2) arithmetic of the reflected CRC-32 polynomial ----
 constexpr uint32_t kPoly = 0xEDB88320u;
 #ifndef RIO_FOLD_COPIES
-#define RIO_FOLD_COPIES 32
+#define RIO_FOLD_COPIES 16  // (round 4: 32 -> 16, so that another kernel's workgroup fits beside k_crc)
 #endif
-constexpr int kFoldCopies = RIO_FOLD_COPIES;     // bank-private replicas of each fold table
+constexpr int kFoldCopies = RIO_FOLD_COPIES;     // replicas of each fold table (lane l reads copy l % copies)
 constexpr int kFoldShift = kFoldCopies == 32 ? 7 : (kFoldCopies == 16 ? 6 : 5);  // log2(4 * copies)
-constexpr int kFoldWords = 4 * 256 * kFoldCopies;  // 128 KiB at 32 copies
+constexpr int kFoldWords = 4 * 256 * kFoldCopies;  // 64 KiB at 16 copies
 constexpr int kMulTables = 7;                    // x^-32, then x^-(128*2^l), l = 0..5
 uint32_t gf_mul(uint32_t a, uint32_t b);         // a*b mod P (reflected; 1 = 0x80000000)
 uint32_t gf_xpow8(int64_t nbytes);               // x^(8*nbytes) mod P, nbytes may be negative

@@ -591,6 +591,10 @@ def main():
             # contexts, two steps are in flight: the latency spans both)
             "pipeline_latency_ms": round(float(np.mean(kern_ms)), 3),
             "pipeline_alg_GBs": round(pipe_alg / (ms_per_step * 1e-3) / 1e9, 1),
+            # the whole step against the peak (k_crc's launches run beside the other
+            # context's parse -- k_lean_end fits on each CU beside it, DESIGN.md
+            # k_crc design -- so its launch time includes that sharing)
+            "step_frac": round(pipe_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "stage_ms": [round(x / args.steps, 3) for x in stage_sum]}
 
     out = {"metric": "recordio scan GiB/s device-resident (compressed in) at 1/2/4/8 MI355X",

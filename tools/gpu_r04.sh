@@ -37,8 +37,16 @@ while [ $# -gt 0 ]; do
         python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread -k "$1" ;;
     testf) shift; step "pytest_$(basename "$1" .py)" 600 \
         python -u -m pytest "$1" -v --timeout 150 --timeout-method thread ;;
-    c2) step c2 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-flate16k --no-zstd \
+    c2) n_c2=$((n_c2 + 1)); step c2_$n_c2 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-flate16k --no-zstd \
         --no-c5 --no-e2e ;;
+    c2v) shift; v=$1  # the C2 bench on an experiment build: exp_lib/<v>, its flags in exp_lib/<v>.flags
+      n_c2v=$((n_c2v + 1))
+      RIO_GPU_LIB=exp_lib/$v/librio_gpu.so RIO_EXTRA_FLAGS="$(cat exp_lib/$v.flags)" step c2_${v}_$n_c2v 300 \
+        python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-flate16k --no-zstd --no-c5 --no-e2e ;;
+    c2v1) shift; v=$1; n_c2v=$((n_c2v + 1))  # the same, one context
+      RIO_GPU_LIB=exp_lib/$v/librio_gpu.so RIO_EXTRA_FLAGS="$(cat exp_lib/$v.flags)" step c2c1_${v}_$n_c2v 300 \
+        python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-flate16k --no-zstd --no-c5 --no-e2e \
+        --c2-contexts 1 ;;
     c2c1) step c2c1 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-flate16k --no-zstd \
         --no-c5 --no-e2e --c2-contexts 1 ;;
     profc2) step profc2 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc2 -o run -- \
