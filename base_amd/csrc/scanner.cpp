@@ -321,7 +321,7 @@ struct rio_scanner {
   // io.ReaderAt: concurrent ReadAt calls are allowed), like the reference's
   // S3 reader's parallel chunk reads (file/s3file/file_chunk_read.go:72-102).
   static constexpr uint64_t kPiece = 16ull << 20;
-  static constexpr int kReaders = 8;
+  static constexpr int kReaders = 16;
   uint64_t read_full(uint8_t *buf, uint64_t n, uint64_t at, int *st) const {
     if (n < 2 * kPiece) return read_serial(buf, n, at, st);
     const uint64_t np = (n + kPiece - 1) / kPiece;
