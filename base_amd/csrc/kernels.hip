@@ -261,15 +261,21 @@ __global__ void __launch_bounds__(kScanThreads) k_chunk_apply(const uint8_t *__r
         meta |= kMetaComplete;
         // the block's payload bytes (its chunks' sizes, as the payload prefix
         // counts them) and whether every chunk but the last is full
-        bool regular = true;
+        bool regular = true, overlap = false;
         for (uint32_t q = 0; q < total; q++) {
           const uint32_t s = d.ck_size[i + q];
           const uint32_t v = s > (uint32_t)kMaxPayload ? 0u : s;
           len += v;
           if (q + 1 < total && v != (uint32_t)kMaxPayload) regular = false;
+          overlap = overlap || (q > 0 && d.ck_index[i + q] == 0);
         }
+        // Another block starting inside this one's chunks (a `total` rewritten
+        // with its CRC): a chunk error comes before this block's end, so it is
+        // never delivered, but its decode must not write into the other
+        // block's regions (token slots, straddlers): it decodes as empty.
+        if (overlap) len = 0, regular = false;
         if (regular) meta |= kMetaRegular;
-        if (codec == RIO_CODEC_NONE) nres = first_uvarint(span, d, i, total, len);
+        if (codec == RIO_CODEC_NONE && len) nres = first_uvarint(span, d, i, total, len);
       }
       d.blk_c0[ef] = i;
       d.blk_meta[ef] = meta;

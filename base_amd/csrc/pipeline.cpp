@@ -980,7 +980,7 @@ extern "C" int rio_ctx_stats(rio_ctx *ctx, rio_stats *out) {
   if (!ctx || !out) return -1;
   *out = ctx->stats;
   out->span_cap = ctx->max_span;
-  if (const rio_ctx *sb = ctx->sibling) {  // (a scanner's spans ahead ran there)
+  for (const rio_ctx *sb = ctx->sibling; sb; sb = sb->sibling) {  // (a scanner's spans ahead ran there)
     out->spans += sb->stats.spans;
     out->h2d_bytes += sb->stats.h2d_bytes;
     out->d2h_bytes += sb->stats.d2h_bytes;

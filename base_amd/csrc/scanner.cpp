@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <deque>
 #include <string>
 #include <thread>
 #include <vector>
@@ -205,27 +206,52 @@ struct rio_scanner {
     ra_running = true;
     ra_th = std::thread([this] { ra_got = read_full(ra_buf + kRaRoom, ra_len, ra_at, &ra_st); });
   }
-  // Span ahead: the body's next span is decoded on a second context (the
-  // ctx's sibling) as soon as the current batch's extent is known -- before
-  // that batch's result copies have come back, so the next span's H2D copy and
-  // decode overlap them (PCIe is full duplex) -- and its own result copies
-  // come back while the caller consumes the current batch. Slots (context,
-  // results) alternate: the current batch's is `slot`, the span ahead's slot ^ 1.
-  // Three staging buffers rotate: the current batch's span (its views point
-  // there), the span ahead, and the read-ahead.
-  rio_ctx *cx[2] = {nullptr, nullptr};
-  rio_results *rs[2] = {nullptr, nullptr};
+  // Spans ahead: the body's next spans are decoded on further contexts (the
+  // ctx's siblings), kSlots - 1 of them in flight beside the current batch, each
+  // begun on a thread of its own so that no span's H2D copy and decode waits
+  // for the caller. A span's result copies come back while the caller consumes
+  // the batches before it, and the copies of different spans overlap on the
+  // full-duplex link. A span ahead starts where the span before it will stop:
+  // for the first, the current batch's extent (known); for the next, the end of
+  // the last complete block of the span before it, read from that span's last
+  // chunk header on the host (a prediction: when the GPU's extent differs --
+  // a corrupt header, an error, a limit -- the span is dropped and the batch is
+  // decoded when it is asked for). A slot is a (context, results) pair: the
+  // current batch's is `slot`, each span ahead holds another. Staging buffers
+  // rotate: the current batch's span (its views point there), one per span
+  // ahead, and the read-ahead's, with spares from batches consumed.
+  static constexpr int kSlots = 3;
+  int depth = spans_ahead();  // spans ahead (RIO_SPANS_AHEAD: 0 .. kSlots - 1, default kSlots - 1)
+  static int spans_ahead() {
+    const char *e = getenv("RIO_SPANS_AHEAD");
+    const int v = e ? atoi(e) : kSlots - 1;
+    return v < 0 ? 0 : (v > kSlots - 1 ? kSlots - 1 : v);
+  }
+  rio_ctx *cx[kSlots] = {};
+  rio_results *rs[kSlots] = {};
   int slot = 0;
-  bool ahead = false;
-  int ahead_rc = 0;
-  rio_batch ahead_b{};
-  uint64_t ahead_at = 0, ahead_n = 0;
-  const uint8_t *ahead_base = nullptr;
-  uint8_t *ahead_buf = nullptr;
-  uint64_t ahead_cap = 0;
+  struct Ahead {
+    int slot = 0;
+    uint64_t at = 0, n = 0;
+    const uint8_t *base = nullptr;
+    uint8_t *buf = nullptr;
+    uint64_t cap = 0;
+    bool ok = false;  // begun (the context held the span)
+    int rc = 0;
+    std::string msg;  // rio_last_error() of the beginning thread, when rc != 0
+    rio_batch b{};
+    std::thread th;
+  };
+  std::deque<Ahead> aq;
+  std::vector<std::pair<uint8_t *, uint64_t>> spare;  // staging buffers free for reuse
+  std::string ahead_msg;                               // the taken span's error text
   void ahead_drop() {
-    if (ahead) rio_scan_span_end(cx[slot ^ 1]);
-    ahead = false;
+    for (Ahead &e : aq) {
+      if (e.th.joinable()) e.th.join();
+      if (e.ok) rio_scan_span_end(cx[e.slot]);
+      spare.emplace_back(e.buf, e.cap);
+    }
+    aq.clear();
   }
   // the current batch's result copies (rio_scan_span_begin) in place
   int finish_cur() { return rio_scan_span_end(cx[slot]); }
@@ -235,49 +261,123 @@ struct rio_scanner {
     if (v1) return rio_scan_v1_span_mode(cx[slot], base, n, at, is_end, rs[slot], out);
     return rio_scan_span_begin(cx[slot], base, n, at, is_end, limit, codec, rs[slot], out);
   }
-  // the span begun ahead becomes the current batch
-  int take_ahead(rio_batch *out) {
-    ahead = false;
-    std::swap(span, ahead_buf);  // (the previous batch's buffer is free now)
-    std::swap(span_cap, ahead_cap);
-    span_data = ahead_base;
-    span_at = ahead_at;
-    span_n = ahead_n;
-    slot ^= 1;
-    *out = ahead_b;
-    return ahead_rc;
+  // the oldest span ahead, if it starts at `at` and spans n bytes
+  bool ahead_matches(uint64_t at, uint64_t n) {
+    if (aq.empty() || aq.front().at != at || aq.front().n != n) return false;
+    Ahead &e = aq.front();
+    if (e.th.joinable()) e.th.join();
+    return e.ok;
   }
-  // begin the body's next span [off, off + n) on the other slot, from the
-  // current span's unconsumed tail and the read-ahead's bytes (only when they
-  // hold it all; otherwise the next batch decodes when it is asked for)
+  // the oldest span ahead becomes the current batch
+  int take_ahead(rio_batch *out) {
+    Ahead &e = aq.front();
+    spare.emplace_back(span, span_cap);  // (the previous batch's buffer is free now)
+    span = e.buf;
+    span_cap = e.cap;
+    span_data = e.base;
+    span_at = e.at;
+    span_n = e.n;
+    slot = e.slot;
+    *out = e.b;
+    const int rc = e.rc;
+    ahead_msg = e.msg;
+    aq.pop_front();
+    return rc;
+  }
+  // where the span [at, at + n) in host memory will stop: after its last
+  // complete block (its last chunk's index and total, chunk.go:31-53); 0 when
+  // that cannot be told (the block runs past the span, or a header is not sane)
+  static uint64_t predict_consumed(const uint8_t *base, uint64_t n) {
+    const uint64_t nck = n / kCk;
+    if (nck == 0) return 0;
+    uint32_t total, index;
+    memcpy(&total, base + (nck - 1) * kCk + 20, 4);
+    memcpy(&index, base + (nck - 1) * kCk + 24, 4);
+    if (total == 0 || index >= total || index >= nck) return 0;
+    return (index + 1 == total ? nck : nck - 1 - index) * kCk;
+  }
+  // fill the spans ahead: each next span is the unconsumed tail of the span
+  // before it (copied here) and the file bytes after that span: the read-ahead's
+  // when it holds them, else read by the span's own thread before its decode
   void begin_ahead() {
-    if (v1 || done || err_set || off >= limit || off >= file_size) return;
+    if (v1 || done || err_set) return;
     const uint64_t maxspan = rio_ctx_max_span(ctx);
-    const uint64_t n = file_size - off < maxspan ? file_size - off : maxspan;
-    ra_join();
-    const uint64_t pend = span_at + span_n;
-    if (!(ra_valid && span_data && ra_at == pend && off >= span_at && off <= pend && pend - off <= kRaRoom &&
-          ra_st == 0 && off + n <= pend + ra_got))
-      return;
-    if (!cx[1]) {
-      cx[1] = rio_ctx_sibling(ctx);
-      if (!cx[1]) return;
-      rs[1] = rio_ctx_take_results(ctx);
+    while ((int)aq.size() < depth) {
+      // the span before the new one: the last one ahead, or the current batch
+      const bool first = aq.empty();
+      const uint8_t *pdata = first ? span_data : aq.back().base;
+      const uint64_t pat = first ? span_at : aq.back().at, pn = first ? span_n : aq.back().n;
+      const uint64_t pend = pat + pn;
+      if (!pdata || pend >= file_size) return;
+      uint64_t at = off;
+      if (!first) {
+        const uint64_t c = predict_consumed(pdata, pn);
+        if (c == 0) return;
+        at = pat + c;
+      }
+      if (at >= limit || at >= file_size || at < pat || at > pend || pend - at > kRaRoom) return;
+      const uint64_t n = file_size - at < maxspan ? file_size - at : maxspan;
+      if (at + n <= pend) return;  // (a span inside the one before it: not a body's next span)
+      int sl = -1;  // a slot neither the current batch nor a span ahead holds
+      for (int i = 0; i < kSlots && sl < 0; i++) {
+        bool used = (i == slot);
+        for (const Ahead &e : aq) used = used || e.slot == i;
+        if (!used) sl = i;
+      }
+      if (!cx[sl]) {  // (slots open in order: slot 0 is the ctx, slot i the sibling of slot i - 1)
+        cx[sl] = rio_ctx_sibling(cx[sl - 1]);
+        if (!cx[sl]) return;
+        rs[sl] = rio_ctx_take_results(ctx);
+      }
+      // the staging: the read-ahead's buffer when it holds [pend, at + n), else a spare
+      bool from_ra = false;
+      if (ra_valid && ra_at == pend) {
+        ra_join();
+        from_ra = ra_st == 0 && at + n <= pend + ra_got;
+      }
+      uint8_t *buf = nullptr;
+      uint64_t cap = 0;
+      if (from_ra) {
+        buf = ra_buf;
+        cap = ra_cap;
+        ra_buf = nullptr;
+        ra_cap = 0;
+        ra_valid = false;
+      } else if (!spare.empty() && spare.back().second >= kRaRoom + maxspan) {
+        buf = spare.back().first;
+        cap = spare.back().second;
+        spare.pop_back();
+      } else if (ensure_buf(&buf, &cap, kRaRoom + maxspan)) {
+        return;
+      }
+      const uint64_t t = pend - at;
+      aq.emplace_back();
+      Ahead &e = aq.back();
+      e.slot = sl;
+      e.at = at;
+      e.n = n;
+      e.buf = buf;
+      e.cap = cap;
+      e.base = buf + kRaRoom - t;
+      if (t) memcpy(buf + kRaRoom - t, pdata + (at - pat), t);
+      rio_ctx *c = cx[sl];
+      rio_results *r = rs[sl];
+      const uint64_t need = from_ra ? 0 : at + n - pend;
+      const int is_end = at + n >= file_size ? 1 : 0;
+      const uint64_t lim = limit;
+      const int32_t cdc = codec;
+      e.th = std::thread([this, &e, c, r, need, pend, is_end, lim, cdc] {
+        if (need) {  // (an io error or a short read: the batch decodes when asked for, and reports it)
+          int st;
+          const uint64_t got = read_full(const_cast<uint8_t *>(e.base) + (pend - e.at), need, pend, &st);
+          if (st != 0 || got != need) return;
+        }
+        if (rio_ctx_reserve_span(c, e.n) != 0) return;
+        e.rc = rio_scan_span_begin(c, e.base, e.n, e.at, is_end, lim, cdc, r, &e.b);
+        if (e.rc != 0) e.msg = rio_last_error();
+        e.ok = true;
+      });
     }
-    if (rio_ctx_reserve_span(cx[slot ^ 1], n) != 0) return;
-    const uint64_t t = pend - off;
-    uint8_t *base = ra_buf + kRaRoom - t;
-    if (t) memcpy(base, span_data + (off - span_at), t);
-    ra_valid = false;
-    std::swap(ahead_buf, ra_buf);
-    std::swap(ahead_cap, ra_cap);
-    ahead_base = base;
-    ahead_at = off;
-    ahead_n = n;
-    read_ahead(off + n);  // (into the buffer of the batch before the current one)
-    ahead_rc = rio_scan_span_begin(cx[slot ^ 1], base, n, off, off + n >= file_size ? 1 : 0, limit, codec,
-                                   rs[slot ^ 1], &ahead_b);
-    ahead = true;
   }
   // rio_scanner_gather: staging, results and the gathered items' bytes
   uint8_t *gspan = nullptr;
@@ -596,14 +696,15 @@ bool next_batch(rio_scanner *s) {
     if (n > maxspan) n = maxspan;
     rio_batch &b = s->batch;
     int rc;
-    if (s->ahead && s->ahead_at == s->off && s->ahead_n == n) {
+    s->ahead_msg.clear();
+    if (s->ahead_matches(s->off, n)) {
       rc = s->take_ahead(&b);
     } else {
       s->ahead_drop();
       rc = s->decode_body(s->off, n, &b);
     }
     if (rc != 0) {
-      s->set_errf(RIO_ERR_HIP, s->off, "%s", rio_last_error());
+      s->set_errf(RIO_ERR_HIP, s->off, "%s", s->ahead_msg.empty() ? rio_last_error() : s->ahead_msg.c_str());
       s->finish_cur();
       return false;
     }
@@ -665,14 +766,10 @@ bool next_batch(rio_scanner *s) {
         continue;  // again, at the grown span
       }
       s->off += b.consumed;
-      // the bytes after this span, read while the batch is consumed (usually
-      // started already, before the span's decode: decode_body)
-      const uint64_t end = s->span_at + s->span_n;
-      if (!(s->ra_valid && s->ra_at == end) && end < s->file_size && s->off < s->limit) {
-        const uint64_t left = s->file_size - end;
-        s->ra_start(end, left < maxspan ? left : maxspan);
-      }
-      s->begin_ahead();  // (its copies and decode overlap this batch's result copies)
+      // the spans after this one, begun while its result copies come back and
+      // the caller consumes it (the read-ahead of the bytes after the last one
+      // ahead -- or after this span -- started when that span was begun)
+      s->begin_ahead();
     }
     if (s->finish_cur() != 0) {
       s->set_errf(RIO_ERR_HIP, s->off, "%s", rio_last_error());
@@ -1147,11 +1244,11 @@ int rio_scanner_finish(rio_scanner *s, rio_error *err) {
   if (s->ctx) {  // buffers and result sets back to the ctx's pools
     s->give_buf(&s->span, &s->span_cap);
     s->give_buf(&s->ra_buf, &s->ra_cap);
-    s->give_buf(&s->ahead_buf, &s->ahead_cap);
+    for (auto &b : s->spare) s->give_buf(&b.first, &b.second);
     s->give_buf(&s->gspan, &s->gspan_cap);
     rio_ctx_give_results(s->ctx, s->gres);
     rio_ctx_give_results(s->ctx, s->res);
-    rio_ctx_give_results(s->ctx, s->rs[1]);
+    for (int i = 1; i < rio_scanner::kSlots; i++) rio_ctx_give_results(s->ctx, s->rs[i]);
   } else {
     rio_results_free(s->res);
   }

@@ -1,10 +1,12 @@
-"""The scanner's span ahead (scanner.cpp begin_ahead): with a file of many
-spans, span i + 1 is decoded on the ctx's sibling context while batch i's
-result copies come back, and batches alternate between the two. Every record,
-error and location must be what the oracle's scanner (scannerv2.go's restated)
-gives, whichever context decoded it: many spans for each codec, a corrupt
-chunk in a later span, Seek in the middle of a scan, shards, and the byte
-accounting across both contexts."""
+"""The scanner's spans ahead (scanner.cpp begin_ahead): with a file of many
+spans, spans i + 1 and i + 2 are decoded on the ctx's sibling contexts (each
+begun on a thread of its own; the second from a host prediction of where span
+i + 1 stops) while batch i's result copies come back, and batches rotate over
+the three contexts. Every record, error and location must be what the oracle's
+scanner (scannerv2.go's restated) gives, whichever context decoded it: many
+spans for each codec, a corrupt chunk in a later span, wrong predictions,
+Seek in the middle of a scan, shards, and the byte accounting across the
+contexts."""
 import random
 import struct
 import zlib
@@ -81,6 +83,45 @@ def test_corrupt_later_span_matches_oracle(oracle, trs):
             ref = oracle.scan(d, read_trailer=False)
             items, err = _scan(d, ctx)
             assert err == ref.err and items == ref.items, (trs, trial, c)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2])
+@pytest.mark.parametrize("trs", [[], ["flate"], ["zstd"]])
+def test_wrong_span_prediction_matches_oracle(oracle, trs, depth, monkeypatch):
+    """The second span ahead starts where the host reads the span before it will
+    stop (its last chunk header): a chunk header whose index or total was
+    rewritten (CRC fixed, so only the block structure is wrong) makes that
+    prediction wrong, or the GPU's extent differ from it. The spans begun on it
+    are dropped: the same records and error as the oracle's, at every depth of
+    spans ahead (RIO_SPANS_AHEAD). A rewritten total or index also makes blocks
+    overlap (a block start inside another block's chunks): the decode of the
+    overlapping block must stay inside its own regions (kernels.hip k_chunk_apply)."""
+    from base_amd.recordio import gpu
+    if "zstd" in trs and not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    monkeypatch.setenv("RIO_SPANS_AHEAD", str(depth))
+    recs, data = _file(trs, 2500, 6)
+    nck = len(data) // 32768
+    rng = random.Random(7)
+    ctx = gpu.Context(0, max_span_bytes=SPAN)
+    try:
+        for trial in range(12):
+            b = bytearray(data)
+            # the last chunk of a span (the predicted one) or any chunk
+            c = rng.randrange(nck // 4, nck - 2)
+            if trial % 2 == 0:
+                c = c - c % 8 + 7 if c - c % 8 + 7 < nck - 1 else c
+            o = c * 32768
+            field = 20 + 4 * rng.randrange(2)  # total or index: + 1, 2 or 5, or index 0
+            v = struct.unpack_from("<I", b, o + field)[0] + rng.choice([1, 2, 5])
+            struct.pack_into("<I", b, o + field, 0 if field == 24 and trial % 3 == 2 else v)
+            struct.pack_into("<I", b, o + 8, zlib.crc32(bytes(b[o + 12:o + 28 + struct.unpack_from("<I", b, o + 16)[0]])))
+            d = bytes(b)
+            ref = oracle.scan(d, read_trailer=False)
+            items, err = _scan(d, ctx)
+            assert err == ref.err and items == ref.items, (trs, trial, c, field)
     finally:
         ctx.close()
 
