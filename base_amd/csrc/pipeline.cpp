@@ -135,7 +135,10 @@ struct rio_ctx {
   bool grown_tmp = false;
   uint64_t base_span = 0, base_side = 0, base_item = 0;
   rio_config cfg{};            // as opened (the sibling opens with it)
-  rio_ctx *sibling = nullptr;  // a scanner's second context (its span ahead), opened on first use
+  rio_ctx *sibling = nullptr;  // a scanner's further context (its spans ahead), opened on first use
+  const uint8_t *staged = nullptr;  // rio_scan_span_stage: the span whose H2D copy is enqueued
+  uint64_t staged_n = 0;
+  hipEvent_t staged_t0{};
   // rio_scan_span_begin: collect enqueues the result copies without waiting;
   // rio_scan_span_end waits for them and finishes the batch
   bool defer_collect = false, pend = false;
@@ -356,7 +359,16 @@ static void dfree(T **p) {
 
 // back to the sizes before a temporary growth (every buffer sized from the
 // grown span is released; the demand-sized ones regrow on use)
+// a span staged by rio_scan_span_stage and not decoded: forgotten (d_span is
+// reused; stream order keeps its copy before anything after it)
+static void unstage(rio_ctx *c) {
+  if (!c->staged) return;
+  c->staged = nullptr;
+  hipEventDestroy(c->staged_t0);
+}
+
 static int settle(rio_ctx *c) {
+  unstage(c);
   if (!c->grown_tmp) return 0;
   c->grown_tmp = false;
   HIP_OK(hipSetDevice(c->device));
@@ -964,6 +976,7 @@ extern "C" int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbyt
   if (!ctx || !out) return -1;
   memset(out, 0, sizeof(*out));
   if (rio_scan_span_end(ctx)) return -1;
+  unstage(ctx);
   if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;  // (consecutive chain calls keep the growth)
   return run_span(ctx, (const uint8_t *)dev_span, (const uint8_t *)dev_span, nbytes, file_off, is_file_end,
                   limit_off, codec, kModeBody, nullptr, out);
@@ -992,20 +1005,31 @@ extern "C" int rio_ctx_stats(rio_ctx *ctx, rio_stats *out) {
 static int scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
                      uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res, rio_batch *out, bool defer) {
   if (!ctx || !out) return -1;
-  if (rio_scan_span_end(ctx)) return -1;  // (a deferred batch of this ctx: complete before its buffers are reused)
-  memset(out, 0, sizeof(*out));
-  if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;
-  if (nbytes > ctx->max_span + kChunk) {
-    rio_set_error(&out->err, RIO_ERR_CAPACITY, file_off, "span of %" PRIu64 " bytes exceeds ctx capacity", nbytes);
-    out->stop = RIO_STOP_ERROR;
-    return 0;
-  }
-  if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+  // staged by rio_scan_span_stage (its H2D copy enqueued, the ctx settled)
+  const bool pre = span && ctx->staged == span && ctx->staged_n == nbytes;
+  if (pre) ctx->staged = nullptr;
+  else unstage(ctx);
   hipEvent_t t0, t1;
-  hipEventCreate(&t0);
-  hipEventCreate(&t1);
-  hipEventRecord(t0, ctx->st);
-  if (stage_span(ctx, span, nbytes)) return -1;
+  if (pre) {
+    memset(out, 0, sizeof(*out));
+    if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+    t0 = ctx->staged_t0;
+    hipEventCreate(&t1);
+  } else {
+    if (rio_scan_span_end(ctx)) return -1;  // (a deferred batch of this ctx: complete before its buffers are reused)
+    memset(out, 0, sizeof(*out));
+    if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;
+    if (nbytes > ctx->max_span + kChunk) {
+      rio_set_error(&out->err, RIO_ERR_CAPACITY, file_off, "span of %" PRIu64 " bytes exceeds ctx capacity", nbytes);
+      out->stop = RIO_STOP_ERROR;
+      return 0;
+    }
+    if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+    hipEventCreate(&t0);
+    hipEventCreate(&t1);
+    hipEventRecord(t0, ctx->st);
+    if (stage_span(ctx, span, nbytes)) return -1;
+  }
   // (a chain's stages read their results on the host: never deferred)
   ctx->defer_collect = defer && !(codec & RIO_CODEC_CHAIN_FLAG);
   const int rc = run_span(ctx, ctx->d_span, span, nbytes, file_off, is_file_end, limit_off, codec, mode,
@@ -1036,6 +1060,21 @@ static int scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_
 int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
                        uint64_t limit_off, int32_t codec, int32_t mode, rio_results *res, rio_batch *out) {
   return scan_span(ctx, span, nbytes, file_off, is_file_end, limit_off, codec, mode, res, out, false);
+}
+
+int rio_scan_span_stage(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, int32_t codec) {
+  if (!ctx || !span) return -1;
+  unstage(ctx);
+  if (rio_scan_span_end(ctx)) return -1;
+  if ((codec & RIO_CODEC_CHAIN_FLAG) || nbytes > ctx->max_span + kChunk) return 0;  // (staged by the decode)
+  if (settle(ctx)) return -1;
+  if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+  hipEventCreate(&ctx->staged_t0);
+  hipEventRecord(ctx->staged_t0, ctx->st);
+  if (stage_span(ctx, span, nbytes)) return -1;
+  ctx->staged = span;
+  ctx->staged_n = nbytes;
+  return 0;
 }
 
 int rio_scan_span_begin(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
@@ -1083,6 +1122,7 @@ extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_
   if (!ctx) return -1;
   HIP_OK(hipSetDevice(ctx->device));
   if (rio_scan_span_end(ctx)) return -1;
+  unstage(ctx);
   if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;
   if (codec & RIO_CODEC_CHAIN_FLAG) {
     // a chain's stages run here, one after the other (each needs the previous

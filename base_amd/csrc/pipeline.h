@@ -20,6 +20,10 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
 // are final, its host arrays arrive by rio_scan_span_end (any later call on the
 // ctx waits for them first; total_ms is not set). Body mode; a chain codec runs
 // as rio_scan_span_mode.
+// the H2D copy of a span rio_scan_span_begin will decode next on this ctx,
+// enqueued now (a scanner's span ahead: its copy overlaps the decode of the
+// span before it); the same span pointer and size to begin skip the staging
+int rio_scan_span_stage(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, int32_t codec);
 int rio_scan_span_begin(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
                         int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_results *res, rio_batch *out);
 int rio_scan_span_end(rio_ctx *ctx);  // 0 (also when nothing is in flight) or -1 (rio_last_error)

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <future>
 #include <string>
 #include <thread>
 #include <vector>
@@ -241,6 +242,8 @@ struct rio_scanner {
     std::string msg;  // rio_last_error() of the beginning thread, when rc != 0
     rio_batch b{};
     std::thread th;
+    std::promise<void> begun;          // set when the thread is done (begun or not)
+    std::shared_future<void> begun_f;  // (the next span's thread waits for it before its decode)
   };
   std::deque<Ahead> aq;
   std::vector<std::pair<uint8_t *, uint64_t>> spare;  // staging buffers free for reuse
@@ -351,8 +354,13 @@ struct rio_scanner {
         return;
       }
       const uint64_t t = pend - at;
+      // the span ahead of this one: its decode first (the kernels of two spans
+      // sharing the GPU would delay the older span's result copies); this
+      // span's H2D copy is enqueued before that wait
+      std::shared_future<void> prev = first ? std::shared_future<void>() : aq.back().begun_f;
       aq.emplace_back();
       Ahead &e = aq.back();
+      e.begun_f = e.begun.get_future().share();
       e.slot = sl;
       e.at = at;
       e.n = n;
@@ -366,13 +374,18 @@ struct rio_scanner {
       const int is_end = at + n >= file_size ? 1 : 0;
       const uint64_t lim = limit;
       const int32_t cdc = codec;
-      e.th = std::thread([this, &e, c, r, need, pend, is_end, lim, cdc] {
+      e.th = std::thread([this, &e, c, r, need, pend, is_end, lim, cdc, prev] {
+        struct Signal {
+          std::promise<void> &p;
+          ~Signal() { p.set_value(); }
+        } signal{e.begun};
         if (need) {  // (an io error or a short read: the batch decodes when asked for, and reports it)
           int st;
           const uint64_t got = read_full(const_cast<uint8_t *>(e.base) + (pend - e.at), need, pend, &st);
           if (st != 0 || got != need) return;
         }
-        if (rio_ctx_reserve_span(c, e.n) != 0) return;
+        if (rio_ctx_reserve_span(c, e.n) != 0 || rio_scan_span_stage(c, e.base, e.n, cdc) != 0) return;
+        if (prev.valid()) prev.wait();
         e.rc = rio_scan_span_begin(c, e.base, e.n, e.at, is_end, lim, cdc, r, &e.b);
         if (e.rc != 0) e.msg = rio_last_error();
         e.ok = true;
