@@ -634,9 +634,10 @@ __global__ void k_resolve(DevBufs d, ResolveArgs a) {
       key = bev;
       kind = 3;
     }
-    unsigned long long tail;
-    if (a.is_file_end) tail = 2 * a.nchunks;
-    else tail = (c->first_incomplete != kNone) ? 2 * c->first_incomplete : 2 * a.nchunks;
+    // the span running out: after every chunk in it -- the reference reads an
+    // unfinished block's chunks one by one, so a chunk error inside the span
+    // (a total of 0, a block start where the block goes on) comes first
+    const unsigned long long tail = 2 * a.nchunks;
     if (tail < key) {
       key = tail;
       kind = 4;

@@ -261,6 +261,8 @@ struct rio_scanner {
   // a body span in host memory, decoded into the current slot (results deferred)
   int scan_body(const uint8_t *base, uint64_t n, uint64_t at, rio_batch *out) {
     const int is_end = (at + n >= file_size);
+    // (a sibling: as large as the ctx, which a block longer than the span grew)
+    if (cx[slot] != ctx && rio_ctx_reserve_span(cx[slot], n) != 0) return -1;
     if (v1) return rio_scan_v1_span_mode(cx[slot], base, n, at, is_end, rs[slot], out);
     return rio_scan_span_begin(cx[slot], base, n, at, is_end, limit, codec, rs[slot], out);
   }
