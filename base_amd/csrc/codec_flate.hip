@@ -899,11 +899,6 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
       int r = 0;
       if (sm == kVFinish) {
         r = (int)rl32(res, gl);
-#ifdef RIO_TOK_DEBUG
-        if (l == 0)
-          printf("tok fin blk %llu r %d nst %u olen %u bit %llu\n", (unsigned long long)rl64(cur_b, gl), r, s_nst, s_olen,
-                 (unsigned long long)s_bit);
-#endif
         FlState *sp = &d.fl[sb];
         uint32_t stm = kFlDone;
         if (r == kTokYield) {
@@ -1005,12 +1000,6 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           s_nst = 0;
           s_fixed = 0;
           in = make_in(span, d, nchunks, c0, total, n, s_reg != 0);
-#ifdef RIO_TOK_DEBUG
-          if (l == 0)
-            printf("tok r%d blk %llu c0 %llu total %llu n %llu reg %u tcap %u cap %u stm %u nchunks %llu tok_cap %llu\n", round,
-                   (unsigned long long)sb, (unsigned long long)c0, (unsigned long long)total, (unsigned long long)n, s_reg,
-                   s_tcap, s_cap, stm, (unsigned long long)nchunks, (unsigned long long)d.tok_cap);
-#endif
           if (n >= (1ull << 28) || c0 >= (1ull << 32)) {  // beyond the 32-bit stream state of this kernel
             r = kCodecUnsupported;
             sm = kVFinish;
