@@ -631,6 +631,13 @@ __device__ __forceinline__ int build_table(const uint8_t *lens, int n, TT *tab, 
           const TT e = (TT)tab_entry(kind, s, L);
           for (uint32_t f = rev; f < (1u << root); f += (1u << L)) tab[f] = e;
         } else {
+#ifdef RIO_CHECKED
+          if ((uint32_t)(fco >> 32) + rank[k] >= (root == kTokLitRoot ? 288u : 32u)) {
+            printf("build_table: sorted %u out of range (root %d, kind %d, n %d)\n", (uint32_t)(fco >> 32) + rank[k],
+                   root, kind, n);
+            continue;
+          }
+#endif
           sorted[(uint32_t)(fco >> 32) + rank[k]] = (TT)tab_entry(kind, s, 0);
           tab[rev & ((1u << root) - 1)] = (TT)kLongMark;
         }
@@ -661,6 +668,12 @@ __device__ __forceinline__ uint32_t slow_walk(const uint64_t *lfco, const TT *so
       len = L;
     }
   }
+#ifdef RIO_CHECKED
+  if (idx != 0xffffffffu && idx >= (kRoot == kTokLitRoot ? 288u : 32u)) {
+    printf("slow_walk: entry %u out of range (root %d, bits %08x)\n", idx, kRoot, bits);
+    return 0u;
+  }
+#endif
   return idx == 0xffffffffu ? 0u : ((uint32_t)sorted[idx] | len);
 }
 
@@ -1113,7 +1126,11 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
     // room for this pass's tokens decodes one literal or one match per step.
     // Anything else -- end of block, a corrupt or oversized symbol -- leaves
     // the state untouched and the stream to the full step below.
+#ifdef RIO_TOK_NOHOT
+    const bool hot0 = false;
+#else
     const bool hot0 = mode == kVHuff && tcap - nst - nv >= kPass + 3;
+#endif
     bool cold = !hot0;
     uint32_t hs = 0;  // hot steps taken: a pass decodes at most kPass symbols
     if (__ballot(hot0)) {
