@@ -1655,7 +1655,7 @@ __global__ void __launch_bounds__(64 * kW) k_flate_sync(const uint8_t *__restric
     if (d.tok_limit && d.tok_limit < tcap64) tcap64 = d.tok_limit < 64 ? 64 : d.tok_limit;
     const CompIn in = make_in(span, d, nchunks, c0, total, n, (meta & kMetaRegular) != 0);
     // outside this kernel's 32-bit bit positions: k_flate_tok
-    bool decline = n >= (1ull << 28) || c0 >= (1ull << 32);
+    bool decline = n >= (1ull << 28) || c0 >= (1ull << 32) || d.fl_tok_only;
     const uint32_t cap = cp > 0xfffff000ull ? 0xfffff000u : (uint32_t)cp;
     const uint32_t tcap = tcap64 > 0xffffff00ull ? 0xffffff00u : (uint32_t)tcap64;
     uint32_t *tok = d.tok + c0 * (uint64_t)kTokPerChunk;

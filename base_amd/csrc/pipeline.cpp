@@ -279,6 +279,7 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   // rounds); few Huffman-pass waves make every stream decode many blocks
   c->d.tok_limit = cfg ? cfg->flate_tok_limit : 0;
   c->d.fl_grid = cfg ? cfg->flate_grid : 0;
+  c->d.fl_tok_only = (cfg && (cfg->flags & RIO_CFG_FLATE_TOK_ONLY)) ? 1 : 0;
   c->item_end_mode = cfg && (cfg->flags & RIO_CFG_ITEM_END);
   c->flate_split = !(cfg && (cfg->flags & RIO_CFG_FLATE_NO_SPLIT));
   uint64_t span = (cfg && cfg->max_span_bytes) ? cfg->max_span_bytes : (256ull << 20);
@@ -572,7 +573,8 @@ static int ensure_side(rio_ctx *c, uint64_t need) {
 enum { kStageNoItems = 1, kStageNoCrc = 2 };
 
 static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t limit_chunk, int is_file_end,
-                   int tail_partial, int32_t codec, int32_t mode, bool sparse, int attempt, int stage_flags = 0) {
+                   int tail_partial, int32_t codec, int32_t mode, bool sparse, int attempt, int stage_flags = 0,
+                   bool may_sync = true) {
   if (sparse && codec == RIO_CODEC_NONE && ensure_side(c, nchunks * (uint64_t)kChunk)) return -1;
   DevBufs &d = c->d;
   hipStream_t st = c->st;
@@ -609,12 +611,14 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
     launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
     if (codec == RIO_CODEC_FLATE) {
       launch_inflate_huff(span, d, c->nblocks_dev, max_blocks, nchunks, c->dec_cap, c->fl_rounds, c->ncu, st);
-      if (d.seg_items && !c->split_probed && d.seg_cap == 0) {
+      if (d.seg_items && !c->split_probed && d.seg_cap == 0 && may_sync) {
         // a context's first flate run: the split copy pass needs scratch the
         // Huffman pass's output decides. Read what the plan asked for, size the
         // scratch and plan again (seg_used / seg_blocks reset), so the first
         // scan of a span of few large blocks splits too (later runs grow the
-        // scratch for the next call instead, without a mid-run sync)
+        // scratch for the next call instead, without a mid-run sync; the
+        // asynchronous entry points never sync here: their first flate run
+        // copies whole blocks and sizes the scratch for the next call)
         c->split_probed = true;
         HIP_OK(hipMemcpyAsync(&c->h_ctl->seg_used, &d.ctl->seg_used, sizeof(unsigned long long),
                               hipMemcpyDeviceToHost, st));
@@ -1151,7 +1155,7 @@ extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_
   ctx->last_span = (const uint8_t *)dev_span;
   ctx->last_nseg = 0;
   return enqueue(ctx, (const uint8_t *)dev_span, nchunks, UINT64_MAX, 1, (nbytes % kChunk) != 0, codec, kModeBody,
-                 true, 0);
+                 true, 0, 0, /*may_sync=*/false);
 }
 
 extern "C" int rio_scan_device_segments_async(rio_ctx *ctx, const void *dev_span, uint64_t nbytes,

@@ -6,6 +6,32 @@
 
 #include "rio_gpu.h"
 
+// RIO_SYNC_EACH (debug builds only): every launch is followed by a stream
+// synchronize that names the kernel on failure, so a fault is pinned to its
+// kernel even when several are queued.
+#ifdef RIO_SYNC_EACH
+#include <stdio.h>
+namespace rio {
+inline void dbg_sync(const char *name, hipStream_t st) {
+  const hipError_t e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    fprintf(stderr, "RIO_SYNC_EACH: %s failed: %s\n", name, hipGetErrorString(e));
+    fflush(stderr);
+  }
+}
+}  // namespace rio
+#undef hipLaunchKernelGGL
+#define hipLaunchKernelGGL(kernelName, ...)                     \
+  do {                                                          \
+    hipLaunchKernelGGLInternal((kernelName), __VA_ARGS__);      \
+    ::rio::dbg_sync(#kernelName, rio_sync_stream(__VA_ARGS__)); \
+  } while (0)
+template <class G, class B, class S, class... A>
+inline hipStream_t rio_sync_stream(G, B, S, hipStream_t st, A &&...) {
+  return st;
+}
+#endif
+
 namespace rio {
 
 constexpr int kChunk = RIO_CHUNK_SIZE;              // chunk.go:25
@@ -185,6 +211,7 @@ struct DevBufs {
   uint64_t tok_cap;              // u32 entries at tok
   uint64_t tok_limit;            // tokens per block and round (0: the whole region; rio_config.flate_tok_limit)
   uint64_t fl_grid;              // Huffman-pass workgroups (0: all resident; rio_config.flate_grid)
+  uint64_t fl_tok_only;          // RIO_CFG_FLATE_TOK_ONLY: k_flate_sync declines every block (tests)
   unsigned long long *fl_more;   // per round: blocks whose token region filled (kFlRounds)
   unsigned long long *fl_ck;     // per chunk: the Huffman pass's (ntok | olen << 32) at the block's input
                                  // chunk k (entry c0 + k; entry c0 = entries written) -- split points

@@ -244,6 +244,12 @@ struct rio_scanner {
     std::thread th;
     std::promise<void> begun;          // set when the thread is done (begun or not)
     std::shared_future<void> begun_f;  // (the next span's thread waits for it before its decode)
+    // set once the span's file bytes are in buf (or the read failed: read_ok
+    // false); the main thread waits for it before it reads the span's last
+    // chunk header and copies its tail into the next span ahead
+    std::promise<void> read;
+    std::shared_future<void> read_f;
+    bool read_ok = false;
   };
   std::deque<Ahead> aq;
   std::vector<std::pair<uint8_t *, uint64_t>> spare;  // staging buffers free for reuse
@@ -305,8 +311,20 @@ struct rio_scanner {
   // before it (copied here) and the file bytes after that span: the read-ahead's
   // when it holds them, else read by the span's own thread before its decode
   void begin_ahead() {
-    if (v1 || done || err_set) return;
+    if (v1 || done || err_set || depth == 0) return;
     const uint64_t maxspan = rio_ctx_max_span(ctx);
+    if (aq.empty()) {
+      // every slot's context opened now, while no span-ahead thread runs (a
+      // sibling is opened from the context before it, which such a thread
+      // would otherwise be using; rio_gpu.h: a scanner's spans ahead hold
+      // `depth` further contexts of the ctx's size until rio_close)
+      for (int i = 1; i <= depth; i++)
+        if (!cx[i]) {
+          cx[i] = rio_ctx_sibling(cx[i - 1]);
+          if (!cx[i]) return;
+          rs[i] = rio_ctx_take_results(ctx);
+        }
+    }
     while ((int)aq.size() < depth) {
       // the span before the new one: the last one ahead, or the current batch
       const bool first = aq.empty();
@@ -316,6 +334,10 @@ struct rio_scanner {
       if (!pdata || pend >= file_size) return;
       uint64_t at = off;
       if (!first) {
+        // the span before this one is still being read by its own thread: its
+        // last chunk header and its tail are only there once that read is done
+        aq.back().read_f.wait();
+        if (!aq.back().read_ok) return;
         const uint64_t c = predict_consumed(pdata, pn);
         if (c == 0) return;
         at = pat + c;
@@ -329,11 +351,7 @@ struct rio_scanner {
         for (const Ahead &e : aq) used = used || e.slot == i;
         if (!used) sl = i;
       }
-      if (!cx[sl]) {  // (slots open in order: slot 0 is the ctx, slot i the sibling of slot i - 1)
-        cx[sl] = rio_ctx_sibling(cx[sl - 1]);
-        if (!cx[sl]) return;
-        rs[sl] = rio_ctx_take_results(ctx);
-      }
+      if (sl < 0 || !cx[sl]) return;  // (opened above)
       // the staging: the read-ahead's buffer when it holds [pend, at + n), else a spare
       bool from_ra = false;
       if (ra_valid && ra_at == pend) {
@@ -363,6 +381,7 @@ struct rio_scanner {
       aq.emplace_back();
       Ahead &e = aq.back();
       e.begun_f = e.begun.get_future().share();
+      e.read_f = e.read.get_future().share();
       e.slot = sl;
       e.at = at;
       e.n = n;
@@ -379,13 +398,20 @@ struct rio_scanner {
       e.th = std::thread([this, &e, c, r, need, pend, is_end, lim, cdc, prev] {
         struct Signal {
           std::promise<void> &p;
-          ~Signal() { p.set_value(); }
-        } signal{e.begun};
+          bool on = true;
+          void set() {
+            if (on) p.set_value();
+            on = false;
+          }
+          ~Signal() { set(); }
+        } signal{e.begun}, read_signal{e.read};
         if (need) {  // (an io error or a short read: the batch decodes when asked for, and reports it)
           int st;
           const uint64_t got = read_full(const_cast<uint8_t *>(e.base) + (pend - e.at), need, pend, &st);
           if (st != 0 || got != need) return;
         }
+        e.read_ok = true;
+        read_signal.set();
         if (rio_ctx_reserve_span(c, e.n) != 0 || rio_scan_span_stage(c, e.base, e.n, cdc) != 0) return;
         if (prev.valid()) prev.wait();
         e.rc = rio_scan_span_begin(c, e.base, e.n, e.at, is_end, lim, cdc, r, &e.b);

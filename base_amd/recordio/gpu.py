@@ -53,6 +53,7 @@ class RioError(ctypes.Structure):
 
 RIO_CFG_ITEM_END = 1  # device results carry item_end (cumSize) + block_data / block_first_off
 RIO_CFG_FLATE_NO_SPLIT = 2  # never split a flate block's copy pass (tuning / tests)
+RIO_CFG_FLATE_TOK_ONLY = 4  # every flate block through the fallback Huffman pass, k_flate_tok (tests)
 
 
 class RioConfig(ctypes.Structure):
@@ -219,9 +220,10 @@ class Context:
 
     def __init__(self, device: int = 0, max_span_bytes: int = 0, max_out_bytes: int = 0, max_items: int = 0,
                  item_end: bool = False, flate_tok_limit: int = 0, flate_grid: int = 0,
-                 flate_split: bool = True):
+                 flate_split: bool = True, flate_tok_only: bool = False):
         self.L = load()
-        flags = (RIO_CFG_ITEM_END if item_end else 0) | (0 if flate_split else RIO_CFG_FLATE_NO_SPLIT)
+        flags = (RIO_CFG_ITEM_END if item_end else 0) | (0 if flate_split else RIO_CFG_FLATE_NO_SPLIT) | \
+            (RIO_CFG_FLATE_TOK_ONLY if flate_tok_only else 0)
         cfg = RioConfig(device, flags, max_span_bytes, max_out_bytes, max_items, flate_tok_limit, flate_grid)
         self.item_end = item_end
         self.h = self.L.rio_open(ctypes.byref(cfg))

@@ -122,6 +122,8 @@ typedef struct rio_error {
 #define RIO_CFG_FLATE_NO_SPLIT 2u  /* tuning / test: never split a flate block's copy pass into
                                      * segments (by default a span of few large blocks is split,
                                      * see DESIGN.md "split copy pass") */
+#define RIO_CFG_FLATE_TOK_ONLY 4u  /* test: the wave-per-block Huffman pass declines every flate
+                                     * block, so the fallback pass (k_flate_tok) decodes them all */
 
 typedef struct rio_config {
     int32_t device;             /* HIP device ordinal */

@@ -184,3 +184,46 @@ def test_scan_batch_views_and_location(oracle, trs):
         assert sc.Finish() is None and got == recs
     finally:
         ctx.close()
+
+
+class _SlowFile:
+    """A file object whose reads past the first span return late, so that the
+    threads of spans ahead are still reading when the scanner plans the next
+    span (scanner.cpp begin_ahead waits for the read of the span before it)."""
+
+    def __init__(self, data, delay):
+        import io
+        self._b = io.BytesIO(data)
+        self.delay = delay
+
+    def seek(self, off, whence=0):
+        return self._b.seek(off, whence)
+
+    def tell(self):
+        return self._b.tell()
+
+    def read(self, n=-1):
+        import time
+        if self._b.tell() > SPAN:
+            time.sleep(self.delay)
+        return self._b.read(n)
+
+
+@pytest.mark.parametrize("trs", [[], ["flate"]])
+def test_slow_reader_spans_ahead(oracle, trs):
+    """Spans ahead over a reader that is slow to return: every record as the
+    oracle's, twice on one ctx (the second scan's staging buffers are recycled
+    ones that still hold the first scan's chunks)."""
+    from base_amd.recordio import gpu
+    recs, data = _file(trs, 1500, 7)
+    ctx = gpu.Context(0, max_span_bytes=SPAN)
+    try:
+        for _ in range(2):
+            sc = gpu.NewScanner(_SlowFile(data, 0.01), ctx=ctx)
+            items = []
+            while sc.Scan():
+                items.append(sc.Get())
+            e = sc.Finish()
+            assert e is None and items == recs, trs
+    finally:
+        ctx.close()
