@@ -23,6 +23,31 @@
 
 namespace rio {
 
+// RIO_TOK_TRACE (debug builds only): every global access of the fallback
+// Huffman pass is logged, per lane, into host-coherent memory before it is
+// made (a 16-entry ring per lane: seq | site << 48, address), so that after a
+// memory fault the host can read each lane's last access.
+#ifdef RIO_TOK_TRACE
+#include <stdio.h>
+#include <string.h>
+__device__ unsigned long long *g_tok_trace;
+__device__ __forceinline__ void tok_trace(uint32_t site, const volatile void *p) {
+  unsigned long long *t = g_tok_trace;
+  if (!t) return;
+  const uint64_t slot = ((uint64_t)blockIdx.x * 64 + (threadIdx.x & 63)) * 34;
+  const unsigned long long seq =
+      __hip_atomic_load(&t[slot + 33], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1;
+  __hip_atomic_store(&t[slot + 33], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t e = slot + 2 * (seq & 15);
+  __hip_atomic_store(&t[e + 1], (unsigned long long)(uintptr_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&t[e], seq | ((unsigned long long)site << 48), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_s_waitcnt(0);
+}
+#define RIO_TT(site, p) tok_trace((site), (p))
+#else
+#define RIO_TT(site, p) ((void)0)
+#endif
+
 constexpr int kLitBits = 10;     // root table bits: literal/length
 constexpr int kDistBits = 8;     // root table bits: distance (and code-length codes)
 constexpr int kMaxBits = 15;
@@ -128,10 +153,12 @@ struct CompIn {
       uint64_t a = c0, b = c0 + total;
       while (b - a > 1) {
         const uint64_t m = (a + b) >> 1;
+        RIO_TT(11, &ck_pay[m]);
         if (ck_pay[m] - pay0 <= p) a = m;
         else b = m;
       }
       c = a;
+      RIO_TT(12, &ck_pay[a]);
       lo = ck_pay[a] - pay0;
     }
     return c * kChunk + kChunkHdr + (p - lo);
@@ -145,6 +172,7 @@ struct CompIn {
       return 0u;
     }
 #endif
+    RIO_TT(10, &span[q]);
     return span[q];
   }
 };
@@ -691,6 +719,7 @@ __device__ __forceinline__ uint32_t fetch_dword(const CompIn &in, uint64_t p) {
       return 0u;
     }
 #endif
+    RIO_TT(13, &reinterpret_cast<const uint32_t *>(in.span)[w]);
     v = reinterpret_cast<const uint32_t *>(in.span)[w];
   } else {
     v = in.byte(p) | (in.byte(p + 1) << 8) | (in.byte(p + 2) << 16) | (in.byte(p + 3) << 24);
@@ -854,6 +883,7 @@ __device__ __forceinline__ CompIn make_in(const uint8_t *span, const DevBufs &d,
   in.c0 = c0;
   in.total = total;
   in.n = n;
+  RIO_TT(14, &d.ck_pay[c0]);
   in.pay0 = d.ck_pay[c0];
   in.regular = regular;
   return in;
@@ -868,6 +898,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
   const uint32_t g = (uint32_t)l / kVG, j = (uint32_t)l % kVG;
   StreamLds &M = S[g];
   if (round > 0 && uni64(d.fl_more[round - 1]) == 0) return;
+  RIO_TT(1, nblocks);
   const uint64_t nblk = uni64(*nblocks);
   const uint64_t stride = (uint64_t)gridDim.x * kVS;
 
@@ -913,6 +944,8 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
       if (sm == kVFinish) {
         r = (int)rl32(res, gl);
         FlState *sp = &d.fl[sb];
+        RIO_TT(20, sp);
+        RIO_TT(21, &d.blk_out_len[sb]);
         uint32_t stm = kFlDone;
         if (r == kTokYield) {
           stm = s_left ? kFlStored : (s_fixed ? kFlFixed : kFlDynamic);
@@ -952,7 +985,6 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
         sm = kVNew;
         r = 0;
       }
-      CompIn in;
       if (sm == kVNew) {
         for (;;) {
           if (s_next >= nblk) {
@@ -962,6 +994,9 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           sb = s_next;
           s_next += stride;
           FlState *sp = &d.fl[sb];
+          RIO_TT(22, sp);
+          RIO_TT(23, &d.blk_c0[sb]);
+          RIO_TT(24, &d.blk_dec_off[sb]);
           const uint64_t c0 = uni64(d.blk_c0[sb]);
           const unsigned long long meta = uni64(d.blk_meta[sb]);
           uint32_t stm;
@@ -1012,7 +1047,6 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           s_cap = cp > 0xfffff000ull ? 0xfffff000u : (uint32_t)cp;
           s_nst = 0;
           s_fixed = 0;
-          in = make_in(span, d, nchunks, c0, total, n, s_reg != 0);
           if (n >= (1ull << 28) || c0 >= (1ull << 32)) {  // beyond the 32-bit stream state of this kernel
             r = kCodecUnsupported;
             sm = kVFinish;
@@ -1020,7 +1054,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           }
           if (stm == kFlDynamic) {
             TokDec t;
-            t.in = in;
+            t.in = make_in(span, d, nchunks, c0, total, n, s_reg != 0);
             t.T = &G;
             t.W = &W;
             t.seek(s_hdr);
@@ -1037,9 +1071,13 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
           seek = sm != kVHeader;
           break;
         }
-      } else {
-        in = make_in(span, d, nchunks, s_c0, s_tot, s_n, s_reg != 0);
       }
+      // The stream's input view, made from its block fields, which are defined
+      // on every path (round 4's fault: a CompIn assigned only on some paths
+      // through the loop above was merged by the compiler with an undefined
+      // value, and a block header read of an irregular block -- the only reads
+      // that take the chunk-payload map from it -- used that as the map's base)
+      const CompIn in = make_in(span, d, nchunks, s_c0, s_tot, s_n, s_reg != 0);
       // DEFLATE block headers until a block with content (or the end)
       while (sm == kVHeader) {
         TokDec t;
@@ -1319,6 +1357,7 @@ __global__ void __launch_bounds__(64) k_flate_tok(const uint8_t *__restrict__ sp
       }
 #endif
       uint32_t *tk = d.tok + (uint64_t)bc0 * kTokPerChunk + nst;
+      if (nv) RIO_TT(30, tk + nv - 1);
       for (uint32_t k = j; k < nv; k += kVG) tk[k] = M.tbuf[k];
       nst += nv;
       nv = 0;
@@ -2510,11 +2549,46 @@ void launch_inflate_copy(const uint8_t *span, const DevBufs &d, const unsigned l
   if (g3 > (uint64_t)ncu * kL2Waves) g3 = (uint64_t)ncu * kL2Waves;
   if (g3 < 1) g3 = 1;
   const bool split = d.seg_items > 0;
+#ifdef RIO_TOK_TRACE
+  static unsigned long long *h_trace = nullptr;
+  const size_t trace_words = (size_t)g1 * 64 * 34;
+  if (!h_trace) {
+    (void)hipHostMalloc((void **)&h_trace, (size_t)(r1 > g1 ? r1 : g1) * 64 * 34 * 8, hipHostMallocCoherent);
+    if (h_trace) memset(h_trace, 0, (size_t)(r1 > g1 ? r1 : g1) * 64 * 34 * 8);
+  }
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tok_trace), &h_trace, sizeof(h_trace), 0, hipMemcpyHostToDevice, st);
+#endif
   for (int r = 0; r < rounds; r++) {
     hipLaunchKernelGGL(k_flate_tok, dim3((unsigned)g1), dim3(64), 0, st, span, d, nblocks, nchunks,
                        dec_cap, r, (int)(r == rounds - 1));
+#ifdef RIO_TOK_TRACE
+    if (hipStreamSynchronize(st) != hipSuccess && h_trace) {
+      fprintf(stderr, "RIO_TOK_TRACE: k_flate_tok round %d failed; span %p..+%llu tok %p..+%llu fl %p ck_pay %p\n", r,
+              (const void *)span, (unsigned long long)(nchunks * kChunk), (void *)d.tok,
+              (unsigned long long)(d.tok_cap * 4), (void *)d.fl, (void *)d.ck_pay);
+      for (size_t w = 0; w < trace_words / (64 * 34); w++)
+        for (int ln = 0; ln < 64; ln++) {
+          const unsigned long long *t = h_trace + (w * 64 + ln) * 34;
+          const unsigned long long n = t[33];
+          if (n <= 1) continue;
+          fprintf(stderr, "wave %zu lane %d: %llu accesses; last:", w, ln, n);
+          for (unsigned long long q = n > 6 ? n - 6 : 1; q <= n; q++) {
+            const unsigned long long *e = t + 2 * (q & 15);
+            fprintf(stderr, " [%llu site %llu %p]", e[0] & 0xffffffffffffull, e[0] >> 48, (void *)e[1]);
+          }
+          fprintf(stderr, "\n");
+        }
+      fflush(stderr);
+    }
+#endif
     hipLaunchKernelGGL(k_flate_lz2, dim3((unsigned)g3), dim3(64), 0, st, d, nblocks, r);
   }
+#ifdef RIO_TOK_TRACE
+  {
+    unsigned long long *z = nullptr;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tok_trace), &z, sizeof(z), 0, hipMemcpyHostToDevice, st);
+  }
+#endif
   if (split) {
     uint64_t gs = max_blocks * kSegMax;
     if (gs > (uint64_t)ncu * kL2Waves) gs = (uint64_t)ncu * kL2Waves;
