@@ -119,6 +119,13 @@ struct rio_ctx {
   int device = 0;
   int ncu = 256;
   hipStream_t st = nullptr;
+  // host <-> device copies of host spans and host results run on a stream of
+  // their own with no kernel ever queued on it (RIO_COPY_STREAM): on the
+  // kernels' stream the runtime ran most large copies as blit kernels on the
+  // compute queue, which slowed the next span's kernels several-fold while a
+  // copy ran (end-to-end). Events hand the order over.
+  hipStream_t cst = nullptr;
+  hipEvent_t ev_k = nullptr, ev_c = nullptr;  // kernels' stream -> copy stream, copy stream -> kernels' stream
   hipEvent_t ev[kNumEv] = {};
   bool last_had_dec = false;
   int ev_parse0 = kEvParse0, ev_crc0 = kEvCrc0;  // the events the last run's parse / CRC stages start at
@@ -219,6 +226,10 @@ const char *rio_last_error(void) { return g_last_error.c_str(); }
 int rio_abi_version(void) { return RIO_ABI_VERSION; }
 void *rio_stream(rio_ctx *ctx) { return ctx ? (void *)ctx->st : nullptr; }
 uint64_t rio_ctx_max_span(rio_ctx *c) { return c->max_span; }
+int rio_ctx_spans_ahead(rio_ctx *c) {
+  const uint32_t v = ((uint32_t)c->cfg.flags >> 8) & 3u;
+  return v ? (int)v - 1 : 2;
+}
 
 template <class T>
 static int dalloc(T **p, uint64_t n) {
@@ -226,6 +237,25 @@ static int dalloc(T **p, uint64_t n) {
   *p = nullptr;
   if (n == 0) n = 1;
   HIP_OK(hipMalloc((void **)p, n * sizeof(T)));
+  return 0;
+}
+
+#ifndef RIO_COPY_STREAM
+#define RIO_COPY_STREAM 1
+#endif
+// the stream large host <-> device copies go on: the copy stream, after
+// everything queued on the kernels' stream so far (copy_begin), and the
+// kernels' stream then waits for the copies (copy_end)
+static hipStream_t copy_begin(rio_ctx *c) {
+  if (!RIO_COPY_STREAM) return c->st;
+  if (hipEventRecord(c->ev_k, c->st) != hipSuccess || hipStreamWaitEvent(c->cst, c->ev_k, 0) != hipSuccess)
+    return c->st;
+  return c->cst;
+}
+static int copy_end(rio_ctx *c, hipStream_t cs) {
+  if (cs == c->st) return 0;
+  HIP_OK(hipEventRecord(c->ev_c, cs));
+  HIP_OK(hipStreamWaitEvent(c->st, c->ev_c, 0));
   return 0;
 }
 
@@ -265,6 +295,9 @@ static void free_all(rio_ctx *c) {
   for (hipEvent_t e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->st) hipStreamDestroy(c->st);
+  if (c->cst) hipStreamDestroy(c->cst);
+  if (c->ev_k) hipEventDestroy(c->ev_k);
+  if (c->ev_c) hipEventDestroy(c->ev_c);
 }
 
 static int ctx_init(rio_ctx *c, const rio_config *cfg) {
@@ -291,6 +324,9 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   c->item_cap = (cfg && cfg->max_items) ? cfg->max_items : span / 64 + 1024;
   c->dec_cap = 0;
   HIP_OK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+  HIP_OK(hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
+  HIP_OK(hipEventCreateWithFlags(&c->ev_k, hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&c->ev_c, hipEventDisableTiming));
   for (hipEvent_t &e : c->ev) HIP_OK(hipEventCreate(&e));
   if (alloc_bufs(c)) return -1;
   DevBufs &d = c->d;
@@ -734,13 +770,15 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
   }
   unsigned long long *h_off = r.items, *h_len = r.items + r.items_cap;
   unsigned long long *first = r.blk, *foff = r.blk + nb + 1;
-  if (k.rec_bytes) HIP_OK(hipMemcpyAsync(r.records, d_records, k.rec_bytes, hipMemcpyDeviceToHost, c->st));
+  const hipStream_t cs = copy_begin(c);
+  if (k.rec_bytes) HIP_OK(hipMemcpyAsync(r.records, d_records, k.rec_bytes, hipMemcpyDeviceToHost, cs));
   if (k.n_items) {
-    HIP_OK(hipMemcpyAsync(h_off, c->d.item_off, k.n_items * 8, hipMemcpyDeviceToHost, c->st));
-    HIP_OK(hipMemcpyAsync(h_len, c->d.item_len, k.n_items * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_OK(hipMemcpyAsync(h_off, c->d.item_off, k.n_items * 8, hipMemcpyDeviceToHost, cs));
+    HIP_OK(hipMemcpyAsync(h_len, c->d.item_len, k.n_items * 8, hipMemcpyDeviceToHost, cs));
   }
-  HIP_OK(hipMemcpyAsync(first, c->d.blk_item_base, (nb + 1) * 8, hipMemcpyDeviceToHost, c->st));
-  if (nb) HIP_OK(hipMemcpyAsync(foff, c->d.blk_c0, nb * 8, hipMemcpyDeviceToHost, c->st));
+  HIP_OK(hipMemcpyAsync(first, c->d.blk_item_base, (nb + 1) * 8, hipMemcpyDeviceToHost, cs));
+  if (nb) HIP_OK(hipMemcpyAsync(foff, c->d.blk_c0, nb * 8, hipMemcpyDeviceToHost, cs));
+  if (copy_end(c, cs)) return -1;  // (the kernels' stream, and its events, follow the copies)
   const uint64_t d2h = k.rec_bytes + 16 * k.n_items + 8 * (2 * nb + 1);
   if (c->defer_collect) {  // rio_scan_span_end waits and converts the block offsets
     c->pend = true;
@@ -988,7 +1026,9 @@ extern "C" int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbyt
 
 static int stage_span(rio_ctx *c, const uint8_t *span, uint64_t nbytes) {
   if (!c->d_span) HIP_OK(hipMalloc((void **)&c->d_span, c->max_span + kChunk));
-  HIP_OK(hipMemcpyAsync(c->d_span, span, nbytes, hipMemcpyHostToDevice, c->st));
+  const hipStream_t cs = copy_begin(c);
+  HIP_OK(hipMemcpyAsync(c->d_span, span, nbytes, hipMemcpyHostToDevice, cs));
+  if (copy_end(c, cs)) return -1;
   c->stats.h2d_bytes += nbytes;
   return 0;
 }

@@ -34,6 +34,8 @@ rio_ctx *rio_ctx_sibling(rio_ctx *c);
 int rio_scan_v1_span_mode(rio_ctx *c, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
                           rio_results *res, rio_batch *out);
 uint64_t rio_ctx_max_span(rio_ctx *c);
+// spans a scanner decodes ahead (RIO_CFG_SPANS_AHEAD in rio_config.flags; default 2)
+int rio_ctx_spans_ahead(rio_ctx *c);
 // grow the ctx's span capacity (and the buffers sized by it) to at least
 // `bytes`; 0 on success (a no-op when it is already that large)
 int rio_ctx_reserve_span(rio_ctx *c, uint64_t bytes);

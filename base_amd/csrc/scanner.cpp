@@ -222,12 +222,7 @@ struct rio_scanner {
   // rotate: the current batch's span (its views point there), one per span
   // ahead, and the read-ahead's, with spares from batches consumed.
   static constexpr int kSlots = 3;
-  int depth = spans_ahead();  // spans ahead (RIO_SPANS_AHEAD: 0 .. kSlots - 1, default kSlots - 1)
-  static int spans_ahead() {
-    const char *e = getenv("RIO_SPANS_AHEAD");
-    const int v = e ? atoi(e) : kSlots - 1;
-    return v < 0 ? 0 : (v > kSlots - 1 ? kSlots - 1 : v);
-  }
+  int depth = 0;  // spans ahead (the ctx's RIO_CFG_SPANS_AHEAD: 0 .. kSlots - 1, default kSlots - 1)
   rio_ctx *cx[kSlots] = {};
   rio_results *rs[kSlots] = {};
   int slot = 0;
@@ -881,6 +876,8 @@ int rio_codec_for_transformers(const char *const *values, int n, int32_t *codec,
 rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int limit, int nshard) {
   rio_scanner *s = new rio_scanner();
   s->ctx = ctx;
+  s->depth = ctx ? rio_ctx_spans_ahead(ctx) : 0;
+  if (s->depth > rio_scanner::kSlots - 1) s->depth = rio_scanner::kSlots - 1;
   s->res = ctx ? rio_ctx_take_results(ctx) : rio_results_new();
   s->cx[0] = ctx;
   s->rs[0] = s->res;

@@ -56,6 +56,11 @@ RIO_CFG_FLATE_NO_SPLIT = 2  # never split a flate block's copy pass (tuning / te
 RIO_CFG_FLATE_TOK_ONLY = 4  # every flate block through the fallback Huffman pass, k_flate_tok (tests)
 
 
+def RIO_CFG_SPANS_AHEAD(n: int) -> int:
+    """Scanners over the ctx decode up to n (0-2) spans ahead (default 2)."""
+    return ((n & 3) + 1) << 8
+
+
 class RioConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_int32), ("max_span_bytes", ctypes.c_uint64),
                 ("max_out_bytes", ctypes.c_uint64), ("max_items", ctypes.c_uint64),
@@ -220,10 +225,11 @@ class Context:
 
     def __init__(self, device: int = 0, max_span_bytes: int = 0, max_out_bytes: int = 0, max_items: int = 0,
                  item_end: bool = False, flate_tok_limit: int = 0, flate_grid: int = 0,
-                 flate_split: bool = True, flate_tok_only: bool = False):
+                 flate_split: bool = True, flate_tok_only: bool = False, spans_ahead: Optional[int] = None):
         self.L = load()
         flags = (RIO_CFG_ITEM_END if item_end else 0) | (0 if flate_split else RIO_CFG_FLATE_NO_SPLIT) | \
-            (RIO_CFG_FLATE_TOK_ONLY if flate_tok_only else 0)
+            (RIO_CFG_FLATE_TOK_ONLY if flate_tok_only else 0) | \
+            (0 if spans_ahead is None else RIO_CFG_SPANS_AHEAD(spans_ahead))
         cfg = RioConfig(device, flags, max_span_bytes, max_out_bytes, max_items, flate_tok_limit, flate_grid)
         self.item_end = item_end
         self.h = self.L.rio_open(ctypes.byref(cfg))

@@ -574,9 +574,22 @@ def main():
     in_bytes = span_len * world
     value = in_bytes * args.steps / dt / 2 ** 30
 
+    # k_crc alone: with two contexts its launches share the GPU with the other
+    # context's parse, so its launch time is not its own. A few steps on one
+    # context, each synchronous (after the timed region), time it alone -- the
+    # roofline's kernel_ms -- and give the one-context step beside the timed one.
+    one_crc, one_ms = [], []
+    for i in range(max(3, min(args.steps, 10))):
+        t1 = time.perf_counter()
+        launch(0)
+        ctxs[0].sync()
+        one_ms.append((time.perf_counter() - t1) * 1e3)
+        one_crc.append(ctxs[0].stage_times()[2])
+    one_step = float(np.median(one_ms))
     # roofline of the dominant kernel (k_crc): it reads every chunk byte once
     # (B_in per launch; DESIGN.md "Roofline")
-    crc_avg = float(np.mean(crc_ms))
+    crc_two = float(np.mean(crc_ms))
+    crc_avg = float(np.mean(one_crc)) if nctx > 1 else crc_two
     alg = span_len
     achieved = alg / (crc_avg * 1e-3) / 1e9
     # whole pipeline (SURVEY.md §8(d) B_alg): chunk bytes in + item_end (8 B per
@@ -586,6 +599,8 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("k_crc", args.replicas),
             "kernel": "k_crc", "kernel_ms": round(crc_avg, 3),
+            "kernel_ms_source": "HIP events around k_crc on its stream, one context, steps synchronous",
+            "kernel_ms_two_contexts": round(crc_two, 3),
             "alg_bytes_per_launch": alg,
             # per-step latency, first kernel's start to the last's end (with two
             # contexts, two steps are in flight: the latency spans both)
@@ -608,6 +623,10 @@ def main():
                       "bytes_in_per_gpu": span_len},
            "roofline": roof,
            "contexts": nctx,
+           # the same step on one context, each step synchronous (host sync and
+           # enqueue included): the serial rate beside the pipelined one
+           "one_context": {"ms_per_step": round(one_step, 3),
+                           "value": round(in_bytes / world / (one_step * 1e-3) / 2 ** 30, 2)},
            "parity": {"ok": ok, "checked": "every record of every replica of the last timed step vs the "
                                            "generator (on the GPU)", "items_checked": chk["items_checked"],
                       "bytes_checked": chk["bytes_checked"], "output": "item_end (RIO_CFG_ITEM_END)"},

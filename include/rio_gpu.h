@@ -122,6 +122,9 @@ typedef struct rio_error {
 #define RIO_CFG_FLATE_NO_SPLIT 2u  /* tuning / test: never split a flate block's copy pass into
                                      * segments (by default a span of few large blocks is split,
                                      * see DESIGN.md "split copy pass") */
+/* scanners over this ctx decode up to n (0-2) spans ahead of the batch handed
+ * out (bits 8-9 hold n + 1; 0 = the default, 2) */
+#define RIO_CFG_SPANS_AHEAD(n) ((((uint32_t)(n) & 3u) + 1u) << 8)
 #define RIO_CFG_FLATE_TOK_ONLY 4u  /* test: the wave-per-block Huffman pass declines every flate
                                      * block, so the fallback pass (k_flate_tok) decodes them all */
 
@@ -381,7 +384,15 @@ typedef struct rio_scanner rio_scanner;
 
 /* NewScanner / NewShardScanner (scannerv2.go:200-235). The reader is used
  * until rio_scanner_finish. Never returns NULL for valid ctx/reader; errors
- * are reported through rio_scanner_err like errorScanner. */
+ * are reported through rio_scanner_err like errorScanner.
+ * Memory: the scanner decodes up to RIO_CFG_SPANS_AHEAD(n) (n 0-2, default 2)
+ * spans ahead of the batch it hands out, each on a further context of the ctx (its
+ * "siblings", opened with the ctx's configuration and span size on the first
+ * scan that needs them). They stay open, and keep their device and pinned
+ * buffers, until rio_close(ctx): with the default depth a scanner's ctx holds
+ * about three times the device memory of one context. Open the ctx with
+ * RIO_CFG_SPANS_AHEAD(0) where that matters, e.g. many ctxs of very large
+ * spans per GPU. */
 rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int limit, int nshard);
 /* Scan (scannerv2.go:390-404): 1 if a new record is available */
 int rio_scanner_scan(rio_scanner *s);

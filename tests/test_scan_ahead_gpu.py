@@ -89,23 +89,22 @@ def test_corrupt_later_span_matches_oracle(oracle, trs):
 
 @pytest.mark.parametrize("depth", [0, 1, 2])
 @pytest.mark.parametrize("trs", [[], ["flate"], ["zstd"]])
-def test_wrong_span_prediction_matches_oracle(oracle, trs, depth, monkeypatch):
+def test_wrong_span_prediction_matches_oracle(oracle, trs, depth):
     """The second span ahead starts where the host reads the span before it will
     stop (its last chunk header): a chunk header whose index or total was
     rewritten (CRC fixed, so only the block structure is wrong) makes that
     prediction wrong, or the GPU's extent differ from it. The spans begun on it
     are dropped: the same records and error as the oracle's, at every depth of
-    spans ahead (RIO_SPANS_AHEAD). A rewritten total or index also makes blocks
+    spans ahead (RIO_CFG_SPANS_AHEAD). A rewritten total or index also makes blocks
     overlap (a block start inside another block's chunks): the decode of the
     overlapping block must stay inside its own regions (kernels.hip k_chunk_apply)."""
     from base_amd.recordio import gpu
     if "zstd" in trs and not oracle_has_zstd(oracle):
         pytest.skip("zstd oracle not built")
-    monkeypatch.setenv("RIO_SPANS_AHEAD", str(depth))
     recs, data = _file(trs, 2500, 6)
     nck = len(data) // 32768
     rng = random.Random(7)
-    ctx = gpu.Context(0, max_span_bytes=SPAN)
+    ctx = gpu.Context(0, max_span_bytes=SPAN, spans_ahead=depth)
     try:
         for trial in range(12):
             b = bytearray(data)
