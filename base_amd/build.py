@@ -28,7 +28,7 @@ ARCH = "gfx950"
 
 SOURCES = ["kernels.hip", "blocks.hip", "crc.hip", "codec.hip", "codec_flate.hip", "codec_zstd.hip", "legacy.hip",
            "encode.hip", "deflate_enc.hip", "zstd_enc.hip", "pipeline.cpp", "messages.cpp", "scanner.cpp",
-           "crc_tables.cpp"]
+           "crc_tables.cpp", "sdma.cpp"]
 # RIO_EXTRA_FLAGS: -D switches of ablation builds (tools/ablate.py); the product
 # build has none, and any flag changes the build id
 FLAGS = os.environ.get("RIO_EXTRA_FLAGS", "").split() + [
@@ -142,7 +142,8 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
         subprocess.check_call([HIPCC, "-O2", "-fPIC", "-c", id_src, "-o", id_obj])
     objs = [_obj(s) for s in srcs] + [id_obj]
     if _stale(LIB, objs) or lib_build_id(LIB) != bid:
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB + ".tmp"] + objs
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB + ".tmp"] + objs + [
+            "-L/opt/rocm/lib", "-lhsa-runtime64", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)

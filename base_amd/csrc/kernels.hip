@@ -68,10 +68,12 @@ __global__ void __launch_bounds__(kScanThreads) k_scan_reduce(F f, const unsigne
   if (threadIdx.x == 0) partial[blockIdx.x] = tot;
 }
 
-// (kScanThreads, not 1024: a 16-wave workgroup does not fit on a CU beside
-// k_crc's 12 waves, so the next step's scans waited for the end of the other
-// context's CRC pass; 4 waves do fit, DESIGN.md "Room beside k_crc")
-__global__ void __launch_bounds__(kScanThreads) k_scan_partials(const unsigned long long *n_dev, uint64_t n_host,
+// (1024 threads: a 16-wave workgroup does not fit on a CU beside k_crc's 12
+// waves, so with two contexts the next step's parse waits for the CRC pass's
+// tail. Round 5 measured 4-wave workgroups, which let the whole parse run beside
+// k_crc: 3.05 -> 3.37 ms per C2 step -- the two passes' concurrent HBM streams
+// lose more than the overlap gains)
+__global__ void __launch_bounds__(1024) k_scan_partials(const unsigned long long *n_dev, uint64_t n_host,
                                                         unsigned long long *partial,
                                                         unsigned long long *total_out,
                                                         unsigned long long *total_at /* out[n] */) {
@@ -158,7 +160,7 @@ struct U64Load {
 //   k_chunk_tiles    the headers (each thread's 8 and the one before them:
 //                    chunk_meta checks against the predecessor), the per-chunk
 //                    fields, the tile's sums of payload sizes and block starts;
-//   k_chunk_partials the two columns of tile sums scanned (one 4-wave workgroup);
+//   k_chunk_partials the two columns of tile sums scanned (one workgroup);
 //   k_chunk_apply    ck_pay, ck_block and the block descriptors (FlagOut).
 __global__ void __launch_bounds__(kScanThreads) k_chunk_tiles(const uint8_t *__restrict__ span, uint64_t nchunks,
                                                               DevBufs d, unsigned long long *psize,
@@ -204,7 +206,7 @@ __global__ void __launch_bounds__(kScanThreads) k_chunk_tiles(const uint8_t *__r
   }
 }
 
-__global__ void __launch_bounds__(kScanThreads) k_chunk_partials(uint64_t nchunks, unsigned long long *psize,
+__global__ void __launch_bounds__(1024) k_chunk_partials(uint64_t nchunks, unsigned long long *psize,
                                                          unsigned long long *pflag, unsigned long long *pay_total,
                                                          unsigned long long *nblocks) {
   __shared__ unsigned long long lds[17];
@@ -322,7 +324,7 @@ void launch_chunk_pass(const uint8_t *span, uint64_t nchunks, const DevBufs &d, 
   const unsigned g = (unsigned)(tiles ? tiles : 1);
   unsigned long long *psize = d.scan_tmp, *pflag = d.scan_tmp + g;
   hipLaunchKernelGGL(k_chunk_tiles, dim3(g), dim3(kScanThreads), 0, st, span, nchunks, d, psize, pflag);
-  hipLaunchKernelGGL(k_chunk_partials, dim3(1), dim3(kScanThreads), 0, st, nchunks, psize, pflag, d.ck_pay + nchunks,
+  hipLaunchKernelGGL(k_chunk_partials, dim3(1), dim3(1024), 0, st, nchunks, psize, pflag, d.ck_pay + nchunks,
                      nblocks_dev);
   hipLaunchKernelGGL(k_chunk_apply, dim3(g), dim3(kScanThreads), 0, st, span, nchunks, d, codec, psize, pflag);
 }
@@ -334,7 +336,7 @@ static void scan(F f, O o, const unsigned long long *n_dev, uint64_t n_host, uin
   const unsigned tiles = (unsigned)((n_max + kScanTile - 1) / kScanTile);
   const unsigned g = tiles ? tiles : 1;
   hipLaunchKernelGGL(k_scan_reduce<F>, dim3(g), dim3(kScanThreads), 0, st, f, n_dev, n_host, partial);
-  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, st, n_dev, n_host, partial, total_out, total_at);
+  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, st, n_dev, n_host, partial, total_out, total_at);
   hipLaunchKernelGGL((k_scan_apply<F, O>), dim3(g), dim3(kScanThreads), 0, st, f, o, n_dev, n_host, partial);
 }
 

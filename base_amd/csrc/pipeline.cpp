@@ -26,6 +26,7 @@
 #include "legacy.h"
 #include "pipeline.h"
 #include "rio_internal.h"
+#include "sdma.h"
 
 namespace rio {
 // kernels.hip
@@ -119,13 +120,11 @@ struct rio_ctx {
   int device = 0;
   int ncu = 256;
   hipStream_t st = nullptr;
-  // host <-> device copies of host spans and host results run on a stream of
-  // their own with no kernel ever queued on it (RIO_COPY_STREAM): on the
-  // kernels' stream the runtime ran most large copies as blit kernels on the
-  // compute queue, which slowed the next span's kernels several-fold while a
-  // copy ran (end-to-end). Events hand the order over.
-  hipStream_t cst = nullptr;
-  hipEvent_t ev_k = nullptr, ev_c = nullptr;  // kernels' stream -> copy stream, copy stream -> kernels' stream
+  // SDMA engines for the copies of host spans (in) and host results (out),
+  // sdma.cpp; null when the runtime offers none (hipMemcpyAsync then). The
+  // flags: copies of that direction issued and not yet waited for.
+  Sdma *sd = nullptr;
+  bool sd_in = false, sd_out = false;
   hipEvent_t ev[kNumEv] = {};
   bool last_had_dec = false;
   int ev_parse0 = kEvParse0, ev_crc0 = kEvCrc0;  // the events the last run's parse / CRC stages start at
@@ -240,22 +239,42 @@ static int dalloc(T **p, uint64_t n) {
   return 0;
 }
 
-#ifndef RIO_COPY_STREAM
-#define RIO_COPY_STREAM 1
+// A host <-> device copy of n bytes on the ctx's SDMA engine for that
+// direction, else (no engine, pageable host memory) hipMemcpyAsync on the
+// kernels' stream. SDMA copies are ordered on the host: an outgoing copy is
+// issued once the kernels that wrote its bytes have completed (collect runs
+// after the control block's sync), and sdma_settle waits for them before
+// anything reuses the buffers; an incoming one completes before the kernels
+// that read it are enqueued (run_span).
+#ifndef RIO_SDMA
+#define RIO_SDMA 3  // directions on SDMA (measurement builds): 1 device -> host, 2 host -> device
 #endif
-// the stream large host <-> device copies go on: the copy stream, after
-// everything queued on the kernels' stream so far (copy_begin), and the
-// kernels' stream then waits for the copies (copy_end)
-static hipStream_t copy_begin(rio_ctx *c) {
-  if (!RIO_COPY_STREAM) return c->st;
-  if (hipEventRecord(c->ev_k, c->st) != hipSuccess || hipStreamWaitEvent(c->cst, c->ev_k, 0) != hipSuccess)
-    return c->st;
-  return c->cst;
+static int copy_to_host(rio_ctx *c, void *dst, const void *src, uint64_t n) {
+  if (n == 0) return 0;
+  if ((RIO_SDMA & 1) && c->sd && sdma_copy(c->sd, dst, src, n, kSdmaOut) == 0) {
+    c->sd_out = true;
+    return 0;
+  }
+  HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->st));
+  return 0;
 }
-static int copy_end(rio_ctx *c, hipStream_t cs) {
-  if (cs == c->st) return 0;
-  HIP_OK(hipEventRecord(c->ev_c, cs));
-  HIP_OK(hipStreamWaitEvent(c->st, c->ev_c, 0));
+static int copy_to_device(rio_ctx *c, void *dst, const void *src, uint64_t n) {
+  if (n == 0) return 0;
+  if ((RIO_SDMA & 2) && c->sd && sdma_copy(c->sd, dst, src, n, kSdmaIn) == 0) {
+    c->sd_in = true;
+    return 0;
+  }
+  HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->st));
+  return 0;
+}
+static int sdma_settle(rio_ctx *c, int dir) {
+  bool &f = dir == kSdmaOut ? c->sd_out : c->sd_in;
+  if (!f) return 0;
+  f = false;
+  if (sdma_wait(c->sd, dir) != 0) {
+    set_last_error("an SDMA copy did not complete");
+    return -1;
+  }
   return 0;
 }
 
@@ -280,6 +299,8 @@ static int alloc_bufs(rio_ctx *c) {
 }
 
 static void free_all(rio_ctx *c) {
+  sdma_close(c->sd);  // (waits for copies in flight)
+  c->sd = nullptr;
   DevBufs &d = c->d;
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
                 d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.blk_data, d.blk_file_off, d.blk_seg, d.cmp, d.item_off, d.item_len, d.side,
@@ -295,9 +316,6 @@ static void free_all(rio_ctx *c) {
   for (hipEvent_t e : c->ev)
     if (e) hipEventDestroy(e);
   if (c->st) hipStreamDestroy(c->st);
-  if (c->cst) hipStreamDestroy(c->cst);
-  if (c->ev_k) hipEventDestroy(c->ev_k);
-  if (c->ev_c) hipEventDestroy(c->ev_c);
 }
 
 static int ctx_init(rio_ctx *c, const rio_config *cfg) {
@@ -324,13 +342,11 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   c->item_cap = (cfg && cfg->max_items) ? cfg->max_items : span / 64 + 1024;
   c->dec_cap = 0;
   HIP_OK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-  HIP_OK(hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking));
-  HIP_OK(hipEventCreateWithFlags(&c->ev_k, hipEventDisableTiming));
-  HIP_OK(hipEventCreateWithFlags(&c->ev_c, hipEventDisableTiming));
   for (hipEvent_t &e : c->ev) HIP_OK(hipEventCreate(&e));
   if (alloc_bufs(c)) return -1;
   DevBufs &d = c->d;
   if (dalloc(&d.ctl, 1) || dalloc(&c->nblocks_dev, 2) || dalloc(&d.fl_more, 64)) return -1;
+  c->sd = sdma_open(d.ctl);  // (null: no SDMA engine; copies go through hipMemcpyAsync)
   // CRC tables
   std::vector<uint32_t> fold(kFoldWords), mul(kMulTables * 1024), fa(kMaxPayload + 1), fb(kMaxPayload + 1);
   build_crc_tables(fold.data(), mul.data(), fa.data(), fb.data());
@@ -770,15 +786,11 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
   }
   unsigned long long *h_off = r.items, *h_len = r.items + r.items_cap;
   unsigned long long *first = r.blk, *foff = r.blk + nb + 1;
-  const hipStream_t cs = copy_begin(c);
-  if (k.rec_bytes) HIP_OK(hipMemcpyAsync(r.records, d_records, k.rec_bytes, hipMemcpyDeviceToHost, cs));
-  if (k.n_items) {
-    HIP_OK(hipMemcpyAsync(h_off, c->d.item_off, k.n_items * 8, hipMemcpyDeviceToHost, cs));
-    HIP_OK(hipMemcpyAsync(h_len, c->d.item_len, k.n_items * 8, hipMemcpyDeviceToHost, cs));
-  }
-  HIP_OK(hipMemcpyAsync(first, c->d.blk_item_base, (nb + 1) * 8, hipMemcpyDeviceToHost, cs));
-  if (nb) HIP_OK(hipMemcpyAsync(foff, c->d.blk_c0, nb * 8, hipMemcpyDeviceToHost, cs));
-  if (copy_end(c, cs)) return -1;  // (the kernels' stream, and its events, follow the copies)
+  // (the kernels that wrote these bytes have completed: the control block's sync)
+  if (copy_to_host(c, r.records, d_records, k.rec_bytes) || copy_to_host(c, h_off, c->d.item_off, k.n_items * 8) ||
+      copy_to_host(c, h_len, c->d.item_len, k.n_items * 8) ||
+      copy_to_host(c, first, c->d.blk_item_base, (nb + 1) * 8) || copy_to_host(c, foff, c->d.blk_c0, nb * 8))
+    return -1;
   const uint64_t d2h = k.rec_bytes + 16 * k.n_items + 8 * (2 * nb + 1);
   if (c->defer_collect) {  // rio_scan_span_end waits and converts the block offsets
     c->pend = true;
@@ -788,6 +800,7 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
     c->pend_d2h = d2h;
   } else {
     HIP_OK(hipStreamSynchronize(c->st));
+    if (sdma_settle(c, kSdmaOut)) return -1;
     c->stats.d2h_bytes += d2h;
     for (uint64_t b = 0; b < nb; b++) foff[b] = file_off + foff[b] * kChunk;
   }
@@ -860,6 +873,7 @@ static int run_chain(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_spa
 static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span, uint64_t nbytes,
                     uint64_t file_off, int32_t is_file_end, uint64_t limit_off, int32_t codec, int32_t mode,
                     rio_results *res, rio_batch *out, int stage_flags = 0) {
+  if (sdma_settle(c, kSdmaIn)) return -1;  // a host span's SDMA copy in, before the kernels that read it
   if (codec & RIO_CODEC_CHAIN_FLAG)
     return run_chain(c, dspan, report_span, nbytes, file_off, is_file_end, limit_off, codec, mode, res, out);
   const bool to_host = res != nullptr;
@@ -1026,9 +1040,9 @@ extern "C" int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbyt
 
 static int stage_span(rio_ctx *c, const uint8_t *span, uint64_t nbytes) {
   if (!c->d_span) HIP_OK(hipMalloc((void **)&c->d_span, c->max_span + kChunk));
-  const hipStream_t cs = copy_begin(c);
-  HIP_OK(hipMemcpyAsync(c->d_span, span, nbytes, hipMemcpyHostToDevice, cs));
-  if (copy_end(c, cs)) return -1;
+  // (the ctx's earlier kernels, which read d_span, have completed: a span's
+  // batch is finished, rio_scan_span_end, before the next one is staged)
+  if (copy_to_device(c, c->d_span, span, nbytes)) return -1;
   c->stats.h2d_bytes += nbytes;
   return 0;
 }
@@ -1130,7 +1144,8 @@ int rio_scan_span_end(rio_ctx *ctx) {
   if (!ctx || !ctx->pend) return 0;
   ctx->pend = false;
   HIP_OK(hipSetDevice(ctx->device));
-  const hipError_t e = hipEventSynchronize(ctx->pend_t1);
+  hipError_t e = hipEventSynchronize(ctx->pend_t1);
+  if (e == hipSuccess && sdma_settle(ctx, kSdmaOut)) e = hipErrorUnknown;  // the results' SDMA copies
   float ms = 0;
   hipEventElapsedTime(&ms, ctx->pend_t0, ctx->pend_t1);
   hipEventDestroy(ctx->pend_t0);
