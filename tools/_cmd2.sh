@@ -1,8 +1,11 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-for v in 3 1 2; do
-  if [ $v = 3 ]; then L=base_amd/lib/librio_gpu.so; F=""; else L=exp_lib/sdma$v/librio_gpu.so; F="$(cat exp_lib/sdma$v.flags)"; fi
-  RIO_GPU_LIB=$L RIO_EXTRA_FLAGS="$F" timeout -k 10 400 python3 tools/bench_e2e.py > gpurun_out/e2e_sdmab$v.log 2>&1 || exit $?
-  echo "RIO_SDMA=$v"; tail -1 gpurun_out/e2e_sdmab$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); [print(' ', w['workload'], w['GiBs'], w['wall_ms'], w['parity']) for w in d['workloads']]"
+c2() {  # c2 <name> <lib> <flags>
+  RIO_GPU_LIB=$2 RIO_EXTRA_FLAGS="$3" timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-flate16k --no-zstd --no-c5 --no-e2e > gpurun_out/c2_$1.log 2>&1 || exit $?
+  grep "^{" gpurun_out/c2_$1.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$1', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['kernel_ms_two_contexts'], d['one_context'], d['parity']['ok'])"
+}
+for i in 1 2; do
+  c2 first$i base_amd/lib/librio_gpu.so ""
+  c2 last$i exp_lib/crclast/librio_gpu.so "$(cat exp_lib/crclast.flags)"
 done
