@@ -57,8 +57,12 @@ namespace rio {
 constexpr int kCrcWaves = RIO_CRC_WAVES;  // waves per workgroup (one workgroup per CU: 92 KiB LDS at 16 copies)
 
 constexpr int kRows = 4;   // rows per pipeline stage (4 KiB per wave)
-constexpr int kBufs = 4;   // register buffers: kBufs - 1 stages in flight during a fold
+#ifndef RIO_CRC_BUFS
+#define RIO_CRC_BUFS 4
+#endif
+constexpr int kBufs = RIO_CRC_BUFS;  // register buffers: kBufs - 1 stages in flight during a fold
 constexpr int kStages = 32 / kRows;
+static_assert(kStages % kBufs == 0, "a chunk's stages must cycle through the buffers evenly");
 
 // fold stage q (rows kRows*q ..) of a chunk whose covered bytes end at `end`
 __device__ __forceinline__ void fold_stage(const uint4 (&u)[kRows], uint32_t (&s)[4], const char *__restrict__ tab,
