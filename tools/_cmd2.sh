@@ -1,11 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-c2() {  # c2 <name> <lib> <flags>
-  RIO_GPU_LIB=$2 RIO_EXTRA_FLAGS="$3" timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-flate --no-flate16k --no-zstd --no-c5 --no-e2e > gpurun_out/c2_$1.log 2>&1 || exit $?
-  grep "^{" gpurun_out/c2_$1.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$1', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['kernel_ms_two_contexts'], d['one_context']['ms_per_step'], d['parity']['ok'])"
-}
-for i in 1 2; do
-  c2 base$i base_amd/lib/librio_gpu.so ""
-  for v in w8b4 w10b4 w16b2 w12b2; do c2 ${v}_$i exp_lib/$v/librio_gpu.so "$(cat exp_lib/$v.flags)"; done
-done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_scan_ahead_gpu.py tests/test_gpu_parity.py tests/test_structural_fuzz_gpu.py tests/test_gather_gpu.py tests/test_legacy.py -m gpu -v > gpurun_out/scan_tests.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -3 gpurun_out/scan_tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python3 tools/bench_e2e.py > gpurun_out/e2e_ramp.log 2>&1 || exit $?
+tail -1 gpurun_out/e2e_ramp.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); [print(' ', w['workload'], w['GiBs'], w['wall_ms'], w['spans'], w['parity']) for w in d['workloads']]"
