@@ -75,7 +75,7 @@ def make_c1_file():
     return make_c2_file(16385)
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r04_c2_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r05_c2_pmc.json")
 
 
 def pmc_traffic(kernel: str, replicas: int):
