@@ -9,9 +9,8 @@
 // streaming kernel beside it 10.04 -> 10.10 ms, the copy 52 GB/s). DESIGN.md §5
 // (end-to-end).
 //
-// Each context has an engine per direction and a completion signal per
-// direction whose value counts the copies in flight (+1 when one is issued,
-// -1 by the engine when it completes). The callers order copies against the
+// Each context has an engine per direction and, per direction, completion
+// signals for the copies in flight (one per copy). The callers order copies against the
 // kernels on the host: a copy is issued only once the kernels it depends on
 // have completed, and the kernels that depend on a copy are enqueued only after
 // sdma_wait. Memory the HSA runtime does not know (pageable host memory) is not
@@ -27,9 +26,14 @@
 
 namespace rio {
 
+// a completion signal per copy in flight (one shared signal counting several
+// copies is valid HSA, but tools that wrap completion signals -- rocprofv3's
+// memory-copy trace -- expect a signal per copy, value 1)
+constexpr int kSdmaSlots = 16;
 struct Sdma {
   hsa_agent_t gpu{}, cpu{};
-  hsa_signal_t sig[2]{};
+  hsa_signal_t sig[2][kSdmaSlots]{};
+  int used[2]{};  // signals of copies issued and not yet waited for
   hsa_amd_sdma_engine_id_t eng[2]{};
   bool hsa_up = false;
 };
@@ -98,12 +102,9 @@ Sdma *sdma_open(const void *dev_ptr) {
     s->eng[kSdmaIn] = (hsa_amd_sdma_engine_id_t)kth_bit(p_in, k);
   }
   if (ok) {
-    ok = hsa_signal_create(0, 0, nullptr, &s->sig[0]) == HSA_STATUS_SUCCESS;
-    if (ok && hsa_signal_create(0, 0, nullptr, &s->sig[1]) != HSA_STATUS_SUCCESS) {
-      hsa_signal_destroy(s->sig[0]);
-      s->sig[0].handle = 0;
-      ok = false;
-    }
+    for (int d = 0; d < 2 && ok; d++)
+      for (int i = 0; i < kSdmaSlots && ok; i++)
+        ok = hsa_signal_create(0, 0, nullptr, &s->sig[d][i]) == HSA_STATUS_SUCCESS;
   }
   if (!ok) {
     sdma_close(s);
@@ -114,11 +115,11 @@ Sdma *sdma_open(const void *dev_ptr) {
 
 void sdma_close(Sdma *s) {
   if (!s) return;
-  for (int d = 0; d < 2; d++)
-    if (s->sig[d].handle) {
-      sdma_wait(s, d);
-      hsa_signal_destroy(s->sig[d]);
-    }
+  for (int d = 0; d < 2; d++) {
+    sdma_wait(s, d);
+    for (int i = 0; i < kSdmaSlots; i++)
+      if (s->sig[d][i].handle) hsa_signal_destroy(s->sig[d][i]);
+  }
   if (s->hsa_up) hsa_shut_down();
   delete s;
 }
@@ -134,13 +135,16 @@ int sdma_copy(Sdma *s, void *dst, const void *src, uint64_t n, int dir) {
   if (!s) return -1;
   if (n == 0) return 0;
   if (!sdma_known(dir == kSdmaOut ? dst : src)) return -1;  // pageable host memory
+  if (s->used[dir] == kSdmaSlots && sdma_wait(s, dir) != 0) return -1;  // (all slots in flight: drain)
   const hsa_agent_t da = dir == kSdmaOut ? s->cpu : s->gpu, sa = dir == kSdmaOut ? s->gpu : s->cpu;
-  hsa_signal_add_relaxed(s->sig[dir], 1);
-  if (hsa_amd_memory_async_copy_on_engine(dst, da, src, sa, n, 0, nullptr, s->sig[dir], s->eng[dir], true) !=
+  const hsa_signal_t sg = s->sig[dir][s->used[dir]];
+  hsa_signal_store_relaxed(sg, 1);
+  if (hsa_amd_memory_async_copy_on_engine(dst, da, src, sa, n, 0, nullptr, sg, s->eng[dir], true) !=
       HSA_STATUS_SUCCESS) {
-    hsa_signal_subtract_relaxed(s->sig[dir], 1);
+    hsa_signal_store_relaxed(sg, 0);
     return -1;
   }
+  s->used[dir]++;
   return 0;
 }
 
@@ -149,8 +153,11 @@ int sdma_copy(Sdma *s, void *dst, const void *src, uint64_t n, int dir) {
 int sdma_wait(Sdma *s, int dir) {
   if (!s) return 0;
   const auto t0 = std::chrono::steady_clock::now();
-  while (hsa_signal_wait_scacquire(s->sig[dir], HSA_SIGNAL_CONDITION_EQ, 0, 1000000000ull, HSA_WAIT_STATE_BLOCKED) != 0)
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return -1;
+  for (int i = 0; i < s->used[dir]; i++)
+    while (hsa_signal_wait_scacquire(s->sig[dir][i], HSA_SIGNAL_CONDITION_EQ, 0, 1000000000ull,
+                                     HSA_WAIT_STATE_BLOCKED) != 0)
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return -1;
+  s->used[dir] = 0;
   return 0;
 }
 
