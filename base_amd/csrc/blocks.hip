@@ -250,20 +250,42 @@ struct LeanArgs {
 constexpr int kLeanHdrLanes = 32;  // header window lanes loaded (16 B each)
 constexpr int kLeanBndLanes = 16;  // boundary window lanes loaded either side of the chunk boundary
 
+// The uvarint of the n <= 4 bytes in x (its last byte the terminator): bytes
+// past n masked off first, then the 7-bit groups packed
+__device__ __forceinline__ uint32_t uvarint4m(uint32_t x, uint32_t n) {
+  x &= 0xffffffffu >> (32u - 8u * n);
+  return (x & 0x7fu) | ((x >> 1) & 0x3f80u) | ((x >> 2) & 0x1fc000u) | ((x >> 3) & 0xfe00000u);
+}
+
+// k_lean_end (round 5). Lane l owns items 4l .. 4l+3, whose size varints are
+// consecutive header bytes: it finds where they start from the terminator of
+// rank 4l, decodes them from the window, and one wave scan of the lanes' sums
+// places them (the round-4 kernel -- lane l owning items l, l+64, ... with four
+// scans and an LDS position per terminator -- issued 19 % more VALU
+// instructions at the same time per launch).
+// What bounds it (C2, `profiles/r05_lean_end.json`): HBM traffic, not issue --
+// 0.36 GB read and 0.60 GB written per launch (0.51 GB of it the 8-byte item
+// ends); without the item stores (a measurement-only build) 0.21 ms instead of
+// 0.30, and neither 8 waves per SIMD, nor two blocks in flight per wave, nor
+// store instructions that never make the loop wait (buffer stores with
+// out-of-range offsets for idle lanes, 0.37 ms) shortened it.
 __global__ void __launch_bounds__(256) k_lean_end(LeanArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_win[4][1040];
-  __shared__ __attribute__((aligned(16))) uint16_t s_tpos[4][264];
+  __shared__ uint32_t s_tm[4][64];  // lane l's terminator mask: window bytes 16 l .. 16 l + 15
+  __shared__ uint16_t s_p4[4][64];  // byte of the terminator of rank 4 j (rank 0: the item count's)
+  uint32_t *ltm = s_tm[threadIdx.x >> 6];
+  uint16_t *lp4 = s_p4[threadIdx.x >> 6];
   uint8_t *lwin = s_win[threadIdx.x >> 6];
-  uint16_t *ltpos = s_tpos[threadIdx.x >> 6];
   const uint64_t nb = *a.nblocks;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const int l = lane_id();
-  // lane j < 4 holds descriptor field j of a block. Software-pipelined (round
-  // 4): while block b is parsed, block b + nwaves's windows and block
-  // b + 2 nwaves's descriptor are in flight, so a block's loads are waited for
-  // one block later (gfx9 vmcnt counts in order)
+  if (wave >= nb) return;
+  // lane j < 4 holds descriptor field j of a block. Software-pipelined: while
+  // block b is parsed, block b + nwaves's windows and block b + 2 nwaves's
+  // descriptor are in flight
   const unsigned long long *dsrc = l == 0 ? a.blk_c0 : l == 1 ? a.blk_meta : l == 2 ? a.blk_len : a.blk_item_base;
+  auto dload = [&](uint64_t x) -> unsigned long long { return dsrc[x < nb ? x : nb - 1]; };  // (x >= nb: unused)
   auto lean_ok = [&](unsigned long long dsc) {
     const uint64_t c0 = readlane_u64(dsc, 0);
     const unsigned long long meta = readlane_u64(dsc, 1), len = readlane_u64(dsc, 2);
@@ -271,134 +293,149 @@ __global__ void __launch_bounds__(256) k_lean_end(LeanArgs a) {
     return (meta & kMetaComplete) && (meta & kMetaRegular) && cls == kMagicPacked && c0 < a.limit_chunk &&
            len < (1ull << 32);
   };
-  // the header window's first 512 B and 256 B either side of the chunk
-  // boundary (a C2 block's 508-byte header and 256-byte straddler); a longer
-  // header or a straddler outside goes to k_parse (was: both 1 KiB windows
-  // whole, 2 KiB fetched per 65 KiB block)
-  auto fetch = [&](unsigned long long dsc, bool ok, uint32_t (&w)[4], uint32_t (&bnd)[4]) {
-    w[0] = w[1] = w[2] = w[3] = 0x80808080u;
-    bnd[0] = bnd[1] = bnd[2] = bnd[3] = 0;
+  // the header window's first 512 B (lanes 0-31) and 256 B either side of the
+  // chunk boundary (lanes 16-47: a C2 block's 508-byte header and 256-byte
+  // straddler); a longer header or a straddler outside goes to k_parse
+  auto hdr_in = [&](unsigned long long dsc, bool ok) {  // this lane's header piece lies in the payload
+    const unsigned long long len = readlane_u64(dsc, 2);
+    const uint32_t size0 = len < (uint64_t)kMaxPayload ? (uint32_t)len : (uint32_t)kMaxPayload;
+    return ok && l < kLeanHdrLanes && 16u * (uint32_t)l + 16u <= size0;
+  };
+  auto fetch = [&](unsigned long long dsc, bool ok, uint4 &w, uint4 &bnd) {
+    w = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+    bnd = make_uint4(0, 0, 0, 0);
     if (!ok) return;
     const uint64_t c0 = readlane_u64(dsc, 0);
-    const unsigned long long meta = readlane_u64(dsc, 1), len = readlane_u64(dsc, 2);
-    const uint8_t *ck = a.span + c0 * kChunk;
-    const uint32_t size0 = len < (uint64_t)kMaxPayload ? (uint32_t)len : (uint32_t)kMaxPayload;
-    if (l < kLeanHdrLanes && 16u * l + 16 <= size0) {  // 4-byte aligned: 28 + 16 l
-      const uint4 v = *reinterpret_cast<const uint4 *>(ck + kChunkHdr + 16 * l);
-      w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
-    }
-    if ((meta & kMetaTotalMask) >= 2 && l >= 32 - kLeanBndLanes && l < 32 + kLeanBndLanes) {
+    const unsigned long long meta = readlane_u64(dsc, 1);
+    const uint8_t *ck = a.span + c0 * kChunk + kChunkHdr;
+    if (hdr_in(dsc, ok)) w = *reinterpret_cast<const uint4 *>(ck + 16 * l);  // 4-byte aligned: 28 + 16 l
+    if ((meta & kMetaTotalMask) >= 2 && l >= 32 - kLeanBndLanes && l < 32 + kLeanBndLanes)
       // payload kBndW0 + 16 l: chunk c0's tail, then c0 + 1's head
-      const uint8_t *src = (l < 32) ? ck + kChunkHdr + kBndW0 + 16 * l : ck + kChunk + kChunkHdr + 16 * (l - 32);
-      const uint4 v = *reinterpret_cast<const uint4 *>(src);
-      bnd[0] = v.x, bnd[1] = v.y, bnd[2] = v.z, bnd[3] = v.w;
-    }
+      bnd = *reinterpret_cast<const uint4 *>(l < 32 ? ck + kBndW0 + 16 * l : ck + kChunk + 16 * (l - 32));
   };
-  unsigned long long desc = (l < 4 && wave < nb) ? dsrc[wave] : 0;
-  bool ok_nx = wave < nb && lean_ok(desc);
-  uint32_t w_nx[4], bnd_nx[4];
-  fetch(desc, ok_nx, w_nx, bnd_nx);
-  unsigned long long desc_nx = (l < 4 && wave + nwaves < nb) ? dsrc[wave + nwaves] : 0;
-  for (uint64_t b = wave; b < nb; b += nwaves) {
+  // one block: parse it from its windows (w, bnd) and write its results
+  auto parse_one = [&](uint64_t b, unsigned long long desc, bool ok, const uint4 &wl, const uint4 &bnd4) {
     const uint64_t c0 = readlane_u64(desc, 0);
-    const unsigned long long meta = readlane_u64(desc, 1), len = readlane_u64(desc, 2);
+    const unsigned long long len = readlane_u64(desc, 2);
     const uint64_t base = readlane_u64(desc, 3);
-    const bool ok = ok_nx;
-    uint32_t w[4], bnd[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) w[k] = w_nx[k], bnd[k] = bnd_nx[k];
-    // the next block's windows and the one after's descriptor, in flight while this one is parsed
-    const uint64_t bn = b + nwaves;
-    ok_nx = bn < nb && lean_ok(desc_nx);
-    fetch(desc_nx, ok_nx, w_nx, bnd_nx);
-    desc = desc_nx;
-    desc_nx = (l < 4 && bn + nwaves < nb) ? dsrc[bn + nwaves] : 0;
+    const uint32_t w[4] = {wl.x, wl.y, wl.z, wl.w}, bnd[4] = {bnd4.x, bnd4.y, bnd4.z, bnd4.w};
     bool done = false;
-    uint32_t hdr = 0;
+    uint32_t hdr = 0, nitems = 0, g = 4u * (uint32_t)l, S = 0, E = 0;
+    unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0, sm = 0;
     if (ok) {
       const uint32_t tmask = term4(w[0]) | (term4(w[1]) << 4) | (term4(w[2]) << 8) | (term4(w[3]) << 12);
       const uint32_t cnt = __popc(tmask);
       const uint32_t incl = wave_incl_sum_dpp(cnt);
       const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       *reinterpret_cast<uint4 *>(lwin + 16 * l) = make_uint4(w[0], w[1], w[2], w[3]);
-      {  // terminator positions of ordinals 0..263 (a header of <= 256 sizes ends by then)
-        uint32_t m = (incl - cnt < 264u) ? tmask : 0u, o = incl - cnt;
-        while (m && o < 264u) {
-          const uint32_t i = __ffs(m) - 1;
-          m &= m - 1;
-          ltpos[o++] = (uint16_t)(16 * l + i);
+      ltm[l] = tmask;
+      // the item count: one or two bytes, the window's first terminator
+      const uint32_t tm0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)tmask);
+      const uint32_t w00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[0]);
+      nitems = (tm0 & 3u) ? uvarint4m(w00, (tm0 & 1u) ? 1u : 2u) : ~0u;
+      const bool hdr_ok = nitems <= 256 && nitems < total;  // every size's terminator inside the window
+      if (hdr_ok) {
+        // positions of the terminators of ranks 0, 4, 8, ... below nitems
+        uint32_t r = incl - cnt, m = tmask;
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+          if (r & 3u) m &= m - 1, r++;
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
+          const bool put = m != 0 && r < nitems;
+          if (!__ballot(put)) break;
+          if (put) lp4[r >> 2] = (uint16_t)(16u * l + (uint32_t)(__ffs(m) - 1));
+          m &= m - 1, m &= m - 1, m &= m - 1, m &= m - 1;
+          r += 4;
         }
       }
       wave_lds_sync();
-      const uint32_t p0 = ltpos[0];
-      const uint32_t nitems = (total > 0 && p0 < 2) ? uvarint4(lds_bytes4(lwin, 0), p0 + 1) : ~0u;
-      if (nitems <= 256 && nitems < total) {
-        hdr = (uint32_t)ltpos[nitems] + 1;
+      if (hdr_ok) {
+        const bool act = g < nitems;
+        const uint32_t s = act ? (uint32_t)lp4[l] + 1u : 0u;  // its size varint's first byte
+        const uint32_t tw = ((ltm[s >> 4] | (ltm[(s >> 4) + 1] << 16)) >> (s & 15u));  // terminators from byte s
+        uint32_t v[4], e[4];
+        bool lng = false;
+        uint32_t mm = tw, prev = ~0u, vor = 0;  // prev: the last byte of the previous varint (s-relative)
+        // (branch-free: a lane past the last item reads in-window bytes and drops them)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          e[i] = (uint32_t)(__ffs(mm) - 1);  // ~0u when none
+          mm &= mm - 1;
+          const uint32_t n = e[i] - prev;
+          const bool valid = g + i < nitems;
+          lng |= valid && n - 1u > 3u;  // a varint longer than 4 bytes (or no terminator)
+          const uint32_t x = lds_bytes4(lwin, s + prev + 1u);
+          const uint32_t c = (x & 0x7fu) | ((x >> 1) & 0x3f80u) | ((x >> 2) & 0x1fc000u) | ((x >> 3) & 0xfe00000u);
+          v[i] = valid ? c & ((1u << (7u * min(n, 4u))) - 1u) : 0u;  // (n > 4 is declined above)
+          vor |= v[i];
+          prev = e[i];
+        }
+        // sizes below 2^24: the u32 sums below cannot wrap (4 x 64 of them)
+        const uint32_t z0 = v[0], z1 = z0 + v[1], z2 = z1 + v[2], z3 = z2 + v[3];
+        const uint32_t inc = wave_incl_sum_dpp(z3);
+        const uint32_t ex = inc - z3, sum = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        // the header's end: the terminator of rank nitems (the last item's varint)
+        if (nitems > 0) {
+          const uint32_t j = (nitems - 1) & 3u;
+          const uint32_t ej = j == 0 ? e[0] : j == 1 ? e[1] : j == 2 ? e[2] : e[3];
+          hdr = (uint32_t)__builtin_amdgcn_readlane((int)(s + ej), (int)((nitems - 1) >> 2)) + 1u;
+        } else {
+          hdr = (uint32_t)(__ffs(tm0) - 1) + 1u;
+        }
         const uint32_t plen = (uint32_t)len;
-        uint32_t v[4], st[4];
-        bool lng = false, bad = false;
+        const bool bad = lng || vor >= (1u << 24);
+        if (!__ballot(bad) && (uint64_t)hdr + sum == (uint64_t)plen) {
+          // chunk crossings (items are payload bytes [hdr + ex + z(i-1), hdr + ex + zi)): only a
+          // straddler across the first chunk boundary, inside the loaded part of the
+          // boundary window, is taken (written from the registers); any other is declined
+          constexpr uint32_t M = (uint32_t)kMaxPayload;
+          constexpr uint32_t W0 = M - 16 * kLeanBndLanes, W1 = W0 + 32 * kLeanBndLanes;
+          const uint32_t L0 = hdr + ex;
+          const bool cross = z3 > 0 && L0 / M != (L0 + z3 - 1) / M;
+          bool far = false, sd = false;
+          uint32_t Sl = 0, El = 0;
+          if (cross) {
+            uint32_t st = L0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          v[k] = 0;
-          const uint32_t o = 64u * k + (uint32_t)l + 1;
-          if (o <= nitems) {
-            const uint32_t e = ltpos[o], n = e - ltpos[o - 1];  // varint o: bytes e-n+1 .. e
-            if (n > 4) lng = true;
-            else v[k] = uvarint4(lds_bytes4(lwin, e + 1 - n), n);
-            bad |= v[k] > plen;
-          }
-        }
-        // item starts: u32 scans (steps below 2^28: a scan's first wrap leaves incl < v)
-        uint32_t carry = hdr;
-        bool wrap = false;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const uint32_t inc = wave_incl_sum_dpp(v[k]);
-          wrap |= inc < v[k];
-          st[k] = carry + inc - v[k];
-          const uint32_t add = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-          wrap |= carry + add < carry;
-          carry += add;
-        }
-        // straddlers: only across the first chunk boundary, inside the loaded
-        // part of the boundary window (written from the registers); any other
-        // crossing is declined
-        constexpr uint32_t W0 = (uint32_t)kMaxPayload - 16 * kLeanBndLanes, W1 = W0 + 32 * kLeanBndLanes;
-        bool far = false, sd[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const uint32_t s_ = st[k], e_ = st[k] + v[k];
-          sd[k] = v[k] > 0 && s_ < (uint32_t)kMaxPayload && e_ > (uint32_t)kMaxPayload;
-          far |= v[k] > 0 && s_ / (uint32_t)kMaxPayload != (e_ - 1) / (uint32_t)kMaxPayload &&
-                 !(sd[k] && s_ >= W0 && e_ <= W1);
-        }
-        if (!__ballot(lng || bad || wrap || far) && carry == plen) {
-          done = true;
-          const uint64_t cap = a.item_cap;
-#pragma unroll
-          for (int k = 0; k < 4; k++) {  // cumSize (scannerv2.go:83-91): the item's end past the header
-            const uint32_t o = 64u * k + (uint32_t)l + 1;
-            const uint64_t slot = base + (o - 1);
-            if (o <= nitems && slot < cap) view_store(a.item_end + slot, (unsigned long long)(st[k] + v[k] - hdr));
-          }
-          if (base + nitems > cap && l == 0) atomicOr(&a.ctl->out_overflow, 1ull);
-          unsigned long long sm = __ballot(sd[0]) | __ballot(sd[1]) | __ballot(sd[2]) | __ballot(sd[3]);
-          if (sm) {  // the straddler at the boundary, from the registers
-            const int L = __ffsll((long long)sm) - 1;
-            uint32_t S = 0, V = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-              const bool has = (__ballot(sd[k]) >> L) & 1ull;
-              if (has) {
-                S = (uint32_t)__builtin_amdgcn_readlane((int)st[k], L);
-                V = (uint32_t)__builtin_amdgcn_readlane((int)v[k], L);
+            for (int i = 0; i < 4; i++) {
+              const uint32_t en = st + v[i];
+              if (v[i] > 0 && st / M != (en - 1) / M) {
+                const bool here = st < M && en > M && st >= W0 && en <= W1;
+                far |= !here;
+                if (here) sd = true, Sl = st, El = en;
               }
+              st = en;
             }
-            straddler_from_regs(bnd, a.side, S, V, c0 * (unsigned long long)kChunk + kChunkHdr + S);
+          }
+          if (!__ballot(far)) {
+            done = true;
+            // cumSize (scannerv2.go:83-91): the item's end past the header
+            q0 = ex + z0, q1 = ex + z1, q2 = ex + z2, q3 = ex + z3;
+            sm = __ballot(sd);  // the straddler at the boundary (at most one item crosses it)
+            if (sm) {
+              const int L = __ffsll((long long)sm) - 1;
+              S = (uint32_t)__builtin_amdgcn_readlane((int)Sl, L);
+              E = (uint32_t)__builtin_amdgcn_readlane((int)El, L);
+            }
           }
         }
       }
-      wave_lds_sync();  // the next block's window reuses lwin / ltpos
+      wave_lds_sync();  // the next block's window reuses lwin / ltm / lp4
+    }
+    if (done) {
+      const uint64_t cap = a.item_cap, slot = base + g;
+      if (g + 3 < nitems && slot + 3 < cap) {
+        view_store2(a.item_end + slot, q0, q1);
+        view_store2(a.item_end + slot + 2, q2, q3);
+      } else if (g < nitems) {
+        if (slot < cap) view_store(a.item_end + slot, q0);
+        if (g + 1 < nitems && slot + 1 < cap) view_store(a.item_end + slot + 1, q1);
+        if (g + 2 < nitems && slot + 2 < cap) view_store(a.item_end + slot + 2, q2);
+        if (g + 3 < nitems && slot + 3 < cap) view_store(a.item_end + slot + 3, q3);
+      }
+      if (base + nitems > cap && l == 0) atomicOr(&a.ctl->out_overflow, 1ull);
+      if (sm) straddler_from_regs(bnd, a.side, S, E - S, c0 * (unsigned long long)kChunk + kChunkHdr + S);
     }
     if (l == 0) {
       if (done) {
@@ -409,6 +446,23 @@ __global__ void __launch_bounds__(256) k_lean_end(LeanArgs a) {
         a.blk_coff[atomicAdd(&a.ctl->n_retry, 1ull)] = b;
       }
     }
+  };
+  unsigned long long desc = dload(wave);
+  bool ok_nx = lean_ok(desc);
+  uint4 w_nx, bnd_nx;
+  fetch(desc, ok_nx, w_nx, bnd_nx);
+  unsigned long long desc_nx = dload(wave + nwaves);
+  for (uint64_t b = wave; b < nb; b += nwaves) {
+    const unsigned long long desc_c = desc;
+    const bool ok = ok_nx;
+    const uint4 w = w_nx, bnd = bnd_nx;
+    // the next block's windows and the one after's descriptor, in flight while this one is parsed
+    const uint64_t bn = b + nwaves;
+    ok_nx = bn < nb && lean_ok(desc_nx);
+    fetch(desc_nx, ok_nx, w_nx, bnd_nx);
+    desc = desc_nx;
+    desc_nx = dload(bn + nwaves);
+    parse_one(b, desc_c, ok, w, bnd);
   }
 }
 

@@ -571,6 +571,16 @@ __device__ __forceinline__ void straddler_from_regs(const uint32_t (&bnd)[4], ui
 
 // item view stores of the fast path: written once, read by the caller (not
 // by this pass) -- RIO_VIEW_NT builds stream them past the caches
+typedef unsigned long long u64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
+__device__ __forceinline__ void view_store2(unsigned long long *p, unsigned long long v0, unsigned long long v1) {
+  const u64x2_a8 v = {v0, v1};
+#if RIO_VIEW_NT
+  __builtin_nontemporal_store(v, reinterpret_cast<u64x2_a8 *>(p));
+#else
+  *reinterpret_cast<u64x2_a8 *>(p) = v;
+#endif
+}
+
 __device__ __forceinline__ void view_store(unsigned long long *p, unsigned long long v) {
 #if RIO_VIEW_NT
   __builtin_nontemporal_store(v, p);

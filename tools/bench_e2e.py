@@ -34,6 +34,8 @@ import struct
 import sys
 import time
 
+_T0 = time.perf_counter()
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -82,8 +84,13 @@ def _scan(gpu, src, ctx, hashes=None, batch=1 << 16):
     return n, tot, bad
 
 
+def _log(msg):
+    print("[bench_e2e %7.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
 def _workload(gpu, name, data, base_hashes, base_bytes, target, span, reps, device):
     import numpy as np
+    _log("scan " + name)
     arr, R = _replicate(data, target)
     src = gpu.MemorySource(arr)
     want = np.tile(base_hashes, R)
@@ -136,6 +143,7 @@ def run_e2e(device: int = 0, gib: float = 2.0, span_mib: int = 512, reps: int = 
     for per in (1024, 16384):
         if only is not None and ("c3_%d" % per) not in only:
             continue
+        _log("C3 file, %d per block" % per)
         data, nrec, rb = c3_data.make_file(128 << 20, per, workers=16)
         recs = []
         for first in range(0, nrec, per):
@@ -144,6 +152,7 @@ def run_e2e(device: int = 0, gib: float = 2.0, span_mib: int = 512, reps: int = 
                              data, viewhash.hash_records(recs), rb, target, span, reps, device))
     if only is None or "c4" in only:
         import bench_zstd
+        _log("C4 file")
         data, nblk, nrec, rb = bench_zstd.load_or_make(128, 16, "/tmp/c4.bin")
         out.append(_workload(gpu, "C4 zstd, 64 B-64 KiB records, 1 MiB blocks", data,
                              viewhash.hash_records(c4_data.all_records(nblk)), rb, target, span, reps, device))
