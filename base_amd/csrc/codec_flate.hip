@@ -1404,6 +1404,9 @@ constexpr int kSyncIters = 8;
 #define RIO_SYNC_WAVES 12
 #endif
 constexpr int kSyncWaves = RIO_SYNC_WAVES;                 // per CU (launch sizing, one wave per block)
+#ifndef RIO_SYNC_W
+#define RIO_SYNC_W 4  // waves per block for spans whose blocks all fit at that width (1: never)
+#endif
 // The kernel is written for kW waves per block (segment g = 64 * wave + lane,
 // cross-wave exchanges at barriers); only kW = 1 is instantiated: kW = 2 / 4
 // for spans of fewer blocks than one-wave slots measured slower for C3 at
@@ -2515,8 +2518,31 @@ void launch_inflate_huff(const uint8_t *span, const DevBufs &d, const unsigned l
   {  // the wave-per-block Huffman pass first; k_flate_tok takes what it declines
     const uint64_t rs = (uint64_t)ncu * kSyncWaves;
     const uint64_t gs = max_blocks < rs ? max_blocks : rs;
+#if RIO_SYNC_W > 1
+    // a span of few blocks (every block resident with kSyncW waves each, e.g. a
+    // scanner's 512 MiB span at MaxItems = 16384: ~250 blocks) runs the
+    // kSyncW-wave variant; the device-side block count picks (each returns
+    // at once on the other's spans)
+    static uint64_t wide_below = 0;
+    if (!wide_below) {
+      int per_cu = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_flate_sync<RIO_SYNC_W>, 64 * RIO_SYNC_W, 0) !=
+              hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      wide_below = (uint64_t)per_cu * (uint64_t)(ncu > 0 ? ncu : 256) + 1;
+    }
+    {
+      const uint64_t gw = max_blocks < wide_below - 1 ? max_blocks : wide_below - 1;
+      hipLaunchKernelGGL(k_flate_sync<RIO_SYNC_W>, dim3((unsigned)(gw ? gw : 1)), dim3(64 * RIO_SYNC_W), 0, st, span,
+                         d, nblocks, nchunks, dec_cap, wide_below);
+    }
+    hipLaunchKernelGGL(k_flate_sync<1>, dim3((unsigned)(gs ? gs : 1)), dim3(64), 0, st, span, d, nblocks, nchunks,
+                       dec_cap, wide_below);
+#else
     hipLaunchKernelGGL(k_flate_sync<1>, dim3((unsigned)(gs ? gs : 1)), dim3(64), 0, st, span, d, nblocks, nchunks,
                        dec_cap, 0);
+#endif
   }
 #ifdef RIO_FLSTAT
   {
