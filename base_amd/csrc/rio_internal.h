@@ -167,7 +167,10 @@ constexpr int kZTokPerChunk = 4 * kTokPerChunk;  // zstd scratch: input copy, li
 constexpr int kZJobsPerChunk = 16;               // zstd job list capacity (a block past it takes the serial path)
 // Split copy pass (codec_flate.hip k_flate_plan / k_flate_seg / k_flate_segfix):
 // segments per block at most, and the shortest segment
-constexpr int kSegMax = 8;
+#ifndef RIO_SEG_MAX
+#define RIO_SEG_MAX 16
+#endif
+constexpr int kSegMax = RIO_SEG_MAX;
 constexpr uint32_t kSegMin = 65536;
 
 // Device arrays of one context (capacities fixed at rio_open, grown on demand).
