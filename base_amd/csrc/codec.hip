@@ -79,18 +79,28 @@ __global__ void k_compact_len(DevBufs d, const unsigned long long *nblocks_dev, 
     padded[b] = b < nv ? (d.blk_out_len[b] + 15) & ~15ull : 0ull;
 }
 
+// A wave per (block, part): a span of few large blocks (MaxItems = 16384:
+// ~250 blocks of 5 MB per 512 MiB span) spreads each block's copy over up to
+// 64 waves instead of one.
 __global__ void __launch_bounds__(256) k_compact(DevBufs d, const unsigned long long *nblocks_dev) {
   const uint64_t nv = d.ctl->n_valid_blocks;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const int l = __lane_id();
   if (wave == 0 && l == 0) d.ctl->rec_bytes = d.blk_coff[nv];
-  for (uint64_t b = wave; b < nv; b += nwaves) {
+  if (nv == 0) return;
+  uint64_t P = nwaves / nv;  // parts per block
+  if (P < 1) P = 1;
+  if (P > 64) P = 64;
+  for (uint64_t u = wave; u < nv * P; u += nwaves) {
+    const uint64_t b = u % nv, part = u / nv;
     const uint64_t off = d.blk_dec_off[b], co = d.blk_coff[b], n = d.blk_out_len[b];
     const uint4 *src = reinterpret_cast<const uint4 *>(d.dec + off);  // regions are 256-aligned
     uint4 *dst = reinterpret_cast<uint4 *>(d.cmp + co);
-    for (uint64_t k = l; k < (n + 15) / 16; k += 64) dst[k] = src[k];
-    for (uint64_t i = d.blk_item_base[b] + l; i < d.blk_item_base[b + 1]; i += 64) {
+    const uint64_t n16 = (n + 15) / 16, k0 = n16 * part / P, k1 = n16 * (part + 1) / P;
+    for (uint64_t k = k0 + l; k < k1; k += 64) dst[k] = src[k];
+    const uint64_t i0 = d.blk_item_base[b], ni = d.blk_item_base[b + 1] - i0;
+    for (uint64_t i = i0 + ni * part / P + l; i < i0 + ni * (part + 1) / P; i += 64) {
       const unsigned long long v = d.item_off[i];
       if (v & kItemInRecords) d.item_off[i] = kItemInRecords | ((v & ~kItemInRecords) - off + co);
     }
@@ -101,8 +111,7 @@ void launch_compact(const DevBufs &d, const unsigned long long *nblocks_dev, uin
   hipLaunchKernelGGL(k_compact_len, dim3(grid_blocks(max_blocks)), dim3(256), 0, st, d, nblocks_dev,
                      d.blk_coff + max_blocks + 1);
   launch_block_scan(d.blk_coff + max_blocks + 1, d.blk_coff, d.scan_tmp, nblocks_dev, max_blocks, st);
-  unsigned g = (unsigned)((max_blocks + 3) / 4);
-  if (g > 4096) g = 4096;
+  unsigned g = (unsigned)(max_blocks * 16 < 4096 ? max_blocks * 16 : 4096);  // (16 parts per block when few)
   hipLaunchKernelGGL(k_compact, dim3(g < 1 ? 1 : g), dim3(256), 0, st, d, nblocks_dev);
 }
 
