@@ -787,32 +787,28 @@ void launch_parse(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hip
   hipLaunchKernelGGL(k_parse, dim3(grid_of(max_blocks, 4 * kBatch, RIO_PARSE_GRID)), dim3(256), 0, st, d, a);
 }
 
+// one resident round of a kernel: workgroups per CU at this build's occupancy x
+// CUs (a function-local static: initialised once, thread-safe -- the scanner's
+// span-ahead threads launch concurrently)
+template <class K>
+static unsigned resident_round(K kernel, int threads) {
+  int per_cu = 0, dev = 0, ncu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu < 1) per_cu = 4;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+    ncu = 256;
+  return (unsigned)(per_cu * ncu);
+}
+
 void launch_lean_end(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
-  static unsigned cap = 0;
-  if (!cap) {  // one resident round: workgroups per CU at this build's occupancy x CUs
-    int per_cu = 0, dev = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lean_end, 256, 0) != hipSuccess || per_cu < 1)
-      per_cu = 4;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
-      ncu = 256;
-    cap = (unsigned)(per_cu * ncu);
-  }
+  static const unsigned cap = resident_round(k_lean_end, 256);
   LeanArgs la{a.span, d.blk_c0, d.blk_meta, d.blk_len, d.blk_item_base, d.blk_status, d.blk_hdr, d.blk_data,
               d.blk_coff, d.item_off, d.side, d.ctl, a.nblocks, a.limit_chunk, a.item_cap};
   hipLaunchKernelGGL(k_lean_end, dim3(grid_of(max_blocks, 4, cap)), dim3(256), 0, st, la);
 }
 
 void launch_parse_lean(const DevBufs &d, const ParseArgs &a, uint64_t max_blocks, hipStream_t st) {
-  // one resident round: workgroups per CU at this build's occupancy x CUs
-  static unsigned cap = 0;
-  if (!cap) {
-    int per_cu = 0, dev = 0, ncu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_parse_lean, 256, 0) != hipSuccess || per_cu < 1)
-      per_cu = 4;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
-      ncu = 256;
-    cap = (unsigned)(per_cu * ncu);
-  }
+  static const unsigned cap = resident_round(k_parse_lean, 256);
   hipLaunchKernelGGL(k_parse_lean, dim3(grid_of(max_blocks, 4 * kLeanBatch, cap)), dim3(256), 0, st, d, a);
 }
 

@@ -2525,15 +2525,16 @@ void launch_inflate_huff(const uint8_t *span, const DevBufs &d, const unsigned l
     // scanner's 512 MiB span at MaxItems = 16384: ~250 blocks) runs the
     // kSyncW-wave variant; the device-side block count picks (each returns
     // at once on the other's spans)
-    static uint64_t wide_below = 0;
-    if (!wide_below) {
+    // (workgroups per CU: a function-local static, initialised once and thread-safe)
+    static const int wide_per_cu = [] {
       int per_cu = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_flate_sync<RIO_SYNC_W>, 64 * RIO_SYNC_W, 0) !=
               hipSuccess ||
           per_cu < 1)
         per_cu = 1;
-      wide_below = (uint64_t)per_cu * (uint64_t)(ncu > 0 ? ncu : 256) + 1;
-    }
+      return per_cu;
+    }();
+    const uint64_t wide_below = (uint64_t)wide_per_cu * (uint64_t)(ncu > 0 ? ncu : 256) + 1;
     {
       const uint64_t gw = max_blocks < wide_below - 1 ? max_blocks : wide_below - 1;
       hipLaunchKernelGGL(k_flate_sync<RIO_SYNC_W>, dim3((unsigned)(gw ? gw : 1)), dim3(64 * RIO_SYNC_W), 0, st, span,

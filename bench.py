@@ -448,7 +448,7 @@ def main():
     ap.add_argument("--e2e-gib", type=float, default=2.0, help="end-to-end: file size per workload")
     ap.add_argument("--cpu-s", type=float, default=4.0, help="seconds per CPU-baseline measurement")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 many-file measurement (configs[4])")
-    ap.add_argument("--c2-contexts", type=int, default=2, help="C2: contexts the steps alternate over (1 or 2)")
+    ap.add_argument("--c2-contexts", type=int, default=2, help="C2: contexts the steps rotate over (1-3; n > 1: n - 1 steps in flight beside the one collected)")
     ap.add_argument("--c5-batch-gib", type=float, default=4.0, help="file bodies per decode batch")
     ap.add_argument("--c5-cache", default="/tmp", help="host directory caching the C5 base files")
     args = ap.parse_args()
@@ -507,7 +507,7 @@ def main():
     # host's per-step work (sync, result read-back, the next enqueue) overlaps
     # the GPU's -- a scanner's read-ahead pipeline (--c2-contexts 1: one context,
     # each step synchronous)
-    nctx = max(1, min(2, args.c2_contexts))
+    nctx = max(1, min(3, args.c2_contexts))
     ctxs = [gpu.Context(local, max_span_bytes=total, max_items=n_items + 1024, item_end=True)
             for _ in range(nctx)]
     span_ptr = dev.data_ptr() + CHUNK
@@ -536,16 +536,17 @@ def main():
                 kern_ms.append(r.kernel_ms)
             return r
 
+        inflight = []  # contexts with a step launched and not yet collected, oldest first
         for i in range(steps):
             c = i % nctx
-            if pending is not None and nctx == 1:
-                out = collect(pending)
+            if nctx == 1 and inflight:
+                out = collect(inflight.pop(0))
             launch(c)
-            if pending is not None and nctx > 1:
-                out = collect(pending)
-            pending = c
-        if pending is not None:
-            out = collect(pending)
+            inflight.append(c)
+            if nctx > 1 and len(inflight) >= nctx:
+                out = collect(inflight.pop(0))
+        while inflight:
+            out = collect(inflight.pop(0))
         return out
 
     run(args.warmup, False)
