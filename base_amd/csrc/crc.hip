@@ -64,6 +64,13 @@ constexpr int kBufs = RIO_CRC_BUFS;  // register buffers: kBufs - 1 stages in fl
 constexpr int kStages = 32 / kRows;
 static_assert(kStages % kBufs == 0, "a chunk's stages must cycle through the buffers evenly");
 
+// the fold tables at LDS address 0 (dynamic LDS, no static LDS in k_crc<false>;
+// k_crc checks it): byte-row lookups use their v_perm address as is
+#ifndef RIO_CRC_DYN
+#define RIO_CRC_DYN 1
+#endif
+constexpr bool kCrcAbs = kFoldPerm && RIO_CRC_DYN;
+
 // fold stage q (rows kRows*q ..) of a chunk whose covered bytes end at `end`
 __device__ __forceinline__ void fold_stage(const uint4 (&u)[kRows], uint32_t (&s)[4], const char *__restrict__ tab,
                                            uint32_t lb, int l, int q, int end, bool fold, uint32_t &stored) {
@@ -86,7 +93,7 @@ __device__ __forceinline__ void fold_stage(const uint4 (&u)[kRows], uint32_t (&s
       v.w = mask_dword(v.w, o + 12, end);
     }
     if (fold) {
-      fold_row(tab, lb, v, s);
+      fold_row<kCrcAbs>(tab, lb, v, s);
     } else {  // ablation: keep the loads live
       s[0] ^= v.x;
       s[1] ^= v.y;
@@ -158,6 +165,13 @@ __global__ void __launch_bounds__(64 * kCrcWaves) RIO_CRC_ATTR k_crc(const uint8
     for (int i = threadIdx.x; i < kMulTables * 1024; i += blockDim.x) s_mul[i] = d.crc_mul[i];
   }
   __syncthreads();
+  if constexpr (kCrcAbs) {  // (a static LDS variable would move the tables: fail loudly)
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    if ((uint32_t)(uintptr_t)(lds_u32 *)s_fold != 0u) {
+      if (threadIdx.x == 0) atomicOr(&d.ctl->out_overflow, 0x2000ull);
+      return;
+    }
+  }
   const int l = lane_id();
   const uint32_t lb = (uint32_t)(l & (kFoldCopies - 1)) << 2;
   const char *tab = reinterpret_cast<const char *>(s_fold);

@@ -31,7 +31,31 @@ __device__ __forceinline__ uint32_t mask_dword(uint32_t v, int off, int hi) {
 
 // one Horner step of the lane's 4 dword streams: 16 independent lookups in the
 // lane's private table copies
+// kAbs: the tables start at LDS address 0 (k_crc: dynamic LDS and no static
+// LDS, checked at its start) -- the lookup address is the v_perm result itself
+// (with a base pointer the compiler adds the dynamic-LDS base, 0, per lookup)
+template <bool kAbs = false>
 __device__ __forceinline__ void fold_row(const char *__restrict__ tab, uint32_t lb, uint4 v, uint32_t (&s)[4]) {
+  if constexpr (kFoldPerm) {
+    // lookup j's byte address (256 b + 64 j + lb): byte 1 = data byte j, byte 0 =
+    // byte j of L = (lb, 64 + lb, 128 + lb, 192 + lb); bytes 2, 3 zero (selector 0x0c)
+    const uint32_t L = lb * 0x01010101u + 0xC0804000u;
+    const uint32_t d[4] = {v.x ^ s[0], v.y ^ s[1], v.z ^ s[2], v.w ^ s[3]};
+    uint32_t t[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t a = __builtin_amdgcn_perm(L, d[k], 0x0c0c0000u | ((uint32_t)j << 8) | (4u + (uint32_t)j));
+        typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+        if constexpr (kAbs) t[k][j] = *(lds_u32 *)(uintptr_t)a;
+        else t[k][j] = *reinterpret_cast<const uint32_t *>(tab + a);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) s[k] = t[k][0] ^ t[k][1] ^ t[k][2] ^ t[k][3];
+    return;
+  }
   const uint32_t d[4] = {v.x ^ s[0], v.y ^ s[1], v.z ^ s[2], v.w ^ s[3]};
   uint32_t t[4][4];
 #pragma unroll

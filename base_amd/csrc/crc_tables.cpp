@@ -66,7 +66,10 @@ void build_crc_tables(uint32_t *fold, uint32_t *mul, uint32_t *fix_a, uint32_t *
     const uint32_t sh = gf_xpow8(1023 - j);
     for (int b = 0; b < 256; b++) {
       const uint32_t v = gf_mul(byte_table((uint32_t)b), sh);
-      for (int k = 0; k < kFoldCopies; k++) fold[(j * 256 + b) * kFoldCopies + k] = v;
+      for (int k = 0; k < kFoldCopies; k++) {
+        if (kFoldPerm) fold[64 * b + 16 * j + k] = v;  // (rio_internal.h: byte-row layout)
+        else fold[(j * 256 + b) * kFoldCopies + k] = v;
+      }
     }
   }
   // mul[m][k][b] = (b << 8k) * c_m: multiply by c_0 = x^-32 (combine the 4

@@ -288,6 +288,13 @@ constexpr uint32_t kPoly = 0xEDB88320u;
 constexpr int kFoldCopies = RIO_FOLD_COPIES;     // replicas of each fold table (lane l reads copy l % copies)
 constexpr int kFoldShift = kFoldCopies == 32 ? 7 : (kFoldCopies == 16 ? 6 : 5);  // log2(4 * copies)
 constexpr int kFoldWords = 4 * 256 * kFoldCopies;  // 64 KiB at 16 copies
+// Byte-row layout (16 copies): entry b of table j, copy c at byte 256 b + 64 j + 4 c, so a
+// lookup's address is one v_perm_b32 -- byte 1 the data byte, byte 0 the lane's
+// (64 j + 4 c) -- instead of an extract, a shift and an add (crc_fold.h fold_row)
+#ifndef RIO_FOLD_PERM
+#define RIO_FOLD_PERM 1
+#endif
+constexpr bool kFoldPerm = RIO_FOLD_PERM && kFoldCopies == 16;
 constexpr int kMulTables = 7;                    // x^-32, then x^-(128*2^l), l = 0..5
 uint32_t gf_mul(uint32_t a, uint32_t b);         // a*b mod P (reflected; 1 = 0x80000000)
 uint32_t gf_xpow8(int64_t nbytes);               // x^(8*nbytes) mod P, nbytes may be negative
