@@ -72,7 +72,8 @@ static_assert(kStages % kBufs == 0, "a chunk's stages must cycle through the buf
 constexpr bool kCrcAbs = kFoldPerm && RIO_CRC_DYN;
 
 // fold stage q (rows kRows*q ..) of a chunk whose covered bytes end at `end`
-__device__ __forceinline__ void fold_stage(const uint4 (&u)[kRows], uint32_t (&s)[4], const char *__restrict__ tab,
+__device__ __forceinline__ void fold_stage(const uint4 (&u)[kRows], uint32_t (&s)[4], uint32_t (&sq)[4],
+                                           const char *__restrict__ tab,
                                            uint32_t lb, int l, int q, int end, bool fold, uint32_t &stored) {
 #pragma unroll
   for (int r = 0; r < kRows; r++) {
@@ -93,7 +94,12 @@ __device__ __forceinline__ void fold_stage(const uint4 (&u)[kRows], uint32_t (&s
       v.w = mask_dword(v.w, o + 12, end);
     }
     if (fold) {
+#if RIO_FOLD_XOR3
+      if constexpr (kFoldPerm) fold_row3<kCrcAbs>(tab, lb, v, s, sq);
+      else fold_row<kCrcAbs>(tab, lb, v, s);
+#else
       fold_row<kCrcAbs>(tab, lb, v, s);
+#endif
     } else {  // ablation: keep the loads live
       s[0] ^= v.x;
       s[1] ^= v.y;
@@ -196,7 +202,7 @@ __global__ void __launch_bounds__(64 * kCrcWaves) RIO_CRC_ATTR k_crc(const uint8
     const bool full = (sz == (uint32_t)kMaxPayload);
     // a block starts here: this wave parses it after the checksum (scalar load)
     const bool starts = kParse && pin.ck_index[c] == 0;
-    uint32_t s[4] = {0, 0, 0, 0};
+    uint32_t s[4] = {0, 0, 0, 0}, sq[4] = {0, 0, 0, 0};
     uint32_t stored = 0;
     const uint32_t fa = fix_a[sz], fb = fix_b[sz];
 #pragma unroll
@@ -208,9 +214,11 @@ __global__ void __launch_bounds__(64 * kCrcWaves) RIO_CRC_ATTR k_crc(const uint8
         *reinterpret_cast<uint4 *>(stage + 16 * l) = buf[0][0];
         if (l < 2) *reinterpret_cast<uint4 *>(stage + 1024 + 16 * l) = buf[0][1];
       }
-      fold_stage(buf[q % kBufs], s, tab, lb, l, q, end, fold, stored);
+      fold_stage(buf[q % kBufs], s, sq, tab, lb, l, q, end, fold, stored);
     }
     // lane: V_t = s0 + s1 x^-32 + s2 x^-64 + s3 x^-96
+#pragma unroll
+    for (int k = 0; k < 4; k++) s[k] ^= sq[k];  // (fold_row3's unfolded part)
     uint32_t v = mul_const(s_mul, s[3]) ^ s[2];
     v = mul_const(s_mul, v) ^ s[1];
     v = mul_const(s_mul, v) ^ s[0];

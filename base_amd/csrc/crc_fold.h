@@ -9,6 +9,10 @@
 
 #include "rio_internal.h"
 
+#ifndef RIO_FOLD_XOR3
+#define RIO_FOLD_XOR3 1
+#endif
+
 namespace rio {
 
 __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
@@ -34,6 +38,33 @@ __device__ __forceinline__ uint32_t mask_dword(uint32_t v, int off, int hi) {
 // kAbs: the tables start at LDS address 0 (k_crc: dynamic LDS and no static
 // LDS, checked at its start) -- the lookup address is the v_perm result itself
 // (with a base pointer the compiler adds the dynamic-LDS base, 0, per lookup)
+// The byte-row (v_perm) fold with its XORs as v_bitop3_b32 (3-input XOR): the
+// state of stream k is s[k] ^ s2[k] (s2: the fourth lookup, not yet folded in),
+// so a step is 4 permutes, 4 lookups and 2 XOR3s per dword -- the data XOR
+// joins the previous step's last one. Callers start with s2 = 0 and take
+// s ^ s2 at the end.
+template <bool kAbs = false>
+__device__ __forceinline__ void fold_row3(const char *__restrict__ tab, uint32_t lb, uint4 v, uint32_t (&s)[4],
+                                          uint32_t (&s2)[4]) {
+  static_assert(kFoldPerm, "the byte-row layout");
+  const uint32_t L = lb * 0x01010101u + 0xC0804000u;
+  const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t d = __builtin_amdgcn_bitop3_b32(vv[k], s[k], s2[k], 0x96);
+    uint32_t t[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t a = __builtin_amdgcn_perm(L, d, 0x0c0c0000u | ((uint32_t)j << 8) | (4u + (uint32_t)j));
+      typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+      if constexpr (kAbs) t[j] = *(lds_u32 *)(uintptr_t)a;
+      else t[j] = *reinterpret_cast<const uint32_t *>(tab + a);
+    }
+    s[k] = __builtin_amdgcn_bitop3_b32(t[0], t[1], t[2], 0x96);
+    s2[k] = t[3];
+  }
+}
+
 template <bool kAbs = false>
 __device__ __forceinline__ void fold_row(const char *__restrict__ tab, uint32_t lb, uint4 v, uint32_t (&s)[4]) {
   if constexpr (kFoldPerm) {
