@@ -56,7 +56,10 @@ namespace rio {
 #endif
 constexpr int kCrcWaves = RIO_CRC_WAVES;  // waves per workgroup (one workgroup per CU: 92 KiB LDS at 16 copies)
 
-constexpr int kRows = 4;   // rows per pipeline stage (4 KiB per wave)
+#ifndef RIO_CRC_ROWS
+#define RIO_CRC_ROWS 4
+#endif
+constexpr int kRows = RIO_CRC_ROWS;  // rows per pipeline stage (4 KiB per wave)
 #ifndef RIO_CRC_BUFS
 #define RIO_CRC_BUFS 4
 #endif
