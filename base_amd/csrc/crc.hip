@@ -12,7 +12,11 @@
 // reads copy l & 15 (32 copies, 128 KiB, made every read conflict-free but left
 // no room on the CU for anything else). A row's 16
 // lookups are independent and issue back to back; only the row-to-row chain
-// per stream is serial.
+// per stream is serial. Round 5: the tables in byte rows (entry b of table j,
+// copy c at byte 256 b + 64 j + 4 c, from LDS address 0), so a lookup's address
+// is one v_perm_b32 of the data and the lane's offsets, and the XORs are
+// 3-input v_bitop3_b32 (crc_fold.h fold_row3): 24 VALU instructions per 1 KiB
+// row where there were 52 (2.84 -> 2.67 ms per C2 launch).
 // After row 31, stream (t, k) holds R(message) * x^(8(16t + 4k)); the lane
 // combines its streams with x^-32 (Horner), a 6-level shuffle tree with
 // x^-(128*2^l) combines the lanes (multiply-by-constant = 4 byte lookups).
