@@ -60,6 +60,9 @@ namespace rio {
 #endif
 constexpr int kCrcWaves = RIO_CRC_WAVES;  // waves per workgroup (one workgroup per CU: 92 KiB LDS at 16 copies)
 
+#ifndef RIO_CRC_MAP
+#define RIO_CRC_MAP 0
+#endif
 #ifndef RIO_CRC_ROWS
 #define RIO_CRC_ROWS 4
 #endif
@@ -191,7 +194,11 @@ __global__ void __launch_bounds__(64 * kCrcWaves) RIO_CRC_ATTR k_crc(const uint8
   const bool fold = !(ca.flags & 1);
   const uint64_t nwaves = (uint64_t)gridDim.x * kCrcWaves;
   // wave-uniform chunk index: sizes are scalar loads and the FULL test a scalar branch
+#if RIO_CRC_MAP  // (wave-major: a CU's waves read chunks gridDim.x apart)
+  uint64_t c = (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+#else
   uint64_t c = (uint64_t)blockIdx.x * kCrcWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#endif
   if (c >= nchunks) return;
   uint4 buf[kBufs][kRows];
   uint8_t *stage = kParse ? s_stage[threadIdx.x >> 6] : nullptr;
