@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(64 * kEncWaves) k_enc_chunks(EncArgs a, uint64
        c += nwaves) {
     const ChunkCtx x = chunk_ctx(a, c);
     uint8_t *ck = a.out + c * kChunk;
-    uint32_t s[4] = {0, 0, 0, 0};
+    uint32_t s[4] = {0, 0, 0, 0}, sq[4] = {0, 0, 0, 0};  // (fold_row3: the stream is s ^ sq)
     uint32_t wa[kEncGroup][4], wb[kEncGroup][4];
 #pragma unroll
     for (int r = 0; r < kEncGroup; r++) unit_words(a, x, 1024 * r + 16 * l, wa[r]);
@@ -256,13 +256,16 @@ __global__ void __launch_bounds__(64 * kEncWaves) k_enc_chunks(EncArgs a, uint64
           v.z = mask_dword(v.z, q0 + 8, x.end);
           v.w = mask_dword(v.w, q0 + 12, x.end);
         }
-        fold_row(tab, lb, v, s);
+        if constexpr (kFoldPerm) fold_row3(tab, lb, v, s, sq);
+        else fold_row(tab, lb, v, s);
       }
 #pragma unroll
       for (int r = 0; r < kEncGroup; r++)
 #pragma unroll
         for (int k = 0; k < 4; k++) wa[r][k] = wb[r][k];
     }
+#pragma unroll
+    for (int k = 0; k < 4; k++) s[k] ^= sq[k];
     // lane: V_t = s0 + s1 x^-32 + s2 x^-64 + s3 x^-96; lanes: V = sum_t V_t x^-128t
     uint32_t v = mul_const(s_mul, s[3]) ^ s[2];
     v = mul_const(s_mul, v) ^ s[1];
