@@ -151,10 +151,12 @@ def c3_flate_16k(args, local, world, dist):
     """BASELINE.json configs[2] at the reference writer's default block size:
     MaxItems = 16384 (recordio/writerv2.go:28-29), i.e. 16,385 records per block
     (~5 MB blocks; SURVEY.md §8(d) C3's sensitivity point), the same ~10 GiB of
-    records. Steps alternate over two contexts (--flate16k-pipeline), each
-    launched before the previous step is collected -- a scanner's read-ahead of
-    its next span: one step's copy pass runs beside the next step's Huffman pass
-    (a span of 2,158 blocks fills neither pass alone). `serial` is the same steps
+    records. Steps rotate over three contexts (--flate16k-pipeline), each
+    launched before the previous steps are collected -- a scanner's read-ahead of
+    its next spans: one step's copy pass runs beside the next steps' Huffman
+    passes (a span of 2,158 blocks fills neither pass alone; three in flight
+    measured 43.4-44.2 GiB/s against 42.0-42.3 for two,
+    profiles/r05_flate_depth_ab.jsonl). `serial` is the same steps
     one at a time. Every record of the last timed step is checked."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -443,7 +445,8 @@ def main():
                     help="C4: steps alternate over this many contexts, each launched before the previous is "
                          "collected (1: one step at a time; the line reports that rate as `serial` too)")
     ap.add_argument("--no-flate16k", action="store_true", help="skip C3 at MaxItems 16384 (configs[2] sensitivity)")
-    ap.add_argument("--flate16k-pipeline", type=int, default=2, help="C3 at MaxItems 16384: contexts steps alternate over")
+    ap.add_argument("--flate16k-pipeline", type=int, default=3,
+                    help="C3 at MaxItems 16384: context sets steps rotate over (n - 1 in flight beside the one collected)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host file in, records out) line")
     ap.add_argument("--e2e-gib", type=float, default=2.0, help="end-to-end: file size per workload")
     ap.add_argument("--cpu-s", type=float, default=4.0, help="seconds per CPU-baseline measurement")

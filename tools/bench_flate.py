@@ -81,25 +81,29 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
             assert bb.n_items == nrec * r
 
     def run(n, record):
-        out, pending = None, None
+        out, last = None, ctxs
+        inflight = []  # context sets with a step launched and not yet collected, oldest first
+
+        def collect():
+            nonlocal out, last
+            last = inflight.pop(0)
+            out = [c.sync() for c in last]
+            if record:
+                stages.append(last[0].stage_times())
+
         for i in range(n):
             cs = sets[i % npipe]
+            if cs in inflight:  # (the oldest: npipe steps in flight)
+                collect()
             launch(cs)
+            inflight.append(cs)
             if npipe == 1:
-                out = [c.sync() for c in cs]
-                if record:
-                    stages.append(cs[0].stage_times())
-                continue
-            if pending is not None:
-                out = [c.sync() for c in pending]
-                if record:
-                    stages.append(pending[0].stage_times())
-            pending = cs
-        if pending is not None:
-            out = [c.sync() for c in pending]
-            if record:
-                stages.append(pending[0].stage_times())
-        return out, (pending or ctxs)
+                collect()
+            elif len(inflight) == npipe:  # collect the oldest once the next set is in flight
+                collect()
+        while inflight:
+            collect()
+        return out, last
 
     stages = []
     run(warmup, False)
