@@ -126,13 +126,16 @@ def c3_flate(args, local, world, dist):
     """BASELINE.json configs[2] beside the headline: ~10 GiB of FASTQ-like records in
     flate blocks (1,024 records per block) per GPU, device-resident, one pass =
     chunk CRC + two-pass DEFLATE decode + packed unpack (tools/bench_flate.py).
-    Whole-job GiB/s of compressed input over the max time across ranks."""
+    Whole-job GiB/s of compressed input over the max time across ranks. Steps
+    rotate over --flate-pipeline context sets (a scanner's read-ahead: the next
+    spans are launched before this one is collected); `serial` is the same steps
+    one at a time (with --flate-pipeline 1, `value` is)."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_flate
     cpu_s = args.cpu_s if (world == 1 and not args.no_cpu_baseline) else 0.0
     r = bench_flate.run_c3(replicas=args.flate_replicas, steps=max(2, min(args.steps, 5)), warmup=1,
-                           device=local, check=True, cpu_s=cpu_s)
+                           device=local, check=True, cpu_s=cpu_s, pipeline=args.flate_pipeline)
     if dist is not None:
         t = torch.tensor([r["ms_per_step"]], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -445,6 +448,8 @@ def main():
                     help="C4: steps alternate over this many contexts, each launched before the previous is "
                          "collected (1: one step at a time; the line reports that rate as `serial` too)")
     ap.add_argument("--no-flate16k", action="store_true", help="skip C3 at MaxItems 16384 (configs[2] sensitivity)")
+    ap.add_argument("--flate-pipeline", type=int, default=3,
+                    help="C3: context sets steps rotate over (n - 1 in flight beside the one collected; 1: serial)")
     ap.add_argument("--flate16k-pipeline", type=int, default=3,
                     help="C3 at MaxItems 16384: context sets steps rotate over (n - 1 in flight beside the one collected)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host file in, records out) line")
