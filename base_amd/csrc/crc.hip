@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(64 * kCrcWaves) RIO_CRC_ATTR k_crc(const uint8
   if constexpr (kCrcAbs) {  // (a static LDS variable would move the tables: fail loudly)
     typedef __attribute__((address_space(3))) uint32_t lds_u32;
     if ((uint32_t)(uintptr_t)(lds_u32 *)s_fold != 0u) {
-      if (threadIdx.x == 0) atomicOr(&d.ctl->out_overflow, 0x2000ull);
+      if (threadIdx.x == 0) atomicOr(&d.ctl->out_overflow, kOvfLayout);
       return;
     }
   }

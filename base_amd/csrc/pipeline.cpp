@@ -361,11 +361,19 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   return 0;
 }
 
+// every SDMA copy of the ctx complete: they run outside its stream, so a stream
+// sync alone does not order them before a buffer they read or write is freed
+static int sdma_quiesce(rio_ctx *c) {
+  const int a = sdma_settle(c, kSdmaIn), b = sdma_settle(c, kSdmaOut);
+  return (a || b) ? -1 : 0;
+}
+
 static int reserve(rio_ctx *c, uint64_t bytes) {
   bytes = (bytes + kChunk - 1) / kChunk * kChunk;
   if (bytes <= c->max_span) return 0;
   HIP_OK(hipSetDevice(c->device));
   HIP_OK(hipStreamSynchronize(c->st));
+  if (sdma_quiesce(c)) return -1;
   c->max_span = bytes;
   c->max_chunks = bytes / kChunk;
   c->max_blocks = c->max_chunks;
@@ -413,19 +421,22 @@ static void dfree(T **p) {
 // back to the sizes before a temporary growth (every buffer sized from the
 // grown span is released; the demand-sized ones regrow on use)
 // a span staged by rio_scan_span_stage and not decoded: forgotten (d_span is
-// reused; stream order keeps its copy before anything after it)
-static void unstage(rio_ctx *c) {
-  if (!c->staged) return;
+// reused; its copy in may run on an SDMA engine, outside the stream's order, so
+// it completes here before anything else writes or frees d_span)
+static int unstage(rio_ctx *c) {
+  if (!c->staged) return 0;
   c->staged = nullptr;
   hipEventDestroy(c->staged_t0);
+  return sdma_settle(c, kSdmaIn);
 }
 
 static int settle(rio_ctx *c) {
-  unstage(c);
+  if (unstage(c)) return -1;
   if (!c->grown_tmp) return 0;
   c->grown_tmp = false;
   HIP_OK(hipSetDevice(c->device));
   HIP_OK(hipStreamSynchronize(c->st));
+  if (sdma_quiesce(c)) return -1;
   c->max_span = c->base_span;
   c->max_chunks = c->max_span / kChunk;
   c->max_blocks = c->max_chunks;
@@ -826,6 +837,14 @@ static int collect(rio_ctx *c, const uint8_t *span, uint64_t file_off, int32_t c
   return 0;
 }
 
+// a run whose output did not fit (after the retries), or a layout fault
+static void report_overflow(unsigned long long ov, uint64_t file_off, rio_error *err) {
+  if (ov & kOvfLayout)
+    rio_set_error(err, RIO_ERR_HIP, file_off, "internal error: k_crc's LDS tables are not at address 0 (build fault)");
+  else
+    rio_set_error(err, RIO_ERR_CAPACITY, file_off, "output capacity exceeded");
+}
+
 static int grow_for_overflow(rio_ctx *c, int32_t codec) {
   unsigned long long nb = 0, items = 0, side = 0;
   HIP_OK(hipMemcpy(&nb, c->nblocks_dev, 8, hipMemcpyDeviceToHost));
@@ -909,7 +928,7 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
     HIP_OK(hipMemcpyAsync(c->h_ctl, c->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->st));
     HIP_OK(hipStreamSynchronize(c->st));
     note_split(c);
-    if (c->h_ctl->out_overflow == 0) break;
+    if (c->h_ctl->out_overflow == 0 || (c->h_ctl->out_overflow & kOvfLayout)) break;
     if (grow_for_overflow(c, codec)) return -1;
     // decode regions: blocks that overflowed theirs carry their exact size (blk_need)
     // into the next attempt; a buffer too small for all regions grows to fit
@@ -940,7 +959,7 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
   out->kernel_ms = ms;
   if (c->h_ctl->out_overflow) {  // still short after the retries: report that, not what it garbled
     memset(&out->err, 0, sizeof(out->err));
-    rio_set_error(&out->err, RIO_ERR_CAPACITY, file_off, "output capacity exceeded");
+    report_overflow(c->h_ctl->out_overflow, file_off, &out->err);
     out->stop = RIO_STOP_ERROR;
   }
   return 0;
@@ -1046,7 +1065,7 @@ extern "C" int rio_scan_device(rio_ctx *ctx, const void *dev_span, uint64_t nbyt
   if (!ctx || !out) return -1;
   memset(out, 0, sizeof(*out));
   if (rio_scan_span_end(ctx)) return -1;
-  unstage(ctx);
+  if (unstage(ctx)) return -1;
   if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;  // (consecutive chain calls keep the growth)
   return run_span(ctx, (const uint8_t *)dev_span, (const uint8_t *)dev_span, nbytes, file_off, is_file_end,
                   limit_off, codec, kModeBody, nullptr, out);
@@ -1080,7 +1099,7 @@ static int scan_span(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_
   // staged by rio_scan_span_stage (its H2D copy enqueued, the ctx settled)
   const bool pre = span && ctx->staged == span && ctx->staged_n == nbytes;
   if (pre) ctx->staged = nullptr;
-  else unstage(ctx);
+  else if (unstage(ctx)) return -1;
   hipEvent_t t0, t1;
   if (pre) {
     memset(out, 0, sizeof(*out));
@@ -1136,7 +1155,7 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
 
 int rio_scan_span_stage(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, int32_t codec) {
   if (!ctx || !span) return -1;
-  unstage(ctx);
+  if (unstage(ctx)) return -1;
   if (rio_scan_span_end(ctx)) return -1;
   if ((codec & RIO_CODEC_CHAIN_FLAG) || nbytes > ctx->max_span + kChunk) return 0;  // (staged by the decode)
   if (settle(ctx)) return -1;
@@ -1195,7 +1214,7 @@ extern "C" int rio_scan_device_async(rio_ctx *ctx, const void *dev_span, uint64_
   if (!ctx) return -1;
   HIP_OK(hipSetDevice(ctx->device));
   if (rio_scan_span_end(ctx)) return -1;
-  unstage(ctx);
+  if (unstage(ctx)) return -1;
   if (!(codec & RIO_CODEC_CHAIN_FLAG) && settle(ctx)) return -1;
   if (codec & RIO_CODEC_CHAIN_FLAG) {
     // a chain's stages run here, one after the other (each needs the previous
@@ -1311,7 +1330,7 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
     return -1;
   out->kernel_ms = ms;
   if (ctx->h_ctl->out_overflow) {
-    rio_set_error(&out->err, RIO_ERR_CAPACITY, 0, "output capacity exceeded");
+    report_overflow(ctx->h_ctl->out_overflow, 0, &out->err);
     out->stop = RIO_STOP_ERROR;
   }
   return sync_segments(ctx, out);

@@ -88,6 +88,10 @@ enum Mode : int32_t { kModeBody = 0, kModeHeader = 1, kModeTrailer = 2, kModeLas
 #define RIO_ABLATE 0
 #endif
 
+// out_overflow bit of a build / layout fault (k_crc's dynamic LDS tables not at
+// address 0): reported as an internal error at once, never retried
+constexpr unsigned long long kOvfLayout = 1ull << 40;
+
 // Control block written by the kernels, read back by the host (one copy).
 struct Ctl {
   unsigned long long first_chunk_err;    // min chunk with size/structural error

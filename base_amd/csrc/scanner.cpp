@@ -308,18 +308,6 @@ struct rio_scanner {
   void begin_ahead() {
     if (v1 || done || err_set || depth == 0) return;
     const uint64_t maxspan = rio_ctx_max_span(ctx);
-    if (aq.empty()) {
-      // every slot's context opened now, while no span-ahead thread runs (a
-      // sibling is opened from the context before it, which such a thread
-      // would otherwise be using; rio_gpu.h: a scanner's spans ahead hold
-      // `depth` further contexts of the ctx's size until rio_close)
-      for (int i = 1; i <= depth; i++)
-        if (!cx[i]) {
-          cx[i] = rio_ctx_sibling(cx[i - 1]);
-          if (!cx[i]) return;
-          rs[i] = rio_ctx_take_results(ctx);
-        }
-    }
     while ((int)aq.size() < depth) {
       // the span before the new one: the last one ahead, or the current batch
       const bool first = aq.empty();
@@ -340,6 +328,19 @@ struct rio_scanner {
       if (at >= limit || at >= file_size || at < pat || at > pend || pend - at > kRaRoom) return;
       const uint64_t n = file_size - at < maxspan ? file_size - at : maxspan;
       if (at + n <= pend) return;  // (a span inside the one before it: not a body's next span)
+      if (first) {
+        // a span ahead will be begun: every slot's context opened now, while no
+        // span-ahead thread runs (a sibling is opened from the context before
+        // it, which such a thread would otherwise be using; rio_gpu.h: a
+        // scanner's spans ahead hold `depth` further contexts of the ctx's size
+        // until rio_close). A file that fits one span never opens them.
+        for (int i = 1; i <= depth; i++)
+          if (!cx[i]) {
+            cx[i] = rio_ctx_sibling(cx[i - 1]);
+            if (!cx[i]) return;
+            rs[i] = rio_ctx_take_results(ctx);
+          }
+      }
       int sl = -1;  // a slot neither the current batch nor a span ahead holds
       for (int i = 0; i < kSlots && sl < 0; i++) {
         bool used = (i == slot);

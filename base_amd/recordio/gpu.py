@@ -57,8 +57,8 @@ RIO_CFG_FLATE_TOK_ONLY = 4  # every flate block through the fallback Huffman pas
 
 
 def RIO_CFG_SPANS_AHEAD(n: int) -> int:
-    """Scanners over the ctx decode up to n (0-2) spans ahead (default 2)."""
-    return ((n & 3) + 1) << 8
+    """Scanners over the ctx decode up to n (0-2) spans ahead (default 2; above 2 is 2)."""
+    return (min(max(int(n), 0), 2) + 1) << 8
 
 
 class RioConfig(ctypes.Structure):

@@ -123,8 +123,8 @@ typedef struct rio_error {
                                      * segments (by default a span of few large blocks is split,
                                      * see DESIGN.md "split copy pass") */
 /* scanners over this ctx decode up to n (0-2) spans ahead of the batch handed
- * out (bits 8-9 hold n + 1; 0 = the default, 2) */
-#define RIO_CFG_SPANS_AHEAD(n) ((((uint32_t)(n) & 3u) + 1u) << 8)
+ * out (bits 8-9 hold n + 1; 0 = the default, 2); n above 2 is taken as 2 */
+#define RIO_CFG_SPANS_AHEAD(n) (((((uint32_t)(n)) > 2u ? 2u : ((uint32_t)(n))) + 1u) << 8)
 #define RIO_CFG_FLATE_TOK_ONLY 4u  /* test: the wave-per-block Huffman pass declines every flate
                                      * block, so the fallback pass (k_flate_tok) decodes them all */
 
