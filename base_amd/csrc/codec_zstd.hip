@@ -1468,6 +1468,201 @@ __device__ __forceinline__ void z_flatten(const uint8_t *span, const DevBufs &d,
   zmem_sync();
 }
 
+// ---------------------------------------------------------------- k_zstd_size
+// Region sizing, thread per block, from the block's headers alone -- frame
+// headers, zstd block headers, each compressed block's literals-section header
+// (Regenerated_Size) and the sequences-section header (Number_of_Sequences),
+// RFC 8878 3.1.1, 3.1.1.3.1.1, 3.1.1.3.2.1; no entropy decode:
+// - the decode region: Frame_Content_Size where every frame declares it (the
+//   writer's single-shot ZSTD_compress does, recordiozstd.go:31-38), else each
+//   compressed block's bound min(window, 128 KiB); a frame whose content exceeds
+//   its declared size is found by the passes and retried at its exact size
+//   (blk_need) as before;
+// - the scratch region the fast passes fill: the flattened input, the literal
+//   area (every block's literals), the execution entries k_zstd_fix reserves
+//   (sequences + pieces of runs over kZPiece + per-job / per-frame marks, its
+//   own 8 * (... + 132) check), and the jobs (ZJobSink::new_job: header, tables
+//   of at most 4 * (512 + 512 + 256) bytes, 8 B per raw sequence) -- or the
+//   serial decoder's (input + zx::State), if larger.
+// Regions are then placed back to back by an exclusive scan (blk_zoff): a C4
+// block needs ~4x its compressed bytes, against the previous fixed 512 KiB per
+// input chunk (16x the span). Every writer still checks its region's limits
+// (lits / new_job / k_zstd_fix's entry check -> the serial path), so a header
+// this walk cannot parse gets a generous region and the passes decide.
+struct ZSzIn {
+  const uint8_t *span;
+  const unsigned long long *ck_pay;
+  uint64_t c0, total, pay0, n;
+  bool regular;
+  __device__ __forceinline__ uint32_t b(uint64_t p) const {  // logical byte p (0 at/after n)
+    if (p >= n) return 0u;
+    if (regular) {
+      const uint64_t j = p / kMaxPayload;
+      return span[(c0 + j) * kChunk + kChunkHdr + (p - j * kMaxPayload)];
+    }
+    uint64_t a = c0, e = c0 + total;
+    while (e - a > 1) {
+      const uint64_t m = (a + e) >> 1;
+      if (ck_pay[m] - pay0 <= p) a = m;
+      else e = m;
+    }
+    return span[a * kChunk + kChunkHdr + (p - (ck_pay[a] - pay0))];
+  }
+  __device__ __forceinline__ uint32_t le(uint64_t p, int k) const {  // k <= 4 bytes, little-endian
+    uint32_t v = 0;
+    for (int i = 0; i < k; i++) v |= b(p + i) << (8 * i);
+    return v;
+  }
+};
+
+struct ZSz {
+  uint64_t content = 0;  // decoded bytes (declared or bounded)
+  uint64_t bound = 0;    // decoded bytes bounded per block (entry pieces)
+  uint64_t lits = 0, nseq = 0, njobs = 0, nframes = 0, jobs_bytes = 0;
+};
+
+// the walk; false if a header does not parse
+__device__ bool z_size_walk(const ZSzIn &in, ZSz &z) {
+  const uint64_t n = in.n;
+  uint64_t pos = 0;
+  while (pos < n) {
+    if (n - pos < 4) return false;
+    const uint32_t magic = in.le(pos, 4);
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
+      if (n - pos < 8) return false;
+      pos += 8 + (uint64_t)in.le(pos + 4, 4);
+      continue;
+    }
+    if (magic != kZMagic || n - pos < 5) return false;
+    const uint32_t fhd = in.b(pos + 4);
+    const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, checksum = (fhd >> 2) & 1, did_flag = fhd & 3;
+    uint64_t p = pos + 5;
+    uint64_t window = 0;
+    if (!single) {
+      if (p >= n) return false;
+      const uint32_t wd = in.b(p++);
+      const uint32_t wlog = 10 + (wd >> 3);
+      if (wlog > 31) return false;
+      window = (1ull << wlog) + ((1ull << wlog) / 8) * (uint64_t)(wd & 7);
+    }
+    p += did_flag == 0 ? 0 : did_flag == 1 ? 1 : did_flag == 2 ? 2 : 4;
+    const uint32_t fcs_len = fcs_flag == 0 ? (single ? 1 : 0) : (fcs_flag == 1 ? 2 : (fcs_flag == 2 ? 4 : 8));
+    if (p + fcs_len > n) return false;
+    int64_t fcs = -1;
+    if (fcs_len == 1) fcs = in.b(p);
+    else if (fcs_len == 2) fcs = in.le(p, 2) + 256;
+    else if (fcs_len == 4) fcs = in.le(p, 4);
+    else if (fcs_len == 8) fcs = (int64_t)(in.le(p, 4) | ((uint64_t)in.le(p + 4, 4) << 32));
+    p += fcs_len;
+    if (single) window = (uint64_t)fcs;
+    const uint64_t block_max = window < (uint64_t)kZBlockMax ? window : (uint64_t)kZBlockMax;
+    uint64_t fb = 0;  // the frame's decoded bytes, bounded per block
+    for (;;) {
+      if (p + 3 > n) return false;
+      const uint32_t bh = in.le(p, 3);
+      p += 3;
+      const uint32_t type = (bh >> 1) & 3;
+      const uint64_t size = bh >> 3;
+      if (type == 3 || size > block_max) return false;
+      z.njobs++;
+      if (type == 0 || type == 1) {  // raw / RLE: literal-only jobs
+        z.lits += size;
+        fb += size;
+        z.jobs_bytes += (uint64_t)kZJobHdr;
+        p += type == 0 ? size : 1;
+      } else {
+        if (size < 1 || p + size > n) return false;
+        const uint32_t b0 = in.b(p);
+        const uint32_t ltype = b0 & 3, sf = (b0 >> 2) & 3;
+        uint64_t regen, lhdr, ldata;
+        if (ltype < 2) {  // raw / RLE literals
+          if (sf == 1) lhdr = 2, regen = (b0 >> 4) + ((uint64_t)in.b(p + 1) << 4);
+          else if (sf == 3) lhdr = 3, regen = (b0 >> 4) + ((uint64_t)in.le(p + 1, 2) << 4);
+          else lhdr = 1, regen = b0 >> 3;
+          ldata = ltype == 0 ? regen : 1;
+          if (lhdr > size) return false;
+        } else {  // Huffman-coded literals: 10/10, 14/14 or 18/18 bits of sizes
+          lhdr = sf < 2 ? 3 : (sf == 2 ? 4 : 5);
+          if (lhdr > size) return false;
+          const uint64_t h = (uint64_t)in.le(p, 4) | (lhdr == 5 ? (uint64_t)in.b(p + 4) << 32 : 0ull);
+          const uint32_t bits = sf < 2 ? 10 : (sf == 2 ? 14 : 18);
+          regen = (h >> 4) & ((1ull << bits) - 1);
+          ldata = (h >> (4 + bits)) & ((1ull << bits) - 1);
+        }
+        const uint64_t q = p + lhdr + ldata;  // the sequences section
+        if (q >= p + size) return false;
+        const uint32_t s0 = in.b(q);
+        uint64_t ns = s0;
+        if (s0 >= 128) {
+          if (q + 2 > p + size) return false;
+          if (s0 < 255) ns = ((uint64_t)(s0 - 128) << 8) + in.b(q + 1);
+          else if (q + 3 > p + size) return false;
+          else ns = (uint64_t)in.le(q + 1, 2) + 0x7F00;
+        }
+        z.lits += regen;
+        z.nseq += ns;
+        z.jobs_bytes += ((uint64_t)kZJobHdr + (ns ? 4 * (512 + 512 + 256) : 0) + 8 * ns + 15) & ~15ull;
+        fb += block_max;
+        p += size;
+      }
+      if (p > n) return false;
+      if (bh & 1) break;
+    }
+    if (checksum) p += 4;
+    if (p > n) return false;
+    z.content += fcs >= 0 ? (uint64_t)fcs : fb;
+    z.bound += fb;
+    z.nframes++;
+    pos = p;
+  }
+  return true;
+}
+
+__global__ void k_zstd_size(const uint8_t *__restrict__ span, DevBufs d, const unsigned long long *nblocks,
+                            uint32_t factor) {
+  const uint64_t nb = *nblocks;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long meta = d.blk_meta[b];
+    const uint32_t cls = (uint32_t)(meta >> kMetaClsShift) & 0xffu;
+    const bool dec = (meta & kMetaComplete) && (cls == kMagicPacked || cls == kMagicTrailer);
+    const uint64_t n = dec ? d.blk_len[b] : 0;
+    uint64_t out = 0, need = 0, half = 0;
+    if (n > 0) {
+      const uint64_t in_area = (n + 16 + 15) & ~15ull;
+      const uint64_t serial = ((n + 64 + 255) & ~255ull) + zx::kStateBytes;
+      ZSzIn in{span, d.ck_pay, d.blk_c0[b], meta & kMetaTotalMask, 0, n, (meta & kMetaRegular) != 0};
+      in.pay0 = d.ck_pay[in.c0];
+      ZSz z;
+      if (z_size_walk(in, z)) {
+        out = z.content;
+        const uint64_t ents = z.nseq + z.bound / kZPiece + 2 * z.njobs + z.nframes + 136;
+        half = (in_area + z.lits + 64 + 8 * ents + 15) & ~15ull;
+        need = half + z.jobs_bytes;
+      } else {  // the passes find the error (or decline to the serial decoder)
+        out = n * factor + 4096;
+        half = (2 * in_area + 65536 + 15) & ~15ull;
+        need = 2 * half;
+      }
+      if (need < serial) need = serial;
+      if (half > need) half = need;
+    }
+    if (d.blk_need[b] > out) out = d.blk_need[b];  // exact size from a previous attempt
+    d.blk_out_len[b] = (out + 255) & ~255ull;
+    d.blk_zneed[b] = (need + 255) & ~255ull;
+    d.blk_zhalf[b] = half;
+    d.blk_status[b] = kBlkOk;
+    d.blk_a[b] = 0;
+    d.blk_b[b] = 0;
+  }
+}
+
+void launch_zstd_size(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
+                      uint32_t factor, hipStream_t st) {
+  uint64_t g = (max_blocks + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(k_zstd_size, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st, span, d, nblocks, factor);
+}
+
 // ---------------------------------------------------------------- k_zstd_ent
 // Frame pass, one wave per recordio block (grid-stride): flattenIov, frames
 // and block headers, Huffman literals (4 streams on 4 lanes) into the block's
@@ -1526,18 +1721,29 @@ __global__ void __launch_bounds__(64) RIO_ZENT_ATTR k_zstd_ent(const uint8_t *__
     zprof_ctl = d.ctl;
 #endif
     ZPROF_T(tb);
-    uint32_t *flat = d.tok + c0 * (uint64_t)kZTokPerChunk;
+    // the block's scratch region (k_zstd_size): all regions must fit tok (else
+    // the host grows it to their total and retries)
+    const uint64_t zoff = uni64(d.blk_zoff[b]), rbytes = uni64(d.blk_zneed[b]);
+    if (zoff + rbytes > d.tok_cap * 4) {
+      if (l == 0) {
+        sp->mode = kZsSkip;
+        atomicOr(&d.ctl->out_overflow, kOvfZTok);
+        atomicMax(&d.ctl->tok_need, d.blk_zoff[nb]);
+        d.blk_out_len[b] = 0;
+      }
+      continue;
+    }
+    uint32_t *flat = d.tok + zoff / 4;
     z_flatten(span, d, c0, meta, n, flat);
     ZFrame z;
     z_init(z, reinterpret_cast<const uint8_t *>(flat), nullptr, (int64_t)cap, nullptr);
     ZJobSink k;
-    const int64_t rbytes = (int64_t)((meta & kMetaTotalMask) * (uint64_t)kZTokPerChunk * 4);
     k.tok8 = reinterpret_cast<uint8_t *>(d.tok);
-    k.region = c0 * (uint64_t)kZTokPerChunk * 4;
-    k.half = rbytes / 2;
+    k.region = zoff;
+    k.half = (int64_t)uni64(d.blk_zhalf[b]);
     k.lit_w = (int64_t)((n + 16 + 15) & ~15ull);
     k.job_w = k.half;
-    k.job_end = rbytes;
+    k.job_end = (int64_t)rbytes;
     k.last = -1;
     k.njobs = 0;
     k.pend_first = 0;
@@ -1924,7 +2130,7 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
   for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     FlState *sp = &d.fl[b];
     if (uni(sp->mode) != kZsJobs) continue;
-    const uint64_t region = uni64(d.blk_c0[b]) * (uint64_t)kZTokPerChunk * 4;
+    const uint64_t region = uni64(d.blk_zoff[b]);
     const int64_t half = (int64_t)uni64(sp->hdrpos), lit_end = (int64_t)uni64(sp->olen2);
     uint8_t *ents = tok8 + region + half;  // entry e at ents - 8 (e + 1)
     const int64_t cap = (int64_t)uni64(d.blk_out_len[b]);
@@ -2143,18 +2349,23 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
     FlState *sp = &d.fl[b];
     const uint32_t mode = uni(sp->mode);
     if (mode != kZsExec && mode != kZsErrCk) continue;
-    const uint8_t *region = reinterpret_cast<const uint8_t *>(d.tok + uni64(d.blk_c0[b]) * (uint64_t)kZTokPerChunk);
+    const uint8_t *region = reinterpret_cast<const uint8_t *>(d.tok) + uni64(d.blk_zoff[b]);
     const uint64_t lit0 = uni64(sp->bitpos), ent_end = uni64(sp->hdrpos);
     const uint32_t ntok = uni(sp->ntok);
     const uint64_t *ents = reinterpret_cast<const uint64_t *>(region + ent_end);  // entry e at ents[-1 - e]
     const uint32_t *lit32 = reinterpret_cast<const uint32_t *>(region + lit0);    // 16-aligned
     uint8_t *out = d.dec + uni64(d.blk_dec_off[b]);
     uint32_t olen = 0, litpos = 0, flushed = 0, fstart = 0, zerr = 0;
-    uint32_t synced = 0;  // bytes below it: flushed and visible to this wave (the last vmcnt(0) drain)
+    uint32_t synced = 0;  // bytes below it: flushed and visible to this wave
     // one group ahead: its 64 entries and the first 256 bytes of its literals
     // (from dword-aligned pf_nx; ~0: not prefetched), so a group usually
-    // starts without waiting for memory
+    // starts without waiting for memory; entries two groups ahead, so that the
+    // next group's far match sources are loaded a group ahead too (below)
     uint64_t e_nx = (uint32_t)l < ntok ? ents[-1 - (int64_t)l] : 0ull;
+    uint64_t e_n2 = 64 + (uint32_t)l < ntok ? ents[-1 - (int64_t)(64 + l)] : 0ull;
+    uint32_t fl_e2 = 0;  // `flushed` when e_n2's load was issued
+    uint32_t pf0 = 0, pf1 = 0, pf2 = 0;  // this lane's far match source in this group: its first 12 dword-aligned bytes
+    bool pfv = false;
     uint32_t pf_nx = ~0u, lit_nx = 0;
     if (lit0 + 256 <= ent_end) {
       pf_nx = 0;
@@ -2164,20 +2375,51 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
     for (uint32_t g0 = 0; g0 < ntok && !zerr; g0 += 64) {
       const uint32_t n = ntok - g0 < 64 ? ntok - g0 : 64;
       const uint64_t e = e_nx;
+      const uint32_t q0 = pf0, q1 = pf1, q2 = pf2;  // (loaded a group ago)
+      const bool qv = pfv;
       uint32_t lit_at = ~0u;  // litbuf holds literal bytes [lit_at, lit_at + 256)
       if (pf_nx != ~0u) {
         wave_lds_sync();
         litbuf[l] = lit_nx;
         lit_at = pf_nx;
       }
-      if (g0 + 64 < ntok)
-        e_nx = (uint32_t)l < ntok - g0 - 64 ? ents[-1 - (int64_t)(g0 + 64 + l)] : 0ull;
+      // The next group's entries were loaded a group ago, before any of the
+      // previous group's flush stores; vmcnt retires a wave's vector memory
+      // operations in issue order, so once their load is waited for (its first
+      // use, below), every byte flushed before it -- fl_e2 -- is visible to
+      // this wave without a vmcnt(0) drain.
+      e_nx = e_n2;
+      const uint32_t vis = fl_e2;
+      fl_e2 = flushed;
+      if (g0 + 128 < ntok)
+        e_n2 = (uint32_t)l < ntok - g0 - 128 ? ents[-1 - (int64_t)(g0 + 128 + l)] : 0ull;
       const uint32_t ll0 = (uint32_t)e & 0xffffu, ml0 = (uint32_t)(e >> 16) & 0xffffu, off = (uint32_t)(e >> 32);
       const bool mark = ll0 == kZMark;
       const uint32_t len = mark ? 0u : ll0 + ml0, lits = mark ? 0u : ll0;
       const uint32_t incl = wave_incl_sum_dpp(len), lincl = wave_incl_sum_dpp(lits);
       const uint32_t excl = incl - len, lexcl = lincl - lits;
       const unsigned long long marks = __ballot(mark);
+      pfv = false;
+      if (g0 + 64 < ntok) {
+        // the next group's far match sources (more than kZHist back, every byte
+        // visible): their first 12 dword-aligned bytes loaded now, used by its
+        // parallel round a group later -- the loads' latency hides behind this
+        // group's work instead of stalling that round (39 % of C4's sequences
+        // reach past the ring, each its own 128-B line: tools/zstd_seqstat.c)
+        const uint32_t l1 = (uint32_t)e_nx & 0xffffu, m1 = (uint32_t)(e_nx >> 16) & 0xffffu, o1 = (uint32_t)(e_nx >> 32);
+        const bool v1 = g0 + 64 + (uint32_t)l < ntok && l1 != kZMark;
+        const uint32_t len1 = v1 ? l1 + m1 : 0u;
+        const uint32_t dst1 = olen + zrl(incl, n - 1) + wave_incl_sum_dpp(len1) - len1 + l1;
+        const uint32_t src1 = dst1 - o1;
+        pfv = v1 && m1 != 0 && o1 > kZHist && o1 <= dst1 && src1 + m1 <= vis;
+        if (pfv) {
+          const uint32_t *w = reinterpret_cast<const uint32_t *>(out + (src1 & ~3u));
+          pf0 = w[0];
+          pf1 = w[1];
+          pf2 = w[2];
+        }
+        if (vis > synced) synced = vis;
+      }
       {  // the next group's literals start where this group's end
         const uint32_t na = (litpos + zrl(lincl, n - 1)) & ~3u;
         pf_nx = ~0u;
@@ -2252,9 +2494,19 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
               if ((off >= 8 || myml <= off) && (all_far || (all_ring && ss + myml + 12 <= kZRing)) &&
                   ds + myml <= kZRing) {
                 for (uint32_t k = 0; k < myml; k += 8) {
-                  const uint32_t *w = all_ring ? reinterpret_cast<const uint32_t *>(ring + ((ss + k) & ~3u))
-                                               : reinterpret_cast<const uint32_t *>(out + ((src + k) & ~3u));
-                  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = (src + k) & 3u;  // ss = src (mod 4)
+                  uint32_t w0, w1, w2;
+                  if (k == 0 && qv && all_far) {  // prefetched a group ago
+                    w0 = q0;
+                    w1 = q1;
+                    w2 = q2;
+                  } else {
+                    const uint32_t *w = all_ring ? reinterpret_cast<const uint32_t *>(ring + ((ss + k) & ~3u))
+                                                 : reinterpret_cast<const uint32_t *>(out + ((src + k) & ~3u));
+                    w0 = w[0];
+                    w1 = w[1];
+                    w2 = w[2];
+                  }
+                  const uint32_t sh = (src + k) & 3u;  // ss = src (mod 4)
                   const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
                   uint8_t *dp = ring + ds + k;
 #pragma unroll
@@ -2372,10 +2624,10 @@ __global__ void __launch_bounds__(64) k_zstd(const uint8_t *__restrict__ span, D
     if (n == 0) {  // DataDog Decompress: ErrEmptySlice
       code = kCodecZstdEmpty;
     } else {
-      uint32_t *flat = d.tok + c0 * (uint64_t)kZTokPerChunk;
+      uint32_t *flat = d.tok + uni64(d.blk_zoff[b]) / 4;
       z_flatten(span, d, c0, meta, n, flat);
       if (l == 0) {
-        // decoder state after the flattened input in the block's region (512 KiB per chunk)
+        // decoder state after the flattened input in the block's region (k_zstd_size)
         uint8_t *region = reinterpret_cast<uint8_t *>(flat);
         zx::Ctx z;
         z.s = reinterpret_cast<zx::State *>(region + ((n + 64 + 255) & ~255ull));

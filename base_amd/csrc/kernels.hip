@@ -312,6 +312,7 @@ __global__ void k_reset(Ctl *ctl, unsigned long long *nblocks) {
   else if (t == 17) ctl->seg_used = 0;
   else if (t == 18) ctl->seg_blocks = 0;
   else if (t < 23) ctl->zx[t - 19] = 0;
+  else if (t == 23) ctl->tok_need = 0;
 }
 
 void launch_reset(const DevBufs &d, unsigned long long *nblocks_dev, hipStream_t st) {

@@ -55,6 +55,11 @@ void launch_crc(const uint8_t *span, uint64_t nchunks, const DevBufs &d, const C
 void launch_compact(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
 void launch_codec_prepare(const DevBufs &d, const unsigned long long *nblocks_dev, uint64_t max_blocks,
                           uint32_t factor, hipStream_t st);
+void launch_block_scan(const unsigned long long *in, unsigned long long *out, unsigned long long *tmp,
+                       const unsigned long long *nblocks_dev, uint64_t max_blocks, hipStream_t st);
+// codec_zstd.hip: per-block decode and scratch regions from the headers
+void launch_zstd_size(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks, uint64_t max_blocks,
+                      uint32_t factor, hipStream_t st);
 void launch_codec_decode(const uint8_t *span, const DevBufs &d, const unsigned long long *nblocks_dev,
                          uint64_t max_blocks, uint64_t nchunks, int codec, uint64_t dec_cap, int rounds, int ncu,
                          hipStream_t st);
@@ -152,6 +157,11 @@ struct rio_ctx {
   unsigned long long *pend_foff = nullptr;
   hipEvent_t pend_t0 = nullptr, pend_t1 = nullptr;
   uint32_t dec_factor = 8;  // first-attempt decode-region bound: compressed bytes x this
+  // zstd: the first attempt's decode buffer (span bytes x this; regions are sized
+  // from the frames' content sizes, k_zstd_size) and scratch (kZTokInitFactor),
+  // each grown to what a run reported it needed
+  uint32_t zdec_factor = 4;
+  uint64_t ztok_want = 0;
   int fl_rounds = kFlRounds;  // flate Huffman/copy rounds per span (doubled if a block needs more)
   DevBufs d{};
   unsigned long long *nblocks_dev = nullptr;
@@ -290,7 +300,8 @@ static int alloc_bufs(rio_ctx *c) {
       dalloc(&d.blk_hdr, nb) || dalloc(&d.blk_item_base, nb + 1) || dalloc(&d.blk_status, nb) ||
       dalloc(&d.blk_a, nb) || dalloc(&d.blk_b, nb) || dalloc(&d.blk_out_len, nb) || dalloc(&d.blk_dec_off, nb + 1) ||
       dalloc(&d.blk_need, nb) || dalloc(&d.fl, nb) || dalloc(&d.blk_coff, 2 * (nb + 1)) || dalloc(&d.blk_data, nb) ||
-      dalloc(&d.blk_file_off, nb) || dalloc(&d.blk_seg, nb))
+      dalloc(&d.blk_file_off, nb) || dalloc(&d.blk_seg, nb) || dalloc(&d.blk_zneed, nb) ||
+      dalloc(&d.blk_zoff, nb + 1) || dalloc(&d.blk_zhalf, nb))
     return -1;
   if (dalloc(&d.scan_tmp, 2 * ((n + 2047) / 2048) + 16) || dalloc(&d.strad, n)) return -1;
   if (dalloc(&d.item_off, c->item_cap) || dalloc(&d.item_len, c->item_cap) || dalloc(&d.side, c->side_cap))
@@ -303,7 +314,7 @@ static void free_all(rio_ctx *c) {
   c->sd = nullptr;
   DevBufs &d = c->d;
   void *ps[] = {d.ck_size, d.ck_total, d.ck_index, d.ck_info, d.ck_crc, d.ck_block, d.ck_pay, d.ck_ssz, d.ck_sbase,
-                d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.blk_data, d.blk_file_off, d.blk_seg, d.cmp, d.item_off, d.item_len, d.side,
+                d.blk_c0, d.blk_meta, d.blk_len, d.blk_nitems, d.blk_hdr, d.blk_item_base, d.blk_status, d.blk_a, d.blk_b, d.blk_out_len, d.blk_dec_off, d.blk_need, d.blk_coff, d.blk_data, d.blk_file_off, d.blk_seg, d.blk_zneed, d.blk_zoff, d.blk_zhalf, d.cmp, d.item_off, d.item_len, d.side,
                 d.strad, d.scan_tmp, d.dec, d.fl, d.tok, d.fl_more, d.fl_ck, d.fl_seg, d.seg_scr, d.fl_stage, d.zlit, d.zjob, d.ctl, d.crc_fold, d.crc_mul, d.crc_fix_a, d.crc_fix_b,
                 c->nblocks_dev, c->d_span, c->d_v1, c->d_v1_jobs, c->d_v1_res, c->d_v1_off, c->d_v1_len,
                 c->e_blk, c->e_hdr, c->e_comp, c->e_comp2, c->e_data, c->e_out, c->e_ends, c->e_boff, c->e_zscr, c->e_ztab, c->e_ckmap, c->e_scan, c->d_seg, c->d_chain[0], c->d_chain[1], c->d_chain_meta};
@@ -556,13 +567,21 @@ static int ensure_dec(rio_ctx *c, uint64_t need) {
   return 0;
 }
 
-// flate token regions: kTokPerChunk u32 per chunk of the span (zstd: kZTokPerChunk)
-static int ensure_tok(rio_ctx *c, uint64_t nchunks, uint64_t per_chunk) {
-  const uint64_t need = nchunks * per_chunk;
+// flate token regions: kTokPerChunk u32 per chunk of the span (zstd: the
+// blocks' scratch regions, sized by k_zstd_size; `need` in u32)
+static int ensure_tok_u32(rio_ctx *c, uint64_t need) {
   if (c->d.tok_cap >= need) return 0;
   if (dalloc(&c->d.tok, need)) return -1;
   c->d.tok_cap = need;
   return 0;
+}
+static int ensure_tok(rio_ctx *c, uint64_t nchunks, uint64_t per_chunk) {
+  return ensure_tok_u32(c, nchunks * per_chunk);
+}
+static int ensure_ztok(rio_ctx *c, uint64_t nchunks) {
+  uint64_t want = nchunks * (uint64_t)kChunk * kZTokInitFactor;
+  if (want < c->ztok_want) want = c->ztok_want;
+  return ensure_tok_u32(c, (want + 3) / 4);
 }
 
 // flate split copy pass: checkpoints per chunk, segment table per block, and
@@ -600,6 +619,13 @@ static int ensure_split(rio_ctx *c, uint64_t nchunks) {
 // the scratch the last flate run's split asked for (read from its control block)
 static void note_split(rio_ctx *c) {
   if (c->h_ctl->seg_used > c->d.seg_cap && c->h_ctl->seg_used > c->seg_want) c->seg_want = c->h_ctl->seg_used;
+}
+
+// zstd scratch: what a run's regions needed (+1/8), kept for the next runs
+static int grow_ztok(rio_ctx *c, uint64_t need_bytes) {
+  const uint64_t want = need_bytes + need_bytes / 8 + 4096;
+  if (want > c->ztok_want) c->ztok_want = want;
+  return ensure_tok_u32(c, (c->ztok_want + 3) / 4);
 }
 
 // zstd job list: kZJobsPerChunk per chunk of the span
@@ -679,13 +705,22 @@ static int enqueue(rio_ctx *c, const uint8_t *span, uint64_t nchunks, uint64_t l
   }
   c->last_had_dec = false;
   if (codec != RIO_CODEC_NONE && nchunks > 0) {
-    // decode regions: factor x the compressed bytes per block (+4 KiB each)
-    if (ensure_dec(c, (uint64_t)c->dec_factor * nchunks * kChunk + nchunks * 4352ull)) return -1;
+    // decode regions: factor x the compressed bytes per block (+4 KiB each);
+    // zstd: the frames' content sizes (k_zstd_size), a smaller first guess
+    if (codec == RIO_CODEC_ZSTD ? ensure_dec(c, (uint64_t)c->zdec_factor * nchunks * kChunk + nchunks * 256ull)
+                                : ensure_dec(c, (uint64_t)c->dec_factor * nchunks * kChunk + nchunks * 4352ull))
+      return -1;
     // flate tokens / flattened zstd blocks
     if (codec == RIO_CODEC_FLATE && (ensure_tok(c, nchunks, kTokPerChunk) || ensure_split(c, nchunks))) return -1;
-    if (codec == RIO_CODEC_ZSTD && ensure_tok(c, nchunks, kZTokPerChunk)) return -1;
+    if (codec == RIO_CODEC_ZSTD && ensure_ztok(c, nchunks)) return -1;
     if (codec == RIO_CODEC_ZSTD && (ensure_zlit(c) || ensure_zjob(c, nchunks))) return -1;
-    launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
+    if (codec == RIO_CODEC_ZSTD) {  // decode and scratch regions from the headers, placed back to back
+      launch_zstd_size(span, d, c->nblocks_dev, max_blocks, c->dec_factor, st);
+      launch_block_scan(d.blk_out_len, d.blk_dec_off, d.scan_tmp, c->nblocks_dev, max_blocks, st);
+      launch_block_scan(d.blk_zneed, d.blk_zoff, d.scan_tmp, c->nblocks_dev, max_blocks, st);
+    } else {
+      launch_codec_prepare(d, c->nblocks_dev, max_blocks, c->dec_factor, st);
+    }
     if (codec == RIO_CODEC_FLATE) {
       launch_inflate_huff(span, d, c->nblocks_dev, max_blocks, nchunks, c->dec_cap, c->fl_rounds, c->ncu, st);
       if (d.seg_items && !c->split_probed && d.seg_cap == 0 && may_sync) {
@@ -933,6 +968,7 @@ static int run_span(rio_ctx *c, const uint8_t *dspan, const uint8_t *report_span
     // decode regions: blocks that overflowed theirs carry their exact size (blk_need)
     // into the next attempt; a buffer too small for all regions grows to fit
     if (codec != RIO_CODEC_NONE && (c->h_ctl->out_overflow & 0x40) && ensure_dec(c, c->h_ctl->dec_need)) return -1;
+    if ((c->h_ctl->out_overflow & kOvfZTok) && grow_ztok(c, c->h_ctl->tok_need)) return -1;
     // a flate block needed more Huffman/copy rounds than were launched
     if ((c->h_ctl->out_overflow & 0x1000) && c->fl_rounds < 64) c->fl_rounds = c->fl_rounds * 2 > 64 ? 64 : c->fl_rounds * 2;
   }
@@ -1308,6 +1344,27 @@ extern "C" int rio_sync(rio_ctx *ctx, rio_batch *out) {
   HIP_OK(hipMemcpyAsync(ctx->h_ctl, ctx->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->st));
   HIP_OK(hipStreamSynchronize(ctx->st));
   note_split(ctx);
+  // a buffer the launch found too small (decode regions, zstd scratch, items,
+  // straddlers, flate rounds): grown to what it reported and the span run
+  // again here, synchronously, as run_span's attempts do -- so an asynchronous
+  // scan's first span sizes the context instead of failing
+  for (int attempt = 1; attempt < 4; attempt++) {
+    const unsigned long long ov = ctx->h_ctl->out_overflow;
+    if (ov == 0 || (ov & kOvfLayout)) break;
+    if (grow_for_overflow(ctx, ctx->last_codec)) return -1;
+    if ((ov & 0x40) && ensure_dec(ctx, ctx->h_ctl->dec_need)) return -1;
+    if ((ov & kOvfZTok) && grow_ztok(ctx, ctx->h_ctl->tok_need)) return -1;
+    if ((ov & 0x1000) && ctx->fl_rounds < 64) ctx->fl_rounds = ctx->fl_rounds * 2 > 64 ? 64 : ctx->fl_rounds * 2;
+    if (enqueue(ctx, ctx->last_span, ctx->last_nchunks, UINT64_MAX, 1, (ctx->last_in_bytes % kChunk) != 0,
+                ctx->last_codec, ctx->last_mode, true, attempt, 0, false))
+      return -1;
+    if (ctx->last_nseg)
+      launch_block_files(ctx->d, ctx->d_seg, ctx->d_seg + ctx->last_nseg, ctx->last_nseg,
+                         ctx->last_nchunks ? ctx->last_nchunks : 1, ctx->st);
+    HIP_OK(hipMemcpyAsync(ctx->h_ctl, ctx->d.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, ctx->st));
+    HIP_OK(hipStreamSynchronize(ctx->st));
+    note_split(ctx);
+  }
 #ifdef RIO_ZPROF  // profiling builds: where the zstd entropy pass spends its cycles
   if (ctx->last_codec == RIO_CODEC_ZSTD)
     fprintf(stderr, "rio: zstd blocks on the serial path: %llu; entropy-pass cycles lit %llu tables %llu seq %llu block %llu\n",
@@ -1427,6 +1484,7 @@ static int decode_raw(rio_ctx *c, const uint8_t *const *payloads, const uint32_t
     const unsigned long long ov = c->h_ctl->out_overflow;
     if (ov == 0) break;
     if ((ov & 0x40) && ensure_dec(c, c->h_ctl->dec_need)) return -1;
+    if ((ov & kOvfZTok) && grow_ztok(c, c->h_ctl->tok_need)) return -1;
     if ((ov & 0x1000) && c->fl_rounds < 64) c->fl_rounds = c->fl_rounds * 2 > 64 ? 64 : c->fl_rounds * 2;
   }
   if (c->h_ctl->out_overflow) {

@@ -124,6 +124,7 @@ struct Ctl {
   unsigned long long seg_used;                    // flate split copy: scratch bytes the blocks asked for (k_flate_plan)
   unsigned long long seg_blocks;                  // flate split copy: blocks split
   unsigned long long zx[4];                       // (RIO_ZPROF builds: zstd execution pass groups, parts, ready, rest matches)
+  unsigned long long tok_need;                    // zstd: scratch bytes every block's region needs (kOvfZTok)
 };
 
 constexpr unsigned long long kNone = ~0ull;
@@ -167,7 +168,12 @@ struct FlState {
 };
 constexpr int kFlRounds = 6;          // Huffman/copy rounds launched per span
 constexpr int kTokPerChunk = kChunk;  // token region: 32,768 u32 per chunk of the block
-constexpr int kZTokPerChunk = 4 * kTokPerChunk;  // zstd scratch: input copy, literals, entries | jobs
+// zstd scratch: each block's region (flattened input, literals, execution
+// entries | jobs) is sized from its headers by k_zstd_size and placed back to
+// back (blk_zoff); the first attempt's buffer is this many bytes per span byte
+// (a run that needs more reports it, tok_need, and the host retries)
+constexpr uint64_t kZTokInitFactor = 5;
+constexpr unsigned long long kOvfZTok = 0x4000;  // out_overflow: the zstd scratch regions exceed tok_cap
 constexpr int kZJobsPerChunk = 16;               // zstd job list capacity (a block past it takes the serial path)
 // Split copy pass (codec_flate.hip k_flate_plan / k_flate_seg / k_flate_segfix):
 // segments per block at most, and the shortest segment
@@ -202,6 +208,9 @@ struct DevBufs {
   unsigned long long *blk_data;       // item-end output: where the block's payload lies (rio_batch.block_data)
   unsigned long long *blk_file_off;   // segment scans: the block's offset in its file
   unsigned long long *blk_seg;        // segment scans: the block's file (segment index)
+  unsigned long long *blk_zneed;      // zstd: the block's scratch region bytes (k_zstd_size)
+  unsigned long long *blk_zoff;       // zstd: exclusive scan of blk_zneed (n + 1): region offsets in tok
+  unsigned long long *blk_zhalf;      // zstd: region bytes below the jobs (input, literals, entries)
   // outputs: item views into the span or the records buffer (side / dec); in
   // item-end mode (ParseArgs::end_mode) item_off holds item_end (cumSize) instead
   unsigned long long *item_off, *item_len;
@@ -214,7 +223,8 @@ struct DevBufs {
   uint64_t cmp_cap;
   uint64_t dec_cap;              // bytes at dec
   FlState *fl;                   // per block (flate)
-  uint32_t *tok;                 // flate tokens: block b's region starts at blk_c0[b] * kTokPerChunk
+  uint32_t *tok;                 // flate tokens: block b's region starts at blk_c0[b] * kTokPerChunk;
+                                 // zstd: block b's scratch at byte blk_zoff[b]
   uint64_t tok_cap;              // u32 entries at tok
   uint64_t tok_limit;            // tokens per block and round (0: the whole region; rio_config.flate_tok_limit)
   uint64_t fl_grid;              // Huffman-pass workgroups (0: all resident; rio_config.flate_grid)

@@ -94,6 +94,17 @@ def pmc_traffic(kernel: str, replicas: int):
 
 
 REHEARSE = os.environ.get("RIO_BENCH_REHEARSE") == "1"  # N ranks on one GPU over gloo (rehearsal only)
+
+
+def mem_share(args, world):
+    """Fraction of the per-GPU workload sizes a rank runs: 1 (every rank has its
+    own GPU); in a rehearsal (RIO_BENCH_REHEARSE=1, every rank on GPU 0) 1/world
+    unless --mem-share says otherwise, so that the ranks' buffers together fit
+    the one GPU's HBM. Only the auto-sized defaults scale (C2 replicas, C3 / C4
+    replicas, C5 batch size); explicit sizes are kept."""
+    if args.mem_share > 0:
+        return args.mem_share
+    return 1.0 / world if REHEARSE else 1.0
 _T0 = time.perf_counter()
 
 
@@ -135,7 +146,8 @@ def c3_flate(args, local, world, dist):
     import bench_flate
     cpu_s = args.cpu_s if (world == 1 and not args.no_cpu_baseline) else 0.0
     r = bench_flate.run_c3(replicas=args.flate_replicas, steps=max(2, min(args.steps, 5)), warmup=1,
-                           device=local, check=True, cpu_s=cpu_s, pipeline=args.flate_pipeline)
+                           device=local, check=True, cpu_s=cpu_s, pipeline=args.flate_pipeline,
+                           share=mem_share(args, world))
     if dist is not None:
         t = torch.tensor([r["ms_per_step"]], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -165,7 +177,8 @@ def c3_flate_16k(args, local, world, dist):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_flate
     r = bench_flate.run_c3(replicas=args.flate_replicas, steps=max(2, min(args.steps, 5)), warmup=2,
-                           per_block=16384, device=local, check=True, pipeline=args.flate16k_pipeline)
+                           per_block=16384, device=local, check=True, pipeline=args.flate16k_pipeline,
+                           share=mem_share(args, world))
     if dist is not None:
         t = torch.tensor([r["ms_per_step"]], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -192,7 +205,8 @@ def c4_zstd(args, local, world, dist):
     import bench_zstd
     cpu_s = args.cpu_s if (world == 1 and not args.no_cpu_baseline) else 0.0
     r = bench_zstd.run_c4(replicas=args.zstd_replicas, steps=max(2, min(args.steps, 3)), warmup=1, device=local,
-                          check=True, cpu_s=cpu_s, contexts=args.zstd_contexts, pipeline=args.zstd_pipeline)
+                          check=True, cpu_s=cpu_s, contexts=args.zstd_contexts, pipeline=args.zstd_pipeline,
+                          share=mem_share(args, world))
     if dist is not None:
         t = torch.tensor([r["ms_per_step"]], device=coll_dev(local), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -274,7 +288,7 @@ def c5_flate(args, local, rank, world, dist):
         nb_, n, cut = len(index[k]), body_len[k], rel[k][rot(f)]
         return [spans[k][0] + (rel[k][(r + j) % nb_] - cut) % n for j in range(nb_)]
     # batches of whole file bodies, <= args.c5_batch_gib each
-    cap = int(args.c5_batch_gib * 2 ** 30)
+    cap = int(args.c5_batch_gib * mem_share(args, world) * 2 ** 30)
     batches, cur, cur_b = [], [], 0
     for f in mine:
         n = body_len[f % c5_data.N_BASE]
@@ -436,7 +450,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--replicas", type=int, default=REPLICAS)
+    ap.add_argument("--replicas", type=int, default=0, help="C2 replicas (0: %d x the rank's memory share)" % REPLICAS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-flate", action="store_true", help="skip the C3 flate measurement (configs[2])")
     ap.add_argument("--flate-replicas", type=int, default=0, help="0: enough for 10 GiB of records")
@@ -459,6 +473,8 @@ def main():
     ap.add_argument("--c2-contexts", type=int, default=2, help="C2: contexts the steps rotate over (1-3; n > 1: n - 1 steps in flight beside the one collected)")
     ap.add_argument("--c5-batch-gib", type=float, default=4.0, help="file bodies per decode batch")
     ap.add_argument("--c5-cache", default="/tmp", help="host directory caching the C5 base files")
+    ap.add_argument("--mem-share", type=float, default=0.0,
+                    help="scale of the auto-sized workloads per rank (0: 1, or 1/world in a RIO_BENCH_REHEARSE run)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -494,6 +510,8 @@ def main():
 
     from base_amd.recordio import gpu
     gpu.load()  # refuses a library whose build id is not this tree's (base_amd/build.py)
+    if args.replicas <= 0:
+        args.replicas = max(1, int(round(REPLICAS * mem_share(args, world))))
 
     progress(rank, "C2: %d GPU(s)" % world)
     data, nrec = make_c2_file()

@@ -815,6 +815,9 @@ static seq_t decode_seq(zctx *z, bitd_t *b, uint32_t *sll, uint32_t *sml, uint32
  * still counted, so that the checks of later sequences see the unlimited
  * buffer's positions. */
 static int exec_seq(zctx *z, const seq_t *s, size_t *lit_pos, size_t lit_size, int *full) {
+#ifdef ORC_SEQ_HOOK /* (tools/zstd_seqstat.c: sequence statistics; never in the oracle build) */
+    ORC_SEQ_HOOK(z, s);
+#endif
     if (s->ll > lit_size - *lit_pos) return -1;
     const int64_t produced = z->olen + (int64_t)s->ll - z->frame_start;
     if (s->off > (uint64_t)produced) return -1;

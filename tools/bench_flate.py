@@ -168,7 +168,7 @@ def replicas_for(rec_bytes: int) -> int:
 
 
 def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0, check=True, cpu_s=0.0,
-           flate_split=True, contexts=1, pipeline=1):
+           flate_split=True, contexts=1, pipeline=1, share=1.0):
     """The C3 workload on cuda:`device` (replicas=0: enough for 10 GiB of records);
     returns the measurement dict (no print). cpu_s > 0 adds the one-core and
     all-core CPU baselines (zlib inflate) on the base file."""
@@ -186,7 +186,7 @@ def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0
         return w
 
     if replicas <= 0:
-        replicas = replicas_for(rec_bytes)
+        replicas = max(1, int(round(replicas_for(rec_bytes) * share)))
     res = measure(data, nrec, rec_bytes, want, gpu.RIO_CODEC_FLATE,
                   "C3-like flate FASTQ, %d records/block" % per_block, replicas, steps, warmup, device, check,
                   flate_split, contexts, pipeline)

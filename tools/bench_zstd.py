@@ -40,7 +40,7 @@ def load_or_make(base_mib, workers, path=None):
 
 
 def run_c4(base_mib=128, replicas=0, steps=5, warmup=1, device=0, check=True, cpu_s=0.0, workers=16, data_path=None,
-           contexts=1, pipeline=1):
+           contexts=1, pipeline=1, share=1.0):
     """The C4 workload (replicas=0: enough for 10 GiB of records); cpu_s > 0 adds
     the one-core and all-core CPU baselines (libzstd) on the base file."""
     import bench_flate
@@ -51,7 +51,7 @@ def run_c4(base_mib=128, replicas=0, steps=5, warmup=1, device=0, check=True, cp
     data, nblk, nrec, rec_bytes = load_or_make(base_mib, workers, data_path)
     gen_s = time.perf_counter() - t0
     if replicas <= 0:
-        replicas = bench_flate.replicas_for(rec_bytes)
+        replicas = max(1, int(round(bench_flate.replicas_for(rec_bytes) * share)))
     res = bench_flate.measure(data, nrec, rec_bytes, lambda: c4_data.all_records(nblk), gpu.RIO_CODEC_ZSTD,
                               "C4-like zstd level 5, records 64 B-64 KiB log-uniform, 1 MiB blocks",
                               replicas, steps, warmup, device, check, contexts=contexts,

@@ -47,6 +47,11 @@ while [ $# -gt 0 ]; do
       step r06_prof_c4 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r06_prof_c4 -o run -- \
         python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 2 ;;
     e2e) step r06_e2e 600 python3 tools/bench_e2e.py ;;
+    c4p*)  # C4 alone, steps rotating over N context sets (c4p1: serial)
+      [ -f /tmp/c4.bin ] || python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/r06_c4data.log 2>&1
+      step r06_$1 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 4 --pipeline ${1#c4p} ;;
+    ztests) step r06_ztests 600 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests/test_zstd_gpu.py \
+        tests/test_zstd_libzstd.py tests/test_chain_gpu.py tests/test_structural_fuzz_gpu.py -m gpu ;;
     pmcc4)  # FETCH_SIZE / WRITE_SIZE per kernel over an 8-replica C4 step (tools/pmc_summary.py)
       [ -f /tmp/c4.bin ] || python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/r06_c4data.log 2>&1
       for g in FETCH_SIZE WRITE_SIZE; do
