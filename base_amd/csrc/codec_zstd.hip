@@ -1071,7 +1071,10 @@ struct ZSerialSink {
 // split so that each is at most kZPiece bytes (copying a long match in pieces
 // with the same offset is the same copy). Frame ends are marked: ll = 0xFFFF
 // with ml = 0xFFFF (checksum = offset field) or 0xFFFE (no checksum).
-constexpr uint32_t kZPiece = 2048;
+#ifndef RIO_ZPIECE
+#define RIO_ZPIECE 2048
+#endif
+constexpr uint32_t kZPiece = RIO_ZPIECE;
 constexpr uint32_t kZMark = 0xFFFF;
 constexpr uint32_t kZMarkCk = 0xFFFF, kZMarkNoCk = 0xFFFE;
 
@@ -1635,7 +1638,7 @@ __global__ void k_zstd_size(const uint8_t *__restrict__ span, DevBufs d, const u
       ZSz z;
       if (z_size_walk(in, z)) {
         out = z.content;
-        const uint64_t ents = z.nseq + z.bound / kZPiece + 2 * z.njobs + z.nframes + 136;
+        const uint64_t ents = z.nseq + z.bound / kZPiece + 2 * z.njobs + z.nframes + 2 * (kZBlockMax / kZPiece) + 8;
         half = (in_area + z.lits + 64 + 8 * ents + 15) & ~15ull;
         need = half + z.jobs_bytes;
       } else {  // the passes find the error (or decline to the serial decoder)
@@ -1808,7 +1811,9 @@ constexpr int kZs2Ring = 32;
 // Measured and kept out (round 3; A/B on one box, C4 ms per step): the ring
 // dword of the next reload loaded a reload ahead (150.2 against 147.0) and the
 // LL / ML code baselines computed instead of looked up (153.2; both 155.0) --
-// this pass's pace is set by where the compiler places its LDS waits.
+// this pass's pace is set by where the compiler places its LDS waits. Round 6:
+// a sequence's three ring dwords read with its table lookups, so that no
+// reload waits on an LDS read of its own: 40.7 GiB/s against 40.7-40.9.
 struct ZBr64 {
   const uint32_t *w;
   uint64_t win;
@@ -2182,12 +2187,18 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
           break;
         }
         const uint64_t *raw = reinterpret_cast<const uint64_t *>(tok8 + raw_off);
-        uint64_t rv_nx = (uint32_t)l < nseq ? raw[l] : 0ull;  // one group ahead
+        // raw sequences three groups ahead: a group's work (~200 instructions)
+        // is far shorter than a load's latency under load, so with one group in
+        // flight each wave waited out most of every load
+        auto ld = [&](uint32_t at) { return at + (uint32_t)l < nseq ? raw[at + l] : 0ull; };
+        uint64_t rv_1 = ld(0), rv_2 = ld(64), rv_3 = ld(128);
         for (uint32_t g0 = 0; g0 < nseq; g0 += 64) {
           const uint32_t cnt = nseq - g0 < 64 ? nseq - g0 : 64;
           const bool v = (uint32_t)l < cnt;
-          const uint64_t rv = rv_nx;
-          if (g0 + 64 < nseq) rv_nx = (uint32_t)l < nseq - g0 - 64 ? raw[g0 + 64 + l] : 0ull;
+          const uint64_t rv = rv_1;
+          rv_1 = rv_2;
+          rv_2 = rv_3;
+          if (g0 + 192 < nseq) rv_3 = ld(g0 + 192);
           const uint32_t ll = (uint32_t)rv & 0x1FFFFu, ml = (uint32_t)(rv >> 17) & 0x3FFFFu;
           const uint32_t ofv = (uint32_t)(rv >> 35);
           // Repeat offsets: a sequence maps the offset history (rep0, rep1, rep2)
@@ -2291,7 +2302,7 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
   }
 }
 
-// ---------------------------------------------------------------- k_zstd_exec (previous)
+// ---------------------------------------------------------------- k_zstd_exec
 // Execution pass, one wave per block: the entries in groups of 64, cut into
 // parts of at most kZPart output bytes (and at frame ends); per part the
 // literals are staged from the literal area into LDS, literal runs written,
@@ -2299,21 +2310,26 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
 // part's first match, the rest in order, each by the whole wave -- into an LDS
 // ring holding the last kZHist bytes; completed 1 KiB units are flushed to the
 // decode region 16 B per lane. Sources further back than the ring are read
-// from the decode region (flushed, made visible by vmcnt(0) first).
+// from the decode region: a group's far sources are loaded a group ahead
+// (visible by vmcnt's in-order retirement, see the loop), the rest after a
+// vmcnt(0) drain. Round 6: with far sources prefetched, an 8 KiB ring at 12
+// waves per CU beats 20 KiB at 6 (C4 33.2 -> 40.8 GiB/s pipelined, 29.6 -> 35.1
+// serial, A/B on one box, profiles/r06_zstd_ring_ab.jsonl).
 #ifndef RIO_ZRING_K
-#define RIO_ZRING_K 5
+#define RIO_ZRING_K 2
 #endif
 #ifndef RIO_ZEXEC_READY_MAX
 #define RIO_ZEXEC_READY_MAX 32  // longest match a lane copies on its own in the parallel round
 #endif
 constexpr uint32_t kZRingK = RIO_ZRING_K;  // ring = kZRingK x 4 KiB
+static_assert(kZRingK >= 2, "zr_slot's multiply-high reciprocal needs kZRingK >= 2");
 constexpr uint32_t kZRing = kZRingK * 4096;
 constexpr uint32_t kZPart = 2 * kZPiece;
 constexpr uint32_t kZHist = kZRing - kZPart;
 #ifndef RIO_ZEXEC_WAVES
-#define RIO_ZEXEC_WAVES 6
+#define RIO_ZEXEC_WAVES 12
 #endif
-constexpr int kZExecWaves = RIO_ZEXEC_WAVES;  // per CU (~25 KiB LDS each)
+constexpr int kZExecWaves = RIO_ZEXEC_WAVES;  // per CU (~12 KiB LDS each at the default ring)
 
 // x mod kZRing: (x >> 12) / kZRingK by a multiply-high, exact below 2^20
 __device__ __forceinline__ uint32_t zr_slot(uint32_t x) {

@@ -142,6 +142,35 @@ def test_high_ratio_blocks_retry(ctx):
     assert err == "" and items == recs + recs
 
 
+def test_async_scan_grows_zstd_scratch(gpu_lib):
+    # an asynchronous device scan whose zstd scratch regions (k_zstd_size: the
+    # literal area holds every block's literals, RLE blocks included) outgrow the
+    # context's first allocation (5x the span): rio_sync grows it and runs the
+    # span again, and the records come back whole -- on the first scan of a
+    # fresh context and on the next one
+    import torch
+    from base_amd.recordio import format as F
+    from base_amd.recordio import gpu
+    from base_amd.recordio.codecs import have_zstd, zstd_compress_ex
+    if not have_zstd():
+        pytest.skip("libzstd not present to write the fixtures")
+    recs = [b"\0" * (3 << 20), b"ab" * 100000, bytes(range(256)) * 64, b""]
+    payload = F.packed_block_payload(recs)
+    blocks = [zstd_compress_ex(payload, 5, False, True), zstd_compress_ex(payload, 1, True, False)]
+    data = zstd_file(blocks)
+    body = data[32768:]
+    dev = torch.frombuffer(bytearray(body), dtype=torch.uint8).to("cuda:0")
+    ctx = gpu.Context(0, max_span_bytes=len(body) + 32768, item_end=True)
+    try:
+        for _ in range(2):
+            ctx.scan_device_async(dev.data_ptr(), len(body), 32768, gpu.RIO_CODEC_ZSTD)
+            b = ctx.sync()
+            assert b.err.code == 0 and b.stop == gpu.RIO_STOP_EOF, b.err.msg
+            assert gpu.device_batch_items(b, body) == recs + recs
+    finally:
+        ctx.close()
+
+
 def test_many_small_blocks(ctx, oracle):
     from base_amd.recordio.writer import write_file, WriterOpts
     recs = mixed_records(21, 3000, big=200)

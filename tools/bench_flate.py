@@ -22,8 +22,53 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md), as bench.py
+
+
+def pmc_decode_traffic(pmc_file, kernels, replicas):
+    """HBM bytes per step of the decode stage's kernels from a committed PMC pass
+    (tools/gpu_r06.sh pmcc4 / pmc16k: rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE over
+    a one-step run of `pmc_replicas` replicas, FETCH_SIZE doubled per
+    MI355X_MICROARCH.md), scaled to this run's replica count; None without it."""
+    if not pmc_file or not os.path.exists(pmc_file):
+        return None
+    with open(pmc_file) as f:
+        pm = json.load(f)
+    n = pm.get("pmc_replicas")
+    tot = 0.0
+    if not n:
+        return None
+    for k in kernels:  # (a kernel the run did not launch -- e.g. no block took that path -- adds nothing)
+        e = pm.get("per_kernel", {}).get(k)
+        if e:
+            tot += e["fetch_bytes"] + e["write_bytes"]
+    return int(tot * replicas / n)
+
+
+def dominant_kernel(trace_summary, name):
+    """A kernel's median launch time from a committed one-context kernel-trace
+    summary (tools/ktrace_summary.py --json over rocprofv3 --kernel-trace of the
+    workload's own bench command): {kernel, ms, source}, or None."""
+    if not os.path.exists(trace_summary):
+        return None
+    with open(trace_summary) as f:
+        tr = json.load(f)
+    for k, v in tr.items():
+        if name in k:
+            return {"kernel": name, "median_ms": v["median_ms"], "launches": v["calls"],
+                    "source": os.path.relpath(trace_summary, ROOT)}
+    return None
+
+
+FLATE_DECODE_KERNELS = ["rio::k_codec_prepare", "rio::k_flate_sync<1>", "rio::k_flate_sync<4>", "rio::k_flate_plan",
+                        "rio::k_flate_tok", "rio::k_flate_lz2", "rio::k_flate_seg", "rio::k_flate_segfix",
+                        "rio::k_inflate_exact"]
+ZSTD_DECODE_KERNELS = ["rio::k_zstd_size", "rio::k_zstd_ent", "rio::k_zstd_seq2", "rio::k_zstd_fix", "rio::k_zstd_exec",
+                       "rio::k_zstd"]
+
+
 def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, warmup, device=0, check=True,
-            flate_split=True, contexts=1, pipeline=1):
+            flate_split=True, contexts=1, pipeline=1, roof=None):
     """One compressed workload on cuda:`device`: the base file `data` copied to
     HBM, its body replicated `replicas` times; one step = the scan pipeline over
     the whole device-resident span. Parity: the base file's items (device path)
@@ -123,6 +168,15 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
     dt = (time.perf_counter() - t0) / steps
     stages = stages or [[0.0] * 5]
     st = np.mean(np.array(stages), axis=0)
+    # the decode stage alone: a few steps on one context set, each synchronous
+    # (after the timed region), its HIP events around the codec's kernels --
+    # the roofline's kernel_ms, as bench.py times k_crc for C2
+    dec_one = []
+    if roof is not None and len(parts) == 1:
+        for _ in range(3):
+            launch(ctxs)
+            ctxs[0].sync()
+            dec_one.append(ctxs[0].stage_times()[1])
     timed_parity = None
     if check:  # the last timed step's output: every record of every replica, on the GPU
         import devcheck
@@ -135,6 +189,21 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
             timed_parity["bytes_checked"] += chk["bytes_checked"]
         del w, wl
     out_bytes = rec_bytes * replicas
+    roofline = None
+    if dec_one:
+        # algorithmic bytes of the decode stage per launch: the compressed span
+        # read once + the decoded records written once (SURVEY.md §8(d) B_in + B_rec)
+        alg = span_len + out_bytes
+        ms = float(np.median(dec_one))
+        ach = alg / (ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4),
+                    "traffic": pmc_decode_traffic(roof.get("pmc"), roof["kernels"], replicas),
+                    "kernel": "decode stage (%s)" % ", ".join(roof["kernels"]), "kernel_ms": round(ms, 3),
+                    "kernel_ms_source": "HIP events around the decode stage on its stream, one context set, steps "
+                                        "synchronous",
+                    "alg_bytes_per_launch": alg, "dominant_kernel": roof.get("dominant"),
+                    "note": roof.get("note")}
     split_blocks = sum(c.flate_split_blocks() for c in last) if codec == gpu.RIO_CODEC_FLATE else 0
     for cs in sets:
         for c in cs:
@@ -153,6 +222,7 @@ def measure(data, nrec, rec_bytes, want_fn, codec, workload, replicas, steps, wa
                    "records_bytes": out_bytes},
         "parity": parity and bool(timed_parity and timed_parity["ok"]),
         "parity_timed_output": timed_parity,
+        "roofline": roofline,
         "split_blocks": split_blocks, "contexts": nctx, "pipeline": npipe,
         "serial": None if serial is None else {
             "value": round(span_len / serial / 2 ** 30, 2), "ms_per_step": round(serial * 1e3, 3),
@@ -187,9 +257,15 @@ def run_c3(base_mib=128, replicas=0, steps=5, warmup=1, per_block=1024, device=0
 
     if replicas <= 0:
         replicas = max(1, int(round(replicas_for(rec_bytes) * share)))
+    tag = "c3_16k" if per_block >= 16384 else "c3"
+    roof = {"kernels": FLATE_DECODE_KERNELS, "pmc": os.path.join(ROOT, "profiles", "r06_%s_pmc.json" % tag),
+            "dominant": dominant_kernel(os.path.join(ROOT, "profiles", "r06_%s_kernel_trace_summary.json" % tag),
+                                        "k_flate_seg" if per_block >= 16384 else "k_flate_sync<1>"),
+            "note": "compressed bytes in + decoded records out over the decode stage; the Huffman and copy "
+                    "passes are instruction-issue and latency bound (DESIGN.md §4), so frac is far below 1"}
     res = measure(data, nrec, rec_bytes, want, gpu.RIO_CODEC_FLATE,
                   "C3-like flate FASTQ, %d records/block" % per_block, replicas, steps, warmup, device, check,
-                  flate_split, contexts, pipeline)
+                  flate_split, contexts, pipeline, roof=roof)
     res["config"]["gen_s"] = round(gen_s, 1)
     if cpu_s > 0:
         import cpu_base

@@ -58,6 +58,11 @@ while [ $# -gt 0 ]; do
         step r06_pmc_c4_$g 150 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c4_$g -o run -- \
           python3 -u tools/bench_zstd.py --data /tmp/c4.bin --steps 1 --warmup 0 --replicas 8
       done ;;
+    pmcc3)
+      for g in FETCH_SIZE WRITE_SIZE; do
+        step r06_pmc_c3_$g 150 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c3_$g -o run -- \
+          python3 -u tools/bench_flate.py --steps 1 --warmup 0 --replicas 8
+      done ;;
     pmc16k)
       for g in FETCH_SIZE WRITE_SIZE; do
         step r06_pmc_c3_16k_$g 150 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c3_16k_$g -o run -- \
