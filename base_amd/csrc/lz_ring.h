@@ -10,6 +10,9 @@ constexpr uint32_t kL2Ring = 4096, kL2Mask = kL2Ring - 1;
 constexpr uint32_t kL2Span = 1536;                   // output bytes per batch at most
 constexpr uint32_t kL2Near = kL2Ring - kL2Span - 16;  // bytes before the batch kept in the ring (the
                                                        // batch's zeroing may round up one dword)
+#ifndef RIO_ABL_FAR
+#define RIO_ABL_FAR 0
+#endif
 #ifndef RIO_L2_WAVES
 #define RIO_L2_WAVES 20  // 5 per SIMD: k_flate_lz2 is register-allocated for that (RIO_LZ2_WPE)
 #endif
@@ -38,6 +41,9 @@ __device__ __forceinline__ void l2_copy4(uint8_t *ring, const uint32_t *gw, cons
                                          const uint32_t (&p)[4], const uint32_t (&n)[4], uint32_t glob,
                                          const uint32_t *gl = nullptr, uint32_t litm = 0) {
   uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
+#if RIO_ABL_FAR  // measurement-only builds: far sources read from the ring (wrong bytes; what their loads cost)
+  glob = 0;
+#endif
   // per slot (recomputed where used, to keep registers for occupancy): the
   // destination t = B0 + p, its dwords [t/4, (t+n+3)/4), and the source dword
   // under the first one, floor((s - t%4) / 4) (~0 for -1)

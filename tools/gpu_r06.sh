@@ -56,17 +56,17 @@ while [ $# -gt 0 ]; do
       [ -f /tmp/c4.bin ] || python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/r06_c4data.log 2>&1
       for g in FETCH_SIZE WRITE_SIZE; do
         step r06_pmc_c4_$g 150 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c4_$g -o run -- \
-          python3 -u tools/bench_zstd.py --data /tmp/c4.bin --steps 1 --warmup 0 --replicas 8
+          python3 -u tools/bench_zstd.py --data /tmp/c4.bin --steps 1 --warmup 0 --replicas ${PMC_REPLICAS:-8}
       done ;;
     pmcc3)
       for g in FETCH_SIZE WRITE_SIZE; do
         step r06_pmc_c3_$g 150 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c3_$g -o run -- \
-          python3 -u tools/bench_flate.py --steps 1 --warmup 0 --replicas 8
+          python3 -u tools/bench_flate.py --steps 1 --warmup 0 --replicas ${PMC_REPLICAS:-8}
       done ;;
     pmc16k)
       for g in FETCH_SIZE WRITE_SIZE; do
         step r06_pmc_c3_16k_$g 150 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c3_16k_$g -o run -- \
-          python3 -u tools/bench_flate.py --steps 1 --warmup 0 --replicas 8 --per-block 16384
+          python3 -u tools/bench_flate.py --steps 1 --warmup 0 --replicas ${PMC_REPLICAS:-8} --per-block 16384
       done ;;
     rehearse2)  # two ranks on the one GPU, collectives over gloo (bench.py REHEARSE sizes)
       step r06_rehearse2 900 env RIO_BENCH_REHEARSE=1 python3 bench.py --gpus 2 --steps 5 --warmup 2 ;;
