@@ -1839,6 +1839,28 @@ struct ZBr64 {
       avail += 32;
     }
   }
+  // the same from three ring dwords read at the sequence's start (D_c0 ..
+  // D_c0+2: a sequence takes at most three), so that no reload waits for an
+  // LDS read of its own (k_zstd_seq4)
+  // (the sequence's first reload can only take D_c0, its second D_c0 or D_c0+1)
+  __device__ __forceinline__ void reload_pf(uint32_t p) {
+    const bool rl = avail <= 32;
+    const uint64_t nw = (win << 32) | p;
+    win = rl ? nw : win;
+    cons += rl ? 1 : 0;
+    avail += rl ? 32 : 0;
+  }
+  __device__ __forceinline__ void reload_pf(uint32_t p0, uint32_t p1, int32_t c0) {
+    reload_pf(cons == c0 ? p0 : p1);
+  }
+  __device__ __forceinline__ void reload_pf(uint32_t p0, uint32_t p1, uint32_t p2, int32_t c0) {
+    const int32_t k = cons - c0;
+    reload_pf(k == 0 ? p0 : (k == 1 ? p1 : p2));
+  }
+  // nb (<= 31) bits at off above the read position (the container's bit avail), not consumed
+  __device__ __forceinline__ uint32_t field(uint32_t off, uint32_t nb) const {
+    return (uint32_t)(win >> (avail + (int32_t)off)) & ((1u << nb) - 1u);
+  }
   __device__ __forceinline__ uint32_t read(int nb) {  // nb <= 31
     avail -= nb;
     return (uint32_t)(win >> avail) & ((1u << nb) - 1u);
@@ -1861,6 +1883,9 @@ __device__ __forceinline__ void zs2_settle(T &x) {
 constexpr int kZs2Jobs = RIO_ZS2_JOBS;         // job slots per wave
 constexpr int kZs2Groups = 15 / kZs2Jobs;      // 4-wave workgroups per CU (60 slots' tables fill the LDS)
 constexpr int kZs2Cells = 512 + 512 + 256;  // ll (log <= 9), ml (<= 9), of (<= 8)
+#ifndef RIO_ZS2_QUAD
+#define RIO_ZS2_QUAD 1  // the sequence pass with a quad of lanes per job (k_zstd_seq4); 0: k_zstd_seq2
+#endif
 
 __device__ __forceinline__ uint16_t zs2_cell(uint32_t c, int log) {
   const uint32_t sym = c & 0xffu, nb = (c >> 8) & 0xffu, base = c >> 16;
@@ -2092,6 +2117,250 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
     if (pne > 5) raw[pi0 + 5] = E5;
     if (pne > 6) raw[pi0 + 6] = E6;
     if (pne > 7) raw[pi0 + 7] = E7;
+  }
+}
+
+// ---------------------------------------------------------------- k_zstd_seq4
+// The sequence pass with a QUAD of lanes per job (round 6). k_zstd_seq2 gives
+// each job one lane, so a step decodes the three FSE symbols (literal length,
+// match length, offset) one after the other in that lane, with 15 of 64 lanes
+// live: ~164 wave instructions per sequence, and with one wave per SIMD (the
+// tables fill the LDS) every instruction is on the chain. Here lanes 4q .. 4q+3
+// share job q: lane role 0 owns the literal-length state, 1 the match-length
+// state, 2 the offset state (3 shadows role 0). Each lane looks up its own
+// table cell and code, the quad exchanges the six bit counts by DPP
+// quad-broadcasts, and every lane advances the same bit container (the reads'
+// positions depend on all six counts) while extracting only its own fields.
+// The three ring dwords a sequence may need are read with the table lookups,
+// so no reload waits on an LDS read of its own. Same tables, rings, jobs,
+// entries, checks and errors as k_zstd_seq2.
+template <int kSel>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {  // lane (4q + kSel)'s v, on all four lanes
+  constexpr int kCtl = kSel | (kSel << 2) | (kSel << 4) | (kSel << 6);  // quad_perm [k, k, k, k]
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtl, 0xf, 0xf, false);
+}
+
+__global__ void __launch_bounds__(256) k_zstd_seq4(DevBufs d) {
+  __shared__ uint16_t tabs[4][kZs2Jobs][kZs2Cells];
+  __shared__ uint32_t rings[4][kZs2Jobs][kZs2Ring];
+  __shared__ uint32_t codes[36 + 53];  // ZCodes: ll at 0, ml at 36
+  const int l = lane_id(), wv = (int)(threadIdx.x >> 6);
+  const int q = l >> 2, role = l & 3;
+  for (int u = (int)threadIdx.x; u < 36; u += 256) codes[u] = kZCodes.ll[u];
+  for (int u = (int)threadIdx.x; u < 53; u += 256) codes[36 + u] = kZCodes.ml[u];
+  __syncthreads();
+  uint8_t *tok8 = reinterpret_cast<uint8_t *>(d.tok);
+  const uint64_t nj0 = d.ctl->zjob_n, nj = nj0 < d.zjob_cap ? nj0 : d.zjob_cap;
+  const bool slot = q < kZs2Jobs;
+  const int qs = slot ? q : 0;
+  // this lane's table: cells at toff, codes at cbase, accuracy log (set per job)
+  const uint32_t toff = role == 1 ? 512u : (role == 2 ? 1024u : 0u);
+  const uint32_t cbase = role == 1 ? 36u : 0u;
+  const uint32_t slim = role == 1 ? 52u : (role == 2 ? 31u : 35u);  // the format's largest code
+  const uint64_t stride = (uint64_t)gridDim.x * 4 * kZs2Jobs;
+  uint64_t j = ((uint64_t)blockIdx.x * 4 + (uint64_t)wv) * kZs2Jobs + (uint64_t)q;
+  bool active = false, exhausted = !slot;
+  ZJob *hp = nullptr;
+  uint32_t nseq = 0, i = 0, err = 0, st = 0;
+  int llg = 0, mlg = 0, ofg = 0, lg = 0;
+  uint64_t *raw = nullptr;
+  ZBr64 r;
+  for (;;) {
+    bool starting = false;
+    uint64_t tab_off = 0;
+    if (!active && !exhausted) {  // (the quad's four lanes take the same job)
+      for (;;) {
+        if (j >= nj) {
+          exhausted = true;
+          break;
+        }
+        hp = reinterpret_cast<ZJob *>(tok8 + d.zjob[j]);
+        j += stride;
+        const uint32_t flags = hp->flags;
+        nseq = hp->nseq;
+        if ((flags & kJLit) || nseq == 0) continue;
+        const uint32_t logs = hp->logs;
+        llg = logs & 0xff;
+        ofg = (logs >> 8) & 0xff;
+        mlg = (logs >> 16) & 0xff;
+        if (llg > 9 || mlg > 9 || ofg > 8) {
+          if (role == 0) hp->err = kZSlow;
+          continue;
+        }
+        tab_off = hp->tab_off;
+        raw = reinterpret_cast<uint64_t *>(tok8 + hp->raw_off);
+        starting = true;
+        zs2_settle(nseq);
+        zs2_settle(llg);
+        zs2_settle(mlg);
+        zs2_settle(ofg);
+        break;
+      }
+    }
+    // the starting quads' tables into their slots, each by the whole wave
+    unsigned long long sm = __ballot(starting && role == 0);
+    while (sm) {
+      const int s = __ffsll((long long)sm) - 1;  // (lane 4 qq of quad qq)
+      sm &= sm - 1;
+      const uint64_t to = readlane_u64(tab_off, s);
+      const int lg0 = __builtin_amdgcn_readlane(llg, s), mg = __builtin_amdgcn_readlane(mlg, s);
+      const int og = __builtin_amdgcn_readlane(ofg, s);
+      const uint32_t nll = 1u << lg0, nml = 1u << mg, nof = 1u << og, n = nll + nml + nof;
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(tok8 + to);
+      uint16_t *dst = tabs[wv][s >> 2];
+      for (uint32_t k0 = 0; k0 < n; k0 += 512) {
+        uint32_t c[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const uint32_t k = k0 + 64 * u + (uint32_t)l;
+          c[u] = k < n ? src[k] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const uint32_t k = k0 + 64 * u + (uint32_t)l;
+          if (k < nll) dst[k] = zs2_cell(c[u], lg0);
+          else if (k < nll + nml) dst[512 + (k - nll)] = zs2_cell(c[u], mg);
+          else if (k < n) dst[1024 + (k - nll - nml)] = zs2_cell(c[u], og);
+        }
+      }
+    }
+    if (starting) {  // the bitstream: container and ring (shared by the quad), this lane's state
+      i = 0;
+      err = 0;
+      lg = role == 1 ? mlg : (role == 2 ? ofg : llg);
+      const int64_t start = (int64_t)hp->seq_off, n = (int64_t)hp->seq_len;
+      const uint32_t last = n > 0 ? tok8[start + n - 1] : 0u;
+      if (last == 0) {
+        err = kZCorrupt;
+      } else {
+        r.w = reinterpret_cast<const uint32_t *>(tok8 + (start & ~3ll));
+        r.lo = 8 * (int32_t)(start & 3);
+        const int32_t P = r.lo + 8 * (int32_t)n - (8 - highbit(last));
+        r.qtop = (P - 1) >> 5;
+        r.win = ((uint64_t)r.D(0) << 32) | r.D(1);
+        r.avail = P - 32 * (r.qtop - 1);
+        r.cons = 2;
+        // D_2 .. D_(kZs2Ring + 1) into the ring, a quarter per lane of the quad
+#pragma unroll
+        for (int t = 2; t < 2 + kZs2Ring; t += 4) rings[wv][qs][(t + role) & (kZs2Ring - 1)] = r.D(t + role);
+        r.nf = 2 + kZs2Ring;
+        const uint32_t sll = r.read(llg), sof = r.read(ofg), sml = r.read(mlg);  // RFC 8878 3.1.1.3.2.2
+        st = role == 1 ? sml : (role == 2 ? sof : sll);
+      }
+      if (err == 0) {
+        wave_lds_sync();
+        r.reload(rings[wv][qs]);
+      }
+      active = err == 0;
+      if (!active && role == 0) hp->err = err;
+      zs2_settle(r.win);
+      zs2_settle(r.avail);
+      zs2_settle(r.qtop);
+      zs2_settle(r.lo);
+      zs2_settle(st);
+    }
+    // top up rings below 24 dwords (a quad that outran its feed; rare: waits)
+    if (active && r.nf - r.cons < 24) {
+      const int32_t nn = r.cons + kZs2Ring;
+      for (int32_t t = r.nf; t < nn; t += 4)
+        if (t + role < nn) rings[wv][qs][(t + role) & (kZs2Ring - 1)] = r.D(t + role);
+      r.nf = nn;
+    }
+    wave_lds_sync();
+    if (!__ballot(active) && !__ballot(!exhausted)) break;
+    // Groups of 8 steps as k_zstd_seq2's; the group's ring refill split over
+    // the quad (lane role k loads dwords k and k + 4 of the group's up to 8)
+    uint64_t E0 = 0, E1 = 0, E2 = 0, E3 = 0, E4 = 0, E5 = 0, E6 = 0, E7 = 0;
+    uint32_t pi0 = 0, pne = 0;
+    do {
+      if (role == 0) {
+        if (pne > 0) raw[pi0 + 0] = E0;
+        if (pne > 1) raw[pi0 + 1] = E1;
+        if (pne > 2) raw[pi0 + 2] = E2;
+        if (pne > 3) raw[pi0 + 3] = E3;
+        if (pne > 4) raw[pi0 + 4] = E4;
+        if (pne > 5) raw[pi0 + 5] = E5;
+        if (pne > 6) raw[pi0 + 6] = E6;
+        if (pne > 7) raw[pi0 + 7] = E7;
+      }
+      const int32_t c = active ? min(8, kZs2Ring - (r.nf - r.cons)) : 0;
+      uint32_t La, Lb;
+      if (role < c) La = r.Dc(r.nf + role);
+      if (role + 4 < c) Lb = r.Dc(r.nf + role + 4);
+      const uint32_t i0 = i;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if (active) {
+          const int32_t c0 = r.cons;  // the ring holds D_c0 .. D_c0+2 (>= 24 - 3k dwords at step k)
+          const uint32_t cell = tabs[wv][qs][toff + st];
+          const uint32_t p0 = rings[wv][qs][c0 & (kZs2Ring - 1)], p1 = rings[wv][qs][(c0 + 1) & (kZs2Ring - 1)],
+                         p2 = rings[wv][qs][(c0 + 2) & (kZs2Ring - 1)];
+          const uint32_t sym = cell & 63u;
+          const uint32_t cx = codes[cbase + (sym < 53u ? sym : 0u)];
+          const uint32_t nbs = zs2_nb(cell, lg);
+          // extra bits and value base of this lane's code (offset: code bits, 1 << code)
+          const uint32_t E = role == 2 ? (sym & 31u) : (cx >> 24);
+          const uint32_t V = role == 2 ? (1u << (sym & 31u)) : (cx & 0xFFFFFFu);
+          const uint32_t flag = (sym > slim ? 1u : 0u) | ((role == 2 && sym > 28u) ? 2u : 0u);
+          const uint32_t pk = E | (nbs << 8) | (flag << 16);
+          const uint32_t pll = quad_bcast<0>(pk), pml = quad_bcast<1>(pk), pof = quad_bcast<2>(pk);
+          // Branch-free: the reads run whatever the checks say (a bad code ends
+          // the job, so what its reads did to the container does not matter),
+          // the state reads with 0 bits after the job's last sequence (a no-op,
+          // as skipping them was), the reloads by selects.
+          const bool more = i + 1 < nseq;
+          // Each of the three groups of reads (offset extra | match + literal
+          // extras | the three states) moves the container once; a lane
+          // extracts only its own field of the group, at its offset in it.
+          const uint32_t eof = pof & 31u, eml = pml & 31u, ell = pll & 31u;
+          const uint32_t nll = more ? (pll >> 8) & 15u : 0u, nml = more ? (pml >> 8) & 15u : 0u,
+                         nof = more ? (pof >> 8) & 15u : 0u;
+          r.avail -= (int32_t)eof;
+          const uint32_t x1 = r.field(0, eof);  // (the offset lane's)
+          r.reload_pf(p0);
+          r.avail -= (int32_t)(eml + ell);
+          const uint32_t x2 = r.field(role == 1 ? ell : 0u, role == 1 ? eml : ell);  // (match / literal lanes')
+          r.reload_pf(p0, p1, c0);
+          r.avail -= (int32_t)(nll + nml + nof);
+          const uint32_t x3 = r.field(role == 1 ? nof : (role == 2 ? 0u : nml + nof), role == 1 ? nml : (role == 2 ? nof : nll));
+          r.reload_pf(p0, p1, p2, c0);
+          const uint32_t val = V + (role == 2 ? x1 : x2);
+          const uint32_t st2 = zs2_base(cell, nbs, lg) + x3;
+          const uint32_t e2 = ((pll | pml | pof) & (1u << 16)) ? kZCorrupt
+                              : (pof & (2u << 16))             ? kZSlow
+                              : r.overrun()                    ? kZCorrupt
+                                                               : 0u;
+          const uint32_t ll = val, ml = quad_bcast<1>(val), ofv = quad_bcast<2>(val);  // (role 0's entry is the one stored)
+          uint64_t &Ek = k == 0 ? E0 : k == 1 ? E1 : k == 2 ? E2 : k == 3 ? E3 : k == 4 ? E4 : k == 5 ? E5 : k == 6 ? E6 : E7;
+          Ek = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
+          if (e2 == 0) {
+            if (more) st = st2;
+            i++;
+            if (!more && !r.exact()) err = kZCorrupt;
+          } else {
+            err = e2;
+          }
+          if (err || i == nseq) active = false;
+        }
+      }
+      const uint32_t ne = i - i0;
+      if (role < c) rings[wv][qs][(r.nf + role) & (kZs2Ring - 1)] = La;
+      if (role + 4 < c) rings[wv][qs][(r.nf + role + 4) & (kZs2Ring - 1)] = Lb;
+      if (c > 0) r.nf += c;
+      pi0 = i0;
+      pne = ne;
+      if (role == 0 && hp && !active && (err || (i == nseq && ne > 0))) hp->err = err;
+    } while (!__ballot((slot && !active && !exhausted) || (active && r.nf - r.cons < 24)));
+    if (role == 0) {
+      if (pne > 0) raw[pi0 + 0] = E0;
+      if (pne > 1) raw[pi0 + 1] = E1;
+      if (pne > 2) raw[pi0 + 2] = E2;
+      if (pne > 3) raw[pi0 + 3] = E3;
+      if (pne > 4) raw[pi0 + 4] = E4;
+      if (pne > 5) raw[pi0 + 5] = E5;
+      if (pne > 6) raw[pi0 + 6] = E6;
+      if (pne > 7) raw[pi0 + 7] = E7;
+    }
   }
 }
 
@@ -2693,7 +2962,10 @@ void launch_zstd(const uint8_t *span, const DevBufs &d, const unsigned long long
   if (g < 1) g = 1;
   hipLaunchKernelGGL(k_zstd_ent, dim3((unsigned)g), dim3(64), 0, st, span, d, nblocks, dec_cap);
   // 4-wave workgroups sharing the CU's LDS (kZs2Groups per CU)
-  hipLaunchKernelGGL(k_zstd_seq2, dim3((unsigned)(grid / kZWaves * kZs2Groups)), dim3(256), 0, st, d);
+  if (RIO_ZS2_QUAD)
+    hipLaunchKernelGGL(k_zstd_seq4, dim3((unsigned)(grid / kZWaves * kZs2Groups)), dim3(256), 0, st, d);
+  else
+    hipLaunchKernelGGL(k_zstd_seq2, dim3((unsigned)(grid / kZWaves * kZs2Groups)), dim3(256), 0, st, d);
   uint64_t g3 = grid / kZWaves * kZFixWaves;
   if (g3 > max_blocks) g3 = max_blocks;
   if (g3 < 1) g3 = 1;
