@@ -63,7 +63,7 @@ def dominant_kernel(trace_summary, name):
 FLATE_DECODE_KERNELS = ["rio::k_codec_prepare", "rio::k_flate_sync<1>", "rio::k_flate_sync<4>", "rio::k_flate_plan",
                         "rio::k_flate_tok", "rio::k_flate_lz2", "rio::k_flate_seg", "rio::k_flate_segfix",
                         "rio::k_inflate_exact"]
-ZSTD_DECODE_KERNELS = ["rio::k_zstd_size", "rio::k_zstd_ent", "rio::k_zstd_seq2", "rio::k_zstd_fix", "rio::k_zstd_exec",
+ZSTD_DECODE_KERNELS = ["rio::k_zstd_size", "rio::k_zstd_ent", "rio::k_zstd_seq4", "rio::k_zstd_seq2", "rio::k_zstd_fix", "rio::k_zstd_exec",
                        "rio::k_zstd"]
 
 

@@ -55,9 +55,9 @@ def run_c4(base_mib=128, replicas=0, steps=5, warmup=1, device=0, check=True, cp
     roof = {"kernels": bench_flate.ZSTD_DECODE_KERNELS,
             "pmc": os.path.join(ROOT, "profiles", "r06_c4_pmc.json"),
             "dominant": bench_flate.dominant_kernel(
-                os.path.join(ROOT, "profiles", "r06_c4_kernel_trace_summary.json"), "k_zstd_seq2"),
+                os.path.join(ROOT, "profiles", "r06_c4_kernel_trace_summary.json"), "k_zstd_seq4"),
             "note": "compressed bytes in + decoded records out over the decode stage; the sequence pass is bound "
-                    "by its FSE chains' LDS latency and the execution pass by far-source loads (DESIGN.md §4)"}
+                    "by its FSE chains' instruction issue and the execution pass by far-source loads (DESIGN.md §4)"}
     res = bench_flate.measure(data, nrec, rec_bytes, lambda: c4_data.all_records(nblk), gpu.RIO_CODEC_ZSTD,
                               "C4-like zstd level 5, records 64 B-64 KiB log-uniform, 1 MiB blocks",
                               replicas, steps, warmup, device, check, contexts=contexts,

@@ -52,20 +52,20 @@ while [ $# -gt 0 ]; do
       step r06_$1 400 python3 tools/bench_zstd.py --data /tmp/c4.bin --steps 4 --pipeline ${1#c4p} ;;
     ztests) step r06_ztests 600 python -u -m pytest -x -v --timeout 150 --timeout-method thread tests/test_zstd_gpu.py \
         tests/test_zstd_libzstd.py tests/test_chain_gpu.py tests/test_structural_fuzz_gpu.py -m gpu ;;
-    pmcc4)  # FETCH_SIZE / WRITE_SIZE per kernel over an 8-replica C4 step (tools/pmc_summary.py)
+    pmcc4)  # FETCH_SIZE / WRITE_SIZE per kernel over a PMC_REPLICAS-replica C4 step (tools/pmc_summary.py)
       [ -f /tmp/c4.bin ] || python3 tools/bench_zstd.py --make-data --data /tmp/c4.bin > gpurun_out/r06_c4data.log 2>&1
       for g in FETCH_SIZE WRITE_SIZE; do
-        step r06_pmc_c4_$g 150 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c4_$g -o run -- \
+        step r06_pmc_c4_$g 300 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c4_$g -o run -- \
           python3 -u tools/bench_zstd.py --data /tmp/c4.bin --steps 1 --warmup 0 --replicas ${PMC_REPLICAS:-8}
       done ;;
     pmcc3)
       for g in FETCH_SIZE WRITE_SIZE; do
-        step r06_pmc_c3_$g 150 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c3_$g -o run -- \
+        step r06_pmc_c3_$g 300 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c3_$g -o run -- \
           python3 -u tools/bench_flate.py --steps 1 --warmup 0 --replicas ${PMC_REPLICAS:-8}
       done ;;
     pmc16k)
       for g in FETCH_SIZE WRITE_SIZE; do
-        step r06_pmc_c3_16k_$g 150 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c3_16k_$g -o run -- \
+        step r06_pmc_c3_16k_$g 300 rocprofv3 --pmc $g --output-format csv -d gpurun_out/r06_pmc_c3_16k_$g -o run -- \
           python3 -u tools/bench_flate.py --steps 1 --warmup 0 --replicas ${PMC_REPLICAS:-8} --per-block 16384
       done ;;
     rehearse2)  # two ranks on the one GPU, collectives over gloo (bench.py REHEARSE sizes)
