@@ -2133,7 +2133,15 @@ __global__ void __launch_bounds__(256) k_zstd_seq2(DevBufs d) {
 // positions depend on all six counts) while extracting only its own fields.
 // The three ring dwords a sequence may need are read with the table lookups,
 // so no reload waits on an LDS read of its own. Same tables, rings, jobs,
-// entries, checks and errors as k_zstd_seq2.
+// entries, checks and errors as k_zstd_seq2. The step's error and the state
+// update are computed by masks (RIO_ZS4_BFERR): C4 44.8 -> 46.3 GiB/s.
+// Measured and not kept (profiles/r06_zstd_seq4_err_ab.jsonl): the literal- and
+// match-length codes' extra-bit counts computed from the symbol (a nibble
+// table in registers), so that the code table's LDS read leaves the state
+// chain -- 44.6 alone, 41.7 together with the mask-based step.
+#ifndef RIO_ZS4_BFERR
+#define RIO_ZS4_BFERR 1  // the step's error and state update by masks (0: by selects, which the compiler branches on)
+#endif
 template <int kSel>
 __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {  // lane (4q + kSel)'s v, on all four lanes
   constexpr int kCtl = kSel | (kSel << 2) | (kSel << 4) | (kSel << 6);  // quad_perm [k, k, k, k]
@@ -2326,13 +2334,27 @@ __global__ void __launch_bounds__(256) k_zstd_seq4(DevBufs d) {
           r.reload_pf(p0, p1, p2, c0);
           const uint32_t val = V + (role == 2 ? x1 : x2);
           const uint32_t st2 = zs2_base(cell, nbs, lg) + x3;
+          const uint32_t ll = val, ml = quad_bcast<1>(val), ofv = quad_bcast<2>(val);  // (role 0's entry is the one stored)
+          uint64_t &Ek = k == 0 ? E0 : k == 1 ? E1 : k == 2 ? E2 : k == 3 ? E3 : k == 4 ? E4 : k == 5 ? E5 : k == 6 ? E6 : E7;
+          Ek = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
+#if RIO_ZS4_BFERR
+          // the step's error, in the serial decoder's order (a bad code, then an
+          // offset code the fast path declines, then an overrun; after the last
+          // sequence, a stream not consumed exactly), by masks: the compiler
+          // branches on a chain of selects, and the state update waited on it
+          const uint32_t bad = (((pll | pml | pof) >> 16) & 1u), slow = (pof >> 17) & 1u;
+          const uint32_t ovr = r.overrun() ? 1u : 0u;
+          const uint32_t isc = bad | (ovr & (slow ^ 1u)), iss = slow & (bad ^ 1u);
+          const uint32_t e2 = ((uint32_t)kZCorrupt & (0u - isc)) | ((uint32_t)kZSlow & (0u - iss));
+          const uint32_t ok = (isc | iss) ^ 1u, mv = more ? 1u : 0u;
+          st = (ok & mv) ? st2 : st;
+          i += ok;
+          err = e2 | ((uint32_t)kZCorrupt & (0u - (ok & (mv ^ 1u) & (r.exact() ? 0u : 1u))));
+#else
           const uint32_t e2 = ((pll | pml | pof) & (1u << 16)) ? kZCorrupt
                               : (pof & (2u << 16))             ? kZSlow
                               : r.overrun()                    ? kZCorrupt
                                                                : 0u;
-          const uint32_t ll = val, ml = quad_bcast<1>(val), ofv = quad_bcast<2>(val);  // (role 0's entry is the one stored)
-          uint64_t &Ek = k == 0 ? E0 : k == 1 ? E1 : k == 2 ? E2 : k == 3 ? E3 : k == 4 ? E4 : k == 5 ? E5 : k == 6 ? E6 : E7;
-          Ek = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
           if (e2 == 0) {
             if (more) st = st2;
             i++;
@@ -2340,6 +2362,7 @@ __global__ void __launch_bounds__(256) k_zstd_seq4(DevBufs d) {
           } else {
             err = e2;
           }
+#endif
           if (err || i == nseq) active = false;
         }
       }
