@@ -222,6 +222,28 @@ struct rio_scanner {
   // rotate: the current batch's span (its views point there), one per span
   // ahead, and the read-ahead's, with spares from batches consumed.
   static constexpr int kSlots = 3;
+  // Span ramp: an uncompressed body's first spans are smaller (the ctx's span
+  // >> ramp_steps, then twice that, ... up to the ctx's span), so that the
+  // first span's copy in is short and the next span's copy follows it at once
+  // (the next span's start is known only once a span is decoded). Only for
+  // spans of at least ramp_min bytes (RIO_SPAN_RAMP_MIN; RIO_SPAN_RAMP: the
+  // steps, 0 off). A span that holds no whole block turns the ramp off.
+  // End to end, A/B (profiles/r06_span_ramp_ab.jsonl): C2 42.3 -> 46.0 GiB/s;
+  // flate and zstd spans measured slower ramped (C4 13.6 -> 12.8, C3 at
+  // MaxItems = 16384 11.6 -> 11.4): a short span of large blocks decodes
+  // almost as long as a whole one, so compressed bodies are not ramped.
+  int ramp_steps = 2;
+  uint64_t ramp_min = 256ull << 20;
+  bool ramp_off = false;
+  uint64_t body_next = 0;  // the index of the next body span to become the current batch
+  uint64_t span_size(uint64_t idx) const {
+    const uint64_t maxspan = rio_ctx_max_span(ctx);
+    if (ramp_off || v1 || codec != RIO_CODEC_NONE || ramp_steps <= 0 || maxspan < ramp_min ||
+        idx >= (uint64_t)ramp_steps)
+      return maxspan;
+    const uint64_t sz = (maxspan >> (ramp_steps - (int)idx)) / kCk * kCk;
+    return sz < 4 * kCk ? maxspan : sz;
+  }
   int depth = 0;  // spans ahead (the ctx's RIO_CFG_SPANS_AHEAD: 0 .. kSlots - 1, default kSlots - 1)
   rio_ctx *cx[kSlots] = {};
   rio_results *rs[kSlots] = {};
@@ -326,7 +348,8 @@ struct rio_scanner {
         at = pat + c;
       }
       if (at >= limit || at >= file_size || at < pat || at > pend || pend - at > kRaRoom) return;
-      const uint64_t n = file_size - at < maxspan ? file_size - at : maxspan;
+      const uint64_t want = span_size(body_next + aq.size());
+      const uint64_t n = file_size - at < want ? file_size - at : want;
       if (at + n <= pend) return;  // (a span inside the one before it: not a body's next span)
       if (first) {
         // a span ahead will be begun: every slot's context opened now, while no
@@ -541,8 +564,9 @@ struct rio_scanner {
   // spans end once one reaches its limit.
   void read_ahead(uint64_t end) {
     if (end < file_size && end < limit) {
-      const uint64_t left = file_size - end, maxspan = rio_ctx_max_span(ctx);
-      ra_start(end, left < maxspan ? left : maxspan);
+      // (the span after the one being decoded: index body_next + 1)
+      const uint64_t left = file_size - end, want = span_size(body_next + 1);
+      ra_start(end, left < want ? left : want);
     }
   }
   // the body's next span [at, at + n): from the read-ahead when it holds it
@@ -728,9 +752,9 @@ bool next_batch(rio_scanner *s) {
       s->done = true;
       return false;
     }
-    const uint64_t maxspan = rio_ctx_max_span(s->ctx);
+    const uint64_t want = s->span_size(s->body_next);
     uint64_t n = s->file_size - s->off;
-    if (n > maxspan) n = maxspan;
+    if (n > want) n = want;
     rio_batch &b = s->batch;
     int rc;
     s->ahead_msg.clear();
@@ -784,6 +808,11 @@ bool next_batch(rio_scanner *s) {
                     s->off);
         return false;
       }
+      if (b.stop == RIO_STOP_MORE && b.consumed == 0 && want < rio_ctx_max_span(s->ctx)) {
+        s->ramp_off = true;  // a ramped span shorter than a block: the ctx's span
+        s->finish_cur();
+        continue;
+      }
       if (b.stop == RIO_STOP_MORE && b.consumed == 0) {
         // a block longer than the ctx's span (the reference reads any block):
         // the span grows to the block's extent (its first chunk's total) and
@@ -803,6 +832,7 @@ bool next_batch(rio_scanner *s) {
         continue;  // again, at the grown span
       }
       s->off += b.consumed;
+      s->body_next++;
       // the spans after this one, begun while its result copies come back and
       // the caller consumes it (the read-ahead of the bytes after the last one
       // ahead -- or after this span -- started when that span was begun)
@@ -879,6 +909,8 @@ rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int l
   s->ctx = ctx;
   s->depth = ctx ? rio_ctx_spans_ahead(ctx) : 0;
   if (s->depth > rio_scanner::kSlots - 1) s->depth = rio_scanner::kSlots - 1;
+  if (const char *e = getenv("RIO_SPAN_RAMP")) s->ramp_steps = std::min(std::max(atoi(e), 0), 6);
+  if (const char *e = getenv("RIO_SPAN_RAMP_MIN")) s->ramp_min = strtoull(e, nullptr, 0);
   s->res = ctx ? rio_ctx_take_results(ctx) : rio_results_new();
   s->cx[0] = ctx;
   s->rs[0] = s->res;

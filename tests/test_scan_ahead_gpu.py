@@ -226,3 +226,30 @@ def test_slow_reader_spans_ahead(oracle, trs):
             assert e is None and items == recs, trs
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("trs,max_items", [([], 23), (["flate"], 23), (["zstd"], 23), ([], 4000), (["flate"], 4000)])
+def test_span_ramp(oracle, trs, max_items, monkeypatch):
+    """The span ramp (scanner.cpp span_size): an uncompressed body's first spans
+    smaller than the ctx's, forced here at small sizes (RIO_SPAN_RAMP_MIN=0, 3
+    steps: 4, 4, 8, then 16-chunk spans at a 16-chunk ctx span). Every record
+    and the error as the oracle's; with MaxItems = 4000 a block is longer than
+    the first spans, which turns the ramp off (the ctx's span from there on).
+    Compressed bodies are not ramped (the same settings, the ctx's spans)."""
+    from base_amd.recordio import gpu
+    from base_amd.recordio.writer import WriterOpts, write_file
+    if "zstd" in trs and not oracle_has_zstd(oracle):
+        pytest.skip("zstd oracle not built")
+    rng = random.Random(11)
+    recs = [rng.randbytes(rng.choice([0, 5, 300, 2000])) * rng.choice([1, 1, 6]) for _ in range(2500)]
+    data = write_file(recs, WriterOpts(Transformers=trs, MaxItems=max_items), trailer=b"RAMP")
+    monkeypatch.setenv("RIO_SPAN_RAMP", "3")
+    monkeypatch.setenv("RIO_SPAN_RAMP_MIN", "0")
+    ctx = gpu.Context(0, max_span_bytes=16 * 32768)
+    try:
+        for shard in [(0, 1, 1), (1, 3, 4)]:
+            want = oracle.scan(data, *shard)
+            items, err = _scan(data, ctx, *shard)
+            assert err == want.err and items == want.items, (trs, max_items, shard)
+    finally:
+        ctx.close()
