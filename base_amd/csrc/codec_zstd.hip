@@ -2148,9 +2148,18 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {  // lane (4q + kSel
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtl, 0xf, 0xf, false);
 }
 
+// The ring with its first three dwords mirrored after its end (RIO_ZS4_MIRROR),
+// so that a step's three dwords D_c0 .. D_c0+2 are adjacent: one address, no
+// wrap masks (140 wave instructions per step instead of 157; C4 46.3-46.6
+// against 46.5-46.5 without, profiles/r06_zstd_seq4_mirror_ab.jsonl: the pass
+// is bound by its step's dependency chain, not by issue).
+#ifndef RIO_ZS4_MIRROR
+#define RIO_ZS4_MIRROR 1
+#endif
+constexpr int kZs4Ring = kZs2Ring + (RIO_ZS4_MIRROR ? 4 : 0);
 __global__ void __launch_bounds__(256) k_zstd_seq4(DevBufs d) {
   __shared__ uint16_t tabs[4][kZs2Jobs][kZs2Cells];
-  __shared__ uint32_t rings[4][kZs2Jobs][kZs2Ring];
+  __shared__ uint32_t rings[4][kZs2Jobs][kZs4Ring];
   __shared__ uint32_t codes[36 + 53];  // ZCodes: ll at 0, ml at 36
   const int l = lane_id(), wv = (int)(threadIdx.x >> 6);
   const int q = l >> 2, role = l & 3;
@@ -2168,6 +2177,15 @@ __global__ void __launch_bounds__(256) k_zstd_seq4(DevBufs d) {
   const uint64_t stride = (uint64_t)gridDim.x * 4 * kZs2Jobs;
   uint64_t j = ((uint64_t)blockIdx.x * 4 + (uint64_t)wv) * kZs2Jobs + (uint64_t)q;
   bool active = false, exhausted = !slot;
+  // ring dword D_t in, D_(c0 + k) out (k <= 2)
+  auto rput = [&](int32_t t, uint32_t v) {
+    const int32_t sl = t & (kZs2Ring - 1);
+    rings[wv][qs][sl] = v;
+    if (RIO_ZS4_MIRROR && sl < 3) rings[wv][qs][kZs2Ring + sl] = v;
+  };
+  auto rget = [&](int32_t c0, int k) -> uint32_t {
+    return RIO_ZS4_MIRROR ? rings[wv][qs][(c0 & (kZs2Ring - 1)) + k] : rings[wv][qs][(c0 + k) & (kZs2Ring - 1)];
+  };
   ZJob *hp = nullptr;
   uint32_t nseq = 0, i = 0, err = 0, st = 0;
   int llg = 0, mlg = 0, ofg = 0, lg = 0;
@@ -2250,14 +2268,14 @@ __global__ void __launch_bounds__(256) k_zstd_seq4(DevBufs d) {
         r.cons = 2;
         // D_2 .. D_(kZs2Ring + 1) into the ring, a quarter per lane of the quad
 #pragma unroll
-        for (int t = 2; t < 2 + kZs2Ring; t += 4) rings[wv][qs][(t + role) & (kZs2Ring - 1)] = r.D(t + role);
+        for (int t = 2; t < 2 + kZs2Ring; t += 4) rput(t + role, r.D(t + role));
         r.nf = 2 + kZs2Ring;
         const uint32_t sll = r.read(llg), sof = r.read(ofg), sml = r.read(mlg);  // RFC 8878 3.1.1.3.2.2
         st = role == 1 ? sml : (role == 2 ? sof : sll);
       }
       if (err == 0) {
         wave_lds_sync();
-        r.reload(rings[wv][qs]);
+        r.reload(*reinterpret_cast<const uint32_t(*)[kZs2Ring]>(rings[wv][qs]));
       }
       active = err == 0;
       if (!active && role == 0) hp->err = err;
@@ -2271,7 +2289,7 @@ __global__ void __launch_bounds__(256) k_zstd_seq4(DevBufs d) {
     if (active && r.nf - r.cons < 24) {
       const int32_t nn = r.cons + kZs2Ring;
       for (int32_t t = r.nf; t < nn; t += 4)
-        if (t + role < nn) rings[wv][qs][(t + role) & (kZs2Ring - 1)] = r.D(t + role);
+        if (t + role < nn) rput(t + role, r.D(t + role));
       r.nf = nn;
     }
     wave_lds_sync();
@@ -2301,8 +2319,8 @@ __global__ void __launch_bounds__(256) k_zstd_seq4(DevBufs d) {
         if (active) {
           const int32_t c0 = r.cons;  // the ring holds D_c0 .. D_c0+2 (>= 24 - 3k dwords at step k)
           const uint32_t cell = tabs[wv][qs][toff + st];
-          const uint32_t p0 = rings[wv][qs][c0 & (kZs2Ring - 1)], p1 = rings[wv][qs][(c0 + 1) & (kZs2Ring - 1)],
-                         p2 = rings[wv][qs][(c0 + 2) & (kZs2Ring - 1)];
+          const uint32_t p0 = rget(c0, 0), p1 = rget(c0, 1),
+                         p2 = rget(c0, 2);
           const uint32_t sym = cell & 63u;
           const uint32_t cx = codes[cbase + (sym < 53u ? sym : 0u)];
           const uint32_t nbs = zs2_nb(cell, lg);
@@ -2367,8 +2385,8 @@ __global__ void __launch_bounds__(256) k_zstd_seq4(DevBufs d) {
         }
       }
       const uint32_t ne = i - i0;
-      if (role < c) rings[wv][qs][(r.nf + role) & (kZs2Ring - 1)] = La;
-      if (role + 4 < c) rings[wv][qs][(r.nf + role + 4) & (kZs2Ring - 1)] = Lb;
+      if (role < c) rput(r.nf + role, La);
+      if (role + 4 < c) rput(r.nf + role + 4, Lb);
       if (c > 0) r.nf += c;
       pi0 = i0;
       pne = ne;
