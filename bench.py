@@ -204,7 +204,9 @@ def c4_zstd(args, local, world, dist):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_zstd
     cpu_s = args.cpu_s if (world == 1 and not args.no_cpu_baseline) else 0.0
-    r = bench_zstd.run_c4(replicas=args.zstd_replicas, steps=max(2, min(args.steps, 3)), warmup=1, device=local,
+    # (6 steps: with two in flight the first step's fill weighs on a 3-step average --
+    # 92.3 ms per step at 3 against 86.0-86.3 at 4-6, profiles/r06_c4_depth_ab.jsonl)
+    r = bench_zstd.run_c4(replicas=args.zstd_replicas, steps=max(2, min(args.steps, 6)), warmup=1, device=local,
                           check=True, cpu_s=cpu_s, contexts=args.zstd_contexts, pipeline=args.zstd_pipeline,
                           share=mem_share(args, world))
     if dist is not None:
