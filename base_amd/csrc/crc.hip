@@ -83,8 +83,8 @@ constexpr bool kCrcAbs = kFoldPerm && RIO_CRC_DYN;
 
 // fold stage q (rows kRows*q ..) of a chunk whose covered bytes end at `end`
 __device__ __forceinline__ void fold_stage(const uint4 (&u)[kRows], uint32_t (&s)[4], uint32_t (&sq)[4],
-                                           const char *__restrict__ tab,
-                                           uint32_t lb, int l, int q, int end, bool fold, uint32_t &stored) {
+                                           const char *__restrict__ tab, uint32_t lb, const uint32_t (&sel)[4],
+                                           int l, int q, int end, bool fold, uint32_t &stored) {
 #pragma unroll
   for (int r = 0; r < kRows; r++) {
     uint4 v = u[r];
@@ -105,7 +105,7 @@ __device__ __forceinline__ void fold_stage(const uint4 (&u)[kRows], uint32_t (&s
     }
     if (fold) {
 #if RIO_FOLD_XOR3
-      if constexpr (kFoldPerm) fold_row3<kCrcAbs>(tab, lb, v, s, sq);
+      if constexpr (kFoldPerm) fold_row3<kCrcAbs>(tab, lb, v, s, sq, sel);
       else fold_row<kCrcAbs>(tab, lb, v, s);
 #else
       fold_row<kCrcAbs>(tab, lb, v, s);
@@ -190,6 +190,12 @@ __global__ void __launch_bounds__(64 * kCrcWaves) RIO_CRC_ATTR k_crc(const uint8
   }
   const int l = lane_id();
   const uint32_t lb = (uint32_t)(l & (kFoldCopies - 1)) << 2;
+  // lanes 16-31 / 48-63 take their lookups in rotated table order (crc_fold.h fold_sel)
+#ifndef RIO_CRC_ROT
+#define RIO_CRC_ROT 1
+#endif
+  const uint32_t rot = RIO_CRC_ROT ? (uint32_t)((l >> 4) & 1) : 0u;
+  const uint32_t sel[4] = {fold_sel(0, rot), fold_sel(1, rot), fold_sel(2, rot), fold_sel(3, rot)};
   const char *tab = reinterpret_cast<const char *>(s_fold);
   const bool fold = !(ca.flags & 1);
   const uint64_t nwaves = (uint64_t)gridDim.x * kCrcWaves;
@@ -228,7 +234,7 @@ __global__ void __launch_bounds__(64 * kCrcWaves) RIO_CRC_ATTR k_crc(const uint8
         *reinterpret_cast<uint4 *>(stage + 16 * l) = buf[0][0];
         if (l < 2) *reinterpret_cast<uint4 *>(stage + 1024 + 16 * l) = buf[0][1];
       }
-      fold_stage(buf[q % kBufs], s, sq, tab, lb, l, q, end, fold, stored);
+      fold_stage(buf[q % kBufs], s, sq, tab, lb, sel, l, q, end, fold, stored);
     }
     // lane: V_t = s0 + s1 x^-32 + s2 x^-64 + s3 x^-96
 #pragma unroll

@@ -43,9 +43,19 @@ __device__ __forceinline__ uint32_t mask_dword(uint32_t v, int off, int hi) {
 // so a step is 4 permutes, 4 lookups and 2 XOR3s per dword -- the data XOR
 // joins the previous step's last one. Callers start with s2 = 0 and take
 // s ^ s2 at the end.
+// sel: lookup j's v_perm selector (byte j of the data and of L, the table offset).
+// With the 16 table copies banked (16 j + copy) mod 32, a ds_read_b32's 32-lane
+// group put lanes l and l + 16 (one copy) on one bank: 2-way conflicts on every
+// lookup (k_crc: 596 M conflict cycles of 1,163 M LDS cycles per C2 launch). A
+// caller whose lanes 16-31 / 48-63 take lookup (j + 1) & 3 as their j-th
+// (fold_sel) spreads the group over 32 banks; the XOR of the four is the same.
+__device__ __forceinline__ uint32_t fold_sel(int j, uint32_t rot) {
+  const uint32_t jj = ((uint32_t)j + rot) & 3u;
+  return 0x0c0c0000u | (jj << 8) | (4u + jj);
+}
 template <bool kAbs = false>
 __device__ __forceinline__ void fold_row3(const char *__restrict__ tab, uint32_t lb, uint4 v, uint32_t (&s)[4],
-                                          uint32_t (&s2)[4]) {
+                                          uint32_t (&s2)[4], const uint32_t (&sel)[4]) {
   static_assert(kFoldPerm, "the byte-row layout");
   const uint32_t L = lb * 0x01010101u + 0xC0804000u;
   const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
@@ -55,7 +65,7 @@ __device__ __forceinline__ void fold_row3(const char *__restrict__ tab, uint32_t
     uint32_t t[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const uint32_t a = __builtin_amdgcn_perm(L, d, 0x0c0c0000u | ((uint32_t)j << 8) | (4u + (uint32_t)j));
+      const uint32_t a = __builtin_amdgcn_perm(L, d, sel[j]);
       typedef const __attribute__((address_space(3))) uint32_t lds_u32;
       if constexpr (kAbs) t[j] = *(lds_u32 *)(uintptr_t)a;
       else t[j] = *reinterpret_cast<const uint32_t *>(tab + a);
@@ -63,6 +73,12 @@ __device__ __forceinline__ void fold_row3(const char *__restrict__ tab, uint32_t
     s[k] = __builtin_amdgcn_bitop3_b32(t[0], t[1], t[2], 0x96);
     s2[k] = t[3];
   }
+}
+template <bool kAbs = false>
+__device__ __forceinline__ void fold_row3(const char *__restrict__ tab, uint32_t lb, uint4 v, uint32_t (&s)[4],
+                                          uint32_t (&s2)[4]) {
+  const uint32_t sel[4] = {fold_sel(0, 0), fold_sel(1, 0), fold_sel(2, 0), fold_sel(3, 0)};
+  fold_row3<kAbs>(tab, lb, v, s, s2, sel);
 }
 
 template <bool kAbs = false>
