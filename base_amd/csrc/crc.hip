@@ -1,7 +1,7 @@
 // Chunk CRC32-IEEE verify (readChunk, recordio/internal/chunk.go:338-343) at
 // HBM read speed, no carry-less multiply.
 //
-// One wave per 32 KiB chunk, kCrcWaves (12) waves per workgroup, one workgroup per CU.
+// One wave per 32 KiB chunk, kCrcWaves (16) waves per workgroup, one workgroup per CU.
 // Lane t loads the 16-byte units at chunk offsets 1024*i + 16*t (i = 0..31): every
 // load instruction is 1 KiB contiguous. Each of the lane's 4 dwords (k = 0..3)
 // is its own CRC stream with one dword per 1 KiB row; the 1020-byte gap to the
@@ -22,9 +22,13 @@
 // x^-(128*2^l) combines the lanes (multiply-by-constant = 4 byte lookups).
 // Bytes outside [12, 28+size) are zeroed, so V = R(0^12 || covered || 0^pad) and
 // crc = ~(~0 * x^(8(16+size)) ^ V * x^(-8 pad)).
-// Loads are software-pipelined in 4 KiB stages through 4 register buffers:
-// while one stage is folded the next three are in flight (12 waves per CU keep
-// 144 KiB outstanding).
+// Loads are software-pipelined in 2 KiB stages through 8 register buffers:
+// while one stage is folded the next seven are in flight (16 waves per CU keep
+// 224 KiB outstanding). Round 6, with the lookups conflict-free (fold_sel): 16
+// waves of 2-row stages, 8 buffers, against 12 waves of 4-row stages, 4 buffers:
+// two-context C2 step 2.846-2.857 -> 2.820-2.824 ms, k_crc 2.625-2.635 ->
+// 2.615-2.628 (profiles/r06_crc_shape_ab2.jsonl); 12 waves of 2-row stages, 8
+// buffers ran k_crc in 2.55-2.58 ms alone but the step in 2.87-2.91.
 //
 // Room beside it (round 4): the tables are dynamic LDS (92 KiB) and the
 // registers are allocated for 4 waves per SIMD (127 VGPRs) while the workgroup
@@ -33,7 +37,8 @@
 // kernel (k_lean_end: 6 KiB of LDS, 71 VGPRs per wave) fits on each CU beside
 // it: with two contexts in flight, step i + 1's parse runs during step i's
 // CRC pass (C2, A/B on one box: 3.114 -> 3.043 ms per step; alone k_crc 2.785
-// -> 2.75 ms).
+// -> 2.75 ms). (Round 6: at 16 waves the registers fill the SIMDs; the parse
+// kernels then take CU slots as k_crc's waves finish.)
 //
 // Fused parse (k_crc<true>, round 2; measured slower and not instantiated:
 // DESIGN.md §5; none codec): the wave that checksums a block's
@@ -56,19 +61,19 @@
 namespace rio {
 
 #ifndef RIO_CRC_WAVES
-#define RIO_CRC_WAVES 12
+#define RIO_CRC_WAVES 16
 #endif
-constexpr int kCrcWaves = RIO_CRC_WAVES;  // waves per workgroup (one workgroup per CU: 92 KiB LDS at 16 copies)
+constexpr int kCrcWaves = RIO_CRC_WAVES;  // waves per workgroup (one workgroup per CU: 92 KiB LDS at 16 copies, 127 VGPRs)
 
 #ifndef RIO_CRC_MAP
 #define RIO_CRC_MAP 0
 #endif
 #ifndef RIO_CRC_ROWS
-#define RIO_CRC_ROWS 4
+#define RIO_CRC_ROWS 2
 #endif
-constexpr int kRows = RIO_CRC_ROWS;  // rows per pipeline stage (4 KiB per wave)
+constexpr int kRows = RIO_CRC_ROWS;  // rows per pipeline stage (2 KiB per wave)
 #ifndef RIO_CRC_BUFS
-#define RIO_CRC_BUFS 4
+#define RIO_CRC_BUFS 8
 #endif
 constexpr int kBufs = RIO_CRC_BUFS;  // register buffers: kBufs - 1 stages in flight during a fold
 constexpr int kStages = 32 / kRows;
