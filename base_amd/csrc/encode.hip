@@ -227,6 +227,9 @@ __global__ void __launch_bounds__(64 * kEncWaves) k_enc_chunks(EncArgs a, uint64
   __syncthreads();
   const int l = lane_id();
   const uint32_t lb = (uint32_t)(l & (kFoldCopies - 1)) << 2;
+  // (lanes 16-31 / 48-63 in rotated table order: conflict-free lookups, crc_fold.h fold_sel)
+  const uint32_t rot = (uint32_t)((l >> 4) & 1);
+  const uint32_t sel[4] = {fold_sel(0, rot), fold_sel(1, rot), fold_sel(2, rot), fold_sel(3, rot)};
   const char *tab = reinterpret_cast<const char *>(s_fold);
   const uint64_t nwaves = (uint64_t)gridDim.x * kEncWaves;
   for (uint64_t c = (uint64_t)blockIdx.x * kEncWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); c < nchunks;
@@ -256,7 +259,7 @@ __global__ void __launch_bounds__(64 * kEncWaves) k_enc_chunks(EncArgs a, uint64
           v.z = mask_dword(v.z, q0 + 8, x.end);
           v.w = mask_dword(v.w, q0 + 12, x.end);
         }
-        if constexpr (kFoldPerm) fold_row3(tab, lb, v, s, sq);
+        if constexpr (kFoldPerm) fold_row3(tab, lb, v, s, sq, sel);
         else fold_row(tab, lb, v, s);
       }
 #pragma unroll
