@@ -75,11 +75,11 @@ def make_c1_file():
     return make_c2_file(16385)
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r05_c2_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r06_c2_pmc.json")
 
 
 def pmc_traffic(kernel: str, replicas: int):
-    """HBM bytes per launch of `kernel` from the committed PMC pass (tools/gpu_r04.sh pmcc2:
+    """HBM bytes per launch of `kernel` from the committed PMC pass (tools/gpu_r06.sh pmcc2:
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over this same bench command, FETCH_SIZE
     doubled per MI355X_MICROARCH.md). Only valid for the default replica count."""
     if replicas != REPLICAS or not os.path.exists(PMC_FILE):
