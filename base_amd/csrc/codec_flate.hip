@@ -2534,9 +2534,10 @@ void launch_inflate_huff(const uint8_t *span, const DevBufs &d, const unsigned l
         per_cu = 1;
       return per_cu;
     }();
-    const uint64_t wide_below = (uint64_t)wide_per_cu * (uint64_t)(ncu > 0 ? ncu : 256) + 1;
+    // (RIO_CFG_FLATE_ONE_WAVE: 0, the one-wave kernel on every span)
+    const uint64_t wide_below = d.fl_one_wave ? 0 : (uint64_t)wide_per_cu * (uint64_t)(ncu > 0 ? ncu : 256) + 1;
     {
-      const uint64_t gw = max_blocks < wide_below - 1 ? max_blocks : wide_below - 1;
+      const uint64_t gw = wide_below == 0 ? 1 : (max_blocks < wide_below - 1 ? max_blocks : wide_below - 1);
       hipLaunchKernelGGL(k_flate_sync<RIO_SYNC_W>, dim3((unsigned)(gw ? gw : 1)), dim3(64 * RIO_SYNC_W), 0, st, span,
                          d, nblocks, nchunks, dec_cap, wide_below);
     }

@@ -342,6 +342,7 @@ static int ctx_init(rio_ctx *c, const rio_config *cfg) {
   c->d.tok_limit = cfg ? cfg->flate_tok_limit : 0;
   c->d.fl_grid = cfg ? cfg->flate_grid : 0;
   c->d.fl_tok_only = (cfg && (cfg->flags & RIO_CFG_FLATE_TOK_ONLY)) ? 1 : 0;
+  c->d.fl_one_wave = (cfg && (cfg->flags & RIO_CFG_FLATE_ONE_WAVE)) ? 1 : 0;
   c->item_end_mode = cfg && (cfg->flags & RIO_CFG_ITEM_END);
   c->flate_split = !(cfg && (cfg->flags & RIO_CFG_FLATE_NO_SPLIT));
   uint64_t span = (cfg && cfg->max_span_bytes) ? cfg->max_span_bytes : (256ull << 20);

@@ -229,6 +229,7 @@ struct DevBufs {
   uint64_t tok_limit;            // tokens per block and round (0: the whole region; rio_config.flate_tok_limit)
   uint64_t fl_grid;              // Huffman-pass workgroups (0: all resident; rio_config.flate_grid)
   uint64_t fl_tok_only;          // RIO_CFG_FLATE_TOK_ONLY: k_flate_sync declines every block (tests)
+  uint64_t fl_one_wave;          // RIO_CFG_FLATE_ONE_WAVE: k_flate_sync<1> on every span (tests)
   unsigned long long *fl_more;   // per round: blocks whose token region filled (kFlRounds)
   unsigned long long *fl_ck;     // per chunk: the Huffman pass's (ntok | olen << 32) at the block's input
                                  // chunk k (entry c0 + k; entry c0 = entries written) -- split points

@@ -54,6 +54,7 @@ class RioError(ctypes.Structure):
 RIO_CFG_ITEM_END = 1  # device results carry item_end (cumSize) + block_data / block_first_off
 RIO_CFG_FLATE_NO_SPLIT = 2  # never split a flate block's copy pass (tuning / tests)
 RIO_CFG_FLATE_TOK_ONLY = 4  # every flate block through the fallback Huffman pass, k_flate_tok (tests)
+RIO_CFG_FLATE_ONE_WAVE = 16  # the one-wave Huffman pass on every span, not its 4-wave variant (tests)
 
 
 def RIO_CFG_SPANS_AHEAD(n: int) -> int:
@@ -225,10 +226,11 @@ class Context:
 
     def __init__(self, device: int = 0, max_span_bytes: int = 0, max_out_bytes: int = 0, max_items: int = 0,
                  item_end: bool = False, flate_tok_limit: int = 0, flate_grid: int = 0,
-                 flate_split: bool = True, flate_tok_only: bool = False, spans_ahead: Optional[int] = None):
+                 flate_split: bool = True, flate_tok_only: bool = False, spans_ahead: Optional[int] = None,
+                 flate_one_wave: bool = False):
         self.L = load()
         flags = (RIO_CFG_ITEM_END if item_end else 0) | (0 if flate_split else RIO_CFG_FLATE_NO_SPLIT) | \
-            (RIO_CFG_FLATE_TOK_ONLY if flate_tok_only else 0) | \
+            (RIO_CFG_FLATE_TOK_ONLY if flate_tok_only else 0) | (RIO_CFG_FLATE_ONE_WAVE if flate_one_wave else 0) | \
             (0 if spans_ahead is None else RIO_CFG_SPANS_AHEAD(spans_ahead))
         cfg = RioConfig(device, flags, max_span_bytes, max_out_bytes, max_items, flate_tok_limit, flate_grid)
         self.item_end = item_end

@@ -127,6 +127,8 @@ typedef struct rio_error {
 #define RIO_CFG_SPANS_AHEAD(n) (((((uint32_t)(n)) > 2u ? 2u : ((uint32_t)(n))) + 1u) << 8)
 #define RIO_CFG_FLATE_TOK_ONLY 4u  /* test: the wave-per-block Huffman pass declines every flate
                                      * block, so the fallback pass (k_flate_tok) decodes them all */
+#define RIO_CFG_FLATE_ONE_WAVE 16u /* test: the Huffman pass one wave per block on every span (by
+                                     * default a span of few blocks takes its 4-wave variant) */
 
 typedef struct rio_config {
     int32_t device;             /* HIP device ordinal */

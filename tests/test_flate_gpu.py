@@ -14,11 +14,12 @@ pytestmark = pytest.mark.gpu
 
 def make_ctx(env=None, span=64 << 20):
     """A ctx with the flate decoder's test parameters (rio_config.flate_tok_limit,
-    flate_grid) from `env` = {"tok_limit": n, "grid": n}."""
+    flate_grid, RIO_CFG_FLATE_ONE_WAVE) from `env` = {"tok_limit": n, "grid": n,
+    "one_wave": bool}."""
     from base_amd.recordio import gpu
     env = env or {}
     return gpu.Context(0, max_span_bytes=span, flate_tok_limit=env.get("tok_limit", 0),
-                       flate_grid=env.get("grid", 0))
+                       flate_grid=env.get("grid", 0), flate_one_wave=env.get("one_wave", False))
 
 
 def scan_all(data, ctx):
@@ -53,9 +54,12 @@ def mixed_records(seed, n):
     return out
 
 
-@pytest.fixture(scope="module")
-def ctx(gpu_lib):
-    c = make_ctx()
+@pytest.fixture(scope="module", params=[False, True], ids=["default", "one_wave"])
+def ctx(gpu_lib, request):
+    """Both Huffman-pass variants: the tests' small spans take the 4-wave
+    k_flate_sync by default; one_wave forces the one-wave kernel that large
+    spans (the C3 bench's) run."""
+    c = make_ctx({"one_wave": request.param})
     yield c
     c.close()
 

@@ -136,7 +136,8 @@ def test_flate_spliced_chunk_regression(oracle):
                 d = dd
                 assert what == (42, 0)
     ctxs = [gpu.Context(0, max_span_bytes=64 << 20), gpu.Context(0, max_span_bytes=8 * CK),
-            gpu.Context(0, max_span_bytes=64 << 20, flate_tok_only=True)]
+            gpu.Context(0, max_span_bytes=64 << 20, flate_tok_only=True),
+            gpu.Context(0, max_span_bytes=64 << 20, flate_one_wave=True)]
     try:
         _check(oracle, d, ctxs, "flate (42, 0)")
     finally:
@@ -151,8 +152,9 @@ def test_payload_splices_match_oracle(oracle, trs, multi):
         pytest.skip("zstd oracle not built")
     rng = random.Random(31 + len(trs) + multi)
     ctxs = [gpu.Context(0, max_span_bytes=64 << 20), gpu.Context(0, max_span_bytes=8 * CK)]
-    if trs == ["flate"]:
+    if trs == ["flate"]:  # (and the one-wave Huffman pass, which small spans do not take by default)
         ctxs.append(gpu.Context(0, max_span_bytes=64 << 20, flate_tok_only=True))
+        ctxs.append(gpu.Context(0, max_span_bytes=64 << 20, flate_one_wave=True))
     try:
         for f in range(3):
             data = _file(trs, 300 * f + 7, multi_frame=multi, text=f > 0)
@@ -172,16 +174,20 @@ def test_structural_rewrites_match_oracle(oracle, trs):
     rng = random.Random(11 + len(trs))
     small = gpu.Context(0, max_span_bytes=8 * CK)
     big = gpu.Context(0, max_span_bytes=64 << 20)
+    # flate: also the one-wave Huffman pass (these small files take its 4-wave variant)
+    one = gpu.Context(0, max_span_bytes=64 << 20, flate_one_wave=True) if trs == ["flate"] else None
     try:
         for f in range(3):
             data = _file(trs, 100 * f + len(trs))
             for trial in range(25):
                 d, what = _mutate(data, rng)
                 ref = oracle.scan(d, read_trailer=False)
-                for ctx in (big, small):
+                for ctx in (big, small) + ((one,) if one else ()):
                     items, err = _scan(d, ctx)
                     assert err == ref.err, (trs, f, trial, what, ctx is small)
                     assert items == ref.items, (trs, f, trial, what, ctx is small)
     finally:
         small.close()
         big.close()
+        if one:
+            one.close()
