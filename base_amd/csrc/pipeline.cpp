@@ -1205,6 +1205,14 @@ int rio_scan_span_stage(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, int3
   return 0;
 }
 
+int rio_ctx_wait_staged(rio_ctx *ctx) {
+  if (!ctx || !ctx->staged) return 0;
+  if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+  if (sdma_settle(ctx, kSdmaIn)) return -1;
+  HIP_OK(hipStreamSynchronize(ctx->st));  // (a copy the stream ran: no SDMA engine)
+  return 0;
+}
+
 int rio_scan_span_begin(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off, int32_t is_file_end,
                         uint64_t limit_off, int32_t codec, rio_results *res, rio_batch *out) {
   return scan_span(ctx, span, nbytes, file_off, is_file_end, limit_off, codec, 0, res, out, true);

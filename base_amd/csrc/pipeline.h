@@ -24,6 +24,8 @@ int rio_scan_span_mode(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint6
 // enqueued now (a scanner's span ahead: its copy overlaps the decode of the
 // span before it); the same span pointer and size to begin skip the staging
 int rio_scan_span_stage(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, int32_t codec);
+// the staged span's copy in complete (no-op when none is staged)
+int rio_ctx_wait_staged(rio_ctx *ctx);
 int rio_scan_span_begin(rio_ctx *ctx, const uint8_t *span, uint64_t nbytes, uint64_t file_off,
                         int32_t is_file_end, uint64_t limit_off, int32_t codec, rio_results *res, rio_batch *out);
 int rio_scan_span_end(rio_ctx *ctx);  // 0 (also when nothing is in flight) or -1 (rio_last_error)

@@ -245,6 +245,28 @@ struct rio_scanner {
     return sz < 4 * kCk ? maxspan : sz;
   }
   int depth = 0;  // spans ahead (the ctx's RIO_CFG_SPANS_AHEAD: 0 .. kSlots - 1, default kSlots - 1)
+  // Early first span ahead (RIO_SCAN_EARLY, default on): a body span read by
+  // the main thread (the first, or after a dropped prediction) is staged, and
+  // once its copy in is complete -- not once it is decoded -- the span after it
+  // is begun from the host's prediction of where it stops. That span's copy in
+  // then runs during this span's decode instead of after it; its decode still
+  // waits for this one (cur_done).
+  // Only for compressed bodies of large blocks (the span's first block at least
+  // kEarlyChunks chunks): their spans decode slowly for their size (few blocks
+  // to spread over the GPU), so the next copy in waited on a long decode. End to
+  // end, A/B (profiles/r06_e2e_early_stage_ab.jsonl): C4 13.5 -> 14.7-14.8 GiB/s,
+  // C3 at MaxItems = 16384 11.4-11.5 -> 12.4; C3 at 1,024 items per block 15.1-15.4
+  // -> 14.7-15.1 and C2 45.1-46.3 -> 43.4-43.6, hence not for those.
+  static constexpr uint32_t kEarlyChunks = 8;
+  static uint32_t first_block_chunks(const uint8_t *base, uint64_t n) {
+    if (n < kCk) return 0;
+    uint32_t total;
+    memcpy(&total, base + 20, 4);  // its first chunk's total (chunk.go:31-53)
+    return total;
+  }
+  bool early = true;
+  std::promise<void> cur_done;
+  std::shared_future<void> cur_done_f;
   rio_ctx *cx[kSlots] = {};
   rio_results *rs[kSlots] = {};
   int slot = 0;
@@ -327,7 +349,7 @@ struct rio_scanner {
   // fill the spans ahead: each next span is the unconsumed tail of the span
   // before it (copied here) and the file bytes after that span: the read-ahead's
   // when it holds them, else read by the span's own thread before its decode
-  void begin_ahead() {
+  void begin_ahead(bool early_first = false) {
     if (v1 || done || err_set || depth == 0) return;
     const uint64_t maxspan = rio_ctx_max_span(ctx);
     while ((int)aq.size() < depth) {
@@ -338,7 +360,11 @@ struct rio_scanner {
       const uint64_t pend = pat + pn;
       if (!pdata || pend >= file_size) return;
       uint64_t at = off;
-      if (!first) {
+      if (first && early_first) {  // (the current span is still to be decoded: predicted as the later ones)
+        const uint64_t c = predict_consumed(pdata, pn);
+        if (c == 0) return;
+        at = pat + c;
+      } else if (!first) {
         // the span before this one is still being read by its own thread: its
         // last chunk header and its tail are only there once that read is done
         aq.back().read_f.wait();
@@ -348,7 +374,8 @@ struct rio_scanner {
         at = pat + c;
       }
       if (at >= limit || at >= file_size || at < pat || at > pend || pend - at > kRaRoom) return;
-      const uint64_t want = span_size(body_next + aq.size());
+      // (the index of this span: body_next counts the current batch once it is decoded)
+      const uint64_t want = span_size(body_next + aq.size() + (early_first ? 1 : 0));
       const uint64_t n = file_size - at < want ? file_size - at : want;
       if (at + n <= pend) return;  // (a span inside the one before it: not a body's next span)
       if (first) {
@@ -396,7 +423,7 @@ struct rio_scanner {
       // the span ahead of this one: its decode first (the kernels of two spans
       // sharing the GPU would delay the older span's result copies); this
       // span's H2D copy is enqueued before that wait
-      std::shared_future<void> prev = first ? std::shared_future<void>() : aq.back().begun_f;
+      std::shared_future<void> prev = first ? (early_first ? cur_done_f : std::shared_future<void>()) : aq.back().begun_f;
       aq.emplace_back();
       Ahead &e = aq.back();
       e.begun_f = e.begun.get_future().share();
@@ -543,6 +570,24 @@ struct rio_scanner {
     }
     const int is_end = (at + got >= file_size);
     if (body) {  // the body's span (the current slot; the bytes after it read meanwhile)
+      if (early && depth > 0 && !v1 && !is_end && at + got < limit && codec != RIO_CODEC_NONE &&
+          first_block_chunks(*buf, got) >= kEarlyChunks) {
+        // staged; the span after it begun once this copy in is done (see `early`)
+        rio_ctx *c = cx[slot];
+        if (c != ctx && rio_ctx_reserve_span(c, got) != 0) return -1;
+        if (rio_scan_span_stage(c, *buf, got, codec) != 0 || rio_ctx_wait_staged(c) != 0) return -1;
+        span_data = *buf;
+        span_at = at;
+        span_n = got;
+        cur_done = std::promise<void>();
+        cur_done_f = cur_done.get_future().share();
+        struct Done {  // (set on every return: the span ahead's thread waits for it)
+          std::promise<void> &p;
+          ~Done() { p.set_value(); }
+        } done_signal{cur_done};
+        begin_ahead(true);
+        return scan_body(*buf, got, at, out);
+      }
       read_ahead(at + got);
       return scan_body(*buf, got, at, out);
     }
@@ -909,6 +954,7 @@ rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int l
   s->ctx = ctx;
   s->depth = ctx ? rio_ctx_spans_ahead(ctx) : 0;
   if (s->depth > rio_scanner::kSlots - 1) s->depth = rio_scanner::kSlots - 1;
+  if (const char *e = getenv("RIO_SCAN_EARLY")) s->early = atoi(e) != 0;
   if (const char *e = getenv("RIO_SPAN_RAMP")) s->ramp_steps = std::min(std::max(atoi(e), 0), 6);
   if (const char *e = getenv("RIO_SPAN_RAMP_MIN")) s->ramp_min = strtoull(e, nullptr, 0);
   s->res = ctx ? rio_ctx_take_results(ctx) : rio_results_new();
