@@ -1400,6 +1400,12 @@ __device__ __forceinline__ void zmem_sync_dev() {
 constexpr uint32_t kSyncSeg = 1024;                       // bits per lane per round
 constexpr uint32_t kSyncBits = 64 * kSyncSeg;             // bits per round and wave
 constexpr int kSyncIters = 8;
+#ifndef RIO_SYNC_LEAD
+#define RIO_SYNC_LEAD 0
+#endif
+// bits of a segment's end the first decode of a round covers (0: the whole segment)
+constexpr uint32_t kSyncLead = RIO_SYNC_LEAD;
+static_assert(kSyncLead < kSyncSeg, "a lead-in within the segment");
 #ifndef RIO_SYNC_WAVES
 #define RIO_SYNC_WAVES 12
 #endif
@@ -1817,7 +1823,11 @@ __global__ void __launch_bounds__(64 * kW) k_flate_sync(const uint8_t *__restric
           if (need && it == 0) {
             nt = no = fl = 0;
             stg = false;
-            ex = sync_count<false>(T, S.win, st, seg_end, lim, nt, no, fl, nullptr, slack);
+            // only the exit is wanted, and a decode from a wrong start falls into
+            // step within a few codes: the segment's last kSyncLead bits suffice
+            // (a lane whose exit comes out wrong makes its successor decode again)
+            const uint32_t st0 = kSyncLead ? seg_end - kSyncLead : st;
+            ex = sync_count<false>(T, S.win, st0, seg_end, lim, nt, no, fl, nullptr, slack);
           } else if (need) {
             nt = no = fl = 0;
             slack = 0x7fffffff;
