@@ -1403,7 +1403,11 @@ constexpr int kSyncIters = 8;
 #ifndef RIO_SYNC_LEAD
 #define RIO_SYNC_LEAD 0
 #endif
-// bits of a segment's end the first decode of a round covers (0: the whole segment)
+// bits of a segment's end the first decode of a round covers (0: the whole segment).
+// Measured and not kept (round 6, profiles/r06_flate_sync_lead_ab.jsonl): the
+// last 128 / 256 / 512 bits only -- serial C3@16k 35.8-36.4 against 37.8, C3
+// 49.6-51.8 against 53.6: exits found from a short lead-in are wrong often
+// enough that whole waves decode a third time.
 constexpr uint32_t kSyncLead = RIO_SYNC_LEAD;
 static_assert(kSyncLead < kSyncSeg, "a lead-in within the segment");
 #ifndef RIO_SYNC_WAVES
