@@ -235,11 +235,16 @@ struct rio_scanner {
   int ramp_steps = 2;
   uint64_t ramp_min = 256ull << 20;
   bool ramp_off = false;
+  // compressed bodies of small blocks (the first block under kEarlyChunks
+  // chunks) ramp too, and stage their next span early (RIO_SPAN_RAMP_C=0: not):
+  // their spans decode in proportion to their size
+  bool ramp_c = true;
+  int ramp_blk = -1;  // the body's first block: 1 small, 0 large, -1 not yet read
   uint64_t body_next = 0;  // the index of the next body span to become the current batch
   uint64_t span_size(uint64_t idx) const {
     const uint64_t maxspan = rio_ctx_max_span(ctx);
-    if (ramp_off || v1 || codec != RIO_CODEC_NONE || ramp_steps <= 0 || maxspan < ramp_min ||
-        idx >= (uint64_t)ramp_steps)
+    if (ramp_off || v1 || (codec != RIO_CODEC_NONE && !(ramp_c && ramp_blk == 1)) || ramp_steps <= 0 ||
+        maxspan < ramp_min || idx >= (uint64_t)ramp_steps)
       return maxspan;
     const uint64_t sz = (maxspan >> (ramp_steps - (int)idx)) / kCk * kCk;
     return sz < 4 * kCk ? maxspan : sz;
@@ -571,7 +576,7 @@ struct rio_scanner {
     const int is_end = (at + got >= file_size);
     if (body) {  // the body's span (the current slot; the bytes after it read meanwhile)
       if (early && depth > 0 && !v1 && !is_end && at + got < limit && codec != RIO_CODEC_NONE &&
-          first_block_chunks(*buf, got) >= kEarlyChunks) {
+          (first_block_chunks(*buf, got) >= kEarlyChunks || (ramp_c && ramp_blk == 1))) {
         // staged; the span after it begun once this copy in is done (see `early`)
         rio_ctx *c = cx[slot];
         if (c != ctx && rio_ctx_reserve_span(c, got) != 0) return -1;
@@ -797,6 +802,14 @@ bool next_batch(rio_scanner *s) {
       s->done = true;
       return false;
     }
+    if (s->ramp_blk < 0 && s->codec != RIO_CODEC_NONE && !s->v1) {  // the body's first block: small or large
+      uint8_t hdr[RIO_CHUNK_HEADER_SIZE];
+      int st = 0;
+      s->read_full(hdr, sizeof(hdr), s->off, &st);
+      uint32_t total = 0;
+      if (st == 0) memcpy(&total, hdr + 20, 4);
+      s->ramp_blk = (st == 0 && total > 0 && total < rio_scanner::kEarlyChunks) ? 1 : 0;
+    }
     const uint64_t want = s->span_size(s->body_next);
     uint64_t n = s->file_size - s->off;
     if (n > want) n = want;
@@ -955,6 +968,7 @@ rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int l
   s->depth = ctx ? rio_ctx_spans_ahead(ctx) : 0;
   if (s->depth > rio_scanner::kSlots - 1) s->depth = rio_scanner::kSlots - 1;
   if (const char *e = getenv("RIO_SCAN_EARLY")) s->early = atoi(e) != 0;
+  if (const char *e = getenv("RIO_SPAN_RAMP_C")) s->ramp_c = atoi(e) != 0;
   if (const char *e = getenv("RIO_SPAN_RAMP")) s->ramp_steps = std::min(std::max(atoi(e), 0), 6);
   if (const char *e = getenv("RIO_SPAN_RAMP_MIN")) s->ramp_min = strtoull(e, nullptr, 0);
   s->res = ctx ? rio_ctx_take_results(ctx) : rio_results_new();
