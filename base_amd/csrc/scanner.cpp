@@ -308,6 +308,20 @@ struct rio_scanner {
   }
   // the current batch's result copies (rio_scan_span_begin) in place
   int finish_cur() { return rio_scan_span_end(cx[slot]); }
+  // A span ahead will be begun: every slot's context opened now, while no
+  // span-ahead thread runs (a sibling is opened from the context before it,
+  // which such a thread would otherwise be using; rio_gpu.h: a scanner's spans
+  // ahead hold `depth` further contexts of the ctx's size until rio_close). A
+  // file that fits one span never opens them.
+  bool open_siblings() {
+    for (int i = 1; i <= depth; i++)
+      if (!cx[i]) {
+        cx[i] = rio_ctx_sibling(cx[i - 1]);
+        if (!cx[i]) return false;
+        rs[i] = rio_ctx_take_results(ctx);
+      }
+    return true;
+  }
   // a body span in host memory, decoded into the current slot (results deferred)
   int scan_body(const uint8_t *base, uint64_t n, uint64_t at, rio_batch *out) {
     const int is_end = (at + n >= file_size);
@@ -383,19 +397,7 @@ struct rio_scanner {
       const uint64_t want = span_size(body_next + aq.size() + (early_first ? 1 : 0));
       const uint64_t n = file_size - at < want ? file_size - at : want;
       if (at + n <= pend) return;  // (a span inside the one before it: not a body's next span)
-      if (first) {
-        // a span ahead will be begun: every slot's context opened now, while no
-        // span-ahead thread runs (a sibling is opened from the context before
-        // it, which such a thread would otherwise be using; rio_gpu.h: a
-        // scanner's spans ahead hold `depth` further contexts of the ctx's size
-        // until rio_close). A file that fits one span never opens them.
-        for (int i = 1; i <= depth; i++)
-          if (!cx[i]) {
-            cx[i] = rio_ctx_sibling(cx[i - 1]);
-            if (!cx[i]) return;
-            rs[i] = rio_ctx_take_results(ctx);
-          }
-      }
+      if (first && !open_siblings()) return;
       int sl = -1;  // a slot neither the current batch nor a span ahead holds
       for (int i = 0; i < kSlots && sl < 0; i++) {
         bool used = (i == slot);
@@ -580,7 +582,9 @@ struct rio_scanner {
         // staged; the span after it begun once this copy in is done (see `early`)
         rio_ctx *c = cx[slot];
         if (c != ctx && rio_ctx_reserve_span(c, got) != 0) return -1;
-        if (rio_scan_span_stage(c, *buf, got, codec) != 0 || rio_ctx_wait_staged(c) != 0) return -1;
+        if (rio_scan_span_stage(c, *buf, got, codec) != 0) return -1;
+        open_siblings();  // (the first time: while the copy in runs, not after it; a failure is seen below)
+        if (rio_ctx_wait_staged(c) != 0) return -1;
         span_data = *buf;
         span_at = at;
         span_n = got;

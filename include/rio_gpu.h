@@ -398,9 +398,10 @@ typedef struct rio_scanner rio_scanner;
  * Span schedule (read from the environment when the scanner is made; results
  * do not depend on it): RIO_SPAN_RAMP=k (default 2, 0 off) -- an uncompressed
  * body's first spans are the ctx's span >> k, >> k-1, ... (spans of at least
- * RIO_SPAN_RAMP_MIN bytes, default 256 MiB); RIO_SCAN_EARLY=0 -- a compressed
- * body span of large blocks is no longer staged and followed by the next
- * span's copy in before it is decoded (DESIGN.md "Round 6 in brief"). */
+ * RIO_SPAN_RAMP_MIN bytes, default 256 MiB), and a compressed body's of small
+ * blocks too (RIO_SPAN_RAMP_C=0: not); RIO_SCAN_EARLY=0 -- a compressed body
+ * span is no longer staged and followed by the next span's copy in before it
+ * is decoded (DESIGN.md "Round 6 in brief"). */
 rio_scanner *rio_scanner_new(rio_ctx *ctx, const rio_reader *r, int start, int limit, int nshard);
 /* Scan (scannerv2.go:390-404): 1 if a new record is available */
 int rio_scanner_scan(rio_scanner *s);
