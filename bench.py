@@ -665,6 +665,15 @@ def main():
     del dev
     torch.cuda.empty_cache()
     progress(rank, "C2 %.2f GiB/s" % value)
+    # the end-to-end scans first among the sub-lines: after the device-resident
+    # workloads (tens of GB of generated files and pinned staging allocated and
+    # freed) the same scans measured ~10 % slower (C2 40 against 45-47 GiB/s,
+    # C3 13.7 against 15-16) than in a process of their own
+    if world == 1 and not args.no_e2e:  # the drop-in path, PCIe included (north_star; DESIGN.md §5e)
+        progress(rank, "end-to-end scans")
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_e2e
+        out["e2e"] = bench_e2e.run_e2e(local, args.e2e_gib)
     if not args.no_flate:
         progress(rank, "C3 flate")
         out["c3_flate"] = c3_flate(args, local, world, dist)
@@ -677,11 +686,6 @@ def main():
     if not args.no_c5:
         progress(rank, "C5 1024 files")
         out["c5_flate"] = c5_flate(args, local, rank, world, dist)
-    if world == 1 and not args.no_e2e:  # the drop-in path, PCIe included (north_star; DESIGN.md §5e)
-        progress(rank, "end-to-end scans")
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        import bench_e2e
-        out["e2e"] = bench_e2e.run_e2e(local, args.e2e_gib)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         progress(rank, "CPU baselines")
         out["cpu_baseline"], out["cpu_baseline_all_cores"], out["c1_cpu"] = cpu_baselines(args)
