@@ -230,12 +230,13 @@ def test_slow_reader_spans_ahead(oracle, trs):
 
 @pytest.mark.parametrize("trs,max_items", [([], 23), (["flate"], 23), (["zstd"], 23), ([], 4000), (["flate"], 4000)])
 def test_span_ramp(oracle, trs, max_items, monkeypatch):
-    """The span ramp (scanner.cpp span_size): an uncompressed body's first spans
-    smaller than the ctx's, forced here at small sizes (RIO_SPAN_RAMP_MIN=0, 3
-    steps: 4, 4, 8, then 16-chunk spans at a 16-chunk ctx span). Every record
-    and the error as the oracle's; with MaxItems = 4000 a block is longer than
-    the first spans, which turns the ramp off (the ctx's span from there on).
-    Compressed bodies are not ramped (the same settings, the ctx's spans)."""
+    """The span ramp (scanner.cpp span_size): a body's first spans smaller than
+    the ctx's, forced here at small sizes (RIO_SPAN_RAMP_MIN=0, 3 steps: 4, 4,
+    8, then 16-chunk spans at a 16-chunk ctx span). Every record and the error
+    as the oracle's. Compressed bodies of small blocks (MaxItems = 23) ramp and
+    stage each next span early too; with MaxItems = 4000 an uncompressed block
+    is longer than the first spans, which turns the ramp off (the ctx's span
+    from there on), and a compressed one is large, so it is not ramped."""
     from base_amd.recordio import gpu
     from base_amd.recordio.writer import WriterOpts, write_file
     if "zstd" in trs and not oracle_has_zstd(oracle):
