@@ -2819,6 +2819,9 @@ __global__ void __launch_bounds__(64) k_zstd_exec(DevBufs d, const unsigned long
               const uint32_t ss = zr_slot(src), ds = zr_slot(dst);
               if ((off >= 8 || myml <= off) && (all_far || (all_ring && ss + myml + 12 <= kZRing)) &&
                   ds + myml <= kZRing) {
+                // (measured and not kept, round 6: a far match's pieces' source dwords
+                // all loaded before any is used -- 44.6 / 37.6 GiB/s against 46.5 /
+                // 39.5, profiles/r06_zstd_exec_unroll_ab.jsonl)
                 for (uint32_t k = 0; k < myml; k += 8) {
                   uint32_t w0, w1, w2;
                   if (k == 0 && qv && all_far) {  // prefetched a group ago
