@@ -2629,7 +2629,12 @@ __global__ void __launch_bounds__(64) k_zstd_fix(DevBufs d, const unsigned long 
 #define RIO_ZRING_K 2
 #endif
 #ifndef RIO_ZEXEC_READY_MAX
-#define RIO_ZEXEC_READY_MAX 32  // longest match a lane copies on its own in the parallel round
+// longest match a lane copies on its own in the parallel round (longer ones: the
+// whole wave, in order). Round 6, with far sources prefetched and 12 waves per
+// CU: 16 -> C4 47.5-47.7 / 40.1-40.3 serial, 12 the same, 8 46.7-46.9, 24
+// 46.8-47.0, 32 (rounds 2-5) 46.6-46.9, 48 45.5-46.1
+// (profiles/r06_zstd_ready_max_ab.jsonl)
+#define RIO_ZEXEC_READY_MAX 16
 #endif
 constexpr uint32_t kZRingK = RIO_ZRING_K;  // ring = kZRingK x 4 KiB
 static_assert(kZRingK >= 2, "zr_slot's multiply-high reciprocal needs kZRingK >= 2");
