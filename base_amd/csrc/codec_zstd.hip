@@ -49,7 +49,9 @@ constexpr uint64_t kZLitStride = kZBlockMax + 256;  // per-wave literal buffer
 #endif
 constexpr int kZWaves = RIO_ZWAVES;  // resident zstd waves per CU (LDS ~10 KiB each)
 #ifndef RIO_ZFIX_WAVES
-#define RIO_ZFIX_WAVES 20  // 5 per SIMD (8: 162.0 ms for C4, 20: 156.1, 28: 159.8)
+// 6 per SIMD (round 2: 8 waves 162.0 ms for C4, 20: 156.1, 28: 159.8; round 6:
+// 24 against 20, serial C4 40.8 against 40.0, profiles/r06_zstd_fix_waves_ab.jsonl)
+#define RIO_ZFIX_WAVES 24
 #endif
 constexpr int kZFixWaves = RIO_ZFIX_WAVES;            // k_zstd_fix waves per CU
 
